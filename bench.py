@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Benchmark: MPC solves/s for arm6.urdf, N=64, SQP with PCG-SS (BASELINE.json).
+
+One "step" = one batched SQP solve (TrajoptMPCReference.SQP semantics, run to
+every problem's exit) of B independent problems of the §8d workload:
+  arm6 (corrected), N=64, dt=0.1, Euler; QuadraticCost(I, 100 I,
+  0.1 I, xg=0); problem i: q0 ~ U(-1,1)^6 from default_rng(seed0 + i),
+  qd0 = 0, x = Euler rollout of u = 0; reference default options, fp64.
+Inputs are resident in HBM before the timed region (each step restores the
+initial trajectories with a device-to-device copy, inside the timed region).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+one process per GPU, each rank solves its own B problems (seeds offset by
+rank * B) -- independent problems, no data-path collective, weak scaling.
+torch.distributed is used only for the barrier and the max-over-ranks time.
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector (= fp64 matrix) spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--N", type=int, default=64)
+    ap.add_argument("--links", type=int, default=6)
+    ap.add_argument("--method", default="PCG-SS")
+    ap.add_argument("--seed0", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 2 per core)")
+    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def initial_states(n, B, seed0):
+    q0 = np.zeros((B, n))
+    for i in range(B):
+        q0[i] = np.random.default_rng(seed0 + i).uniform(-1.0, 1.0, n)
+    return q0
+
+
+# ------------------------------------------------------------------ byte / flop model
+def pcg_bytes_per_iter(N, nx):
+    return 8 * (2 * (2 * N - 1) * nx * nx + 10 * N * nx)
+
+
+def pcg_flops_per_iter(N, nx, method):
+    # SpMV with S (3 blocks per block row) + preconditioner apply + dots/axpys
+    spmv = 2 * (3 * N - 2) * nx * nx
+    pre = {"PCG-J": N * nx, "PCG-BJ": 2 * N * nx * nx, "PCG-SS": 2 * (N + 2 * (N - 1) + N) * nx * nx}[method]
+    return spmv + pre + 10 * N * nx
+
+
+# ------------------------------------------------------------------ CPU baseline (oracle = restatement)
+def _cpu_solve(args):
+    seed, n, N = args
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    m = parse_urdf(planar_arm_urdf(n))
+    x, u = osqp.initial_problem(m, N, 0.1, seed)
+    cost = osqp.QuadCost(np.eye(2 * n), 100 * np.eye(2 * n), 0.1 * np.eye(n), np.zeros(2 * n))
+    r = osqp.sqp(m, cost, x, u, N, 0.1, "PCG-SS")
+    return r["exit_sqp"], r["sqp_iter"]
+
+
+def cpu_baseline(n, N, sample, procs, seed0):
+    ctx = mp.get_context("fork")
+    jobs = [(seed0 + i, n, N) for i in range(sample)]
+    t0 = time.perf_counter()
+    with ctx.Pool(procs, initializer=os.environ.__setitem__, initargs=("OMP_NUM_THREADS", "1")) as pool:
+        res = pool.map(_cpu_solve, jobs, chunksize=1)
+    wall = time.perf_counter() - t0
+    return sample / wall, wall, res
+
+
+# ------------------------------------------------------------------ KKT residual vs the reference (golden QP)
+def kkt_residual_check(ctx, model, n):
+    """|r_build - r_ref| for the first QP of arm6 N=64 seed 0, r = ||[G+rho I, C^T; C, 0] dxul - [g; c]||_inf
+    computed identically on both sides; the reference's r comes from tests/golden."""
+    path = os.path.join(ROOT, "tests", "golden", "qp_arm6fix_N64.npz")
+    if n != 6 or not os.path.exists(path):
+        return None
+    d = np.load(path)
+    N = d["x"].shape[1]
+    nx, nu = 2 * n, n
+    r = ctx.qp_batch(d["x"][None], d["u"][None], N, float(d["dt"]), float(d["rho"]), "PCG-SS", want_blocks=False)
+    dxul = r["dxul"][0]
+    nz = (nx + nu) * (N - 1) + nx
+    G = np.zeros((nz, nz))
+    for k in range(N - 1):
+        G[k * (nx + nu):k * (nx + nu) + nx, k * (nx + nu):k * (nx + nu) + nx] = np.eye(nx)
+        G[k * (nx + nu) + nx:(k + 1) * (nx + nu), k * (nx + nu) + nx:(k + 1) * (nx + nu)] = 0.1 * np.eye(nu)
+    G[nz - nx:, nz - nx:] = 100 * np.eye(nx)
+    G += float(d["rho"]) * np.eye(nz)
+    C = np.zeros((nx * N, nz))
+    C[:nx, :nx] = np.eye(nx)
+    for k in range(N - 1):
+        c0 = k * (nx + nu)
+        C[(k + 1) * nx:(k + 2) * nx, c0:c0 + nx] = -d["A"][k]
+        C[(k + 1) * nx:(k + 2) * nx, c0 + nx:c0 + nx + nu] = -d["B"][k]
+        C[(k + 1) * nx:(k + 2) * nx, c0 + nx + nu:c0 + 2 * nx + nu] = np.eye(nx)
+    K = np.block([[G, C.T], [C, np.zeros((nx * N, nx * N))]])
+    rhs = np.concatenate([d["g"], d["c"]])
+    r_build = float(np.max(np.abs(K @ dxul - rhs)))
+    r_ref = float(d["kkt_res_SS"])
+    return {"r_build": r_build, "r_ref": r_ref, "abs_diff": abs(r_build - r_ref),
+            "pcg_iters_build": int(r["pcg_iters"][0]), "pcg_iters_ref": int(d["iters_SS"])}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group(backend="nccl")
+        dist = (torch, tdist)
+
+    def barrier_max(v):
+        if dist is None:
+            return v
+        torch, tdist = dist
+        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier():
+        if dist is not None:
+            dist[1].barrier()
+
+    from trajoptmpcreference_amd import _native
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+
+    n, N, B, dt = a.links, a.N, a.batch, 0.1
+    nx, nu = 2 * n, n
+    model = parse_urdf(planar_arm_urdf(n))
+    ctx = _native.Context(local_rank)
+    ctx.set_model(model)
+    ctx.set_cost_quadratic(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
+
+    # ---- workload resident in HBM
+    seed_base = a.seed0 + rank * B
+    x0 = np.zeros((B, nx, N))
+    x0[:, :n, 0] = initial_states(n, B, seed_base)
+    u0 = np.zeros((B, nu, N - 1))
+    xb, ub = x0.nbytes, u0.nbytes
+    d_x0, d_u0, d_x, d_u = ctx.alloc(xb), ctx.alloc(ub), ctx.alloc(xb), ctx.alloc(ub)
+    ctx.h2d(d_x0, x0)
+    ctx.h2d(d_u0, u0)
+    ctx.rollout_device(B, N, dt, d_x0, d_u0)
+
+    def step():
+        ctx.d2d(d_x, d_x0, xb)
+        ctx.d2d(d_u, d_u0, ub)
+        ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method)
+
+    for _ in range(a.warmup):
+        step()
+    ctx.synchronize()
+    ctx.set_options(profile=1)
+    ctx.reset_stats()
+    counters = np.zeros(4, dtype=np.int64)
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        counters += np.array(ctx.solve_counters(), dtype=np.int64)
+    ctx.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = barrier_max(t1 - t0)
+    ctx.set_options(profile=0)
+
+    kernels = {}
+    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "schur", "pcg", "dxu", "ls_terms", "ls_decide"]:
+        cnt, ms = ctx.kernel_stats(name)
+        kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt if cnt else 0.0}
+    dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
+
+    total_solves = B * a.steps * world
+    value = total_solves / elapsed
+    ms_per_step = 1000.0 * elapsed / a.steps
+
+    # ---- status of one solve (exit codes / iteration counts) for the record
+    ctx.d2d(d_x, d_x0, xb)
+    ctx.d2d(d_u, d_u0, ub)
+    exit_codes, iters = ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=True)
+
+    if rank != 0:
+        if dist is not None:
+            dist[1].destroy_process_group()
+        return
+
+    pcg = kernels["pcg"]
+    n_pcg_iters = int(counters[1])
+    per_launch_iters = n_pcg_iters / max(1, pcg["launches"])
+    alg_bytes = per_launch_iters * pcg_bytes_per_iter(N, nx)
+    alg_flops = per_launch_iters * pcg_flops_per_iter(N, nx, a.method)
+    pcg_avg_s = pcg["avg_ms"] / 1000.0 if pcg["avg_ms"] > 0 else float("nan")
+    ach_gbs = alg_bytes / pcg_avg_s / 1e9
+    ach_tf = alg_flops / pcg_avg_s / 1e12
+    roofline = {"kernel": "k_pcg", "bound": "mfma", "achieved": ach_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                "algorithmic_flops_per_launch": alg_flops, "avg_launch_ms": pcg["avg_ms"],
+                "streaming_model": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": ach_gbs / HBM_PEAK_GBS,
+                                    "algorithmic_bytes_per_launch": alg_bytes}}
+
+    cpu = None
+    if not a.no_cpu_baseline:
+        procs = max(1, min(a.cpu_procs, os.cpu_count() or 1))
+        sample = a.cpu_sample if a.cpu_sample > 0 else 2 * procs
+        v, wall, res = cpu_baseline(n, N, sample, procs, a.seed0)
+        cpu = {"value": v, "unit": "solves/s", "cores": procs, "kind": "port",
+               "sample": f"{sample} problems of the same workload (seeds {a.seed0}..{a.seed0 + sample - 1}), "
+                         f"oracle NumPy restatement (no SymPy), {procs} processes x 1 BLAS thread, {wall:.1f} s"}
+
+    kkt = kkt_residual_check(ctx, model, n)
+    out = {
+        "metric": "MPC solves/sec (arm6.urdf, N=64, SQP-PCG) at 1/2/4/8 GPUs; KKT residual vs ref",
+        "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
+        "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} SQP {a.method}, batch {B} per GPU",
+                   "global_batch": B * world, "N": N, "method": a.method, "parallelism": f"shard{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "kkt_residual": kkt,
+        "kernels": kernels, "dominant_kernel": dominant,
+        "work": {"problem_qps_per_step": int(counters[0]) / a.steps, "pcg_iters_per_step": n_pcg_iters / a.steps,
+                 "grad_evals_per_step": int(counters[2]) / a.steps, "ls_trials_per_qp": int(counters[3]) // max(1, a.steps)},
+        "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(exit_codes, return_counts=True))},
+        "sqp_iters_mean": float(np.mean(iters)),
+    }
+    print(json.dumps(out))
+    if dist is not None:
+        dist[1].destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

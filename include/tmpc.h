@@ -1,0 +1,186 @@
+/*
+ * tmpc.h -- C ABI of the MI355X-native batched trajectory-optimisation solver
+ * (libtmpc.so).  Drop-in boundary for the hot path of
+ * VCA-EPFL/TrajoptMPCReference:
+ *
+ *   TrajoptMPCReference.SQP(x, u, N, dt, METHOD, options)   TrajoptMPCReference.py:510-760
+ *     formKKTSystemBlocks                                    TrajoptMPCReference.py:200-271
+ *     solveKKTSystem_Schur (+ PCG)                           TrajoptMPCReference.py:415-455
+ *   PCG(A, b, block_size, Nblocks, guess, options).solve()   GBD-PCG-Python/PCG.py:5-16,66-111,214
+ *   URDFPlant.forward_dynamics / forward_dynamics_gradient   TrajoptPlant.py:283-323
+ *   TrajoptPlant.integrator (Euler, type 0)                  TrajoptPlant.py:83-108
+ *
+ * The reference has no FFI of its own (it is pure Python); these are the
+ * entry points a ctypes binding of that Python surface needs (see
+ * INTEGRATION.md).  Conventions:
+ *   - every entry point returns 0 on success and < 0 on error; the message is
+ *     available from tmpc_last_error(ctx) (the reference print()s and exit()s);
+ *   - host pointers are caller-owned and only accessed during the call;
+ *     "_device" entry points take device pointers obtained from
+ *     tmpc_device_alloc on the same context;
+ *   - one context per GPU, used by one host thread; calls are synchronous on
+ *     the context's HIP stream;
+ *   - all arithmetic is IEEE fp64, as in the reference.
+ *
+ * Array layouts follow the reference's NumPy arrays in C order:
+ *   x: [B][nx][N] (state column per knot), u: [B][nu][N-1],
+ *   per-knot matrices row-major [K][rows][cols].
+ */
+#ifndef TMPC_H
+#define TMPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMPC_ABI_VERSION 1
+
+/* SQPSolverMethods (TrajoptMPCReference.py:13-18). N (dense KKT) is not offered on the GPU. */
+#define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (not yet on GPU: returns error) */
+#define TMPC_LINSYS_PCG_J 2  /* PCG, Jacobi preconditioner            PCG.py:168-169 */
+#define TMPC_LINSYS_PCG_BJ 3 /* PCG, block-Jacobi preconditioner      PCG.py:171-179 */
+#define TMPC_LINSYS_PCG_SS 4 /* PCG, symmetric-stair preconditioner   PCG.py:181-212 */
+
+/* preconditioner ids for tmpc_pcg_batch (PCG options['preconditioner_type']) */
+#define TMPC_PRECOND_J 1
+#define TMPC_PRECOND_BJ 2
+#define TMPC_PRECOND_SS 3
+
+/* joint types of the model arrays */
+#define TMPC_JOINT_REVOLUTE 0  /* X(q) = X0 + cos(q) Xa + sin(q) Xb */
+#define TMPC_JOINT_PRISMATIC 1 /* X(q) = X0 + q Xa                  */
+
+typedef struct tmpc_ctx tmpc_ctx;
+
+/* Every key of TrajoptMPCReference.set_default_options (TrajoptMPCReference.py:91-115)
+ * that the unconstrained SQP path reads, plus the PCG keys (PCG.py:19-25). */
+typedef struct tmpc_options {
+  double exit_tolerance_linSys;          /* 1e-6   */
+  int32_t max_iter_linSys;               /* 100    */
+  int32_t max_iter_SQP_DDP;              /* 100    */
+  double exit_tolerance_SQP_DDP;         /* 1e-6   */
+  double alpha_factor_SQP_DDP;           /* 0.5    */
+  double alpha_min_SQP_DDP;              /* 0.005  */
+  double rho_factor_SQP_DDP;             /* 4      */
+  double rho_min_SQP_DDP;                /* 1e-3   */
+  double rho_max_SQP_DDP;                /* 1e3    */
+  double rho_init_SQP_DDP;               /* 1e-3   */
+  double expected_reduction_min_SQP_DDP; /* 0.05   */
+  double expected_reduction_max_SQP_DDP; /* 3      */
+  double merit_mu;                       /* 10 (fixed in the reference, :545-546) */
+  int32_t profile;                       /* 1: time kernels with HIP events (tmpc_kernel_stats) */
+  int32_t reserved;
+} tmpc_options;
+
+/* Per-problem SQP trace, the numeric fields of self.trace (TrajoptMPCReference.py:555-569,691-743).
+ * Every member is nullable; each array is [B][max_iter_SQP_DDP + 1]; row 0 is the initial entry,
+ * row i+1 the entry appended by SQP iteration i; rows used = sqp_iter + 1. */
+typedef struct tmpc_trace {
+  int32_t* iteration;
+  int32_t* line_search_iteration;
+  double* alpha;
+  double* rho;
+  double* J;
+  double* c;
+  double* merit;
+  double* D;               /* NaN in row 0 (None in the reference) */
+  double* reduction_ratio; /* NaN in row 0 */
+  int32_t* succeeded_line_search;
+  int32_t* pcg_iters;      /* PCG iterations of the QP solved in that SQP iteration (0 in row 0) */
+} tmpc_trace;
+
+int tmpc_abi_version(void);
+int tmpc_device_count(int* count);
+int tmpc_create(int device, tmpc_ctx** out);
+void tmpc_destroy(tmpc_ctx* ctx);
+const char* tmpc_last_error(const tmpc_ctx* ctx);
+
+/* Robot model in DFS order, as built by the reference's URDF parser
+ * (GRiD/URDFParser/URDFParser.py:227-435): parent[n] (-1 = base), joint type,
+ * index of the unit motion-subspace vector S (0..5), transform coefficient
+ * matrices X0/Xa/Xb [n][6][6] and spatial inertias I [n][6][6]; gravity is
+ * options['gravity'] (TrajoptPlant.py:31, -9.81).  Replaces URDFPlant.__init__
+ * (TrajoptPlant.py:275-281) + RBDReference(robot) state.  1 <= n <= 7. */
+int tmpc_set_model(tmpc_ctx* ctx, int n, const int32_t* parent, const int32_t* jtype, const int32_t* saxis,
+                   const double* X0, const double* Xa, const double* Xb, const double* I, double gravity);
+
+/* QuadraticCost(Q, QF, R, xg, QF_start) (TrajoptCost.py:24-47); QF_start < 0 means None. */
+int tmpc_set_cost_quadratic(tmpc_ctx* ctx, int nx, int nu, const double* Q, const double* QF, const double* R,
+                            const double* xg, int32_t QF_start);
+
+void tmpc_default_options(tmpc_options* opts);
+int tmpc_set_options(tmpc_ctx* ctx, const tmpc_options* opts);
+
+/* Batched TrajoptMPCReference.SQP (TrajoptMPCReference.py:510-760) for B independent problems,
+ * unconstrained (TrajoptConstraint() default).  x [B][nx][N] and u [B][nu][N-1] are read as the
+ * initial trajectory and overwritten with the result; per-problem outputs mirror the returned
+ * tuple (x, u, exit_sqp, exit_soft, outer_iter, sqp_iter).  trace is nullable. */
+int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* x, double* u,
+                         int32_t* exit_sqp, int32_t* exit_soft, int32_t* outer_iter, int32_t* sqp_iter,
+                         tmpc_trace* trace);
+
+/* Same solve with x/u already resident in device memory (tmpc_device_alloc); exit_sqp and
+ * sqp_iter are host arrays [B] (nullable). */
+int tmpc_sqp_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
+                                int32_t* exit_sqp, int32_t* sqp_iter);
+
+/* Euler rollout x_{k+1} = f(x_k, u_k) from x[:, 0] (device pointers), the §8d initial trajectory. */
+int tmpc_rollout_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, const double* d_u);
+
+/* ---- kernel-level entry points (unit parity) ---- */
+
+/* URDFPlant.forward_dynamics + Euler integrator for K independent knots
+ * (TrajoptPlant.py:92-99,283-299): x [K][nx], u [K][nu] -> xnext [K][nx], qdd [K][n],
+ * Minv [K][n][n] (outputs nullable). */
+int tmpc_fd_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const double* u, double* xnext, double* qdd,
+                  double* Minv);
+
+/* URDFPlant.forward_dynamics_gradient + integrator(return_gradient=True)
+ * (TrajoptPlant.py:100-108,301-323): -> A [K][nx][nx], B [K][nx][nu], dqdd [K][n][3n] (nullable). */
+int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const double* u, double* A, double* B,
+                       double* dqdd);
+
+/* One QP of the SQP loop for B problems: formKKTSystemBlocks + solveKKTSystem_Schur with PCG
+ * (TrajoptMPCReference.py:200-271,415-455) at the given trajectories and regularisation rho[B].
+ * dxul [B][n_xu(N-1)+nx + nx N] in the reference's interleaved order [x0,u0,x1,...,x_{N-1}; lambda].
+ * S_diag [B][N][nx][nx], S_lo [B][N-1][nx][nx] (= S_{k+1,k}), gamma [B][N nx], P_diag [B][N][nx][nx]
+ * are optional (nullable) copies of the intermediate blocks. */
+int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
+                  const double* u, double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma,
+                  double* P_diag);
+
+/* PCG(S, gamma, nx, N, options={'preconditioner_type': J|BJ|SS, exit_tolerance, max_iter}).solve()
+ * (GBD-PCG-Python/PCG.py:66-111) on B block-tridiagonal systems given by their blocks:
+ * S_diag [B][N][nx][nx], S_lo [B][N-1][nx][nx] = S_{k+1,k}, S_up [B][N-1][nx][nx] = S_{k,k+1}
+ * (nullable: S_lo^T is used), gamma [B][N nx], guess [B][N nx] (initial iterate, nullable = zeros,
+ * PCG.py:11-12,33-34).  Outputs lambda [B][N nx], iters [B],
+ * trace_nu / trace_res [B][max_iter+1] (|nu| and ||b - A x|| per iteration, nullable; entries past
+ * iters[b] are left untouched), P_diag [B][N][nx][nx] (the inverted diagonal blocks, nullable). */
+int tmpc_pcg_batch(tmpc_ctx* ctx, int B, int N, int nx, int precond, const double* S_diag, const double* S_lo,
+                   const double* S_up, const double* gamma, const double* guess, double tol, int max_iter,
+                   double* lambda, int32_t* iters, double* trace_nu, double* trace_res, double* P_diag);
+
+/* ---- device memory / timing helpers (the bench keeps inputs resident in HBM) ---- */
+int tmpc_device_alloc(tmpc_ctx* ctx, size_t bytes, void** ptr);
+int tmpc_device_free(tmpc_ctx* ctx, void* ptr);
+int tmpc_memcpy_h2d(tmpc_ctx* ctx, void* dst, const void* src, size_t bytes);
+int tmpc_memcpy_d2h(tmpc_ctx* ctx, void* dst, const void* src, size_t bytes);
+int tmpc_memcpy_d2d(tmpc_ctx* ctx, void* dst, const void* src, size_t bytes);
+int tmpc_synchronize(tmpc_ctx* ctx);
+
+/* Kernel timing collected with HIP events on the context stream when options.profile = 1.
+ * name: "pcg", "qp_fd", "qp_grad", "ginv", "schur", "dxu", "ls_terms", "ls_decide". */
+int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
+int tmpc_reset_stats(tmpc_ctx* ctx);
+
+/* Work counters of the last SQP solve on this context: [0] problem-QPs solved, [1] total PCG
+ * iterations, [2] QPs that recomputed the dynamics gradient, [3] line-search trials per QP. */
+int tmpc_solve_counters(tmpc_ctx* ctx, int64_t* counters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMPC_H */

@@ -1,0 +1,327 @@
+"""SQP / Schur / GBD-PCG restated from the reference, blockwise.
+
+Follows TrajoptMPCReference.py (SQP :510-760, formKKTSystemBlocks :200-271,
+solveKKTSystem_Schur :415-455, reduce_regularization :457-461,
+check_for_exit_or_error :463-481) and GBD-PCG-Python/PCG.py (pcg :66-111,
+compute_preconditioner :166-212).  The reference forms dense G (n_xu(N-1)+nx)^2,
+inverts it and multiplies dense C G^-1 C^T; S is exactly block-tridiagonal
+ so we form the same blocks directly:
+
+  Ghat_k = (G_k + rho I)^-1,  AB_k = [A_k B_k],  E = [I_nx 0]
+  S_00 = -E Ghat_0 E^T
+  S_{k+1,k+1} = -(AB_k Ghat_k AB_k^T + E Ghat_{k+1} E^T)
+  S_{k+1,k} = AB_k Ghat_k E^T,   S_{k,k+1} = S_{k+1,k}^T
+  gamma_0 = c_0 - E Ghat_0 g_0
+  gamma_{k+1} = c_{k+1} + AB_k Ghat_k g_k - E Ghat_{k+1} g_{k+1}
+  dxu_k = Ghat_k (g_k - (C^T lambda)_k),
+  (C^T lambda)_k = [lambda_k - A_k^T lambda_{k+1}; -B_k^T lambda_{k+1}]
+
+Only QuadraticCost (TrajoptCost.py:24-104) and no constraints (the reference
+default TrajoptConstraint()) -- the pinned configuration.
+"""
+import copy
+
+import numpy as np
+
+from . import rbd
+
+
+class QuadCost:
+    """QuadraticCost (TrajoptCost.py:24-104)."""
+
+    def __init__(self, Q, QF, R, xg, QF_start=None):
+        self.Q, self.QF, self.R, self.xg, self.QF_start = Q, QF, R, xg, QF_start
+
+    def currQ(self, terminal, k):
+        shifted = self.QF_start is not None and k is not None and k >= self.QF_start
+        return self.QF if (terminal or shifted) else self.Q
+
+    def value(self, x, u, k):
+        dx = x - self.xg
+        Qc = self.currQ(u is None, k)
+        v = 0.5 * np.matmul(dx.T, np.matmul(Qc, dx))
+        if u is not None:
+            v += 0.5 * np.matmul(u.T, np.matmul(self.R, u))
+        return v
+
+    def gradient(self, x, u, k):
+        dx = x - self.xg
+        top = np.matmul(dx.T, self.currQ(u is None, k))
+        return top if u is None else np.hstack((top, np.matmul(u.T, self.R)))
+
+    def hessian(self, u_is_none, k):
+        Qc = self.currQ(u_is_none, k)
+        if u_is_none:
+            return Qc
+        nx, nu = self.Q.shape[0], self.R.shape[0]
+        return np.vstack((np.hstack((Qc, np.zeros((nx, nu)))), np.hstack((np.zeros((nu, nx)), self.R))))
+
+
+def default_options(options=None):
+    """set_default_options (TrajoptMPCReference.py:91-115)."""
+    o = {} if options is None else dict(options)
+    for k, v in [("exit_tolerance_linSys", 1e-6), ("max_iter_linSys", 100), ("exit_tolerance_SQP_DDP", 1e-6),
+                 ("max_iter_SQP_DDP", 100), ("alpha_factor_SQP_DDP", 0.5), ("alpha_min_SQP_DDP", 0.005),
+                 ("rho_factor_SQP_DDP", 4), ("rho_min_SQP_DDP", 1e-3), ("rho_max_SQP_DDP", 1e3),
+                 ("rho_init_SQP_DDP", 0.001), ("expected_reduction_min_SQP_DDP", 0.05),
+                 ("expected_reduction_max_SQP_DDP", 3), ("exit_tolerance_softConstraints", 1e-6),
+                 ("max_iter_softConstraints", 10)]:
+        o.setdefault(k, v)
+    return o
+
+
+# ------------------------------------------------------------------- QP pieces
+def kkt_blocks(model, cost, x, u, xs, N, dt):
+    """formKKTSystemBlocks (:200-271), returned blockwise:
+    G (list of n_xu^2 / terminal nx^2), g (list), A, B (N-1), c (N, nx)."""
+    n = model.n
+    nx = 2 * n
+    X = x[:, :N - 1].T
+    U = u.T
+    A, B = rbd.euler_gradient(model, X, U, dt)
+    xkp1 = rbd.euler(model, X, U, dt)
+    c = np.zeros((N, nx))
+    c[0] = x[:, 0] - xs
+    c[1:] = x[:, 1:].T - xkp1
+    G = [cost.hessian(False, k) for k in range(N - 1)] + [cost.hessian(True, N - 1)]
+    g = [cost.gradient(x[:, k], u[:, k], k) for k in range(N - 1)] + [cost.gradient(x[:, N - 1], None, N - 1)]
+    return G, g, A, B, c
+
+
+def schur_blocks(G, g, A, B, c, rho, nx):
+    N = len(G)
+    Gh = [np.linalg.inv(Gk + rho * np.eye(Gk.shape[0])) for Gk in G]
+    Sd = np.zeros((N, nx, nx))
+    Sl = np.zeros((N - 1, nx, nx))       # S_{k+1,k}
+    gam = np.zeros((N, nx))
+    Sd[0] = -Gh[0][:nx, :nx]
+    gam[0] = c[0] - (Gh[0] @ g[0])[:nx]
+    for k in range(N - 1):
+        AB = np.hstack((A[k], B[k]))
+        ABG = AB @ Gh[k]
+        Sd[k + 1] = -(ABG @ AB.T + Gh[k + 1][:nx, :nx])
+        Sl[k] = ABG[:, :nx]
+        gam[k + 1] = c[k + 1] + ABG @ g[k] - (Gh[k + 1] @ g[k + 1])[:nx]
+    return Gh, Sd, Sl, gam
+
+
+def dense_from_blocks(Dg, Lo, Up):
+    N, b, _ = Dg.shape
+    M = np.zeros((N * b, N * b))
+    for k in range(N):
+        M[k * b:(k + 1) * b, k * b:(k + 1) * b] = Dg[k]
+    for k in range(N - 1):
+        M[(k + 1) * b:(k + 2) * b, k * b:(k + 1) * b] = Lo[k]
+        M[k * b:(k + 1) * b, (k + 1) * b:(k + 2) * b] = Up[k]
+    return M
+
+
+def preconditioner(Sd, Sl, Su, ptype):
+    """compute_preconditioner, numpy branch (PCG.py:166-212), blockwise.
+    Returns (P_diag, P_lo[k]=P_{k+1,k}, P_up[k]=P_{k,k+1})."""
+    N, b, _ = Sd.shape
+    Pl = np.zeros((N - 1, b, b))
+    Pu = np.zeros((N - 1, b, b))
+    if ptype == "J":
+        Pd = np.array([np.linalg.inv(np.diag(np.diag(Sd[k]))) for k in range(N)])
+        return Pd, Pl, Pu
+    Pd = np.array([np.linalg.inv(Sd[k]) for k in range(N)])
+    if ptype == "BJ":
+        return Pd, Pl, Pu
+    if ptype != "SS":
+        raise ValueError(ptype)
+    for k in range(N):
+        if k % 2:     # odd row: P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1})
+            Pl[k - 1] = -np.matmul(Pd[k], np.matmul(Sl[k - 1], Pd[k - 1]))
+        elif k > 0:   # previous odd row: P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk)
+            Pu[k - 1] = -np.matmul(Pd[k - 1], np.matmul(Su[k - 1], Pd[k]))
+    for k in range(N):
+        if k % 2:
+            Pu[k - 1] = Pl[k - 1].T
+            if k < N - 1:
+                Pl[k] = Pu[k].T
+    return Pd, Pl, Pu
+
+
+def block_tridiag_mv(Dg, Lo, Up, v):
+    N, b, _ = Dg.shape
+    V = v.reshape(N, b)
+    out = np.einsum("kij,kj->ki", Dg, V)
+    out[1:] += np.einsum("kij,kj->ki", Lo, V[:-1])
+    out[:-1] += np.einsum("kij,kj->ki", Up, V[1:])
+    return out.reshape(-1)
+
+
+def pcg(Sd, Sl, Su, b, Pd, Pl, Pu, tol=1e-6, max_iter=100):
+    """PCG.pcg (PCG.py:66-111): x0 = 0, exit on |nu'| < tol.
+    Returns (x, trace_nu (abs), trace_res, iterations)."""
+    def A(v):
+        return block_tridiag_mv(Sd, Sl, Su, v)
+
+    def P(v):
+        return block_tridiag_mv(Pd, Pl, Pu, v)
+    x = np.zeros_like(b)
+    r = b - A(x)
+    rt = P(r)
+    p = rt
+    nu = r @ rt
+    trace = [nu]
+    trace2 = [np.linalg.norm(b - A(x))]
+    for _ in range(max_iter):
+        Ap = A(p)
+        alpha = nu / (p @ Ap)
+        r = r - Ap * alpha
+        x = x + p * alpha
+        rt = P(r)
+        nu_p = r @ rt
+        trace.append(nu_p)
+        trace2.append(np.linalg.norm(b - A(x)))
+        if abs(nu_p) < tol:
+            break
+        beta = nu_p / nu
+        p = rt + p * beta
+        nu = nu_p
+    return x, [abs(t) for t in trace], trace2, len(trace) - 1
+
+
+def recover_dxu(Gh, g, A, B, lam, nx):
+    N = len(Gh)
+    L = lam.reshape(N, nx)
+    out = []
+    for k in range(N - 1):
+        ctl = np.concatenate([L[k] - A[k].T @ L[k + 1], -B[k].T @ L[k + 1]])
+        out.append(Gh[k] @ (g[k] - ctl))
+    out.append(Gh[N - 1] @ (g[N - 1] - L[N - 1]))
+    return np.concatenate(out + [lam])
+
+
+def solve_qp(model, cost, x, u, xs, N, dt, rho, method, options):
+    """One QP: returns (dxul, pcg_iters or None, extras)."""
+    nx = 2 * model.n
+    G, g, A, B, c = kkt_blocks(model, cost, x, u, xs, N, dt)
+    Gh, Sd, Sl, gam = schur_blocks(G, g, A, B, c, rho, nx)
+    Su = np.transpose(Sl, (0, 2, 1))
+    gamma = gam.reshape(-1)
+    if method == "S":
+        lam = np.linalg.solve(dense_from_blocks(Sd, Sl, Su), gamma)
+        iters = None
+    elif method.startswith("PCG-"):
+        Pd, Pl, Pu = preconditioner(Sd, Sl, Su, method[4:])
+        lam, _, _, iters = pcg(Sd, Sl, Su, gamma, Pd, Pl, Pu, options["exit_tolerance_linSys"],
+                               options["max_iter_linSys"])
+    else:
+        raise ValueError(f"oracle supports S / PCG-J / PCG-BJ / PCG-SS, got {method}")
+    return recover_dxu(Gh, g, A, B, lam, nx), iters, dict(G=G, g=g, A=A, B=B, c=c, Sd=Sd, Sl=Sl, gamma=gamma)
+
+
+# ------------------------------------------------------------------- merit pieces
+def total_cost(cost, x, u, N):
+    """totalCost (:296-310), sequential sum as the reference."""
+    J = 0
+    for k in range(N - 1):
+        J = J + cost.value(x[:, k], u[:, k], k)
+    return J + cost.value(x[:, N - 1], None, N - 1)
+
+
+def total_violation(model, x, u, xs, N, dt):
+    """totalHardConstraintViolation (:273-294), mode sum, no other constraints."""
+    cval = sum(map(abs, x[:, 0] - xs))
+    xkp1 = rbd.euler(model, x[:, :N - 1].T, u.T, dt)
+    for k in range(N - 1):
+        cval = cval + sum(map(abs, x[:, k + 1] - xkp1[k]))
+    return cval
+
+
+# ------------------------------------------------------------------- SQP
+def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None):
+    """TrajoptMPCReference.SQP (:510-760), unconstrained.  Returns a dict."""
+    o = default_options(options)
+    nx, nu = 2 * model.n, model.n
+    n = nx + nu
+    x = np.array(x, dtype=float)
+    u = np.array(u, dtype=float)
+    xs = copy.deepcopy(x[:, 0])
+    rho = o["rho_init_SQP_DDP"]
+    drho = 1
+    J = total_cost(cost, x, u, N)
+    c = total_violation(model, x, u, xs, N, dt)
+    mu = 10
+    merit = J + mu * c
+    trace = [dict(iteration=0, line_search_iteration=0, alpha=1, rho=rho, J=J, c=c, merit=merit, D=None,
+                  reduction_ratio=None, succeeded_line_search=False)]
+    pcg_iters, dxuls = [], []
+    it = 0
+    exit_sqp = 0
+    while True:
+        dxul, iters, _ = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o)
+        dxul = dxul.reshape(-1, 1)
+        dxuls.append(dxul[:, 0].copy())
+        if iters is not None:
+            pcg_iters.append(iters)
+        alpha = 1
+        error = False
+        ls = 0
+        while True:
+            x_new = copy.deepcopy(x)
+            u_new = copy.deepcopy(u)
+            for k in range(N):
+                x_new[:, k] = x_new[:, k] - alpha * dxul[n * k:n * k + nx, 0]
+                if k < N - 1:
+                    u_new[:, k] = u_new[:, k] - alpha * dxul[n * k + nx:n * (k + 1), 0]
+            J_new = total_cost(cost, x_new, u_new, N)
+            c_new = total_violation(model, x_new, u_new, xs, N, dt)
+            D = 0
+            for k in range(N - 1):
+                D += float(cost.gradient(x_new[:, k], u_new[:, k], k) @ dxul[n * k:n * (k + 1), 0])
+            D += float(cost.gradient(x_new[:, N - 1], None, N - 1) @ dxul[n * (N - 1):n * (N - 1) + nx, 0])
+            merit_new = J_new + mu * c_new
+            delta_J = J - J_new
+            delta_merit = merit - merit_new
+            with np.errstate(divide="ignore", invalid="ignore"):
+                ratio = np.float64(delta_merit) / np.float64(alpha * (D - mu * c_new))
+            if (delta_merit >= 0 and ratio >= o["expected_reduction_min_SQP_DDP"]
+                    and ratio <= o["expected_reduction_max_SQP_DDP"]):
+                x, u, J, c, merit = x_new, u_new, J_new, c_new, merit_new
+                drho = min(drho / o["rho_factor_SQP_DDP"], 1 / o["rho_factor_SQP_DDP"])
+                rho = max(rho * drho, o["rho_min_SQP_DDP"])
+                trace.append(dict(iteration=it, line_search_iteration=ls, alpha=alpha, rho=rho, J=J, c=c,
+                                  merit=merit, D=D, reduction_ratio=ratio, succeeded_line_search=True))
+                break
+            elif alpha > o["alpha_min_SQP_DDP"]:
+                alpha *= o["alpha_factor_SQP_DDP"]
+                ls += 1
+            else:
+                error = True
+                trace.append(dict(iteration=it, line_search_iteration=ls, alpha=alpha, rho=rho, J=J, c=c,
+                                  merit=merit, D=D, reduction_ratio=ratio, succeeded_line_search=False))
+                break
+        # check_for_exit_or_error (:463-481)
+        exit_flag = False
+        if error:
+            drho = max(drho * o["rho_factor_SQP_DDP"], o["rho_factor_SQP_DDP"])
+            rho = max(rho * drho, o["rho_min_SQP_DDP"])
+            if rho > o["rho_max_SQP_DDP"]:
+                exit_sqp, exit_flag = 2, True
+        elif delta_J < o["exit_tolerance_SQP_DDP"]:
+            exit_sqp, exit_flag = 1, True
+        if it == o["max_iter_SQP_DDP"] - 1:
+            exit_sqp, exit_flag = 3, True
+        else:
+            it += 1
+        if exit_flag:
+            break
+    # unconstrained outer loop: max soft violation 0 < tol -> exit_soft 1, outer iteration 0 -> 1 (:483-508)
+    return dict(x=x, u=u, exit_sqp=exit_sqp, exit_soft=1, outer_iter=1, sqp_iter=it, trace=trace,
+                pcg_iters=pcg_iters, dxul=dxuls)
+
+
+def initial_problem(model, N, dt, seed):
+    """§8d workload: q0 ~ U(-1,1)^n (default_rng(seed)), qd0 = 0, Euler rollout of u = 0."""
+    n = model.n
+    rng = np.random.default_rng(seed)
+    x = np.zeros((2 * n, N))
+    x[:n, 0] = rng.uniform(-1.0, 1.0, n)
+    u = np.zeros((n, N - 1))
+    for k in range(N - 1):
+        x[:, k + 1] = rbd.euler(model, x[:, k][None], u[:, k][None], dt)[0]
+    return x, u

@@ -1,0 +1,36 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+ARM_N = {"arm2": 2, "arm3": 3, "arm6fix": 6}
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built libtmpc.so")
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def arm_model(name):
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    return parse_urdf(planar_arm_urdf(ARM_N[name]))
+
+
+def quad_cost_arrays(n):
+    nx = 2 * n
+    return np.eye(nx), 100.0 * np.eye(nx), 0.1 * np.eye(n), np.zeros(nx)
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    from trajoptmpcreference_amd import _native
+    return _native.default_context(0)

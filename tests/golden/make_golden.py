@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE
+(VCA-EPFL/TrajoptMPCReference, read-only at /root/reference) in this container.
+
+This script is test infrastructure.  It is the only place that imports the
+reference, it runs only here (the reference does not exist on the GPU box),
+and what it writes is data: inputs and the reference's outputs, as .npz.
+
+Import recipe:
+  * /root/reference on sys.path, PYTHONDONTWRITEBYTECODE=1 (read-only tree);
+  * a one-line ``bs4`` stub ahead on sys.path for the dead import at
+    GRiD/URDFParser/URDFParser.py:212;
+  * arm6.urdf is malformed (joint6 repeats joint5's parent/child,
+    models/arm6.urdf:75-80); we feed the reference a corrected copy
+    (joint6: link5 -> link6) written to a temp dir;
+  * QuadraticCost methods do not accept the iter_* kwargs SQP passes
+    (TrajoptCost.py:49,58,71 vs TrajoptMPCReference.py:218-219);
+    we subclass it with pass-through signatures (public plugin subclassing).
+
+Usage:  python tests/golden/make_golden.py [--quick]
+"""
+import argparse
+import copy
+import multiprocessing as mp
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+_STUB_DIR = None
+
+
+def _setup_reference():
+    global _STUB_DIR
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    if _STUB_DIR is None:
+        _STUB_DIR = tempfile.mkdtemp(prefix="tmpc_stub_")
+        with open(os.path.join(_STUB_DIR, "bs4.py"), "w") as f:
+            f.write("BeautifulSoup = None\n")
+    for p in (REF, _STUB_DIR):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def model_path(name):
+    """arm2/arm3 as shipped; arm6 with the 2-line joint6 fix."""
+    src = os.path.join(REF, "models", name.replace("fix", "") + ".urdf")
+    if not name.endswith("fix"):
+        return src
+    text = open(src).read()
+    head, tail = text.split('<joint name="joint6"', 1)
+    tail = tail.replace('<parent link="link4"/>', '<parent link="link5"/>', 1)
+    tail = tail.replace('<child link="link5"/>', '<child link="link6"/>', 1)
+    d = tempfile.mkdtemp(prefix="tmpc_urdf_")
+    p = os.path.join(d, name + ".urdf")
+    with open(p, "w") as f:
+        f.write(head + '<joint name="joint6"' + tail)
+    return p
+
+
+def make_plant(name):
+    _setup_reference()
+    from TrajoptPlant import URDFPlant
+    return URDFPlant(options={"path_to_urdf": model_path(name), "overloading": False})
+
+
+def make_cost(nx, nu):
+    _setup_reference()
+    from TrajoptCost import QuadraticCost
+
+    class PassThroughQuadraticCost(QuadraticCost):
+        # accepts the iter_* arguments SQP passes
+        def value(self, x, u=None, timestep=None, *a, **k):
+            return QuadraticCost.value(self, x, u, timestep)
+
+        def gradient(self, x, u=None, timestep=None, *a, **k):
+            return QuadraticCost.gradient(self, x, u, timestep)
+
+        def hessian(self, x, u=None, timestep=None, *a, **k):
+            return QuadraticCost.hessian(self, x, u, timestep)
+
+    return PassThroughQuadraticCost(np.eye(nx), 100.0 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
+
+
+def initial_problem(plant, N, dt, seed):
+    """The §8d workload: q0 ~ U(-1,1)^n from default_rng(seed), qd0 = 0,
+    x = Euler rollout of u = 0, u = 0."""
+    n = plant.get_num_pos()
+    rng = np.random.default_rng(seed)
+    x = np.zeros((2 * n, N))
+    x[:n, 0] = rng.uniform(-1.0, 1.0, n)
+    u = np.zeros((n, N - 1))
+    for k in range(N - 1):
+        x[:, k + 1] = plant.integrator(x[:, k], u[:, k], dt)
+    return x, u
+
+
+# ---------------------------------------------------------------- model + dynamics
+def gen_model_and_dynamics(name, K=32, seed=1234):
+    plant = make_plant(name)
+    robot = plant.robot
+    rbd = plant.rbdReference
+    n = robot.get_num_pos()
+    qs = np.array([[0.0] * n, [0.3] * n, [-1.7] * n, list(np.linspace(-3.0, 3.0, n)), list(np.linspace(2.5, -0.4, n))])
+    X = np.zeros((len(qs), n, 6, 6))
+    for a, q in enumerate(qs):
+        for j in range(n):
+            X[a, j] = np.asarray(robot.get_Xmat_Func_by_id(j)(q[j]), dtype=float)
+    np.savez_compressed(
+        os.path.join(OUT, f"model_{name}.npz"),
+        parent=np.array([robot.get_parent_id(j) for j in range(n)], dtype=np.int32),
+        S=np.array([robot.get_S_by_id(j) for j in range(n)], dtype=float),
+        I=np.array([robot.get_Imat_by_id(j) for j in range(n)], dtype=float),
+        qs=qs, X=X)
+
+    from GRiD.util import util
+    q0, qd0, u0, _ = util.initializeValues(robot, MATCH_CPP_RANDOM=True)
+    rng = np.random.default_rng(seed)
+    xs = [np.concatenate([q0, qd0])]
+    us = [u0]
+    for _ in range(K - 1):
+        xs.append(np.concatenate([rng.uniform(-np.pi, np.pi, n), rng.uniform(-2, 2, n)]))
+        us.append(rng.uniform(-1.5, 1.5, n))
+    xs = np.array(xs)
+    us = np.array(us)
+    dt = 0.1
+    out = {k: [] for k in ["qdd", "dqdd", "xnext", "A", "B", "c", "Minv", "dc_du"]}
+    for x, u in zip(xs, us):
+        q, qd = x[:n], x[n:]
+        out["qdd"].append(plant.forward_dynamics(x, u))
+        out["dqdd"].append(plant.forward_dynamics_gradient(x, u))
+        out["xnext"].append(plant.integrator(x, u, dt))
+        A, B = plant.integrator(x, u, dt, return_gradient=True)
+        out["A"].append(A)
+        out["B"].append(B)
+        c, _, _, _ = rbd.rnea(q, qd, None, -9.81)
+        out["c"].append(c)
+        out["Minv"].append(rbd.minv(q))
+        out["dc_du"].append(rbd.rnea_grad(q, qd, out["qdd"][-1], -9.81))
+    np.savez_compressed(os.path.join(OUT, f"dyn_{name}.npz"), x=xs, u=us, dt=dt,
+                        **{k: np.array(v) for k, v in out.items()})
+    print(f"[golden] model/dyn {name}: n={n} K={K}", flush=True)
+
+
+# ---------------------------------------------------------------- one QP
+def _blocks(M, nx, N):
+    d = np.array([M[k * nx:(k + 1) * nx, k * nx:(k + 1) * nx] for k in range(N)])
+    lo = np.array([M[(k + 1) * nx:(k + 2) * nx, k * nx:(k + 1) * nx] for k in range(N - 1)])
+    up = np.array([M[k * nx:(k + 1) * nx, (k + 1) * nx:(k + 2) * nx] for k in range(N - 1)])
+    return d, lo, up
+
+
+def gen_qp(name, N, seed=0, dt=0.1, rho=1e-3):
+    _setup_reference()
+    from TrajoptMPCReference import TrajoptMPCReference
+    import importlib
+    PCG = importlib.import_module("GBD-PCG-Python").PCG
+    plant = make_plant(name)
+    n = plant.get_num_pos()
+    nx, nu = 2 * n, n
+    cost = make_cost(nx, nu)
+    x, u = initial_problem(plant, N, dt, seed)
+    xs = copy.deepcopy(x[:, 0])
+    solver = TrajoptMPCReference(plant, cost)
+    G, g, C, c = solver.formKKTSystemBlocks(x, u, xs, N, dt)
+    Ak = np.array([d["value"] for d in solver.saved_Ak])
+    Bk = np.array([d["value"] for d in solver.saved_Bk])
+    G = G + rho * np.eye(G.shape[0])
+    invG = np.linalg.inv(G)
+    S = -np.matmul(C, np.matmul(invG, C.T))
+    gamma = c - np.matmul(C, np.matmul(invG, g))
+    rec = dict(x=x, u=u, rho=rho, dt=dt, g=g[:, 0], c=c[:, 0], A=Ak, B=Bk, gamma=gamma[:, 0])
+    rec["S_diag"], rec["S_lo"], rec["S_up"] = _blocks(S, nx, N)
+    l_direct = np.linalg.solve(S, gamma)
+    rec["lam_direct"] = l_direct[:, 0]
+    rec["dxul_direct"] = np.vstack((np.matmul(invG, g - np.matmul(C.T, l_direct)), l_direct))[:, 0]
+    for p in ["J", "BJ", "SS"]:
+        opts = {"exit_tolerance": 1e-6, "max_iter": 100, "DEBUG_MODE": False, "RETURN_TRACE": False,
+                "preconditioner_type": p}
+        pcg = PCG(S, gamma, nx, N, options=opts)
+        lam, (tr_nu, tr_res) = pcg.solve()
+        P = pcg.Pinv
+        rec[f"P_{p}_diag"], rec[f"P_{p}_lo"], rec[f"P_{p}_up"] = _blocks(P, nx, N)
+        rec[f"lam_{p}"] = lam[:, 0]
+        rec[f"trace_nu_{p}"] = np.array(tr_nu)
+        rec[f"trace_res_{p}"] = np.array(tr_res)
+        rec[f"iters_{p}"] = len(tr_nu) - 1
+        rec[f"dxul_{p}"] = np.vstack((np.matmul(invG, g - np.matmul(C.T, lam)), lam))[:, 0]
+        # KKT residual computed the §8d way on the reference's own iterate
+        KKT = np.block([[G, C.T], [C, np.zeros((C.shape[0], C.shape[0]))]])
+        rec[f"kkt_res_{p}"] = np.max(np.abs(KKT @ rec[f"dxul_{p}"] - np.concatenate([g[:, 0], c[:, 0]])))
+    np.savez_compressed(os.path.join(OUT, f"qp_{name}_N{N}.npz"), **rec)
+    print(f"[golden] qp {name} N={N}: iters J/BJ/SS = {rec['iters_J']}/{rec['iters_BJ']}/{rec['iters_SS']}", flush=True)
+
+
+# ---------------------------------------------------------------- full SQP
+def run_sqp(args):
+    name, N, seed, method, dt = args
+    _setup_reference()
+    from TrajoptMPCReference import TrajoptMPCReference, SQPSolverMethods
+    from overloading import matrix_
+    matrix_.iteration = 0
+    matrix_.soft_constraint_iteration = 0
+    matrix_.line_search_iteration = 0
+    plant = make_plant(name)
+    n = plant.get_num_pos()
+    nx, nu = 2 * n, n
+    cost = make_cost(nx, nu)
+    x0, u0 = initial_problem(plant, N, dt, seed)
+    solver = TrajoptMPCReference(plant, cost)
+    m = {"S": SQPSolverMethods.S, "PCG-J": SQPSolverMethods.PCG_J, "PCG-BJ": SQPSolverMethods.PCG_BJ,
+         "PCG-SS": SQPSolverMethods.PCG_SS, "N": SQPSolverMethods.N}[method]
+    t0 = time.time()
+    import io
+    import contextlib
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(copy.deepcopy(x0), copy.deepcopy(u0), N, dt, m, {})
+    wall = time.time() - t0
+    tr = solver.trace
+    keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
+            "succeeded_line_search", "inner_iters"]
+    rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(t[k]) for t in tr]) for k in keys}
+    pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
+    dxul = np.array([d["value"][:, 0] for d in solver.saved_dxul])
+    np.savez_compressed(os.path.join(OUT, f"sqp_{name}_N{N}_s{seed}_{method}.npz"),
+                        x0=x0, u0=u0, x=np.asarray(x), u=np.asarray(u), dt=dt,
+                        exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer_iter, sqp_iter=sqp_iter,
+                        pcg_iters=pcg_iters, dxul=dxul, wall_s=wall, **rec)
+    return f"[golden] sqp {name} N={N} seed={seed} {method}: exit={exit_sqp} iters={sqp_iter} " \
+           f"pcg={list(pcg_iters)} wall={wall:.1f}s"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="skip the slow arm6 N=64 solves")
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    _setup_reference()
+    if a.only in (None, "dyn"):
+        for name in ["arm2", "arm3", "arm6fix"]:
+            gen_model_and_dynamics(name)
+    if a.only in (None, "qp"):
+        gen_qp("arm3", 32)
+        gen_qp("arm6fix", 64)
+        gen_qp("arm2", 8)
+    if a.only in (None, "sqp"):
+        jobs = [("arm2", 8, 0, "PCG-SS", 0.1), ("arm3", 8, 0, "PCG-SS", 0.1), ("arm3", 8, 1, "PCG-BJ", 0.1),
+                ("arm3", 8, 2, "PCG-J", 0.1), ("arm3", 8, 3, "S", 0.1)]
+        jobs += [("arm3", 32, s, "PCG-SS", 0.1) for s in range(4)]
+        jobs += [("arm3", 32, 0, m, 0.1) for m in ["PCG-J", "PCG-BJ", "S"]]
+        if not a.quick:
+            jobs += [("arm6fix", 64, s, "PCG-SS", 0.1) for s in range(2)]
+        # slow ones first so the pool drains evenly
+        jobs.sort(key=lambda j: -j[1] * (2 if j[0].startswith("arm6") else 1))
+        with mp.get_context("fork").Pool(min(8, len(jobs))) as pool:
+            for msg in pool.imap_unordered(run_sqp, jobs):
+                print(msg, flush=True)
+
+
+if __name__ == "__main__":
+    main()

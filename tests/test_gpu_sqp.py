@@ -1,0 +1,109 @@
+"""GPU parity: full batched SQP solves (tmpc_sqp_solve_batch through the
+TrajoptMPCReference drop-in) against the reference's own recorded solves
+(tests/golden/sqp_*.npz) and against the oracle on larger batches.
+
+Integer outputs -- exit codes, SQP iteration counts, the PCG iteration count
+of every QP, line-search iterations and the alpha sequence -- must be
+identical.  Trajectories and merit values: relative tolerance 1e-7 (PCG-J:
+1e-4, it saturates at 100 iterations and amplifies rounding).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, arm_model, quad_cost_arrays
+
+pytestmark = pytest.mark.gpu
+
+FILES = sorted(glob.glob(os.path.join(GOLDEN, "sqp_*.npz")))
+
+
+def _parse(f):
+    b = os.path.basename(f)[4:-4]
+    name, Ns, ss, method = b.split("_")
+    return name, int(Ns[1:]), int(ss[1:]), method
+
+
+def _solver(name):
+    from trajoptmpcreference_amd import QuadraticCost, TrajoptMPCReference, URDFPlant, planar_arm_urdf
+    from conftest import ARM_N
+    plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(ARM_N[name])})
+    n = ARM_N[name]
+    return TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(n)))
+
+
+@pytest.mark.parametrize("f", [f for f in FILES if _parse(f)[3] != "S"], ids=lambda f: os.path.basename(f))
+def test_sqp_matches_reference(f):
+    name, N, seed, method = _parse(f)
+    d = np.load(f)
+    solver = _solver(name)
+    x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(d["x0"], d["u0"], N, float(d["dt"]), method, {})
+    assert exit_sqp == int(d["exit_sqp"])
+    assert exit_soft == int(d["exit_soft"])
+    assert outer_iter == int(d["outer_iter"])
+    assert sqp_iter == int(d["sqp_iter"])
+    tr = solver.trace
+    assert len(tr) == len(d["tr_alpha"])
+    assert [t["alpha"] for t in tr] == list(d["tr_alpha"])
+    assert [t["line_search_iteration"] for t in tr] == list(d["tr_line_search_iteration"].astype(int))
+    assert [t["succeeded_line_search"] for t in tr] == list(d["tr_succeeded_line_search"].astype(bool))
+    assert [t["inner_iters"] for t in tr[1:]] == list(d["pcg_iters"])
+    rtol = 1e-4 if method == "PCG-J" else 1e-7
+    for key in ("J", "c", "merit", "rho"):
+        ours = np.array([t[key] for t in tr])
+        ref = d["tr_" + key]
+        assert np.allclose(ours, ref, rtol=rtol, atol=1e-12), key
+    scale = max(1.0, float(np.max(np.abs(d["x"]))))
+    assert float(np.max(np.abs(x - d["x"]))) < rtol * scale
+    scale = max(1.0, float(np.max(np.abs(d["u"]))))
+    assert float(np.max(np.abs(u - d["u"]))) < rtol * scale
+
+
+@pytest.mark.parametrize("name,N,B", [("arm3", 32, 64), ("arm6fix", 64, 16)])
+def test_sqp_batch_matches_oracle(ctx, name, N, B):
+    """A batch of §8d problems (seeds 100..100+B) against the oracle, problem by problem."""
+    from oracle import sqp as osqp
+    m = arm_model(name)
+    solver = _solver(name)
+    xs, us = zip(*[osqp.initial_problem(m, N, 0.1, 100 + i) for i in range(B)])
+    r = solver.SQP_batch(np.array(xs), np.array(us), N, 0.1, "PCG-SS", {})
+    cost = osqp.QuadCost(*quad_cost_arrays(m.n))
+    mism = 0
+    for i in range(B):
+        o = osqp.sqp(m, cost, xs[i], us[i], N, 0.1, "PCG-SS")
+        same = (int(r["exit_sqp"][i]) == o["exit_sqp"] and int(r["sqp_iter"][i]) == o["sqp_iter"]
+                and list(r["trace"]["pcg_iters"][i, 1:o["sqp_iter"] + 1]) == o["pcg_iters"])
+        if same:
+            scale = max(1.0, float(np.max(np.abs(o["x"]))))
+            assert float(np.max(np.abs(r["x"][i] - o["x"]))) < 1e-6 * scale
+        mism += not same
+    # integer parity is expected for every problem; allow none to differ
+    assert mism == 0, f"{mism} of {B} problems differ in exit code / iteration counts"
+
+
+def test_batch_equals_single(ctx):
+    """Sharding invariance: a problem's result does not depend on its batch neighbours (bitwise)."""
+    from oracle import sqp as osqp
+    m = arm_model("arm3")
+    solver = _solver("arm3")
+    xs, us = zip(*[osqp.initial_problem(m, 16, 0.1, s) for s in range(5)])
+    r = solver.SQP_batch(np.array(xs), np.array(us), 16, 0.1, "PCG-BJ", {})
+    r1 = solver.SQP_batch(np.array(xs[3:4]), np.array(us[3:4]), 16, 0.1, "PCG-BJ", {})
+    assert np.array_equal(r["x"][3], r1["x"][0])
+    assert np.array_equal(r["u"][3], r1["u"][0])
+    assert r["sqp_iter"][3] == r1["sqp_iter"][0]
+
+
+def test_options_are_honoured():
+    """max_iter_SQP_DDP and rho_init change the run exactly as the oracle predicts."""
+    from oracle import sqp as osqp
+    m = arm_model("arm3")
+    solver = _solver("arm3")
+    x, u = osqp.initial_problem(m, 8, 0.1, 5)
+    opts = {"max_iter_SQP_DDP": 2, "rho_init_SQP_DDP": 0.01, "expected_reduction_min_SQP_DDP": -100.0}
+    res = solver.SQP(x, u, 8, 0.1, "PCG-SS", dict(opts))
+    o = osqp.sqp(m, osqp.QuadCost(*quad_cost_arrays(3)), x, u, 8, 0.1, "PCG-SS", dict(opts))
+    assert res[2] == o["exit_sqp"] and res[5] == o["sqp_iter"]
+    assert np.allclose(res[0], o["x"], rtol=1e-8, atol=1e-10)

@@ -1,0 +1,327 @@
+"""ctypes binding of libtmpc.so (include/tmpc.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C trajoptmpcreference_amd/csrc``).  There is no CPU fallback: if the
+library or a GPU is missing, every solver entry point raises.
+"""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtmpc.so")
+
+LINSYS = {"S": 1, "PCG-J": 2, "PCG-BJ": 3, "PCG-SS": 4}
+PRECOND = {"J": 1, "BJ": 2, "SS": 3}
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class tmpc_options(C.Structure):
+    _fields_ = [
+        ("exit_tolerance_linSys", C.c_double),
+        ("max_iter_linSys", C.c_int32),
+        ("max_iter_SQP_DDP", C.c_int32),
+        ("exit_tolerance_SQP_DDP", C.c_double),
+        ("alpha_factor_SQP_DDP", C.c_double),
+        ("alpha_min_SQP_DDP", C.c_double),
+        ("rho_factor_SQP_DDP", C.c_double),
+        ("rho_min_SQP_DDP", C.c_double),
+        ("rho_max_SQP_DDP", C.c_double),
+        ("rho_init_SQP_DDP", C.c_double),
+        ("expected_reduction_min_SQP_DDP", C.c_double),
+        ("expected_reduction_max_SQP_DDP", C.c_double),
+        ("merit_mu", C.c_double),
+        ("profile", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+class tmpc_trace(C.Structure):
+    _fields_ = [
+        ("iteration", _ip), ("line_search_iteration", _ip), ("alpha", _dp), ("rho", _dp), ("J", _dp),
+        ("c", _dp), ("merit", _dp), ("D", _dp), ("reduction_ratio", _dp), ("succeeded_line_search", _ip),
+        ("pcg_iters", _ip),
+    ]
+
+
+# every symbol include/tmpc.h declares, with its ctypes signature
+SIGNATURES = {
+    "tmpc_abi_version": (C.c_int, []),
+    "tmpc_device_count": (C.c_int, [_ip]),
+    "tmpc_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "tmpc_destroy": (None, [C.c_void_p]),
+    "tmpc_last_error": (C.c_char_p, [C.c_void_p]),
+    "tmpc_set_model": (C.c_int, [C.c_void_p, C.c_int, _ip, _ip, _ip, _dp, _dp, _dp, _dp, C.c_double]),
+    "tmpc_set_cost_quadratic": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp, _dp, C.c_int32]),
+    "tmpc_default_options": (None, [C.POINTER(tmpc_options)]),
+    "tmpc_set_options": (C.c_int, [C.c_void_p, C.POINTER(tmpc_options)]),
+    "tmpc_sqp_solve_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _ip, _ip, _ip,
+                                       _ip, C.POINTER(tmpc_trace)]),
+    "tmpc_sqp_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p,
+                                              C.c_void_p, _ip, _ip]),
+    "tmpc_rollout_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p]),
+    "tmpc_fd_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
+    "tmpc_fd_grad_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
+    "tmpc_qp_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _dp, _dp, _ip, _dp, _dp,
+                                _dp, _dp]),
+    "tmpc_pcg_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, C.c_double,
+                                 C.c_int, _dp, _ip, _dp, _dp, _dp]),
+    "tmpc_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "tmpc_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "tmpc_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "tmpc_memcpy_d2h": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "tmpc_memcpy_d2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "tmpc_synchronize": (C.c_int, [C.c_void_p]),
+    "tmpc_kernel_stats": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
+    "tmpc_reset_stats": (C.c_int, [C.c_void_p]),
+    "tmpc_solve_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libtmpc.so and bind every exported symbol (raises if missing)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeError(f"{path} not found: build it with __graft_entry__.build() "
+                              "(or `make -C trajoptmpcreference_amd/csrc`); there is no CPU fallback")
+        lib = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = C.c_int32(0)
+    lib.tmpc_device_count(C.byref(n))
+    return int(n.value)
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if a.dtype == np.float64:
+        return a.ctypes.data_as(_dp)
+    if a.dtype == np.int32:
+        return a.ctypes.data_as(_ip)
+    raise TypeError(a.dtype)
+
+
+def _c64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Context:
+    """One libtmpc context (one GPU, one HIP stream)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.tmpc_create(int(device), C.byref(h))
+        if rc != 0:
+            n = device_count()
+            raise NativeError(f"tmpc_create(device={device}) failed (code {rc}; {n} HIP device(s) visible). "
+                              "The solver runs on an AMD GPU only.")
+        self.h = h
+        self.device = device
+        self.model = None
+        self.nx = self.nu = None
+        self.options = tmpc_options()
+        self.lib.tmpc_default_options(C.byref(self.options))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tmpc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.tmpc_last_error(self.h)
+            raise NativeError(f"{what}: {msg.decode() if msg else 'error'} (code {rc})")
+
+    # ---------------------------------------------------------------- configuration
+    def set_model(self, model, gravity=-9.81):
+        n = model.n
+        saxis = np.array([int(np.argmax(model.S[j])) for j in range(n)], dtype=np.int32)
+        self._check(self.lib.tmpc_set_model(
+            self.h, n, _ptr(np.ascontiguousarray(model.parent, dtype=np.int32)),
+            _ptr(np.ascontiguousarray(model.jtype, dtype=np.int32)), _ptr(saxis),
+            _ptr(_c64(model.X0)), _ptr(_c64(model.Xa)), _ptr(_c64(model.Xb)), _ptr(_c64(model.I)), float(gravity)),
+            "tmpc_set_model")
+        self.model = model
+
+    def set_cost_quadratic(self, Q, QF, R, xg, QF_start=None):
+        Q, QF, R, xg = _c64(Q), _c64(QF), _c64(R), _c64(xg).reshape(-1)
+        self.nx, self.nu = Q.shape[0], R.shape[0]
+        self._check(self.lib.tmpc_set_cost_quadratic(self.h, self.nx, self.nu, _ptr(Q), _ptr(QF), _ptr(R), _ptr(xg),
+                                                     -1 if QF_start is None else int(QF_start)),
+                    "tmpc_set_cost_quadratic")
+
+    def set_options(self, **kw):
+        for k, v in kw.items():
+            if not hasattr(self.options, k):
+                raise KeyError(k)
+            setattr(self.options, k, v)
+        self._check(self.lib.tmpc_set_options(self.h, C.byref(self.options)), "tmpc_set_options")
+
+    # ---------------------------------------------------------------- solves
+    def sqp_solve_batch(self, x, u, N, dt, method="PCG-SS", with_trace=True):
+        """x [B][nx][N], u [B][nu][N-1] -> dict of results (arrays per problem)."""
+        x = _c64(x).copy()
+        u = _c64(u).copy()
+        B = x.shape[0]
+        W = int(self.options.max_iter_SQP_DDP) + 1
+        out = {k: np.zeros(B, dtype=np.int32) for k in ("exit_sqp", "exit_soft", "outer_iter", "sqp_iter")}
+        tr = None
+        arrays = {}
+        if with_trace:
+            for name, dt_ in [("iteration", np.int32), ("line_search_iteration", np.int32), ("alpha", np.float64),
+                              ("rho", np.float64), ("J", np.float64), ("c", np.float64), ("merit", np.float64),
+                              ("D", np.float64), ("reduction_ratio", np.float64),
+                              ("succeeded_line_search", np.int32), ("pcg_iters", np.int32)]:
+                arrays[name] = np.zeros((B, W), dtype=dt_)
+            tr = tmpc_trace(**{k: _ptr(v) for k, v in arrays.items()})
+        self._check(self.lib.tmpc_sqp_solve_batch(
+            self.h, B, int(N), float(dt), LINSYS[method], _ptr(x), _ptr(u), _ptr(out["exit_sqp"]),
+            _ptr(out["exit_soft"]), _ptr(out["outer_iter"]), _ptr(out["sqp_iter"]),
+            C.byref(tr) if tr is not None else None), "tmpc_sqp_solve_batch")
+        out.update(x=x, u=u, trace=arrays)
+        return out
+
+    def fd_batch(self, x, u, dt=0.0, want_minv=True):
+        x, u = _c64(x), _c64(u)
+        K, nx = x.shape
+        n = nx // 2
+        xn = np.zeros((K, nx))
+        qdd = np.zeros((K, n))
+        Mi = np.zeros((K, n, n)) if want_minv else None
+        self._check(self.lib.tmpc_fd_batch(self.h, K, float(dt), _ptr(x), _ptr(u), _ptr(xn), _ptr(qdd), _ptr(Mi)),
+                    "tmpc_fd_batch")
+        return xn, qdd, Mi
+
+    def fd_grad_batch(self, x, u, dt):
+        x, u = _c64(x), _c64(u)
+        K, nx = x.shape
+        n = nx // 2
+        A = np.zeros((K, nx, nx))
+        Bm = np.zeros((K, nx, n))
+        dq = np.zeros((K, n, 3 * n))
+        self._check(self.lib.tmpc_fd_grad_batch(self.h, K, float(dt), _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(dq)),
+                    "tmpc_fd_grad_batch")
+        return A, Bm, dq
+
+    def qp_batch(self, x, u, N, dt, rho, method="PCG-SS", want_blocks=True):
+        x, u = _c64(x), _c64(u)
+        B, nx, _ = x.shape
+        nu = u.shape[1]
+        rho = _c64(np.broadcast_to(np.asarray(rho, dtype=np.float64), (B,)))
+        L = (nx + nu) * (N - 1) + nx + nx * N
+        dxul = np.zeros((B, L))
+        iters = np.zeros(B, dtype=np.int32)
+        Sd = np.zeros((B, N, nx, nx)) if want_blocks else None
+        Sl = np.zeros((B, N - 1, nx, nx)) if want_blocks else None
+        g = np.zeros((B, N * nx)) if want_blocks else None
+        Pd = np.zeros((B, N, nx, nx)) if want_blocks else None
+        self._check(self.lib.tmpc_qp_batch(self.h, B, int(N), float(dt), LINSYS[method], _ptr(rho), _ptr(x), _ptr(u),
+                                           _ptr(dxul), _ptr(iters), _ptr(Sd), _ptr(Sl), _ptr(g), _ptr(Pd)),
+                    "tmpc_qp_batch")
+        return dict(dxul=dxul, pcg_iters=iters, S_diag=Sd, S_lo=Sl, gamma=g, P_diag=Pd)
+
+    def pcg_batch(self, S_diag, S_lo, gamma, precond="SS", S_up=None, guess=None, tol=1e-6, max_iter=100,
+                  trace=True):
+        S_diag, gamma = _c64(S_diag), _c64(gamma)
+        B, N, nx, _ = S_diag.shape
+        S_lo = _c64(S_lo) if N > 1 else np.zeros((B, 1, nx, nx))
+        S_up = _c64(S_up) if S_up is not None else None
+        guess = _c64(guess) if guess is not None else None
+        lam = np.zeros((B, N * nx))
+        it = np.zeros(B, dtype=np.int32)
+        tn = np.full((B, max_iter + 1), np.nan) if trace else None
+        tr = np.full((B, max_iter + 1), np.nan) if trace else None
+        Pd = np.zeros((B, N, nx, nx))
+        self._check(self.lib.tmpc_pcg_batch(self.h, B, N, nx, PRECOND[precond], _ptr(S_diag), _ptr(S_lo), _ptr(S_up),
+                                            _ptr(gamma), _ptr(guess), float(tol), int(max_iter), _ptr(lam), _ptr(it),
+                                            _ptr(tn), _ptr(tr), _ptr(Pd)), "tmpc_pcg_batch")
+        return lam, it, tn, tr, Pd
+
+    # ---------------------------------------------------------------- device memory (bench)
+    def alloc(self, nbytes):
+        p = C.c_void_p()
+        self._check(self.lib.tmpc_device_alloc(self.h, int(nbytes), C.byref(p)), "tmpc_device_alloc")
+        return p
+
+    def free(self, p):
+        self._check(self.lib.tmpc_device_free(self.h, p), "tmpc_device_free")
+
+    def h2d(self, dst, arr):
+        arr = np.ascontiguousarray(arr)
+        self._check(self.lib.tmpc_memcpy_h2d(self.h, dst, arr.ctypes.data_as(C.c_void_p), arr.nbytes), "h2d")
+
+    def d2h(self, arr, src):
+        self._check(self.lib.tmpc_memcpy_d2h(self.h, arr.ctypes.data_as(C.c_void_p), src, arr.nbytes), "d2h")
+
+    def d2d(self, dst, src, nbytes):
+        self._check(self.lib.tmpc_memcpy_d2d(self.h, dst, src, int(nbytes)), "d2d")
+
+    def synchronize(self):
+        self._check(self.lib.tmpc_synchronize(self.h), "tmpc_synchronize")
+
+    def rollout_device(self, B, N, dt, d_x, d_u):
+        self._check(self.lib.tmpc_rollout_batch_device(self.h, B, N, float(dt), d_x, d_u), "tmpc_rollout_batch_device")
+
+    def sqp_solve_batch_device(self, B, N, dt, d_x, d_u, method="PCG-SS", want_status=False):
+        ex = np.zeros(B, dtype=np.int32) if want_status else None
+        it = np.zeros(B, dtype=np.int32) if want_status else None
+        self._check(self.lib.tmpc_sqp_solve_batch_device(self.h, B, int(N), float(dt), LINSYS[method], d_x, d_u,
+                                                         _ptr(ex), _ptr(it)), "tmpc_sqp_solve_batch_device")
+        return ex, it
+
+    def kernel_stats(self, name):
+        n = C.c_int64(0)
+        ms = C.c_double(0.0)
+        self._check(self.lib.tmpc_kernel_stats(self.h, name.encode(), C.byref(n), C.byref(ms)), "tmpc_kernel_stats")
+        return int(n.value), float(ms.value)
+
+    def solve_counters(self):
+        """[problem-QPs, PCG iterations, gradient recomputations, line-search trials per QP] of the last solve."""
+        c = (C.c_int64 * 4)()
+        self._check(self.lib.tmpc_solve_counters(self.h, c), "tmpc_solve_counters")
+        return [int(v) for v in c]
+
+    def reset_stats(self):
+        self._check(self.lib.tmpc_reset_stats(self.h), "tmpc_reset_stats")
+
+
+_default_ctx = {}
+
+
+def default_context(device: int = 0) -> Context:
+    """Process-wide context per device (the Python plugin classes share it)."""
+    ctx = _default_ctx.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _default_ctx[device] = ctx
+    return ctx

@@ -1,0 +1,794 @@
+// C ABI (include/tmpc.h) and the batched SQP driver.
+//
+// The driver is the host half of TrajoptMPCReference.SQP
+// (TrajoptMPCReference.py:510-760): it launches, per SQP iteration, the
+// masked device phases QP-build (dynamics + gradients) -> Schur -> PCG ->
+// dxu -> line-search terms -> decision, and stops when no problem of the
+// batch is active.  All per-problem branching lives on the device
+// (k_ls_decide); the host reads back one integer per iteration.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/tmpc.h"
+#include "tmpc_internal.h"
+
+using namespace tmpc;
+
+namespace {
+
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+struct Stat {
+  int64_t launches = 0;
+  double total_ms = 0.0;
+};
+
+struct PendingTiming {
+  std::string name;
+  hipEvent_t start, stop;
+};
+
+}  // namespace
+
+struct tmpc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool has_model = false, has_cost = false;
+  ModelDev hmodel{};
+  CostDev hcost{};
+  ModelDev* dmodel = nullptr;
+  CostDev* dcost = nullptr;
+  tmpc_options opts{};
+  std::map<std::string, DevBuf> bufs;
+  std::map<std::string, Stat> stats;
+  std::vector<PendingTiming> pending;
+  std::vector<hipEvent_t> event_pool;
+  int* h_count = nullptr;  // pinned
+  int64_t last_counters[4] = {0, 0, 0, 0};
+};
+
+static int fail(tmpc_ctx* c, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return -1;
+}
+
+#define HIP_OK(call)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess) return fail(ctx, "%s failed: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+#define LAUNCH_OK(call)                                                                       \
+  do {                                                                                        \
+    int r_ = (call);                                                                          \
+    if (r_ != 0) return fail(ctx, "unsupported size for %s (code %d)", #call, r_);           \
+    hipError_t e_ = hipGetLastError();                                                        \
+    if (e_ != hipSuccess) return fail(ctx, "launch %s failed: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+static hipEvent_t get_event(tmpc_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// RAII timing of one launch on the context stream (options.profile)
+struct Timed {
+  tmpc_ctx* ctx;
+  PendingTiming pt;
+  bool on;
+  Timed(tmpc_ctx* c, const char* name) : ctx(c), on(c->opts.profile != 0) {
+    if (!on) return;
+    pt.name = name;
+    pt.start = get_event(ctx);
+    pt.stop = get_event(ctx);
+    hipEventRecord(pt.start, ctx->stream);
+  }
+  ~Timed() {
+    if (!on) return;
+    hipEventRecord(pt.stop, ctx->stream);
+    ctx->pending.push_back(pt);
+  }
+};
+
+static void resolve_timings(tmpc_ctx* ctx) {
+  for (auto& p : ctx->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.stop) == hipSuccess && hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
+      Stat& s = ctx->stats[p.name];
+      s.launches += 1;
+      s.total_ms += ms;
+    }
+    ctx->event_pool.push_back(p.start);
+    ctx->event_pool.push_back(p.stop);
+  }
+  ctx->pending.clear();
+}
+
+template <typename T>
+static T* buf(tmpc_ctx* ctx, const char* name, size_t count) {
+  DevBuf& b = ctx->bufs[name];
+  const size_t bytes = count * sizeof(T);
+  if (b.bytes < bytes) {
+    if (b.ptr) hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+    if (hipMalloc(&b.ptr, bytes) != hipSuccess) {
+      b.ptr = nullptr;
+      return nullptr;
+    }
+    b.bytes = bytes;
+  }
+  return static_cast<T*>(b.ptr);
+}
+
+#define BUF(T, name, count)                                                            \
+  T* name = buf<T>(ctx, #name, (size_t)(count));                                       \
+  if (!name) return fail(ctx, "device allocation of %s (%zu elements) failed", #name, \
+                         (size_t)(count));
+
+static SolverOpts solver_opts(const tmpc_options& o) {
+  SolverOpts s{};
+  s.exit_tol_sqp = o.exit_tolerance_SQP_DDP;
+  s.alpha_factor = o.alpha_factor_SQP_DDP;
+  s.alpha_min = o.alpha_min_SQP_DDP;
+  s.rho_factor = o.rho_factor_SQP_DDP;
+  s.rho_min = o.rho_min_SQP_DDP;
+  s.rho_max = o.rho_max_SQP_DDP;
+  s.rho_init = o.rho_init_SQP_DDP;
+  s.exp_red_min = o.expected_reduction_min_SQP_DDP;
+  s.exp_red_max = o.expected_reduction_max_SQP_DDP;
+  s.mu = o.merit_mu;
+  s.max_iter_sqp = o.max_iter_SQP_DDP;
+  return s;
+}
+
+// alpha schedule of the line search (:606, :712-718): 1, f, f^2, ... while alpha > alpha_min
+static std::vector<double> alpha_list(const tmpc_options& o) {
+  std::vector<double> a;
+  double al = 1.0;
+  a.push_back(al);
+  while (al > o.alpha_min_SQP_DDP && a.size() < 64) {
+    al *= o.alpha_factor_SQP_DDP;
+    a.push_back(al);
+  }
+  return a;
+}
+
+static int precond_of(int linsys) {
+  switch (linsys) {
+    case TMPC_LINSYS_PCG_J: return PRECOND_J;
+    case TMPC_LINSYS_PCG_BJ: return PRECOND_BJ;
+    case TMPC_LINSYS_PCG_SS: return PRECOND_SS;
+    default: return -1;
+  }
+}
+
+static int check_ready(tmpc_ctx* ctx, int B, int N) {
+  if (!ctx) return -1;
+  if (!ctx->has_model) return fail(ctx, "no model: call tmpc_set_model first");
+  if (!ctx->has_cost) return fail(ctx, "no cost: call tmpc_set_cost_quadratic first");
+  if (ctx->hcost.nx != 2 * ctx->hmodel.n || ctx->hcost.nu != ctx->hmodel.n)
+    return fail(ctx, "cost sizes (nx=%d, nu=%d) do not match the model (n=%d)", ctx->hcost.nx, ctx->hcost.nu,
+                ctx->hmodel.n);
+  if (B < 1) return fail(ctx, "batch size must be >= 1 (got %d)", B);
+  if (N < 2) return fail(ctx, "N must be >= 2 (got %d)", N);
+  if (N * ctx->hcost.nx > 1024)
+    return fail(ctx, "N * nx = %d exceeds 1024 rows (one PCG workgroup per problem); larger horizons are not "
+                "supported yet", N * ctx->hcost.nx);
+  return 0;
+}
+
+// ------------------------------------------------------------------ QP phase (shared by SQP and tmpc_qp_batch)
+struct Work {
+  double *xs, *qdd, *minv, *cvec, *A, *Bm, *G, *Sd, *Sl, *gam, *lam, *dx, *du, *Pd;
+  int* iters;
+};
+
+static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
+                  const ProbState& st, Work& w, bool keep_Pd) {
+  const int nj = ctx->hmodel.n, nx = 2 * nj;
+  const bool chain = ctx->hmodel.chain != 0;
+  {
+    Timed t(ctx, "qp_fd");
+    LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
+                           w.cvec));
+  }
+  {
+    Timed t(ctx, "qp_minv");
+    LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
+  }
+  {
+    Timed t(ctx, "qp_grad");
+    LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv, w.A,
+                             w.Bm));
+  }
+  {
+    Timed t(ctx, "ginv");
+    LAUNCH_OK(launch_ginv(ctx->stream, nj, ctx->dcost, B, st.rho, st.active, w.G));
+  }
+  {
+    Timed t(ctx, "schur");
+    LAUNCH_OK(launch_schur(ctx->stream, nj, ctx->dcost, B, N, d_x, d_u, st.active, w.G, w.A, w.Bm, w.cvec, w.Sd,
+                           w.Sl, w.gam));
+  }
+  {
+    Timed t(ctx, "pcg");
+    LAUNCH_OK(launch_pcg(ctx->stream, nx, B, N, precond, w.Sd, w.Sl, nullptr, w.gam, nullptr, st.active,
+                         ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.lam, w.iters, nullptr,
+                         nullptr, keep_Pd ? w.Pd : nullptr));
+  }
+  {
+    Timed t(ctx, "dxu");
+    LAUNCH_OK(launch_dxu(ctx->stream, nj, ctx->dcost, B, N, d_x, d_u, st.active, w.G, w.A, w.Bm, w.lam, w.dx,
+                         w.du));
+  }
+  return 0;
+}
+
+static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_Pd) {
+  const int nj = ctx->hmodel.n, nx = 2 * nj, K = N - 1;
+  BUF(double, xs, (size_t)B * nx);
+  BUF(double, qdd, (size_t)B * K * nj);
+  BUF(double, minv, (size_t)B * K * nj * nj);
+  BUF(double, cvec, (size_t)B * N * nx);
+  BUF(double, Amat, (size_t)B * K * nx * nx);
+  BUF(double, Bmat, (size_t)B * K * nx * nj);
+  BUF(double, Ginv, (size_t)B * 3 * nx * nx);
+  BUF(double, Sdiag, (size_t)B * N * nx * nx);
+  BUF(double, Slo, (size_t)B * K * nx * nx);
+  BUF(double, gam, (size_t)B * N * nx);
+  BUF(double, lam, (size_t)B * N * nx);
+  BUF(double, dx, (size_t)B * N * nx);
+  BUF(double, du, (size_t)B * K * nj);
+  BUF(int, iters, (size_t)B);
+  w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, Sdiag, Slo, gam, lam, dx, du, nullptr, iters};
+  if (with_Pd) {
+    BUF(double, Pdiag, (size_t)B * N * nx * nx);
+    w.Pd = Pdiag;
+  }
+  return 0;
+}
+
+static int alloc_state(tmpc_ctx* ctx, int B, ProbState& st) {
+  BUF(double, st_rho, B);
+  BUF(double, st_drho, B);
+  BUF(double, st_J, B);
+  BUF(double, st_c, B);
+  BUF(double, st_merit, B);
+  BUF(int, st_iter, B);
+  BUF(int, st_active, B);
+  BUF(int, st_need, B);
+  BUF(int, st_exit, B);
+  st = ProbState{st_rho, st_drho, st_J, st_c, st_merit, st_iter, st_active, st_need, st_exit};
+  return 0;
+}
+
+static int alloc_trace(tmpc_ctx* ctx, int B, int W, TraceDev& tr) {
+  BUF(int, tr_iteration, (size_t)B * W);
+  BUF(int, tr_ls, (size_t)B * W);
+  BUF(double, tr_alpha, (size_t)B * W);
+  BUF(double, tr_rho, (size_t)B * W);
+  BUF(double, tr_J, (size_t)B * W);
+  BUF(double, tr_c, (size_t)B * W);
+  BUF(double, tr_merit, (size_t)B * W);
+  BUF(double, tr_D, (size_t)B * W);
+  BUF(double, tr_ratio, (size_t)B * W);
+  BUF(int, tr_acc, (size_t)B * W);
+  BUF(int, tr_pcg, (size_t)B * W);
+  tr = TraceDev{tr_iteration, tr_ls, tr_alpha, tr_rho, tr_J, tr_c, tr_merit, tr_D, tr_ratio, tr_acc, tr_pcg};
+  return 0;
+}
+
+static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
+                      TraceDev* tr_out) {
+  int rc = check_ready(ctx, B, N);
+  if (rc) return rc;
+  const int precond = precond_of(linsys);
+  if (precond < 0)
+    return fail(ctx, "linear system method %d is not available on the GPU (use PCG-J/BJ/SS = 2/3/4)", linsys);
+  const int nj = ctx->hmodel.n, nx = 2 * nj;
+  const bool chain = ctx->hmodel.chain != 0;
+  const tmpc_options& o = ctx->opts;
+  const SolverOpts so = solver_opts(o);
+  const std::vector<double> al = alpha_list(o);
+  const int T = (int)al.size();
+  const int W = o.max_iter_SQP_DDP + 1;
+  Work w;
+  if ((rc = alloc_work(ctx, B, N, w, false))) return rc;
+  ProbState st;
+  if ((rc = alloc_state(ctx, B, st))) return rc;
+  TraceDev tr;
+  if ((rc = alloc_trace(ctx, B, W, tr))) return rc;
+  BUF(double, alphas, T + 1);
+  BUF(double, terms, (size_t)B * T * N * 3);
+  BUF(int, active_count, 1);
+  BUF(unsigned long long, counters, 4);
+  HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
+  std::vector<double> al_h(al);
+  al_h.push_back(0.0);  // slot T: alpha = 0 for the initial merit evaluation
+  HIP_OK(hipMemcpyAsync(alphas, al_h.data(), al_h.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  // xs = x[:, 0] (:527)
+  HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
+                          hipMemcpyDeviceToDevice, ctx->stream));
+  launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st);
+  // initial J, c, merit (:541-548)
+  LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, B, N, 1, dt, alphas + T, d_x, d_u,
+                            w.xs, nullptr, nullptr, st.active, terms));
+  HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
+  launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, alphas + T, so, terms, d_x, d_u, w.dx, w.du, st,
+                   nullptr, tr, active_count, nullptr);
+  for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
+    if ((rc = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false))) return rc;
+    {
+      Timed t(ctx, "ls_terms");
+      LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, B, N, T, dt, alphas, d_x, d_u,
+                                w.xs, w.dx, w.du, st.active, terms));
+    }
+    HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
+    {
+      Timed t(ctx, "ls_decide");
+      launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, alphas, so, terms, d_x, d_u, w.dx, w.du, st,
+                       w.iters, tr, active_count, counters);
+      HIP_OK(hipGetLastError());
+    }
+    HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (*ctx->h_count == 0) break;
+  }
+  unsigned long long hc[4] = {0, 0, 0, 0};
+  HIP_OK(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->last_counters[0] = (int64_t)hc[0];
+  ctx->last_counters[1] = (int64_t)hc[1];
+  ctx->last_counters[2] = (int64_t)hc[2];
+  ctx->last_counters[3] = (int64_t)T;
+  resolve_timings(ctx);
+  if (tr_out) *tr_out = tr;
+  return 0;
+}
+
+// ======================================================================= C ABI
+extern "C" {
+
+int tmpc_abi_version(void) { return TMPC_ABI_VERSION; }
+
+int tmpc_device_count(int* count) {
+  if (!count) return -1;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return 0;
+}
+
+int tmpc_create(int device, tmpc_ctx** out) {
+  if (!out) return -1;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return -2;
+  if (device < 0 || device >= n) return -3;
+  tmpc_ctx* ctx = new tmpc_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&ctx->dmodel, sizeof(ModelDev)) != hipSuccess || hipMalloc(&ctx->dcost, sizeof(CostDev)) != hipSuccess ||
+      hipHostMalloc(&ctx->h_count, sizeof(int)) != hipSuccess) {
+    delete ctx;
+    return -4;
+  }
+  pcg_set_max_lds();
+  tmpc_default_options(&ctx->opts);
+  *out = ctx;
+  return 0;
+}
+
+void tmpc_destroy(tmpc_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (auto& p : ctx->pending) {
+    hipEventDestroy(p.start);
+    hipEventDestroy(p.stop);
+  }
+  for (auto e : ctx->event_pool) hipEventDestroy(e);
+  for (auto& kv : ctx->bufs)
+    if (kv.second.ptr) hipFree(kv.second.ptr);
+  if (ctx->dmodel) hipFree(ctx->dmodel);
+  if (ctx->dcost) hipFree(ctx->dcost);
+  if (ctx->h_count) hipHostFree(ctx->h_count);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* tmpc_last_error(const tmpc_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int tmpc_set_model(tmpc_ctx* ctx, int n, const int32_t* parent, const int32_t* jtype, const int32_t* saxis,
+                   const double* X0, const double* Xa, const double* Xb, const double* I, double gravity) {
+  if (!ctx) return -1;
+  if (n < 1 || n > 7) return fail(ctx, "model must have 1..7 joints (got %d)", n);
+  if (!parent || !jtype || !saxis || !X0 || !Xa || !Xb || !I) return fail(ctx, "null model array");
+  ModelDev m{};
+  m.n = n;
+  m.gravity = gravity;
+  bool chain = true;
+  for (int j = 0; j < n; ++j) {
+    if (parent[j] < -1 || parent[j] >= j)
+      return fail(ctx, "parent[%d] = %d: joints must be in DFS order (parent id < child id)", j, parent[j]);
+    if (jtype[j] != TMPC_JOINT_REVOLUTE && jtype[j] != TMPC_JOINT_PRISMATIC)
+      return fail(ctx, "joint %d: unsupported joint type %d", j, jtype[j]);
+    if (saxis[j] < 0 || saxis[j] > 5) return fail(ctx, "joint %d: motion subspace index %d out of range", j, saxis[j]);
+    m.parent[j] = parent[j];
+    m.jtype[j] = jtype[j];
+    m.saxis[j] = saxis[j];
+    if (parent[j] != j - 1) chain = false;
+    for (int e = 0; e < 6; ++e) m.S[j][e] = (e == saxis[j]) ? 1.0 : 0.0;
+    memcpy(m.X0[j], X0 + 36 * j, 36 * sizeof(double));
+    memcpy(m.Xa[j], Xa + 36 * j, 36 * sizeof(double));
+    memcpy(m.Xb[j], Xb + 36 * j, 36 * sizeof(double));
+    memcpy(m.I[j], I + 36 * j, 36 * sizeof(double));
+  }
+  for (int j = n - 1; j >= 0; --j) {
+    m.subtree[j] |= 1u << j;
+    if (parent[j] >= 0) m.subtree[parent[j]] |= m.subtree[j];
+  }
+  m.chain = chain ? 1 : 0;
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMemcpyAsync(ctx->dmodel, &m, sizeof(m), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->hmodel = m;
+  ctx->has_model = true;
+  return 0;
+}
+
+int tmpc_set_cost_quadratic(tmpc_ctx* ctx, int nx, int nu, const double* Q, const double* QF, const double* R,
+                            const double* xg, int32_t QF_start) {
+  if (!ctx) return -1;
+  if (nx < 1 || nx > NXMAX || nu < 1 || nu > NJMAX) return fail(ctx, "cost sizes out of range (nx=%d, nu=%d)", nx, nu);
+  if (!Q || !QF || !R || !xg) return fail(ctx, "null cost array");
+  CostDev c{};
+  c.nx = nx;
+  c.nu = nu;
+  c.QF_start = QF_start < 0 ? -1 : QF_start;
+  memcpy(c.Q, Q, sizeof(double) * nx * nx);
+  memcpy(c.QF, QF, sizeof(double) * nx * nx);
+  memcpy(c.R, R, sizeof(double) * nu * nu);
+  memcpy(c.xg, xg, sizeof(double) * nx);
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMemcpyAsync(ctx->dcost, &c, sizeof(c), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->hcost = c;
+  ctx->has_cost = true;
+  return 0;
+}
+
+void tmpc_default_options(tmpc_options* o) {
+  if (!o) return;
+  memset(o, 0, sizeof(*o));
+  o->exit_tolerance_linSys = 1e-6;
+  o->max_iter_linSys = 100;
+  o->max_iter_SQP_DDP = 100;
+  o->exit_tolerance_SQP_DDP = 1e-6;
+  o->alpha_factor_SQP_DDP = 0.5;
+  o->alpha_min_SQP_DDP = 0.005;
+  o->rho_factor_SQP_DDP = 4;
+  o->rho_min_SQP_DDP = 1e-3;
+  o->rho_max_SQP_DDP = 1e3;
+  o->rho_init_SQP_DDP = 0.001;
+  o->expected_reduction_min_SQP_DDP = 0.05;
+  o->expected_reduction_max_SQP_DDP = 3;
+  o->merit_mu = 10.0;
+  o->profile = 0;
+}
+
+int tmpc_set_options(tmpc_ctx* ctx, const tmpc_options* o) {
+  if (!ctx || !o) return -1;
+  if (o->max_iter_linSys < 1 || o->max_iter_SQP_DDP < 1) return fail(ctx, "max_iter options must be >= 1");
+  if (!(o->alpha_factor_SQP_DDP > 0.0 && o->alpha_factor_SQP_DDP < 1.0))
+    return fail(ctx, "alpha_factor_SQP_DDP must be in (0, 1)");
+  ctx->opts = *o;
+  return 0;
+}
+
+int tmpc_sqp_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
+                                int32_t* exit_sqp, int32_t* sqp_iter) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  int rc = sqp_device(ctx, B, N, dt, linsys, d_x, d_u, nullptr);
+  if (rc) return rc;
+  if (exit_sqp) HIP_OK(hipMemcpy(exit_sqp, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (sqp_iter) HIP_OK(hipMemcpy(sqp_iter, ctx->bufs["st_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* x, double* u,
+                         int32_t* exit_sqp, int32_t* exit_soft, int32_t* outer_iter, int32_t* sqp_iter,
+                         tmpc_trace* trace) {
+  if (!ctx) return -1;
+  int rc = check_ready(ctx, B, N);
+  if (rc) return rc;
+  if (!x || !u) return fail(ctx, "null x/u");
+  hipSetDevice(ctx->device);
+  const int nx = ctx->hcost.nx, nu = ctx->hcost.nu;
+  const size_t xn = (size_t)B * nx * N, un = (size_t)B * nu * (N - 1);
+  BUF(double, io_x, xn);
+  BUF(double, io_u, un);
+  HIP_OK(hipMemcpyAsync(io_x, x, xn * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(io_u, u, un * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  TraceDev tr;
+  if ((rc = sqp_device(ctx, B, N, dt, linsys, io_x, io_u, &tr))) return rc;
+  HIP_OK(hipMemcpy(x, io_x, xn * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(u, io_u, un * sizeof(double), hipMemcpyDeviceToHost));
+  if (exit_sqp) HIP_OK(hipMemcpy(exit_sqp, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (sqp_iter) HIP_OK(hipMemcpy(sqp_iter, ctx->bufs["st_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  // unconstrained: the soft-constraint outer loop runs once and exits with code 1 (:483-508)
+  for (int b = 0; b < B; ++b) {
+    if (exit_soft) exit_soft[b] = 1;
+    if (outer_iter) outer_iter[b] = 1;
+  }
+  if (trace) {
+    const size_t n = (size_t)B * (ctx->opts.max_iter_SQP_DDP + 1);
+#define CP(field, src, T) \
+  if (trace->field) HIP_OK(hipMemcpy(trace->field, tr.src, n * sizeof(T), hipMemcpyDeviceToHost));
+    CP(iteration, iteration, int)
+    CP(line_search_iteration, ls_iter, int)
+    CP(alpha, alpha, double)
+    CP(rho, rho, double)
+    CP(J, J, double)
+    CP(c, c, double)
+    CP(merit, merit, double)
+    CP(D, D, double)
+    CP(reduction_ratio, ratio, double)
+    CP(succeeded_line_search, accepted, int)
+    CP(pcg_iters, pcg_iters, int)
+#undef CP
+  }
+  return 0;
+}
+
+int tmpc_rollout_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, const double* d_u) {
+  if (!ctx) return -1;
+  if (!ctx->has_model) return fail(ctx, "no model");
+  hipSetDevice(ctx->device);
+  LAUNCH_OK(launch_rollout(ctx->stream, ctx->hmodel.n, ctx->hmodel.chain != 0, ctx->dmodel, B, N, dt, d_x, d_u));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int tmpc_fd_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const double* u, double* xnext, double* qdd,
+                  double* Minv) {
+  if (!ctx) return -1;
+  if (!ctx->has_model) return fail(ctx, "no model");
+  if (K < 1) return 0;
+  hipSetDevice(ctx->device);
+  const int nj = ctx->hmodel.n, nx = 2 * nj;
+  BUF(double, u_x, (size_t)K * nx);
+  BUF(double, u_u, (size_t)K * nj);
+  BUF(double, u_xn, (size_t)K * nx);
+  BUF(double, u_qdd, (size_t)K * nj);
+  BUF(double, u_minv, (size_t)K * nj * nj);
+  HIP_OK(hipMemcpyAsync(u_x, x, sizeof(double) * K * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(u_u, u, sizeof(double) * K * nj, hipMemcpyHostToDevice, ctx->stream));
+  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->dmodel, K, dt, u_x, u_u, u_xn, u_qdd));
+  if (Minv) LAUNCH_OK(launch_unit_minv(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->dmodel, K, u_x, u_minv));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (xnext) HIP_OK(hipMemcpy(xnext, u_xn, sizeof(double) * K * nx, hipMemcpyDeviceToHost));
+  if (qdd) HIP_OK(hipMemcpy(qdd, u_qdd, sizeof(double) * K * nj, hipMemcpyDeviceToHost));
+  if (Minv) HIP_OK(hipMemcpy(Minv, u_minv, sizeof(double) * K * nj * nj, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const double* u, double* A, double* Bo,
+                       double* dqdd) {
+  if (!ctx) return -1;
+  if (!ctx->has_model) return fail(ctx, "no model");
+  if (K < 1) return 0;
+  hipSetDevice(ctx->device);
+  const int nj = ctx->hmodel.n, nx = 2 * nj;
+  const bool chain = ctx->hmodel.chain != 0;
+  BUF(double, u_x, (size_t)K * nx);
+  BUF(double, u_u, (size_t)K * nj);
+  BUF(double, u_qdd, (size_t)K * nj);
+  BUF(double, u_minv, (size_t)K * nj * nj);
+  BUF(double, u_A, (size_t)K * nx * nx);
+  BUF(double, u_B, (size_t)K * nx * nj);
+  BUF(double, u_dqdd, (size_t)K * nj * 3 * nj);
+  HIP_OK(hipMemcpyAsync(u_x, x, sizeof(double) * K * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(u_u, u, sizeof(double) * K * nj, hipMemcpyHostToDevice, ctx->stream));
+  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, chain, ctx->dmodel, K, 0.0, u_x, u_u, nullptr, u_qdd));
+  LAUNCH_OK(launch_unit_minv(ctx->stream, nj, chain, ctx->dmodel, K, u_x, u_minv));
+  LAUNCH_OK(launch_unit_grad(ctx->stream, nj, chain, ctx->dmodel, K, dt, u_x, u_qdd, u_minv, u_A, u_B, u_dqdd));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (A) HIP_OK(hipMemcpy(A, u_A, sizeof(double) * K * nx * nx, hipMemcpyDeviceToHost));
+  if (Bo) HIP_OK(hipMemcpy(Bo, u_B, sizeof(double) * K * nx * nj, hipMemcpyDeviceToHost));
+  if (dqdd) HIP_OK(hipMemcpy(dqdd, u_dqdd, sizeof(double) * K * nj * 3 * nj, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
+                  const double* u, double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma,
+                  double* P_diag) {
+  if (!ctx) return -1;
+  int rc = check_ready(ctx, B, N);
+  if (rc) return rc;
+  const int precond = precond_of(linsys);
+  if (precond < 0) return fail(ctx, "linear system method %d is not available on the GPU", linsys);
+  if (!rho || !x || !u) return fail(ctx, "null input");
+  hipSetDevice(ctx->device);
+  const int nj = ctx->hmodel.n, nx = 2 * nj, K = N - 1, nxu = nx + nj;
+  Work w;
+  if ((rc = alloc_work(ctx, B, N, w, true))) return rc;
+  ProbState st;
+  if ((rc = alloc_state(ctx, B, st))) return rc;
+  BUF(double, io_x, (size_t)B * nx * N);
+  BUF(double, io_u, (size_t)B * nj * K);
+  HIP_OK(hipMemcpyAsync(io_x, x, sizeof(double) * B * nx * N, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(io_u, u, sizeof(double) * B * nj * K, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(st.rho, rho, sizeof(double) * B, hipMemcpyHostToDevice, ctx->stream));
+  launch_init_state(ctx->stream, B, 0.0, ProbState{st.drho, st.drho, st.J, st.c, st.merit, st.iter, st.active,
+                                                   st.need_grad, st.exit_sqp});
+  HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), io_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
+                          hipMemcpyDeviceToDevice, ctx->stream));
+  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, precond != PRECOND_J))) return rc;
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  resolve_timings(ctx);
+  if (dxul) {
+    std::vector<double> dx((size_t)B * N * nx), du((size_t)B * K * nj), lam((size_t)B * N * nx);
+    HIP_OK(hipMemcpy(dx.data(), w.dx, dx.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(du.data(), w.du, du.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(lam.data(), w.lam, lam.size() * sizeof(double), hipMemcpyDeviceToHost));
+    const size_t L = (size_t)nxu * K + nx + (size_t)nx * N;
+    for (int b = 0; b < B; ++b) {
+      double* o = dxul + b * L;
+      for (int k = 0; k < N; ++k) {
+        for (int i = 0; i < nx; ++i) o[(size_t)k * nxu + i] = dx[((size_t)b * N + k) * nx + i];
+        if (k < K)
+          for (int i = 0; i < nj; ++i) o[(size_t)k * nxu + nx + i] = du[((size_t)b * K + k) * nj + i];
+      }
+      memcpy(o + (size_t)nxu * K + nx, lam.data() + (size_t)b * N * nx, sizeof(double) * N * nx);
+    }
+  }
+  if (pcg_iters) HIP_OK(hipMemcpy(pcg_iters, w.iters, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (S_diag) HIP_OK(hipMemcpy(S_diag, w.Sd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
+  if (S_lo) HIP_OK(hipMemcpy(S_lo, w.Sl, sizeof(double) * B * K * nx * nx, hipMemcpyDeviceToHost));
+  if (gamma) HIP_OK(hipMemcpy(gamma, w.gam, sizeof(double) * B * N * nx, hipMemcpyDeviceToHost));
+  if (P_diag && precond != PRECOND_J)
+    HIP_OK(hipMemcpy(P_diag, w.Pd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_pcg_batch(tmpc_ctx* ctx, int B, int N, int nx, int precond, const double* S_diag, const double* S_lo,
+                   const double* S_up, const double* gamma, const double* guess, double tol, int max_iter,
+                   double* lambda,
+                   int32_t* iters, double* trace_nu, double* trace_res, double* P_diag) {
+  if (!ctx) return -1;
+  if (B < 1 || N < 1 || nx < 1) return fail(ctx, "bad sizes B=%d N=%d nx=%d", B, N, nx);
+  if (N * nx > 1024) return fail(ctx, "N * nx = %d exceeds 1024 rows", N * nx);
+  if (precond != PRECOND_J && precond != PRECOND_BJ && precond != PRECOND_SS)
+    return fail(ctx, "preconditioner %d: valid are J=1, BJ=2, SS=3 (PCG.py:52-55)", precond);
+  if (max_iter < 0) return fail(ctx, "max_iter must be >= 0");
+  if (!S_diag || !gamma || (N > 1 && !S_lo)) return fail(ctx, "null input");
+  hipSetDevice(ctx->device);
+  const int K = N - 1;
+  BUF(double, p_Sd, (size_t)B * N * nx * nx);
+  BUF(double, p_Sl, (size_t)B * (K > 0 ? K : 1) * nx * nx);
+  BUF(double, p_Su, (size_t)B * (K > 0 ? K : 1) * nx * nx);
+  BUF(double, p_g, (size_t)B * N * nx);
+  BUF(double, p_lam, (size_t)B * N * nx);
+  BUF(int, p_it, (size_t)B);
+  BUF(double, p_tn, (size_t)B * (max_iter + 1));
+  BUF(double, p_tr, (size_t)B * (max_iter + 1));
+  BUF(double, p_Pd, (size_t)B * N * nx * nx);
+  BUF(double, p_x0, (size_t)B * N * nx);
+  if (guess) HIP_OK(hipMemcpyAsync(p_x0, guess, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(p_Sd, S_diag, sizeof(double) * B * N * nx * nx, hipMemcpyHostToDevice, ctx->stream));
+  if (K > 0) HIP_OK(hipMemcpyAsync(p_Sl, S_lo, sizeof(double) * B * K * nx * nx, hipMemcpyHostToDevice, ctx->stream));
+  if (K > 0 && S_up)
+    HIP_OK(hipMemcpyAsync(p_Su, S_up, sizeof(double) * B * K * nx * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(p_g, gamma, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
+  {
+    Timed t(ctx, "pcg");
+    LAUNCH_OK(launch_pcg(ctx->stream, nx, B, N, precond, p_Sd, p_Sl, S_up ? p_Su : nullptr, p_g,
+                         guess ? p_x0 : nullptr, nullptr, tol,
+                         max_iter, p_lam, p_it, trace_nu ? p_tn : nullptr, trace_res ? p_tr : nullptr,
+                         P_diag ? p_Pd : nullptr));
+  }
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  resolve_timings(ctx);
+  if (lambda) HIP_OK(hipMemcpy(lambda, p_lam, sizeof(double) * B * N * nx, hipMemcpyDeviceToHost));
+  if (iters) HIP_OK(hipMemcpy(iters, p_it, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (trace_nu) HIP_OK(hipMemcpy(trace_nu, p_tn, sizeof(double) * B * (max_iter + 1), hipMemcpyDeviceToHost));
+  if (trace_res) HIP_OK(hipMemcpy(trace_res, p_tr, sizeof(double) * B * (max_iter + 1), hipMemcpyDeviceToHost));
+  if (P_diag && precond != PRECOND_J)
+    HIP_OK(hipMemcpy(P_diag, p_Pd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_device_alloc(tmpc_ctx* ctx, size_t bytes, void** ptr) {
+  if (!ctx || !ptr) return -1;
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMalloc(ptr, bytes));
+  return 0;
+}
+
+int tmpc_device_free(tmpc_ctx* ctx, void* ptr) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  HIP_OK(hipFree(ptr));
+  return 0;
+}
+
+int tmpc_memcpy_h2d(tmpc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int tmpc_memcpy_d2h(tmpc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int tmpc_memcpy_d2d(tmpc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int tmpc_synchronize(tmpc_ctx* ctx) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  resolve_timings(ctx);
+  return 0;
+}
+
+int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms) {
+  if (!ctx || !name) return -1;
+  resolve_timings(ctx);
+  auto it = ctx->stats.find(name);
+  if (launches) *launches = it == ctx->stats.end() ? 0 : it->second.launches;
+  if (total_ms) *total_ms = it == ctx->stats.end() ? 0.0 : it->second.total_ms;
+  return 0;
+}
+
+int tmpc_solve_counters(tmpc_ctx* ctx, int64_t* counters) {
+  if (!ctx || !counters) return -1;
+  for (int i = 0; i < 4; ++i) counters[i] = ctx->last_counters[i];
+  return 0;
+}
+
+int tmpc_reset_stats(tmpc_ctx* ctx) {
+  if (!ctx) return -1;
+  resolve_timings(ctx);
+  ctx->stats.clear();
+  return 0;
+}
+
+}  // extern "C"

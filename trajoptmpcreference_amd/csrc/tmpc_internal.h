@@ -1,0 +1,92 @@
+// Internal declarations shared by the kernels (tmpc_kernels.hip) and the
+// C-ABI / solver driver (tmpc_api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tmpc_device.h"
+
+namespace tmpc {
+
+enum { PRECOND_J = 1, PRECOND_BJ = 2, PRECOND_SS = 3 };
+enum { LS_MODE_INIT = 0, LS_MODE_STEP = 1 };
+
+// set_default_options (TrajoptMPCReference.py:91-115) + the fixed merit
+// weight mu = 10 (:545-546)
+struct SolverOpts {
+  double exit_tol_sqp;
+  double alpha_factor;
+  double alpha_min;
+  double rho_factor;
+  double rho_min;
+  double rho_max;
+  double rho_init;
+  double exp_red_min;
+  double exp_red_max;
+  double mu;
+  int max_iter_sqp;
+  int pad;
+};
+
+// per-problem solver state (device arrays, SoA)
+struct ProbState {
+  double* rho;
+  double* drho;
+  double* J;
+  double* c;
+  double* merit;
+  int* iter;
+  int* active;
+  int* need_grad;
+  int* exit_sqp;
+};
+
+// per-problem trace rows [B][max_iter_sqp + 1] (self.trace, :555-569, :691-743)
+struct TraceDev {
+  int* iteration;
+  int* ls_iter;
+  double* alpha;
+  double* rho;
+  double* J;
+  double* c;
+  double* merit;
+  double* D;
+  double* ratio;
+  int* accepted;
+  int* pcg_iters;
+};
+
+int launch_qp_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, const double* x,
+                 const double* u, const double* xs, const int* need, double* qdd, double* cvec);
+int launch_qp_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, const double* x,
+                   const int* need, double* minv);
+int launch_qp_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, const double* x,
+                   const int* need, const double* qdd, const double* minv, double* A, double* Bm);
+int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, int B, int N, int T,
+                    double dt, const double* alphas, const double* x, const double* u, const double* xs,
+                    const double* dx, const double* du, const int* active, double* terms);
+int launch_unit_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
+                   const double* u, double* xnext, double* qdd);
+int launch_unit_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, const double* x, double* minv);
+int launch_unit_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
+                     const double* qdd, const double* minv, double* A, double* Bm, double* dqdd);
+int launch_rollout(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, double* x,
+                   const double* u);
+int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G);
+int launch_schur(hipStream_t s, int nj, const CostDev* C, int B, int N, const double* x, const double* u,
+                 const int* active, const double* G, const double* A, const double* Bm, const double* cvec,
+                 double* Sd, double* Sl, double* gam);
+int launch_dxu(hipStream_t s, int nj, const CostDev* C, int B, int N, const double* x, const double* u,
+               const int* active, const double* G, const double* A, const double* Bm, const double* lam, double* dx,
+               double* du);
+int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
+               const double* Su, const double* gam, const double* guess, const int* active, double tol, int max_iter, double* lam,
+               int* iters, double* tnu, double* tres, double* Pd);
+int pcg_set_max_lds();
+void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, const double* alphas,
+                      const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
+                      const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
+                      int* active_count, unsigned long long* counters);
+void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st);
+
+}  // namespace tmpc

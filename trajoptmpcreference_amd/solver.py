@@ -1,0 +1,194 @@
+"""TrajoptMPCReference -- the reference's solver class
+(TrajoptMPCReference.py:29-760) with the SQP hot path on the GPU.
+
+``SQP(x, u, N, dt, METHOD, options)`` keeps the reference signature and
+return tuple ``(x, u, exit_sqp, exit_soft, outer_iter, sqp_iter)`` and fills
+``self.trace`` with one dict per SQP step (:555-569, :691-743).
+``SQP_batch`` solves B independent problems in one call -- the batched form
+the GPU is built for.  Invalid plugins/options raise instead of exit().
+"""
+import copy
+import enum
+
+import numpy as np
+
+from . import _native
+from .constraint import TrajoptConstraint
+from .cost import QuadraticCost, TrajoptCost
+from .plant import TrajoptPlant, URDFPlant
+
+
+class SQPSolverMethods(enum.Enum):
+    N = "N"
+    S = "S"
+    PCG_J = "PCG-J"
+    PCG_BJ = "PCG-BJ"
+    PCG_SS = "PCG-SS"
+
+
+class MPCSolverMethods(enum.Enum):
+    iLQR = "iLQR"
+    QP_N = "QP-N"
+    QP_S = "QP-S"
+    QP_PCG_J = "QP-PCG-J"
+    QP_PCG_BJ = "QP-PCG-BJ"
+    QP_PCG_SS = "QP-PCG-SS"
+
+
+_OPTION_MAP = {
+    "exit_tolerance_linSys": "exit_tolerance_linSys",
+    "max_iter_linSys": "max_iter_linSys",
+    "exit_tolerance_SQP_DDP": "exit_tolerance_SQP_DDP",
+    "max_iter_SQP_DDP": "max_iter_SQP_DDP",
+    "alpha_factor_SQP_DDP": "alpha_factor_SQP_DDP",
+    "alpha_min_SQP_DDP": "alpha_min_SQP_DDP",
+    "rho_factor_SQP_DDP": "rho_factor_SQP_DDP",
+    "rho_min_SQP_DDP": "rho_min_SQP_DDP",
+    "rho_max_SQP_DDP": "rho_max_SQP_DDP",
+    "rho_init_SQP_DDP": "rho_init_SQP_DDP",
+    "expected_reduction_min_SQP_DDP": "expected_reduction_min_SQP_DDP",
+    "expected_reduction_max_SQP_DDP": "expected_reduction_max_SQP_DDP",
+}
+
+
+def _method_name(m):
+    if isinstance(m, SQPSolverMethods):
+        return m.value
+    if isinstance(m, str) and m in [e.value for e in SQPSolverMethods]:
+        return m
+    raise ValueError("Invalid QP Solver options are: N, S, PCG-J, PCG-BJ, PCG-SS")
+
+
+class TrajoptMPCReference:
+    def __init__(self, plantObj: TrajoptPlant, costObj: TrajoptCost, constraintObj: TrajoptConstraint = None):
+        if not isinstance(plantObj, TrajoptPlant) or not isinstance(costObj, TrajoptCost):
+            raise TypeError("Must pass in a TrajoptPlant and TrajoptCost object to TrajoptMPCReference.")
+        if constraintObj is None:
+            constraintObj = TrajoptConstraint()
+        elif not isinstance(constraintObj, TrajoptConstraint):
+            raise TypeError("If passing in additional constraints must pass in a TrajoptConstraint object.")
+        self.plant = plantObj
+        self.cost = costObj
+        self.other_constraints = constraintObj
+        self.trace = []
+        self.n_inner_iter = 0
+        self.exit_soft = 0
+        self.exit_sqp = 0
+        self.singular = False
+
+    def update_cost(self, costObj: TrajoptCost):
+        if not isinstance(costObj, TrajoptCost):
+            raise TypeError("Must pass in a TrajoptCost object to update_cost in TrajoptMPCReference.")
+        self.cost = costObj
+
+    def update_plant(self, plantObj: TrajoptPlant):
+        if not isinstance(plantObj, TrajoptPlant):
+            raise TypeError("Must pass in a TrajoptPlant object to update_plant in TrajoptMPCReference.")
+        self.plant = plantObj
+
+    def update_constraints(self, constraintObj: TrajoptConstraint):
+        if not isinstance(constraintObj, TrajoptConstraint):
+            raise TypeError("Must pass in a TrajoptConstraint object to update_constraints in TrajoptMPCReference.")
+        self.other_constraints = constraintObj
+
+    def set_default_options(self, options: dict):
+        """TrajoptMPCReference.py:91-115 (mutates the dict, as the reference does)."""
+        options.setdefault("exit_tolerance_linSys", 1e-6)
+        options.setdefault("max_iter_linSys", 100)
+        options.setdefault("DEBUG_MODE_linSys", False)
+        options.setdefault("RETURN_TRACE_linSys", False)
+        options.setdefault("overloading", self.plant.rbdReference.overloading)
+        options.setdefault("exit_tolerance_SQP_DDP", 1e-6)
+        options.setdefault("max_iter_SQP_DDP", 100)
+        options.setdefault("DEBUG_MODE_SQP_DDP", False)
+        options.setdefault("alpha_factor_SQP_DDP", 0.5)
+        options.setdefault("alpha_min_SQP_DDP", 0.005)
+        options.setdefault("rho_factor_SQP_DDP", 4)
+        options.setdefault("rho_min_SQP_DDP", 1e-3)
+        options.setdefault("rho_max_SQP_DDP", 1e3)
+        options.setdefault("rho_init_SQP_DDP", 0.001)
+        options.setdefault("expected_reduction_min_SQP_DDP", 0.05)
+        options.setdefault("expected_reduction_max_SQP_DDP", 3)
+        options.setdefault("merit_factor_SQP", 1.5)
+        options.setdefault("exit_tolerance_softConstraints", 1e-6)
+        options.setdefault("max_iter_softConstraints", 10)
+
+    # ------------------------------------------------------------------ lowering to libtmpc
+    def _context(self, options):
+        if not isinstance(self.plant, URDFPlant):
+            raise NotImplementedError("the GPU solver needs a URDFPlant (custom TrajoptPlant subclasses have no "
+                                      "device implementation)")
+        if not isinstance(self.cost, QuadraticCost):
+            raise NotImplementedError("the GPU solver supports QuadraticCost (UrdfCost is SURVEY §8f row 4)")
+        if self.other_constraints.has_any():
+            raise NotImplementedError("box constraints are not on the GPU path yet (SURVEY §8f row 1)")
+        if options.get("overloading"):
+            raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
+        ctx = self.plant._ctx()
+        c = self.cost
+        ctx.set_cost_quadratic(c.Q, c.QF, c.R, c.xg, c.QF_start)
+        ctx.set_options(**{v: options[k] for k, v in _OPTION_MAP.items()})
+        return ctx
+
+    def SQP_batch(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.PCG_SS, options=None):
+        """B problems at once: x [B][nx][N], u [B][nu][N-1] -> dict of per-problem results."""
+        options = {} if options is None else options
+        self.set_default_options(options)
+        method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
+        if method in ("N", "S"):
+            raise NotImplementedError("direct KKT / Schur solves (methods N, S) are not on the GPU yet; "
+                                      "use PCG-J, PCG-BJ or PCG-SS")
+        ctx = self._context(options)
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        if x.ndim != 3 or u.ndim != 3 or x.shape[2] != N or u.shape[2] != N - 1 or x.shape[0] != u.shape[0]:
+            raise ValueError(f"expected x [B][nx][{N}] and u [B][nu][{N - 1}], got {x.shape} and {u.shape}")
+        return ctx.sqp_solve_batch(x, u, N, dt, method)
+
+    def SQP(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.N, options=None):
+        """TrajoptMPCReference.SQP (:510-760) for one problem."""
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        r = self.SQP_batch(x[None], u[None], N, dt, LINEAR_SYSTEM_SOLVER_METHOD, options)
+        method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
+        it = int(r["sqp_iter"][0])
+        t = r["trace"]
+        rows = min(it + 1, t["alpha"].shape[1])
+        self.trace = []
+        for i in range(rows):
+            self.trace.append({
+                "outer_iteration": 0,
+                "iteration": int(t["iteration"][0, i]),
+                "line_search_iteration": int(t["line_search_iteration"][0, i]),
+                "alpha": float(t["alpha"][0, i]) if i else 1,
+                "rho": float(t["rho"][0, i]),
+                "J": float(t["J"][0, i]),
+                "c": float(t["c"][0, i]),
+                "merit": float(t["merit"][0, i]),
+                "D": None if i == 0 else float(t["D"][0, i]),
+                "reduction_ratio": None if i == 0 else float(t["reduction_ratio"][0, i]),
+                # the true PCG iteration count (the reference stores len((trace, trace2)) == 2: SURVEY F7)
+                "inner_iters": int(t["pcg_iters"][0, i]) if method.startswith("PCG") else 0,
+                "singular": False,
+                "succeeded_line_search": bool(t["succeeded_line_search"][0, i]),
+            })
+        self.exit_sqp = int(r["exit_sqp"][0])
+        self.exit_soft = int(r["exit_soft"][0])
+        return (r["x"][0], r["u"][0], self.exit_sqp, self.exit_soft, int(r["outer_iter"][0]), it)
+
+    def solveKKTSystem_Schur(self, x, u, xs, N, dt, rho=0.0, use_PCG=True, options=None):
+        """One QP (formKKTSystemBlocks + solveKKTSystem_Schur, :361-455) -> dxul column.
+        xs must equal x[:, 0] (the SQP always passes the initial state)."""
+        options = {} if options is None else dict(options)
+        if not use_PCG:
+            raise NotImplementedError("direct Schur solve is not on the GPU yet")
+        self.set_default_options(options)
+        ptype = options.get("preconditioner_type", "BJ")
+        ctx = self._context(options)
+        x = np.asarray(x, dtype=np.float64)
+        if not np.array_equal(np.asarray(xs), x[:, 0]):
+            raise NotImplementedError("xs != x[:, 0] is not supported by the batched QP entry point")
+        r = ctx.qp_batch(x[None], np.asarray(u, dtype=np.float64)[None], N, dt, rho, "PCG-" + ptype,
+                         want_blocks=False)
+        self.n_inner_iter = int(r["pcg_iters"][0])
+        return r["dxul"][0].reshape(-1, 1)
