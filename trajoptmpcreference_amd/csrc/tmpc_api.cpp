@@ -207,8 +207,8 @@ struct Work {
 };
 
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
-                  const ProbState& st, Work& w, bool keep_Pd) {
-  const int nj = ctx->hmodel.n, nx = 2 * nj;
+                  const ProbState& st, Work& w, bool keep_blocks) {
+  const int nj = ctx->hmodel.n;
   const bool chain = ctx->hmodel.chain != 0;
   {
     Timed t(ctx, "qp_fd");
@@ -229,25 +229,16 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     LAUNCH_OK(launch_ginv(ctx->stream, nj, ctx->dcost, B, st.rho, st.active, w.G));
   }
   {
-    Timed t(ctx, "schur");
-    LAUNCH_OK(launch_schur(ctx->stream, nj, ctx->dcost, B, N, d_x, d_u, st.active, w.G, w.A, w.Bm, w.cvec, w.Sd,
-                           w.Sl, w.gam));
-  }
-  {
-    Timed t(ctx, "pcg");
-    LAUNCH_OK(launch_pcg(ctx->stream, nx, B, N, precond, w.Sd, w.Sl, nullptr, w.gam, nullptr, st.active,
-                         ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.lam, w.iters, nullptr,
-                         nullptr, keep_Pd ? w.Pd : nullptr));
-  }
-  {
-    Timed t(ctx, "dxu");
-    LAUNCH_OK(launch_dxu(ctx->stream, nj, ctx->dcost, B, N, d_x, d_u, st.active, w.G, w.A, w.Bm, w.lam, w.dx,
-                         w.du));
+    Timed t(ctx, "qp");
+    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, precond, d_x, d_u, st.active, w.G, w.A, w.Bm, w.cvec,
+                        ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx, w.du,
+                        keep_blocks ? w.lam : nullptr, keep_blocks ? w.Sd : nullptr, keep_blocks ? w.Sl : nullptr,
+                        keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr));
   }
   return 0;
 }
 
-static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_Pd) {
+static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   const int nj = ctx->hmodel.n, nx = 2 * nj, K = N - 1;
   BUF(double, xs, (size_t)B * nx);
   BUF(double, qdd, (size_t)B * K * nj);
@@ -256,16 +247,20 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_Pd) {
   BUF(double, Amat, (size_t)B * K * nx * nx);
   BUF(double, Bmat, (size_t)B * K * nx * nj);
   BUF(double, Ginv, (size_t)B * 3 * nx * nx);
-  BUF(double, Sdiag, (size_t)B * N * nx * nx);
-  BUF(double, Slo, (size_t)B * K * nx * nx);
-  BUF(double, gam, (size_t)B * N * nx);
-  BUF(double, lam, (size_t)B * N * nx);
   BUF(double, dx, (size_t)B * N * nx);
   BUF(double, du, (size_t)B * K * nj);
   BUF(int, iters, (size_t)B);
-  w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, Sdiag, Slo, gam, lam, dx, du, nullptr, iters};
-  if (with_Pd) {
+  w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters};
+  if (with_blocks) {
+    BUF(double, Sdiag, (size_t)B * N * nx * nx);
+    BUF(double, Slo, (size_t)B * (K > 0 ? K : 1) * nx * nx);
+    BUF(double, gam, (size_t)B * N * nx);
+    BUF(double, lam, (size_t)B * N * nx);
     BUF(double, Pdiag, (size_t)B * N * nx * nx);
+    w.Sd = Sdiag;
+    w.Sl = Slo;
+    w.gam = gam;
+    w.lam = lam;
     w.Pd = Pdiag;
   }
   return 0;
@@ -648,7 +643,7 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
                                                    st.need_grad, st.exit_sqp});
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), io_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
-  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, precond != PRECOND_J))) return rc;
+  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, true))) return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
   resolve_timings(ctx);
   if (dxul) {
@@ -708,7 +703,7 @@ int tmpc_pcg_batch(tmpc_ctx* ctx, int B, int N, int nx, int precond, const doubl
   {
     Timed t(ctx, "pcg");
     LAUNCH_OK(launch_pcg(ctx->stream, nx, B, N, precond, p_Sd, p_Sl, S_up ? p_Su : nullptr, p_g,
-                         guess ? p_x0 : nullptr, nullptr, tol,
+                         guess ? p_x0 : nullptr, tol,
                          max_iter, p_lam, p_it, trace_nu ? p_tn : nullptr, trace_res ? p_tr : nullptr,
                          P_diag ? p_Pd : nullptr));
   }

@@ -154,43 +154,68 @@ __device__ __forceinline__ constexpr int sidx(int r, int c) {
   return r <= c ? r * 6 - (r * (r - 1)) / 2 + (c - r) : c * 6 - (c * (c - 1)) / 2 + (r - c);
 }
 
-// out = X^T A X for symmetric A (21 entries), X formed column-wise on the fly
+// out = X^T A X for symmetric A (21 entries).  Column-at-a-time so that only
+// two 6-vectors of X and one of A X are live (X columns are recomputed).
+__device__ __forceinline__ void Xcol(const ModelDev* __restrict__ M, int j, double c, double s, int k, double x[6]) {
+#pragma unroll
+  for (int r = 0; r < 6; ++r) x[r] = M->X0[j][r * 6 + k] + c * M->Xa[j][r * 6 + k] + s * M->Xb[j][r * 6 + k];
+}
+
 __device__ __forceinline__ void XtAX(const ModelDev* __restrict__ M, int j, double c, double s, const double A[21],
                                      double out[21]) {
   opaque(c, s);
-  double Y[6][6];  // Y[:, k] = A X[:, k]
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
-    double xk[6];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) xk[r] = M->X0[j][r * 6 + k] + c * M->Xa[j][r * 6 + k] + s * M->Xb[j][r * 6 + k];
+    double xk[6], z[6];
+    Xcol(M, j, c, s, k, xk);
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       double acc = 0.0;
 #pragma unroll
       for (int m = 0; m < 6; ++m) acc += A[sidx(r, m)] * xk[m];
-      Y[r][k] = acc;
+      z[r] = acc;
     }
-  }
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    double xr[6];
+    for (int r = 0; r <= k; ++r) {
+      double xr[6];
+      if (r == k) {
 #pragma unroll
-    for (int m = 0; m < 6; ++m) xr[m] = M->X0[j][m * 6 + r] + c * M->Xa[j][m * 6 + r] + s * M->Xb[j][m * 6 + r];
-#pragma unroll
-    for (int k = r; k < 6; ++k) {
+        for (int m = 0; m < 6; ++m) xr[m] = xk[m];
+      } else {
+        Xcol(M, j, c, s, r, xr);
+      }
       double acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < 6; ++m) acc += xr[m] * Y[m][k];
+      for (int m = 0; m < 6; ++m) acc += xr[m] * z[m];
       out[sidx(r, k)] = acc;
     }
+  }
+}
+
+// y1 = X v1, y2 = X v2 sharing the formation of each X row
+__device__ __forceinline__ void mvX2(const ModelDev* __restrict__ M, int j, double c, double s, const double v1[6],
+                                     const double v2[6], double y1[6], double y2[6]) {
+  opaque(c, s);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double a1 = 0.0, a2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const double x = M->X0[j][r * 6 + k] + c * M->Xa[j][r * 6 + k] + s * M->Xb[j][r * 6 + k];
+      a1 += x * v1[k];
+      a2 += x * v2[k];
+    }
+    y1[r] = a1;
+    y2[r] = a2;
   }
 }
 
 // ----------------------------------------------------------------- forward dynamics (ABA)
 // qdd = M(q)^-1 (tau - c(q, qd)), gravity as the fictitious base acceleration
 // a_base[5] = -gravity (RBDReference.py:456).  With UNIT = true it returns
-// M^-1 tau (qd = 0, no gravity): used for unit-torque columns.
+// M^-1 tau (qd = 0, no gravity).  Velocities are recomputed in pass 3
+// instead of being kept from pass 1, so at most ~8 doubles per joint are
+// stored across passes.
 template <int NJ, bool CHAIN, bool UNIT = false>
 __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const double cq[NJ], const double sq[NJ],
                                        const double qd[NJ], const double tau[NJ], double qdd[NJ]) {
@@ -228,11 +253,11 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
 #pragma unroll
       for (int k = r; k < 6; ++k) IA[sidx(r, k)] = M->I[j][r * 6 + k] + chIA[j][sidx(r, k)];
     double pA[6], cj[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) pA[i] = chpA[j][i];
     if (!UNIT) {
       double Iv[6];
       mvI(M->I[j], v[j], Iv);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) pA[i] = chpA[j][i];
       add_fxv(v[j], Iv, pA);
       double cc[6];
       crmS(v[j], M->S[j], cc);
@@ -240,7 +265,7 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
       for (int i = 0; i < 6; ++i) cj[i] = qd[j] * cc[i];
     } else {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) { pA[i] = chpA[j][i]; cj[i] = 0.0; }
+      for (int i = 0; i < 6; ++i) cj[i] = 0.0;
     }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
@@ -254,40 +279,51 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
     const int p = parent_of<CHAIN>(M, j);
     if (p >= 0) {
       const double dinv = 1.0 / Dd[j];
-      double Ia[21];
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int k = r; k < 6; ++k) Ia[sidx(r, k)] = IA[sidx(r, k)] - U[j][r] * (dinv * U[j][k]);
+        for (int k = r; k < 6; ++k) IA[sidx(r, k)] -= U[j][r] * (dinv * U[j][k]);   // Ia
       double pa[6];
       const double ud = uu[j] * dinv;
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
         double acc = pA[r] + U[j][r] * ud;
+        if (!UNIT) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) acc += Ia[sidx(r, k)] * cj[k];
+          for (int k = 0; k < 6; ++k) acc += IA[sidx(r, k)] * cj[k];
+        }
         pa[r] = acc;
       }
       double t[21];
-      XtAX(M, j, cq[j], sq[j], Ia, t);
+      XtAX(M, j, cq[j], sq[j], IA, t);
 #pragma unroll
       for (int e = 0; e < 21; ++e) chIA[p][e] += t[e];
       add_mtvX(M, j, cq[j], sq[j], pa, chpA[p]);
     }
   }
-  // pass 3: accelerations, root to leaf
-  double a[NJ][6];
+  // pass 3: accelerations, root to leaf (velocities recomputed)
+  double v3[NJ][6], a[NJ][6];
   const double g[6] = {0.0, 0.0, 0.0, 0.0, 0.0, UNIT ? 0.0 : -M->gravity};
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int p = parent_of<CHAIN>(M, j);
-    if (p < 0)
-      mvX(M, j, cq[j], sq[j], g, a[j]);
-    else
-      mvX(M, j, cq[j], sq[j], a[p], a[j]);
-    if (!UNIT) {
+    if (UNIT) {
+      if (p < 0)
+        mvX(M, j, cq[j], sq[j], g, a[j]);
+      else
+        mvX(M, j, cq[j], sq[j], a[p], a[j]);
+    } else {
+      if (p < 0) {
+        mvX(M, j, cq[j], sq[j], g, a[j]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) v3[j][i] = 0.0;
+      } else {
+        mvX2(M, j, cq[j], sq[j], v3[p], a[p], v3[j], a[j]);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) v3[j][i] += M->S[j][i] * qd[j];
       double cc[6];
-      crmS(v[j], M->S[j], cc);
+      crmS(v3[j], M->S[j], cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) a[j][i] += qd[j] * cc[i];
     }

@@ -1,0 +1,277 @@
+// Per-knot forward-dynamics kernels (one lane per knot): the QP-build
+// defects, the line-search merit terms, the unit-test entry point and the
+// workload rollout.  Compiled in their own translation unit with the
+// register-minimising scheduler (see Makefile): the fully unrolled
+// articulated-body recursion for n = 6 otherwise spills to scratch.
+#include "tmpc_internal.h"
+
+namespace tmpc {
+
+__device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
+  return (k == N - 1) || (C->QF_start >= 0 && k >= C->QF_start);
+}
+
+// ======================================================================= per-knot forward dynamics
+// Solver mode: lane = (b, k), k < N-1.  Writes qdd (the point the gradient is
+// evaluated at, TrajoptPlant.py:313) and the dynamics defect
+// c_{k+1} = x_{k+1} - f(x_k, u_k) (formKKTSystemBlocks :227-231); lane k = 0
+// also writes c_0 = x_0 - xs (:213-214).
+template <int NJ, bool CHAIN>
+__global__ void __launch_bounds__(256) k_qp_fd(const ModelDev* __restrict__ M, int B, int N, double dt,
+                                               const double* __restrict__ x, const double* __restrict__ u,
+                                               const double* __restrict__ xs, const int* __restrict__ need,
+                                               double* __restrict__ qdd_out, double* __restrict__ cvec) {
+  constexpr int NX = 2 * NJ;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = N - 1;
+  if (gid >= B * K) return;
+  const int b = gid / K, k = gid - b * K;
+  if (!need[b]) return;
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NJ * K;
+  double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    q[j] = xb[j * N + k];
+    qd[j] = xb[(NJ + j) * N + k];
+    uu[j] = ub[j * K + k];
+    joint_cs(M, j, q[j], cq[j], sq[j]);
+  }
+  fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
+  const size_t kk = (size_t)b * K + k;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) qdd_out[kk * NJ + j] = qdd[j];
+  double* cb = cvec + (size_t)b * N * NX;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    // x_{k+1} = x_k + dt * [qd; qdd]  (TrajoptPlant.py:95-97), rounded as NumPy does
+    const double xq = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
+    const double xv = __dadd_rn(qd[j], __dmul_rn(dt, qdd[j]));
+    cb[(k + 1) * NX + j] = xb[j * N + k + 1] - xq;
+    cb[(k + 1) * NX + NJ + j] = xb[(NJ + j) * N + k + 1] - xv;
+  }
+  if (k == 0) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) cb[i] = xb[i * N] - xs[(size_t)b * NX + i];
+  }
+}
+
+// ======================================================================= line-search merit terms
+// lane = (b, t, k): for trial step alpha_t evaluate the per-knot pieces of
+// totalCost (:296-310), totalHardConstraintViolation (:273-294) and the
+// directional derivative D (:635-648, gradient taken at x_new as the
+// reference does).  Knot lane N-1 carries the terminal cost / D term and the
+// |x_0 - xs| violation term.
+template <int NJ, bool CHAIN>
+__global__ void __launch_bounds__(256) k_ls_terms(const ModelDev* __restrict__ M, const CostDev* __restrict__ C,
+                                                  int B, int N, int T, double dt, const double* __restrict__ alphas,
+                                                  const double* __restrict__ x, const double* __restrict__ u,
+                                                  const double* __restrict__ xs, const double* __restrict__ dx,
+                                                  const double* __restrict__ du, const int* __restrict__ active,
+                                                  double* __restrict__ terms) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * T * N) return;
+  const int k = gid % N;
+  const int bt = gid / N;
+  const int b = bt / T, t = bt - b * T;
+  if (!active[b]) return;
+  const int K = N - 1;
+  const double al = alphas[t];
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NU * K;
+  const double* dxb = dx ? dx + (size_t)b * N * NX : nullptr;
+  const double* dub = du ? du + (size_t)b * K * NU : nullptr;
+  double xk[NX], dxk[NX];
+#pragma unroll
+  for (int m = 0; m < NX; ++m) {
+    dxk[m] = dxb ? dxb[k * NX + m] : 0.0;
+    // x_new = x - alpha dx  (:619-622; alpha is a power of two: exact)
+    xk[m] = dxb ? xb[m * N + k] - al * dxk[m] : xb[m * N + k];
+  }
+  const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
+  double d[NX];
+#pragma unroll
+  for (int m = 0; m < NX; ++m) d[m] = xk[m] - C->xg[m];
+  // value: 0.5 dx^T (Q dx) [+ 0.5 u^T (R u)]; gradient: [dx^T Q, u^T R]
+  double vq = 0.0, Dk = 0.0;
+#pragma unroll
+  for (int r = 0; r < NX; ++r) {
+    double qd = 0.0, gq = 0.0;
+#pragma unroll
+    for (int c = 0; c < NX; ++c) {
+      qd += Qk[r * NX + c] * d[c];
+      gq += d[c] * Qk[c * NX + r];
+    }
+    vq += d[r] * qd;
+    Dk += gq * dxk[r];
+  }
+  double cost = 0.5 * vq;
+  double viol = 0.0;
+  double* out = terms + ((size_t)bt * N + k) * 3;
+  if (k < K) {
+    double uk[NU], duk[NU];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) {
+      duk[m] = dub ? dub[k * NU + m] : 0.0;
+      uk[m] = dub ? ub[m * K + k] - al * duk[m] : ub[m * K + k];
+    }
+    double vr = 0.0;
+#pragma unroll
+    for (int r = 0; r < NU; ++r) {
+      double ru = 0.0, gr = 0.0;
+#pragma unroll
+      for (int c = 0; c < NU; ++c) {
+        ru += C->R[r * NU + c] * uk[c];
+        gr += uk[c] * C->R[c * NU + r];
+      }
+      vr += uk[r] * ru;
+      Dk += gr * duk[r];
+    }
+    cost += 0.5 * vr;
+    // dynamics defect at the trial point
+    double cq[NJ], sq[NJ], qd[NJ], qdd[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      qd[j] = xk[NJ + j];
+      joint_cs(M, j, xk[j], cq[j], sq[j]);
+    }
+    fd_aba<NJ, CHAIN>(M, cq, sq, qd, uk, qdd);
+#pragma unroll
+    for (int m = 0; m < NX; ++m) {
+      const double dxn = dxb ? dxb[(k + 1) * NX + m] : 0.0;
+      const double xn = dxb ? xb[m * N + k + 1] - al * dxn : xb[m * N + k + 1];
+      const double xdot = m < NJ ? qd[m] : qdd[m - NJ];
+      const double f = __dadd_rn(xk[m], __dmul_rn(dt, xdot));
+      viol += fabs(xn - f);
+    }
+  } else {
+    // |x_0 - xs|_1 for the initial-state constraint
+#pragma unroll
+    for (int m = 0; m < NX; ++m) {
+      const double x0 = dxb ? xb[m * N] - al * dxb[m] : xb[m * N];
+      viol += fabs(x0 - xs[(size_t)b * NX + m]);
+    }
+  }
+  out[0] = cost;
+  out[1] = viol;
+  out[2] = Dk;
+}
+
+// ======================================================================= kernel-level entry points
+template <int NJ, bool CHAIN>
+__global__ void __launch_bounds__(256) k_unit_fd(const ModelDev* __restrict__ M, int K, double dt,
+                                                 const double* __restrict__ x, const double* __restrict__ u,
+                                                 double* __restrict__ xnext, double* __restrict__ qdd_out) {
+  constexpr int NX = 2 * NJ;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    q[j] = x[(size_t)k * NX + j];
+    qd[j] = x[(size_t)k * NX + NJ + j];
+    uu[j] = u[(size_t)k * NJ + j];
+    joint_cs(M, j, q[j], cq[j], sq[j]);
+  }
+  fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    qdd_out[(size_t)k * NJ + j] = qdd[j];
+    if (xnext) {
+      xnext[(size_t)k * NX + j] = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
+      xnext[(size_t)k * NX + NJ + j] = __dadd_rn(qd[j], __dmul_rn(dt, qdd[j]));
+    }
+  }
+}
+
+// sequential Euler rollout, one lane per problem (workload setup: §8d)
+template <int NJ, bool CHAIN>
+__global__ void __launch_bounds__(64) k_rollout(const ModelDev* __restrict__ M, int B, int N, double dt,
+                                                double* __restrict__ x, const double* __restrict__ u) {
+  constexpr int NX = 2 * NJ;
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int K = N - 1;
+  double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NJ * K;
+  double q[NJ], qd[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) { q[j] = xb[j * N]; qd[j] = xb[(NJ + j) * N]; }
+  for (int k = 0; k < K; ++k) {
+    double uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      uu[j] = ub[j * K + k];
+      joint_cs(M, j, q[j], cq[j], sq[j]);
+    }
+    fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const double nq = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
+      const double nv = __dadd_rn(qd[j], __dmul_rn(dt, qdd[j]));
+      q[j] = nq;
+      qd[j] = nv;
+      xb[j * N + k + 1] = nq;
+      xb[(NJ + j) * N + k + 1] = nv;
+    }
+  }
+}
+
+#define TMPC_GRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
+
+template <int NJ, bool CHAIN>
+struct LaunchFD {
+  static void qp_fd(hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const double* u,
+                    const double* xs, const int* need, double* qdd, double* cvec) {
+    hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN>), TMPC_GRID(B * (N - 1), 256), 0, s, M, B, N, dt, x, u, xs, need, qdd,
+                       cvec);
+  }
+  static void ls_terms(hipStream_t s, const ModelDev* M, const CostDev* C, int B, int N, int T, double dt,
+                       const double* alphas, const double* x, const double* u, const double* xs, const double* dx,
+                       const double* du, const int* active, double* terms) {
+    hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN>), TMPC_GRID(B * T * N, 256), 0, s, M, C, B, N, T, dt, alphas, x, u,
+                       xs, dx, du, active, terms);
+  }
+  static void unit_fd(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
+                      double* xnext, double* qdd) {
+    hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN>), TMPC_GRID(K, 256), 0, s, M, K, dt, x, u, xnext, qdd);
+  }
+  static void rollout(hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u) {
+    hipLaunchKernelGGL((k_rollout<NJ, CHAIN>), TMPC_GRID(B, 64), 0, s, M, B, N, dt, x, u);
+  }
+};
+
+// dispatch tables over the joint count and the chain specialisation
+#define TMPC_DISPATCH_NJ(nj, chain, CALL)                                          \
+  switch (nj) {                                                                    \
+    case 1: if (chain) LaunchFD<1, true>::CALL; else LaunchFD<1, false>::CALL; break;  \
+    case 2: if (chain) LaunchFD<2, true>::CALL; else LaunchFD<2, false>::CALL; break;  \
+    case 3: if (chain) LaunchFD<3, true>::CALL; else LaunchFD<3, false>::CALL; break;  \
+    case 4: if (chain) LaunchFD<4, true>::CALL; else LaunchFD<4, false>::CALL; break;  \
+    case 5: if (chain) LaunchFD<5, true>::CALL; else LaunchFD<5, false>::CALL; break;  \
+    case 6: if (chain) LaunchFD<6, true>::CALL; else LaunchFD<6, false>::CALL; break;  \
+    case 7: if (chain) LaunchFD<7, true>::CALL; else LaunchFD<7, false>::CALL; break;  \
+    default: return -2;                                                            \
+  }                                                                                \
+  return 0;
+
+int launch_qp_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, const double* x,
+                 const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
+  TMPC_DISPATCH_NJ(nj, chain, qp_fd(s, M, B, N, dt, x, u, xs, need, qdd, cvec))
+}
+int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, int B, int N, int T,
+                    double dt, const double* alphas, const double* x, const double* u, const double* xs,
+                    const double* dx, const double* du, const int* active, double* terms) {
+  TMPC_DISPATCH_NJ(nj, chain, ls_terms(s, M, C, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
+}
+int launch_unit_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
+                   const double* u, double* xnext, double* qdd) {
+  TMPC_DISPATCH_NJ(nj, chain, unit_fd(s, M, K, dt, x, u, xnext, qdd))
+}
+int launch_rollout(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, double* x,
+                   const double* u) {
+  TMPC_DISPATCH_NJ(nj, chain, rollout(s, M, B, N, dt, x, u))
+}
+
+}  // namespace tmpc

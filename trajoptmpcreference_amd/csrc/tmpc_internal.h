@@ -73,14 +73,12 @@ int launch_unit_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int K
 int launch_rollout(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, double* x,
                    const double* u);
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G);
-int launch_schur(hipStream_t s, int nj, const CostDev* C, int B, int N, const double* x, const double* u,
-                 const int* active, const double* G, const double* A, const double* Bm, const double* cvec,
-                 double* Sd, double* Sl, double* gam);
-int launch_dxu(hipStream_t s, int nj, const CostDev* C, int B, int N, const double* x, const double* u,
-               const int* active, const double* G, const double* A, const double* Bm, const double* lam, double* dx,
-               double* du);
+int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, const double* x, const double* u,
+              const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
+              int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
+              double* Pd);
 int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
-               const double* Su, const double* gam, const double* guess, const int* active, double tol, int max_iter, double* lam,
+               const double* Su, const double* gam, const double* guess, double tol, int max_iter, double* lam,
                int* iters, double* tnu, double* tres, double* Pd);
 int pcg_set_max_lds();
 void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, const double* alphas,

@@ -21,51 +21,6 @@
 
 namespace tmpc {
 
-// ======================================================================= per-knot forward dynamics
-// Solver mode: lane = (b, k), k < N-1.  Writes qdd (the point the gradient is
-// evaluated at, TrajoptPlant.py:313) and the dynamics defect
-// c_{k+1} = x_{k+1} - f(x_k, u_k) (formKKTSystemBlocks :227-231); lane k = 0
-// also writes c_0 = x_0 - xs (:213-214).
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_qp_fd(const ModelDev* __restrict__ M, int B, int N, double dt,
-                                               const double* __restrict__ x, const double* __restrict__ u,
-                                               const double* __restrict__ xs, const int* __restrict__ need,
-                                               double* __restrict__ qdd_out, double* __restrict__ cvec) {
-  constexpr int NX = 2 * NJ;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int K = N - 1;
-  if (gid >= B * K) return;
-  const int b = gid / K, k = gid - b * K;
-  if (!need[b]) return;
-  const double* xb = x + (size_t)b * NX * N;
-  const double* ub = u + (size_t)b * NJ * K;
-  double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    q[j] = xb[j * N + k];
-    qd[j] = xb[(NJ + j) * N + k];
-    uu[j] = ub[j * K + k];
-    joint_cs(M, j, q[j], cq[j], sq[j]);
-  }
-  fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
-  const size_t kk = (size_t)b * K + k;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) qdd_out[kk * NJ + j] = qdd[j];
-  double* cb = cvec + (size_t)b * N * NX;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    // x_{k+1} = x_k + dt * [qd; qdd]  (TrajoptPlant.py:95-97), rounded as NumPy does
-    const double xq = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
-    const double xv = __dadd_rn(qd[j], __dmul_rn(dt, qdd[j]));
-    cb[(k + 1) * NX + j] = xb[j * N + k + 1] - xq;
-    cb[(k + 1) * NX + NJ + j] = xb[(NJ + j) * N + k + 1] - xv;
-  }
-  if (k == 0) {
-#pragma unroll
-    for (int i = 0; i < NX; ++i) cb[i] = xb[i * N] - xs[(size_t)b * NX + i];
-  }
-}
-
 // ======================================================================= analytic M^-1 columns
 // lane = (knot, col), col < NJ; writes the full symmetric matrix (column col
 // above the diagonal and row col left of it, :908-930).  x is [K][NX] rows
@@ -222,107 +177,6 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
   return (k == N - 1) || (C->QF_start >= 0 && k >= C->QF_start);
 }
 
-// ======================================================================= Schur blocks
-// lane = (b, k, i): row i of S_kk, of S_{k,k-1} and gamma_k[i]
-template <int NJ>
-__global__ void __launch_bounds__(256) k_schur(const CostDev* __restrict__ C, int B, int N,
-                                               const double* __restrict__ x, const double* __restrict__ u,
-                                               const int* __restrict__ active, const double* __restrict__ Ginv,
-                                               const double* __restrict__ Aall, const double* __restrict__ Ball,
-                                               const double* __restrict__ cvec, double* __restrict__ Sd,
-                                               double* __restrict__ Sl, double* __restrict__ gam) {
-  constexpr int NX = 2 * NJ, NU = NJ;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * N * NX) return;
-  const int i = gid % NX;
-  const int bk = gid / NX;
-  const int b = bk / N, k = bk - b * N;
-  if (!active[b]) return;
-  const int K = N - 1;
-  const double* xb = x + (size_t)b * NX * N;
-  const double* ub = u + (size_t)b * NU * K;
-  const double* G3 = Ginv + (size_t)b * 3 * NX * NX;
-  const double* GxK = G3 + (use_QF(C, k, N) ? NX * NX : 0);
-  const double* QK = use_QF(C, k, N) ? C->QF : C->Q;
-  // gx_k = (x_k - xg)^T Q_k  (QuadraticCost.gradient, TrajoptCost.py:58-69)
-  double dxk[NX], gxk[NX];
-#pragma unroll
-  for (int m = 0; m < NX; ++m) dxk[m] = xb[m * N + k] - C->xg[m];
-#pragma unroll
-  for (int j = 0; j < NX; ++j) {
-    double acc = 0.0;
-#pragma unroll
-    for (int m = 0; m < NX; ++m) acc += dxk[m] * QK[m * NX + j];
-    gxk[j] = acc;
-  }
-  double Gxg = 0.0;
-#pragma unroll
-  for (int j = 0; j < NX; ++j) Gxg += GxK[i * NX + j] * gxk[j];
-  const double cki = cvec[(size_t)b * N * NX + k * NX + i];
-  double* sdr = Sd + ((size_t)bk * NX + i) * NX;
-  if (k == 0) {
-#pragma unroll
-    for (int j = 0; j < NX; ++j) sdr[j] = -GxK[i * NX + j];
-    gam[(size_t)bk * NX + i] = cki - Gxg;
-    return;
-  }
-  const int km = k - 1;
-  const double* A = Aall + ((size_t)b * K + km) * NX * NX;
-  const double* Bm = Ball + ((size_t)b * K + km) * NX * NU;
-  const double* Gxm = G3 + (use_QF(C, km, N) ? NX * NX : 0);
-  const double* Gu = G3 + 2 * NX * NX;
-  const double* Qm = use_QF(C, km, N) ? C->QF : C->Q;
-  double AG[NX], BG[NU];
-#pragma unroll
-  for (int j = 0; j < NX; ++j) {
-    double acc = 0.0;
-#pragma unroll
-    for (int m = 0; m < NX; ++m) acc += A[i * NX + m] * Gxm[m * NX + j];
-    AG[j] = acc;
-  }
-#pragma unroll
-  for (int j = 0; j < NU; ++j) {
-    double acc = 0.0;
-#pragma unroll
-    for (int m = 0; m < NU; ++m) acc += Bm[i * NU + m] * Gu[m * NU + j];
-    BG[j] = acc;
-  }
-  double* slr = Sl + (((size_t)b * K + km) * NX + i) * NX;
-#pragma unroll
-  for (int j = 0; j < NX; ++j) slr[j] = AG[j];
-#pragma unroll 1
-  for (int j = 0; j < NX; ++j) {
-    double acc = 0.0;
-#pragma unroll
-    for (int m = 0; m < NX; ++m) acc += AG[m] * A[j * NX + m];
-#pragma unroll
-    for (int m = 0; m < NU; ++m) acc += BG[m] * Bm[j * NU + m];
-    sdr[j] = -(acc + GxK[i * NX + j]);
-  }
-  // gamma_k = c_k + AB_{k-1} Ghat_{k-1} g_{k-1} - E Ghat_k g_k
-  double dxm[NX], um[NU];
-#pragma unroll
-  for (int m = 0; m < NX; ++m) dxm[m] = xb[m * N + km] - C->xg[m];
-#pragma unroll
-  for (int m = 0; m < NU; ++m) um[m] = ub[m * K + km];
-  double s = 0.0;
-#pragma unroll
-  for (int j = 0; j < NX; ++j) {
-    double g = 0.0;
-#pragma unroll
-    for (int m = 0; m < NX; ++m) g += dxm[m] * Qm[m * NX + j];
-    s += AG[j] * g;
-  }
-#pragma unroll
-  for (int j = 0; j < NU; ++j) {
-    double g = 0.0;
-#pragma unroll
-    for (int m = 0; m < NU; ++m) g += um[m] * C->R[m * NU + j];
-    s += BG[j] * g;
-  }
-  gam[(size_t)bk * NX + i] = cki + s - Gxg;
-}
-
 // ======================================================================= block-tridiagonal PCG
 // One workgroup per problem, one lane per row of S (PCG.pcg, PCG.py:66-111).
 __device__ __forceinline__ double wave_sum(double v) {
@@ -331,7 +185,8 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// every thread returns the same value; `red` must alternate between calls
+// every thread returns the same value (fixed summation order: deterministic);
+// `red` must alternate between consecutive calls
 __device__ __forceinline__ double block_sum(double v, double* red, int nwaves) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -342,126 +197,111 @@ __device__ __forceinline__ double block_sum(double v, double* red, int nwaves) {
   return s;
 }
 
-template <int NX, int MAXT>
-__global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const double* __restrict__ Sd,
-                                              const double* __restrict__ Sl, const double* __restrict__ Su,
-                                              const double* __restrict__ gam, const double* __restrict__ guess,
-                                              const int* __restrict__ active, double tol, int max_iter,
-                                              double* __restrict__ lam,
-                                              int* __restrict__ iters, double* __restrict__ trace_nu,
-                                              double* __restrict__ trace_res, double* __restrict__ Pd_out) {
-  const int b = blockIdx.x;
-  if (active && !active[b]) return;
-  extern __shared__ __align__(16) double lds[];
+// the rows of S (and of P_kk^-1) a lane keeps in registers for the whole solve
+template <int NX>
+struct PcgRows {
+  double sd[NX];   // S_kk row i
+  double sl[NX];   // S_{k,k-1} row i
+  double su[NX];   // S_{k,k+1} row i
+  double pr[NX];   // (S_kk)^-1 row i  (J: pr[0] = 1 / S_ii)
+};
+
+struct PcgLds {
+  double *pbuf, *rbuf, *wbuf, *tbuf, *xbuf, *red, *piv;
+};
+
+__host__ __device__ inline size_t pcg_lds_doubles(int N, int NX) { return (size_t)5 * N * NX + 32 + 4 * N * NX; }
+
+__device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
   const int rows = N * NX;
-  const int nwaves = (blockDim.x + 63) >> 6;
-  double* pbuf = lds;
-  double* rbuf = pbuf + rows;
-  double* wbuf = rbuf + rows;
-  double* tbuf = wbuf + rows;
-  double* xbuf = tbuf + rows;
-  double* red = xbuf + rows;          // 2 x 16
-  double* piv = red + 32;             // 2 x N x 2NX
-  const int t = threadIdx.x;
-  const bool valid = t < rows;
-  const int k = valid ? t / NX : 0;
-  const int i = valid ? t - k * NX : 0;
-  const int K = N - 1;
+  PcgLds L;
+  L.pbuf = lds;
+  L.rbuf = L.pbuf + rows;
+  L.wbuf = L.rbuf + rows;
+  L.tbuf = L.wbuf + rows;
+  L.xbuf = L.tbuf + rows;
+  L.red = L.xbuf + rows;   // 2 x 16
+  L.piv = L.red + 32;      // 2 x N x 2NX
+  return L;
+}
 
-  double sd[NX], sl[NX], su[NX], pr[NX];
-#pragma unroll
-  for (int j = 0; j < NX; ++j) { sd[j] = 0.0; sl[j] = 0.0; su[j] = 0.0; pr[j] = 0.0; }
-  if (valid) {
-    const double* d = Sd + (((size_t)b * N + k) * NX + i) * NX;
-#pragma unroll
-    for (int j = 0; j < NX; ++j) sd[j] = d[j];
-    if (k > 0) {
-      const double* l = Sl + (((size_t)b * K + (k - 1)) * NX + i) * NX;
-#pragma unroll
-      for (int j = 0; j < NX; ++j) sl[j] = l[j];
-    }
-    if (k < K) {
-      if (Su) {
-        const double* up = Su + (((size_t)b * K + k) * NX + i) * NX;
-#pragma unroll
-        for (int j = 0; j < NX; ++j) su[j] = up[j];
-      } else {
-        const double* l = Sl + ((size_t)b * K + k) * NX * NX;
-#pragma unroll
-        for (int j = 0; j < NX; ++j) su[j] = l[j * NX + i];
-      }
-    }
-  }
-
-  // ---- preconditioner (compute_preconditioner, PCG.py:166-212)
+// compute_preconditioner (PCG.py:166-212): J -> 1/S_ii; BJ and SS -> the
+// diagonal block inverses, Gauss-Jordan with one row per lane and the pivot
+// rows broadcast through LDS (S_kk is negative definite: no pivoting needed).
+template <int NX>
+__device__ __forceinline__ void pcg_precondition(PcgRows<NX>& R, int precond, bool valid, int k, int i, int N,
+                                                 double* piv, double* Pd_row) {
   if (precond == PRECOND_J) {
-    // inv(diag(diag(S)))  (PCG.py:168-169)
     double dii = 1.0;
 #pragma unroll
     for (int j = 0; j < NX; ++j)
-      if (j == i) dii = sd[j];
-    if (valid) pr[0] = 1.0 / dii;
-  } else {
-    // Gauss-Jordan of the diagonal block, one row per lane, pivot rows via LDS
-    double aug[2 * NX];
+      if (j == i) dii = R.sd[j];
+    if (valid) R.pr[0] = 1.0 / dii;
+    return;
+  }
+  double aug[2 * NX];
 #pragma unroll
-    for (int j = 0; j < NX; ++j) { aug[j] = sd[j]; aug[NX + j] = (j == i) ? 1.0 : 0.0; }
+  for (int j = 0; j < NX; ++j) { aug[j] = R.sd[j]; aug[NX + j] = (j == i) ? 1.0 : 0.0; }
 #pragma unroll
-    for (int p = 0; p < NX; ++p) {
-      double* pv = piv + ((p & 1) * N + k) * 2 * NX;
-      if (valid && i == p) {
-        const double d = aug[p];
+  for (int p = 0; p < NX; ++p) {
+    double* pv = piv + ((p & 1) * N + k) * 2 * NX;
+    if (valid && i == p) {
+      const double d = aug[p];
 #pragma unroll
-        for (int j = 0; j < 2 * NX; ++j) { aug[j] = aug[j] / d; pv[j] = aug[j]; }
-      }
-      __syncthreads();
-      if (valid && i != p) {
-        const double f = aug[p];
-#pragma unroll
-        for (int j = 0; j < 2 * NX; ++j) aug[j] -= f * pv[j];
-      }
+      for (int j = 0; j < 2 * NX; ++j) { aug[j] = aug[j] / d; pv[j] = aug[j]; }
     }
+    __syncthreads();
+    if (valid && i != p) {
+      const double f = aug[p];
 #pragma unroll
-    for (int j = 0; j < NX; ++j) pr[j] = aug[NX + j];
-    if (Pd_out && valid) {
-      double* o = Pd_out + (((size_t)b * N + k) * NX + i) * NX;
-#pragma unroll
-      for (int j = 0; j < NX; ++j) o[j] = pr[j];
+      for (int j = 0; j < 2 * NX; ++j) aug[j] -= f * pv[j];
     }
   }
+#pragma unroll
+  for (int j = 0; j < NX; ++j) R.pr[j] = aug[NX + j];
+  if (Pd_row && valid) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) Pd_row[j] = R.pr[j];
+  }
+}
 
-  // z = P r  (J: diagonal, BJ: block diagonal, SS: P_D (r - S_off P_D r))
+// The CG iteration.  Returns this lane's entry of the solution.
+template <int NX>
+__device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, int precond, bool valid, int t, int k, int N,
+                                          const PcgLds& L, double bi, bool has_guess, double guess_i, double tol,
+                                          int max_iter, int nwaves, double* tn, double* tr, int* iters_out) {
+  const int K = N - 1;
+  const int kb = k * NX;
   auto apply_P = [&](double r_i) -> double {
-    if (precond == PRECOND_J) return pr[0] * r_i;
-    if (valid) rbuf[t] = r_i;
+    if (precond == PRECOND_J) return R.pr[0] * r_i;
+    if (valid) L.rbuf[t] = r_i;
     __syncthreads();
     double w = 0.0;
     if (valid) {
 #pragma unroll
-      for (int j = 0; j < NX; ++j) w += pr[j] * rbuf[k * NX + j];
+      for (int j = 0; j < NX; ++j) w += R.pr[j] * L.rbuf[kb + j];
     }
     if (precond == PRECOND_BJ) return w;
-    if (valid) wbuf[t] = w;
+    // SS: z = P_D (r - S_off P_D r)  ==  the symmetric-stair P^-1 r
+    if (valid) L.wbuf[t] = w;
     __syncthreads();
-    double tv = 0.0;
     if (valid) {
       double acc = 0.0;
       if (k > 0) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) acc += sl[j] * wbuf[(k - 1) * NX + j];
+        for (int j = 0; j < NX; ++j) acc += R.sl[j] * L.wbuf[kb - NX + j];
       }
       if (k < K) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) acc += su[j] * wbuf[(k + 1) * NX + j];
+        for (int j = 0; j < NX; ++j) acc += R.su[j] * L.wbuf[kb + NX + j];
       }
-      tv = r_i - acc;
-      tbuf[t] = tv;
+      L.tbuf[t] = r_i - acc;
     }
     __syncthreads();
     double z = 0.0;
     if (valid) {
 #pragma unroll
-      for (int j = 0; j < NX; ++j) z += pr[j] * tbuf[k * NX + j];
+      for (int j = 0; j < NX; ++j) z += R.pr[j] * L.tbuf[kb + j];
     }
     return z;
   };
@@ -470,41 +310,37 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
     if (valid) {
       if (k > 0) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) acc += sl[j] * vbuf[(k - 1) * NX + j];
+        for (int j = 0; j < NX; ++j) acc += R.sl[j] * vbuf[kb - NX + j];
       }
 #pragma unroll
-      for (int j = 0; j < NX; ++j) acc += sd[j] * vbuf[k * NX + j];
+      for (int j = 0; j < NX; ++j) acc += R.sd[j] * vbuf[kb + j];
       if (k < K) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) acc += su[j] * vbuf[(k + 1) * NX + j];
+        for (int j = 0; j < NX; ++j) acc += R.su[j] * vbuf[kb + NX + j];
       }
     }
     return acc;
   };
-
-  const double bi = valid ? gam[(size_t)b * rows + t] : 0.0;
+  int rsel = 0;
   // x0 = guess (default zeros, PCG.py:11-12); r = b - A x0 (:76)
   double xi = 0.0, ri = bi;
-  if (guess) {
-    xi = valid ? guess[(size_t)b * rows + t] : 0.0;
-    if (valid) xbuf[t] = xi;
+  if (has_guess) {
+    xi = valid ? guess_i : 0.0;
+    if (valid) L.xbuf[t] = xi;
     __syncthreads();
-    ri = bi - spmv(xbuf);
+    ri = bi - spmv(L.xbuf);
     __syncthreads();
   }
   double zi = apply_P(ri);
   double pi = zi;
-  int rsel = 0;
-  double nu = block_sum(valid ? ri * zi : 0.0, red + 16 * rsel, nwaves);
+  double nu = block_sum(valid ? ri * zi : 0.0, L.red + 16 * rsel, nwaves);
   rsel ^= 1;
-  double* tn = trace_nu ? trace_nu + (size_t)b * (max_iter + 1) : nullptr;
-  double* tr = trace_res ? trace_res + (size_t)b * (max_iter + 1) : nullptr;
   auto true_residual = [&]() -> double {
-    // ||b - A x|| (PCG.py:83,95), debug/trace only
-    if (valid) xbuf[t] = xi;
+    // ||b - A x|| (PCG.py:83,95), trace only
+    if (valid) L.xbuf[t] = xi;
     __syncthreads();
-    const double e = valid ? bi - spmv(xbuf) : 0.0;
-    const double s = block_sum(e * e, red + 16 * rsel, nwaves);
+    const double e = valid ? bi - spmv(L.xbuf) : 0.0;
+    const double s = block_sum(e * e, L.red + 16 * rsel, nwaves);
     rsel ^= 1;
     return sqrt(s);
   };
@@ -515,16 +351,16 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
   }
   int it_done = max_iter;
   for (int it = 0; it < max_iter; ++it) {
-    if (valid) pbuf[t] = pi;
+    if (valid) L.pbuf[t] = pi;
     __syncthreads();
-    const double api = spmv(pbuf);
-    const double pap = block_sum(valid ? pi * api : 0.0, red + 16 * rsel, nwaves);
+    const double api = spmv(L.pbuf);
+    const double pap = block_sum(valid ? pi * api : 0.0, L.red + 16 * rsel, nwaves);
     rsel ^= 1;
     const double alpha = nu / pap;
     ri = ri - api * alpha;
     xi = xi + pi * alpha;
     zi = apply_P(ri);
-    const double nup = block_sum(valid ? ri * zi : 0.0, red + 16 * rsel, nwaves);
+    const double nup = block_sum(valid ? ri * zi : 0.0, L.red + 16 * rsel, nwaves);
     rsel ^= 1;
     if (tn && t == 0) tn[it + 1] = fabs(nup);
     if (tr) {
@@ -539,179 +375,288 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
     pi = zi + pi * beta;
     nu = nup;
   }
+  *iters_out = it_done;
+  return xi;
+}
+
+// ---- standalone PCG on given blocks (tmpc_pcg_batch: the PCG class)
+template <int NX, int MAXT>
+__global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const double* __restrict__ Sd,
+                                              const double* __restrict__ Sl, const double* __restrict__ Su,
+                                              const double* __restrict__ gam, const double* __restrict__ guess,
+                                              double tol, int max_iter, double* __restrict__ lam,
+                                              int* __restrict__ iters, double* __restrict__ trace_nu,
+                                              double* __restrict__ trace_res, double* __restrict__ Pd_out) {
+  const int b = blockIdx.x;
+  extern __shared__ __align__(16) double lds[];
+  const int rows = N * NX;
+  const int nwaves = (blockDim.x + 63) >> 6;
+  const PcgLds L = pcg_lds(lds, N, NX);
+  const int t = threadIdx.x;
+  const bool valid = t < rows;
+  const int k = valid ? t / NX : 0;
+  const int i = valid ? t - k * NX : 0;
+  const int K = N - 1;
+  PcgRows<NX> R;
+#pragma unroll
+  for (int j = 0; j < NX; ++j) { R.sd[j] = 0.0; R.sl[j] = 0.0; R.su[j] = 0.0; R.pr[j] = 0.0; }
+  if (valid) {
+    const double* d = Sd + (((size_t)b * N + k) * NX + i) * NX;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) R.sd[j] = d[j];
+    if (k > 0) {
+      const double* l = Sl + (((size_t)b * K + (k - 1)) * NX + i) * NX;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) R.sl[j] = l[j];
+    }
+    if (k < K) {
+      if (Su) {
+        const double* up = Su + (((size_t)b * K + k) * NX + i) * NX;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) R.su[j] = up[j];
+      } else {
+        const double* l = Sl + ((size_t)b * K + k) * NX * NX;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) R.su[j] = l[j * NX + i];
+      }
+    }
+  }
+  pcg_precondition<NX>(R, precond, valid, k, i, N, L.piv,
+                       Pd_out ? Pd_out + (((size_t)b * N + k) * NX + i) * NX : nullptr);
+  const double bi = valid ? gam[(size_t)b * rows + t] : 0.0;
+  const double gi = (guess && valid) ? guess[(size_t)b * rows + t] : 0.0;
+  int it_done = 0;
+  const double xi = pcg_run<NX>(R, precond, valid, t, k, N, L, bi, guess != nullptr, gi, tol, max_iter, nwaves,
+                                trace_nu ? trace_nu + (size_t)b * (max_iter + 1) : nullptr,
+                                trace_res ? trace_res + (size_t)b * (max_iter + 1) : nullptr, &it_done);
   if (valid) lam[(size_t)b * rows + t] = xi;
   if (t == 0) iters[b] = it_done;
 }
 
-// ======================================================================= dxul recovery
-// dxu = Ghat (g - C^T lambda)  (solveKKTSystem_Schur :449-452), lane = (b, k, i)
-template <int NJ>
-__global__ void __launch_bounds__(256) k_dxu(const CostDev* __restrict__ C, int B, int N,
+// ======================================================================= fused QP kernel
+// One QP of the SQP loop for one problem per workgroup:
+//   prologue  Schur blocks (blockwise form of
+//             solveKKTSystem_Schur :419-424): lane (k, i) computes row i of
+//             S_kk, S_{k,k-1}, S_{k,k+1} and gamma_k[i] straight into registers
+//             from A, B (qp_grad), the defects c (qp_fd) and Ghat (ginv),
+//             all staged once into LDS with coalesced loads;
+//   body      preconditioner + PCG (pcg_precondition / pcg_run);
+//   epilogue  dxu = Ghat (g - C^T lambda) (:449-452).
+// S and lambda never leave the chip.
+__host__ __device__ inline size_t qp_stage_doubles(int N, int NX, int NU) {
+  const size_t K = N - 1;
+  return K * NX * NX + K * NX * NU + 3 * (size_t)NX * NX + (size_t)NX * N + (size_t)NU * K;
+}
+
+// LDS layout of k_qp: [staging area | lambda] is reused by the PCG buffers
+// (which start at 0); the cost gradients g_k = [dx_k^T Q_k, u_k^T R] live past
+// both because they must survive the PCG.
+__host__ __device__ inline size_t qp_g_offset(int N, int NX, int NU) {
+  const size_t a = qp_stage_doubles(N, NX, NU) + (size_t)N * NX;
+  const size_t p = pcg_lds_doubles(N, NX);
+  return a > p ? a : p;
+}
+
+__host__ __device__ inline size_t qp_lds_doubles(int N, int NX, int NU) {
+  return qp_g_offset(N, NX, NU) + (size_t)N * (NX + NU);
+}
+
+struct QpStage {
+  double *A, *B, *G, *x, *u;
+};
+
+__device__ __forceinline__ QpStage qp_stage(double* lds, int N, int NX, int NU) {
+  const int K = N - 1;
+  QpStage S;
+  S.A = lds;
+  S.B = S.A + (size_t)K * NX * NX;
+  S.G = S.B + (size_t)K * NX * NU;
+  S.x = S.G + 3 * NX * NX;
+  S.u = S.x + NX * N;
+  return S;
+}
+
+__device__ __forceinline__ void lds_copy(double* dst, const double* __restrict__ src, int count) {
+  for (int e = threadIdx.x; e < count; e += blockDim.x) dst[e] = src[e];
+}
+
+template <int NJ, int MAXT>
+__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond,
                                              const double* __restrict__ x, const double* __restrict__ u,
                                              const int* __restrict__ active, const double* __restrict__ Ginv,
                                              const double* __restrict__ Aall, const double* __restrict__ Ball,
-                                             const double* __restrict__ lam, double* __restrict__ dx,
-                                             double* __restrict__ du) {
-  constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * N * NXU) return;
-  const int i = gid % NXU;
-  const int bk = gid / NXU;
-  const int b = bk / N, k = bk - b * N;
+                                             const double* __restrict__ cvec, double tol, int max_iter,
+                                             int* __restrict__ iters, double* __restrict__ dx,
+                                             double* __restrict__ du, double* __restrict__ lam_out,
+                                             double* __restrict__ Sd_out, double* __restrict__ Sl_out,
+                                             double* __restrict__ gam_out, double* __restrict__ Pd_out) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int b = blockIdx.x;
   if (!active[b]) return;
+  extern __shared__ __align__(16) double lds[];
+  const int rows = N * NX;
+  const int nwaves = (blockDim.x + 63) >> 6;
+  const int t = threadIdx.x;
+  const bool valid = t < rows;
+  const int k = valid ? t / NX : 0;
+  const int i = valid ? t - k * NX : 0;
   const int K = N - 1;
-  if (k == K && i >= NX) return;
-  const double* xb = x + (size_t)b * NX * N;
-  const double* G3 = Ginv + (size_t)b * 3 * NX * NX;
-  const double* L = lam + (size_t)b * N * NX;
-  if (i < NX) {
-    const double* Gx = G3 + (use_QF(C, k, N) ? NX * NX : 0);
+  const QpStage S = qp_stage(lds, N, NX, NU);
+  double* lam_lds = S.u + NU * K;
+  auto stage_in = [&]() {
+    lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
+    lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
+    lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
+    lds_copy(S.x, x + (size_t)b * NX * N, NX * N);
+    lds_copy(S.u, u + (size_t)b * NU * K, NU * K);
+  };
+  const double* Gu = S.G + 2 * NX * NX;
+  stage_in();
+  __syncthreads();
+
+  // cost gradients g_k = [(x_k - xg)^T Q_k, u_k^T R] (QuadraticCost.gradient, TrajoptCost.py:58-69):
+  // lane (k, i) computes entry i (and entry NX + i of the control part for i < NU)
+  double* g_lds = lds + qp_g_offset(N, NX, NU);    // [N][NX + NU]
+  if (valid) {
     const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
-    double dxk[NX], h[NX];
+    double g = 0.0;
 #pragma unroll
-    for (int m = 0; m < NX; ++m) dxk[m] = xb[m * N + k] - C->xg[m];
-    const double* A = (k < K) ? Aall + ((size_t)b * K + k) * NX * NX : nullptr;
+    for (int m = 0; m < NX; ++m) g += (S.x[m * N + k] - C->xg[m]) * Qk[m * NX + i];
+    g_lds[k * (NX + NU) + i] = g;
+    if (i < NU && k < K) {
+      double gu = 0.0;
+#pragma unroll
+      for (int m = 0; m < NU; ++m) gu += S.u[m * K + k] * C->R[m * NU + i];
+      g_lds[k * (NX + NU) + NX + i] = gu;
+    }
+  }
+  __syncthreads();
+
+  PcgRows<NX> R;
+#pragma unroll
+  for (int j = 0; j < NX; ++j) { R.sd[j] = 0.0; R.sl[j] = 0.0; R.su[j] = 0.0; R.pr[j] = 0.0; }
+  double bi = 0.0;
+  if (valid) {
+    const double* Gxk = S.G + (use_QF(C, k, N) ? NX * NX : 0);
+    const double* gk = g_lds + k * (NX + NU);
+    // gamma_k[i] = c_k[i] + [AB Ghat g]_{k-1} - (Ghat_k g_k)_x[i]
+    double gam = cvec[(size_t)b * N * NX + k * NX + i];
+    {
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) s += Gxk[i * NX + j] * gk[j];
+      gam -= s;
+    }
+    if (k == 0) {
+#pragma unroll
+      for (int j = 0; j < NX; ++j) R.sd[j] = -Gxk[i * NX + j];
+    } else {
+      const int km = k - 1;
+      const double* Gxm = S.G + (use_QF(C, km, N) ? NX * NX : 0);
+      const double* gm = g_lds + km * (NX + NU);
+      const double* A = S.A + km * NX * NX;
+      const double* Bm = S.B + km * NX * NU;
+      // S_{k,k-1} row i = (A_{k-1} Ghat_x)[i, :]
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) acc += A[i * NX + m] * Gxm[m * NX + j];
+        R.sl[j] = acc;
+      }
+      double BG[NU];
+#pragma unroll
+      for (int j = 0; j < NU; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) acc += Bm[i * NU + m] * Gu[m * NU + j];
+        BG[j] = acc;
+      }
+      // S_kk row i = -(A G A^T + B G B^T + Ghat_x,k)[i, :]
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) acc += R.sl[m] * A[j * NX + m];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) acc += BG[m] * Bm[j * NU + m];
+        R.sd[j] = -(acc + Gxk[i * NX + j]);
+      }
+      // + (A G g)[i] with g_{k-1} = [dx^T Q, u^T R]
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) s += R.sl[j] * gm[j];
+#pragma unroll
+      for (int j = 0; j < NU; ++j) s += BG[j] * gm[NX + j];
+      gam += s;
+    }
+    if (k < K) {
+      // S_{k,k+1} row i = S_{k+1,k}^T row i = (A_k Ghat_x,k)[:, i]
+      const double* A = S.A + k * NX * NX;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) acc += A[j * NX + m] * Gxk[m * NX + i];
+        R.su[j] = acc;
+      }
+    }
+    bi = gam;
+    if (Sd_out) {
+#pragma unroll
+      for (int j = 0; j < NX; ++j) Sd_out[(((size_t)b * N + k) * NX + i) * NX + j] = R.sd[j];
+      if (k > 0) {
+#pragma unroll
+        for (int j = 0; j < NX; ++j) Sl_out[(((size_t)b * K + k - 1) * NX + i) * NX + j] = R.sl[j];
+      }
+      gam_out[(size_t)b * rows + t] = gam;
+    }
+  }
+  __syncthreads();   // the PCG buffers alias the staging area
+  const PcgLds L = pcg_lds(lds, N, NX);
+  pcg_precondition<NX>(R, precond, valid, k, i, N, L.piv,
+                       Pd_out ? Pd_out + (((size_t)b * N + k) * NX + i) * NX : nullptr);
+  int it_done = 0;
+  const double xi = pcg_run<NX>(R, precond, valid, t, k, N, L, bi, false, 0.0, tol, max_iter, nwaves, nullptr,
+                                nullptr, &it_done);
+  if (t == 0) iters[b] = it_done;
+  // ---- epilogue: dxu = Ghat (g - C^T lambda), operands re-staged into LDS
+  __syncthreads();
+  stage_in();
+  if (valid) {
+    lam_lds[t] = xi;
+    if (lam_out) lam_out[(size_t)b * rows + t] = xi;
+  }
+  __syncthreads();
+  if (valid) {
+    const double* Gxk = S.G + (use_QF(C, k, N) ? NX * NX : 0);
+    const double* lk = lam_lds + k * NX;
+    const double* gk = g_lds + k * (NX + NU);
+    const double* A = S.A + (k < K ? k : 0) * NX * NX;
+    double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      double g = 0.0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) g += dxk[m] * Qk[m * NX + j];
       double atl = 0.0;
       if (k < K) {
 #pragma unroll
-        for (int m = 0; m < NX; ++m) atl += A[m * NX + j] * L[(k + 1) * NX + m];
+        for (int m = 0; m < NX; ++m) atl += A[m * NX + j] * lk[NX + m];
       }
-      h[j] = g - (L[k * NX + j] - atl);
+      acc += Gxk[i * NX + j] * (gk[j] - (lk[j] - atl));
     }
-    double acc = 0.0;
+    dx[((size_t)b * N + k) * NX + i] = acc;
+    if (k < K && i < NU) {
+      const double* Bm = S.B + k * NX * NU;
+      double accu = 0.0;
 #pragma unroll
-    for (int j = 0; j < NX; ++j) acc += Gx[i * NX + j] * h[j];
-    dx[(size_t)bk * NX + i] = acc;
-  } else {
-    const int iu = i - NX;
-    const double* ub = u + (size_t)b * NU * K;
-    const double* Gu = G3 + 2 * NX * NX;
-    const double* Bm = Ball + ((size_t)b * K + k) * NX * NU;
-    double uk[NU], h[NU];
+      for (int j = 0; j < NU; ++j) {
+        double btl = 0.0;
 #pragma unroll
-    for (int m = 0; m < NU; ++m) uk[m] = ub[m * K + k];
-#pragma unroll
-    for (int j = 0; j < NU; ++j) {
-      double g = 0.0;
-#pragma unroll
-      for (int m = 0; m < NU; ++m) g += uk[m] * C->R[m * NU + j];
-      double btl = 0.0;
-#pragma unroll
-      for (int m = 0; m < NX; ++m) btl += Bm[m * NU + j] * L[(k + 1) * NX + m];
-      h[j] = g - (-btl);
-    }
-    double acc = 0.0;
-#pragma unroll
-    for (int j = 0; j < NU; ++j) acc += Gu[iu * NU + j] * h[j];
-    du[((size_t)b * K + k) * NU + iu] = acc;
-  }
-}
-
-// ======================================================================= line-search merit terms
-// lane = (b, t, k): for trial step alpha_t evaluate the per-knot pieces of
-// totalCost (:296-310), totalHardConstraintViolation (:273-294) and the
-// directional derivative D (:635-648, gradient taken at x_new as the
-// reference does).  Knot lane N-1 carries the terminal cost / D term and the
-// |x_0 - xs| violation term.
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_ls_terms(const ModelDev* __restrict__ M, const CostDev* __restrict__ C,
-                                                  int B, int N, int T, double dt, const double* __restrict__ alphas,
-                                                  const double* __restrict__ x, const double* __restrict__ u,
-                                                  const double* __restrict__ xs, const double* __restrict__ dx,
-                                                  const double* __restrict__ du, const int* __restrict__ active,
-                                                  double* __restrict__ terms) {
-  constexpr int NX = 2 * NJ, NU = NJ;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * T * N) return;
-  const int k = gid % N;
-  const int bt = gid / N;
-  const int b = bt / T, t = bt - b * T;
-  if (!active[b]) return;
-  const int K = N - 1;
-  const double al = alphas[t];
-  const double* xb = x + (size_t)b * NX * N;
-  const double* ub = u + (size_t)b * NU * K;
-  const double* dxb = dx ? dx + (size_t)b * N * NX : nullptr;
-  const double* dub = du ? du + (size_t)b * K * NU : nullptr;
-  double xk[NX], dxk[NX];
-#pragma unroll
-  for (int m = 0; m < NX; ++m) {
-    dxk[m] = dxb ? dxb[k * NX + m] : 0.0;
-    // x_new = x - alpha dx  (:619-622; alpha is a power of two: exact)
-    xk[m] = dxb ? xb[m * N + k] - al * dxk[m] : xb[m * N + k];
-  }
-  const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
-  double d[NX];
-#pragma unroll
-  for (int m = 0; m < NX; ++m) d[m] = xk[m] - C->xg[m];
-  // value: 0.5 dx^T (Q dx) [+ 0.5 u^T (R u)]; gradient: [dx^T Q, u^T R]
-  double vq = 0.0, Dk = 0.0;
-#pragma unroll
-  for (int r = 0; r < NX; ++r) {
-    double qd = 0.0, gq = 0.0;
-#pragma unroll
-    for (int c = 0; c < NX; ++c) {
-      qd += Qk[r * NX + c] * d[c];
-      gq += d[c] * Qk[c * NX + r];
-    }
-    vq += d[r] * qd;
-    Dk += gq * dxk[r];
-  }
-  double cost = 0.5 * vq;
-  double viol = 0.0;
-  double* out = terms + ((size_t)bt * N + k) * 3;
-  if (k < K) {
-    double uk[NU], duk[NU];
-#pragma unroll
-    for (int m = 0; m < NU; ++m) {
-      duk[m] = dub ? dub[k * NU + m] : 0.0;
-      uk[m] = dub ? ub[m * K + k] - al * duk[m] : ub[m * K + k];
-    }
-    double vr = 0.0;
-#pragma unroll
-    for (int r = 0; r < NU; ++r) {
-      double ru = 0.0, gr = 0.0;
-#pragma unroll
-      for (int c = 0; c < NU; ++c) {
-        ru += C->R[r * NU + c] * uk[c];
-        gr += uk[c] * C->R[c * NU + r];
+        for (int m = 0; m < NX; ++m) btl += Bm[m * NU + j] * lk[NX + m];
+        accu += Gu[i * NU + j] * (gk[NX + j] - (-btl));
       }
-      vr += uk[r] * ru;
-      Dk += gr * duk[r];
-    }
-    cost += 0.5 * vr;
-    // dynamics defect at the trial point
-    double cq[NJ], sq[NJ], qd[NJ], qdd[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      qd[j] = xk[NJ + j];
-      joint_cs(M, j, xk[j], cq[j], sq[j]);
-    }
-    fd_aba<NJ, CHAIN>(M, cq, sq, qd, uk, qdd);
-#pragma unroll
-    for (int m = 0; m < NX; ++m) {
-      const double dxn = dxb ? dxb[(k + 1) * NX + m] : 0.0;
-      const double xn = dxb ? xb[m * N + k + 1] - al * dxn : xb[m * N + k + 1];
-      const double xdot = m < NJ ? qd[m] : qdd[m - NJ];
-      const double f = __dadd_rn(xk[m], __dmul_rn(dt, xdot));
-      viol += fabs(xn - f);
-    }
-  } else {
-    // |x_0 - xs|_1 for the initial-state constraint
-#pragma unroll
-    for (int m = 0; m < NX; ++m) {
-      const double x0 = dxb ? xb[m * N] - al * dxb[m] : xb[m * N];
-      viol += fabs(x0 - xs[(size_t)b * NX + m]);
+      du[((size_t)b * K + k) * NU + i] = accu;
     }
   }
-  out[0] = cost;
-  out[1] = viol;
-  out[2] = Dk;
 }
 
 // ======================================================================= line-search decision + state machine
@@ -861,32 +806,6 @@ __global__ void k_init_state(int B, double rho_init, ProbState st) {
 // ======================================================================= kernel-level entry points
 // [K][nx] / [K][nu] row layout, one lane per knot (or per knot and column)
 template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_unit_fd(const ModelDev* __restrict__ M, int K, double dt,
-                                                 const double* __restrict__ x, const double* __restrict__ u,
-                                                 double* __restrict__ xnext, double* __restrict__ qdd_out) {
-  constexpr int NX = 2 * NJ;
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    q[j] = x[(size_t)k * NX + j];
-    qd[j] = x[(size_t)k * NX + NJ + j];
-    uu[j] = u[(size_t)k * NJ + j];
-    joint_cs(M, j, q[j], cq[j], sq[j]);
-  }
-  fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    qdd_out[(size_t)k * NJ + j] = qdd[j];
-    if (xnext) {
-      xnext[(size_t)k * NX + j] = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
-      xnext[(size_t)k * NX + NJ + j] = __dadd_rn(qd[j], __dmul_rn(dt, qdd[j]));
-    }
-  }
-}
-
-template <int NJ, bool CHAIN>
 __global__ void __launch_bounds__(256) k_unit_minv(const ModelDev* __restrict__ M, int K, const double* __restrict__ x,
                                                    double* __restrict__ minv_out) {
   constexpr int NX = 2 * NJ;
@@ -920,49 +839,11 @@ __global__ void __launch_bounds__(256) k_unit_grad(const ModelDev* __restrict__ 
                              dqdd ? dqdd + (size_t)k * NJ * 3 * NJ : nullptr);
 }
 
-// sequential Euler rollout, one lane per problem (workload setup: §8d)
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(64) k_rollout(const ModelDev* __restrict__ M, int B, int N, double dt,
-                                                double* __restrict__ x, const double* __restrict__ u) {
-  constexpr int NX = 2 * NJ;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int K = N - 1;
-  double* xb = x + (size_t)b * NX * N;
-  const double* ub = u + (size_t)b * NJ * K;
-  double q[NJ], qd[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) { q[j] = xb[j * N]; qd[j] = xb[(NJ + j) * N]; }
-  for (int k = 0; k < K; ++k) {
-    double uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      uu[j] = ub[j * K + k];
-      joint_cs(M, j, q[j], cq[j], sq[j]);
-    }
-    fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const double nq = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
-      const double nv = __dadd_rn(qd[j], __dmul_rn(dt, qdd[j]));
-      q[j] = nq;
-      qd[j] = nv;
-      xb[j * N + k + 1] = nq;
-      xb[(NJ + j) * N + k + 1] = nv;
-    }
-  }
-}
-
 // ======================================================================= launchers
 #define TMPC_GRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
 
 template <int NJ, bool CHAIN>
 struct Launch {
-  static void qp_fd(hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const double* u,
-                    const double* xs, const int* need, double* qdd, double* cvec) {
-    hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN>), TMPC_GRID(B * (N - 1), 256), 0, s, M, B, N, dt, x, u, xs, need, qdd,
-                       cvec);
-  }
   static void qp_minv(hipStream_t s, const ModelDev* M, int B, int N, const double* x, const int* need, double* minv) {
     hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, M, B, N, x, need, minv);
   }
@@ -970,16 +851,6 @@ struct Launch {
                       const double* qdd, const double* minv, double* A, double* Bm) {
     hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, M, B, N, dt, x, need,
                        qdd, minv, A, Bm);
-  }
-  static void ls_terms(hipStream_t s, const ModelDev* M, const CostDev* C, int B, int N, int T, double dt,
-                       const double* alphas, const double* x, const double* u, const double* xs, const double* dx,
-                       const double* du, const int* active, double* terms) {
-    hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN>), TMPC_GRID(B * T * N, 256), 0, s, M, C, B, N, T, dt, alphas, x, u,
-                       xs, dx, du, active, terms);
-  }
-  static void unit_fd(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
-                      double* xnext, double* qdd) {
-    hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN>), TMPC_GRID(K, 256), 0, s, M, K, dt, x, u, xnext, qdd);
   }
   static void unit_minv(hipStream_t s, const ModelDev* M, int K, const double* x, double* minv) {
     hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN>), TMPC_GRID(K * NJ, 256), 0, s, M, K, x, minv);
@@ -989,9 +860,6 @@ struct Launch {
     hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN>), TMPC_GRID(K * 2 * NJ, 256), 0, s, M, K, dt, x, qdd, minv, A, Bm,
                        dqdd);
   }
-  static void rollout(hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u) {
-    hipLaunchKernelGGL((k_rollout<NJ, CHAIN>), TMPC_GRID(B, 64), 0, s, M, B, N, dt, x, u);
-  }
 };
 
 template <int NJ>
@@ -999,16 +867,20 @@ struct LaunchNJ {
   static void ginv(hipStream_t s, const CostDev* C, int B, const double* rho, const int* active, double* G) {
     hipLaunchKernelGGL((k_ginv<NJ>), TMPC_GRID(B * 3 * 16, 64), 0, s, C, B, rho, active, G);
   }
-  static void schur(hipStream_t s, const CostDev* C, int B, int N, const double* x, const double* u,
-                    const int* active, const double* G, const double* A, const double* Bm, const double* cvec,
-                    double* Sd, double* Sl, double* gam) {
-    hipLaunchKernelGGL((k_schur<NJ>), TMPC_GRID(B * N * 2 * NJ, 256), 0, s, C, B, N, x, u, active, G, A, Bm, cvec,
-                       Sd, Sl, gam);
-  }
-  static void dxu(hipStream_t s, const CostDev* C, int B, int N, const double* x, const double* u, const int* active,
-                  const double* G, const double* A, const double* Bm, const double* lam, double* dx, double* du) {
-    hipLaunchKernelGGL((k_dxu<NJ>), TMPC_GRID(B * N * 3 * NJ, 256), 0, s, C, B, N, x, u, active, G, A, Bm, lam, dx,
-                       du);
+  static void qp(hipStream_t s, const CostDev* C, int B, int N, int precond, const double* x, const double* u,
+                 const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
+                 int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
+                 double* Pd) {
+    constexpr int NX = 2 * NJ;
+    const int rows = N * NX;
+    const int threads = ((rows + 63) / 64) * 64;
+    const size_t lds = qp_lds_doubles(N, NX, NJ) * sizeof(double);
+    if (threads <= 768)
+      hipLaunchKernelGGL((k_qp<NJ, 768>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
+                         cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
+    else
+      hipLaunchKernelGGL((k_qp<NJ, 1024>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
+                         cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
   }
 };
 
@@ -1020,31 +892,36 @@ int pcg_set_max_lds() {
   err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
   SETA(2) SETA(4) SETA(6) SETA(8) SETA(10) SETA(12) SETA(14) SETA(16)
 #undef SETA
+#define SETQ(V)                                                                                                \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 768>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  SETQ(1) SETQ(2) SETQ(3) SETQ(4) SETQ(5) SETQ(6) SETQ(7)
+#undef SETQ
   return err;
 }
 
 template <int NX>
 static void launch_pcg_nx(hipStream_t s, int B, int N, int precond, const double* Sd, const double* Sl,
-                          const double* Su, const double* gam, const double* guess, const int* active, double tol, int max_iter,
+                          const double* Su, const double* gam, const double* guess, double tol, int max_iter,
                           double* lam, int* iters, double* tnu, double* tres, double* Pd) {
   const int rows = N * NX;
   const int threads = ((rows + 63) / 64) * 64;
-  const size_t lds = (size_t)(5 * rows + 32 + 2 * N * 2 * NX) * sizeof(double);
+  const size_t lds = pcg_lds_doubles(N, NX) * sizeof(double);
   if (threads <= 768)
-    hipLaunchKernelGGL((k_pcg<NX, 768>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess, active,
-                       tol, max_iter, lam, iters, tnu, tres, Pd);
+    hipLaunchKernelGGL((k_pcg<NX, 768>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess, tol,
+                       max_iter, lam, iters, tnu, tres, Pd);
   else
-    hipLaunchKernelGGL((k_pcg<NX, 1024>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess, active,
-                       tol, max_iter, lam, iters, tnu, tres, Pd);
+    hipLaunchKernelGGL((k_pcg<NX, 1024>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess, tol,
+                       max_iter, lam, iters, tnu, tres, Pd);
 }
 
 int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
-               const double* Su, const double* gam, const double* guess, const int* active, double tol, int max_iter, double* lam,
+               const double* Su, const double* gam, const double* guess, double tol, int max_iter, double* lam,
                int* iters, double* tnu, double* tres, double* Pd) {
   if (N * nx > 1024) return -1;
   switch (nx) {
 #define CASE_NX(V) \
-  case V: launch_pcg_nx<V>(s, B, N, precond, Sd, Sl, Su, gam, guess, active, tol, max_iter, lam, iters, tnu, tres, Pd); return 0;
+  case V: launch_pcg_nx<V>(s, B, N, precond, Sd, Sl, Su, gam, guess, tol, max_iter, lam, iters, tnu, tres, Pd); return 0;
     CASE_NX(2) CASE_NX(4) CASE_NX(6) CASE_NX(8) CASE_NX(10) CASE_NX(12) CASE_NX(14) CASE_NX(16)
 #undef CASE_NX
     default: return -2;
@@ -1090,10 +967,6 @@ void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& s
   }                                                                                \
   return 0;
 
-int launch_qp_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, const double* x,
-                 const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
-  TMPC_DISPATCH_NJ(nj, chain, qp_fd(s, M, B, N, dt, x, u, xs, need, qdd, cvec))
-}
 int launch_qp_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, const double* x,
                    const int* need, double* minv) {
   TMPC_DISPATCH_NJ(nj, chain, qp_minv(s, M, B, N, x, need, minv))
@@ -1102,15 +975,6 @@ int launch_qp_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, 
                    const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
   TMPC_DISPATCH_NJ(nj, chain, qp_grad(s, M, B, N, dt, x, need, qdd, minv, A, Bm))
 }
-int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, int B, int N, int T,
-                    double dt, const double* alphas, const double* x, const double* u, const double* xs,
-                    const double* dx, const double* du, const int* active, double* terms) {
-  TMPC_DISPATCH_NJ(nj, chain, ls_terms(s, M, C, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
-}
-int launch_unit_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
-                   const double* u, double* xnext, double* qdd) {
-  TMPC_DISPATCH_NJ(nj, chain, unit_fd(s, M, K, dt, x, u, xnext, qdd))
-}
 int launch_unit_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, const double* x, double* minv) {
   TMPC_DISPATCH_NJ(nj, chain, unit_minv(s, M, K, x, minv))
 }
@@ -1118,22 +982,17 @@ int launch_unit_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int K
                      const double* qdd, const double* minv, double* A, double* Bm, double* dqdd) {
   TMPC_DISPATCH_NJ(nj, chain, unit_grad(s, M, K, dt, x, qdd, minv, A, Bm, dqdd))
 }
-int launch_rollout(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, double* x,
-                   const double* u) {
-  TMPC_DISPATCH_NJ(nj, chain, rollout(s, M, B, N, dt, x, u))
-}
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G) {
   TMPC_DISPATCH_NJ2(nj, ginv(s, C, B, rho, active, G))
 }
-int launch_schur(hipStream_t s, int nj, const CostDev* C, int B, int N, const double* x, const double* u,
-                 const int* active, const double* G, const double* A, const double* Bm, const double* cvec,
-                 double* Sd, double* Sl, double* gam) {
-  TMPC_DISPATCH_NJ2(nj, schur(s, C, B, N, x, u, active, G, A, Bm, cvec, Sd, Sl, gam))
-}
-int launch_dxu(hipStream_t s, int nj, const CostDev* C, int B, int N, const double* x, const double* u,
-               const int* active, const double* G, const double* A, const double* Bm, const double* lam, double* dx,
-               double* du) {
-  TMPC_DISPATCH_NJ2(nj, dxu(s, C, B, N, x, u, active, G, A, Bm, lam, dx, du))
+int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, const double* x, const double* u,
+              const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
+              int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
+              double* Pd) {
+  if (N * 2 * nj > 1024) return -1;
+  if (qp_lds_doubles(N, 2 * nj, nj) * sizeof(double) > 160 * 1024) return -3;
+  TMPC_DISPATCH_NJ2(nj, qp(s, C, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd,
+                           Sl, gam, Pd))
 }
 
 }  // namespace tmpc
