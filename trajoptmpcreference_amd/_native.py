@@ -11,7 +11,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtmpc.so")
+LIB_PATH = os.environ.get("TMPC_LIBRARY") or os.path.join(_HERE, "libtmpc.so")
 
 LINSYS = {"S": 1, "PCG-J": 2, "PCG-BJ": 3, "PCG-SS": 4}
 PRECOND = {"J": 1, "BJ": 2, "SS": 3}

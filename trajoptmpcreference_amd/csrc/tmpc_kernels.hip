@@ -179,50 +179,103 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
 
 // ======================================================================= block-tridiagonal PCG
 // One workgroup per problem, one lane per row of S (PCG.pcg, PCG.py:66-111).
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+//
+// Reductions are DPP butterflies inside the wave (VALU only; ds_bpermute
+// shuffles cost an LDS round trip per step) and one LDS fan-in of the
+// per-wave totals, reduced again by DPP: a fixed tree, so the result is
+// deterministic and identical for a problem whatever its batch neighbours.
+// lanes outside ROW_MASK read 0
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_get(double v) {
+  int lo, hi;
+  if (ROW_MASK == 0xf) {
+    lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+  } else {
+    lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  }
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// every lane of each 16-lane row ends with the sum over its row
+__device__ __forceinline__ double dpp_row_sum(double v) {
+  v += dpp_get<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]
+  v += dpp_get<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]
+  v += dpp_get<0x141, 0xf>(v);   // row_half_mirror
+  v += dpp_get<0x140, 0xf>(v);   // row_mirror
   return v;
 }
 
-// every thread returns the same value (fixed summation order: deterministic);
-// `red` must alternate between consecutive calls
-__device__ __forceinline__ double block_sum(double v, double* red, int nwaves) {
+// wave64 sum, returned uniform (SGPR broadcast)
+__device__ __forceinline__ double wave_sum(double v) {
+  v = dpp_row_sum(v);
+  v += dpp_get<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+  v += dpp_get<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
+  return readlane_f64(v, 63);
+}
+
+// Workgroup sum, uniform in every lane.  `red` is one of two 16-slot halves
+// used alternately by consecutive calls (slots of absent waves hold 0).
+__device__ __forceinline__ double block_sum(double v, double* red) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) red[w] = v;
   __syncthreads();
-  double s = 0.0;
-  for (int i = 0; i < nwaves; ++i) s += red[i];
-  return s;
+  return readlane_f64(dpp_row_sum(red[lane & 15]), 0);
 }
 
 // the rows of S (and of P_kk^-1) a lane keeps in registers for the whole solve
 template <int NX>
 struct PcgRows {
   double sd[NX];   // S_kk row i
-  double sl[NX];   // S_{k,k-1} row i
-  double su[NX];   // S_{k,k+1} row i
+  double sl[NX];   // S_{k,k-1} row i   (0 for k = 0)
+  double su[NX];   // S_{k,k+1} row i   (0 for k = N-1)
   double pr[NX];   // (S_kk)^-1 row i  (J: pr[0] = 1 / S_ii)
 };
 
+// LDS vectors are [pad NX | N*NX rows | pad NX]: the pads stay zero so the
+// block-tridiagonal products need no edge branches.
 struct PcgLds {
   double *pbuf, *rbuf, *wbuf, *tbuf, *xbuf, *red, *piv;
 };
 
-__host__ __device__ inline size_t pcg_lds_doubles(int N, int NX) { return (size_t)5 * N * NX + 32 + 4 * N * NX; }
+__host__ __device__ inline size_t pcg_vec_doubles(int N, int NX) { return (size_t)(N + 2) * NX; }
+__host__ __device__ inline size_t pcg_lds_doubles(int N, int NX) {
+  return 5 * pcg_vec_doubles(N, NX) + 32 + (size_t)4 * N * NX;
+}
 
 __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
-  const int rows = N * NX;
+  const size_t v = pcg_vec_doubles(N, NX);
   PcgLds L;
-  L.pbuf = lds;
-  L.rbuf = L.pbuf + rows;
-  L.wbuf = L.rbuf + rows;
-  L.tbuf = L.wbuf + rows;
-  L.xbuf = L.tbuf + rows;
-  L.red = L.xbuf + rows;   // 2 x 16
+  L.pbuf = lds + NX;
+  L.rbuf = L.pbuf + v;
+  L.wbuf = L.rbuf + v;
+  L.tbuf = L.wbuf + v;
+  L.xbuf = L.tbuf + v;
+  L.red = lds + 5 * v;     // 2 x 16
   L.piv = L.red + 32;      // 2 x N x 2NX
   return L;
+}
+
+// zero the pads and the reduction slots (callers barrier before first use)
+__device__ __forceinline__ void pcg_lds_clear(double* lds, int N, int NX) {
+  const size_t v = pcg_vec_doubles(N, NX);
+  const int rows = N * NX;
+  for (int e = threadIdx.x; e < 5 * 2 * NX + 32; e += blockDim.x) {
+    if (e < 10 * NX) {
+      const int buf = e / (2 * NX), o = e - buf * 2 * NX;
+      lds[buf * v + (o < NX ? o : rows + o)] = 0.0;
+    } else {
+      lds[5 * v + (e - 10 * NX)] = 0.0;
+    }
+  }
 }
 
 // compute_preconditioner (PCG.py:166-212): J -> 1/S_ii; BJ and SS -> the
@@ -265,84 +318,107 @@ __device__ __forceinline__ void pcg_precondition(PcgRows<NX>& R, int precond, bo
   }
 }
 
-// The CG iteration.  Returns this lane's entry of the solution.
+// (S v) for this lane's row: three independent accumulation chains
 template <int NX>
-__device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, int precond, bool valid, int t, int k, int N,
-                                          const PcgLds& L, double bi, bool has_guess, double guess_i, double tol,
-                                          int max_iter, int nwaves, double* tn, double* tr, int* iters_out) {
-  const int K = N - 1;
+__device__ __forceinline__ double pcg_spmv(const PcgRows<NX>& R, const double* __restrict__ v, int kb) {
+  const double* vm = v + kb - NX;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    a0 += R.sl[j] * vm[j];
+    a1 += R.sd[j] * vm[NX + j];
+    a2 += R.su[j] * vm[2 * NX + j];
+  }
+  return (a0 + a1) + a2;
+}
+
+template <int NX>
+__device__ __forceinline__ double pcg_block_dot(const double* __restrict__ pr, const double* __restrict__ v) {
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NX; j += 2) {
+    a0 += pr[j] * v[j];
+    if (j + 1 < NX) a1 += pr[j + 1] * v[j + 1];
+  }
+  return a0 + a1;
+}
+
+// Diagnostic build only (-DTMPC_PCG_STAMPS, tools/pcg_microbench.py --stamps):
+// per-phase s_memtime cycle totals of the first and last wave of each
+// workgroup replace the |nu| trace; the true-residual trace is disabled.
+#ifdef TMPC_PCG_STAMPS
+#define PCG_STAMP(i)                                          \
+  do {                                                        \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+    st_[i] += n_ - st_prev_;                                  \
+    st_prev_ = n_;                                            \
+  } while (0)
+#else
+#define PCG_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
+// The CG iteration.  Returns this lane's entry of the solution.
+template <int NX, int PRE>
+__device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, bool valid, int t, int k, int N, const PcgLds& L,
+                                          double bi, bool has_guess, double guess_i, double tol, int max_iter,
+                                          double* tn, double* tr, int* iters_out) {
   const int kb = k * NX;
+#ifdef TMPC_PCG_STAMPS
+  unsigned long long st_[16] = {}, st_prev_ = __builtin_amdgcn_s_memtime();
+  double* const tn_st = tn;
+  tn = nullptr;
+  tr = nullptr;
+#endif
+  // z = P^-1 r (PCG.py:88-90)
   auto apply_P = [&](double r_i) -> double {
-    if (precond == PRECOND_J) return R.pr[0] * r_i;
+    if (PRE == PRECOND_J) return R.pr[0] * r_i;
     if (valid) L.rbuf[t] = r_i;
     __syncthreads();
-    double w = 0.0;
-    if (valid) {
-#pragma unroll
-      for (int j = 0; j < NX; ++j) w += R.pr[j] * L.rbuf[kb + j];
-    }
-    if (precond == PRECOND_BJ) return w;
+    PCG_STAMP(5);
+    const double w = pcg_block_dot<NX>(R.pr, L.rbuf + kb);
+    if (PRE == PRECOND_BJ) return w;
     // SS: z = P_D (r - S_off P_D r)  ==  the symmetric-stair P^-1 r
     if (valid) L.wbuf[t] = w;
     __syncthreads();
-    if (valid) {
-      double acc = 0.0;
-      if (k > 0) {
+    PCG_STAMP(6);
+    const double* wm = L.wbuf + kb - NX;
+    double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-        for (int j = 0; j < NX; ++j) acc += R.sl[j] * L.wbuf[kb - NX + j];
-      }
-      if (k < K) {
-#pragma unroll
-        for (int j = 0; j < NX; ++j) acc += R.su[j] * L.wbuf[kb + NX + j];
-      }
-      L.tbuf[t] = r_i - acc;
+    for (int j = 0; j < NX; ++j) {
+      a0 += R.sl[j] * wm[j];
+      a1 += R.su[j] * wm[2 * NX + j];
     }
+    if (valid) L.tbuf[t] = r_i - (a0 + a1);
     __syncthreads();
-    double z = 0.0;
-    if (valid) {
-#pragma unroll
-      for (int j = 0; j < NX; ++j) z += R.pr[j] * L.tbuf[kb + j];
-    }
-    return z;
-  };
-  auto spmv = [&](const double* vbuf) -> double {
-    double acc = 0.0;
-    if (valid) {
-      if (k > 0) {
-#pragma unroll
-        for (int j = 0; j < NX; ++j) acc += R.sl[j] * vbuf[kb - NX + j];
-      }
-#pragma unroll
-      for (int j = 0; j < NX; ++j) acc += R.sd[j] * vbuf[kb + j];
-      if (k < K) {
-#pragma unroll
-        for (int j = 0; j < NX; ++j) acc += R.su[j] * vbuf[kb + NX + j];
-      }
-    }
-    return acc;
+    PCG_STAMP(7);
+    return pcg_block_dot<NX>(R.pr, L.tbuf + kb);
   };
   int rsel = 0;
+  auto reduce = [&](double v) -> double {
+    const double s = block_sum(valid ? v : 0.0, L.red + 16 * rsel);
+    rsel ^= 1;
+    return s;
+  };
   // x0 = guess (default zeros, PCG.py:11-12); r = b - A x0 (:76)
   double xi = 0.0, ri = bi;
   if (has_guess) {
     xi = valid ? guess_i : 0.0;
     if (valid) L.xbuf[t] = xi;
     __syncthreads();
-    ri = bi - spmv(L.xbuf);
+    ri = bi - pcg_spmv<NX>(R, L.xbuf, kb);
     __syncthreads();
   }
   double zi = apply_P(ri);
   double pi = zi;
-  double nu = block_sum(valid ? ri * zi : 0.0, L.red + 16 * rsel, nwaves);
-  rsel ^= 1;
+  double nu = reduce(ri * zi);
   auto true_residual = [&]() -> double {
     // ||b - A x|| (PCG.py:83,95), trace only
     if (valid) L.xbuf[t] = xi;
     __syncthreads();
-    const double e = valid ? bi - spmv(L.xbuf) : 0.0;
-    const double s = block_sum(e * e, L.red + 16 * rsel, nwaves);
-    rsel ^= 1;
-    return sqrt(s);
+    const double e = bi - pcg_spmv<NX>(R, L.xbuf, kb);
+    return sqrt(reduce(e * e));
   };
   if (tn && t == 0) tn[0] = fabs(nu);
   if (tr) {
@@ -351,17 +427,21 @@ __device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, int precond, boo
   }
   int it_done = max_iter;
   for (int it = 0; it < max_iter; ++it) {
+    PCG_STAMP(0);
     if (valid) L.pbuf[t] = pi;
     __syncthreads();
-    const double api = spmv(L.pbuf);
-    const double pap = block_sum(valid ? pi * api : 0.0, L.red + 16 * rsel, nwaves);
-    rsel ^= 1;
+    PCG_STAMP(1);
+    const double api = pcg_spmv<NX>(R, L.pbuf, kb);
+    const double pap = reduce(pi * api);
+    PCG_STAMP(2);
     const double alpha = nu / pap;
     ri = ri - api * alpha;
     xi = xi + pi * alpha;
+    PCG_STAMP(3);
     zi = apply_P(ri);
-    const double nup = block_sum(valid ? ri * zi : 0.0, L.red + 16 * rsel, nwaves);
-    rsel ^= 1;
+    PCG_STAMP(8);
+    const double nup = reduce(ri * zi);
+    PCG_STAMP(9);
     if (tn && t == 0) tn[it + 1] = fabs(nup);
     if (tr) {
       const double rn = true_residual();
@@ -374,9 +454,27 @@ __device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, int precond, boo
     const double beta = nup / nu;
     pi = zi + pi * beta;
     nu = nup;
+    PCG_STAMP(10);
   }
+#ifdef TMPC_PCG_STAMPS
+  if (tn_st && (t == 0 || t == ((int)blockDim.x - 1) / 64 * 64)) {
+    double* o = tn_st + (t == 0 ? 0 : 16);
+    for (int i = 0; i < 16; ++i) o[i] = (double)st_[i];
+  }
+#endif
   *iters_out = it_done;
   return xi;
+}
+
+template <int NX>
+__device__ __forceinline__ double pcg_dispatch(int precond, const PcgRows<NX>& R, bool valid, int t, int k, int N,
+                                               const PcgLds& L, double bi, bool has_guess, double guess_i,
+                                               double tol, int max_iter, double* tn, double* tr, int* iters_out) {
+  if (precond == PRECOND_J)
+    return pcg_run<NX, PRECOND_J>(R, valid, t, k, N, L, bi, has_guess, guess_i, tol, max_iter, tn, tr, iters_out);
+  if (precond == PRECOND_BJ)
+    return pcg_run<NX, PRECOND_BJ>(R, valid, t, k, N, L, bi, has_guess, guess_i, tol, max_iter, tn, tr, iters_out);
+  return pcg_run<NX, PRECOND_SS>(R, valid, t, k, N, L, bi, has_guess, guess_i, tol, max_iter, tn, tr, iters_out);
 }
 
 // ---- standalone PCG on given blocks (tmpc_pcg_batch: the PCG class)
@@ -390,7 +488,7 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
   const int b = blockIdx.x;
   extern __shared__ __align__(16) double lds[];
   const int rows = N * NX;
-  const int nwaves = (blockDim.x + 63) >> 6;
+  pcg_lds_clear(lds, N, NX);
   const PcgLds L = pcg_lds(lds, N, NX);
   const int t = threadIdx.x;
   const bool valid = t < rows;
@@ -426,9 +524,9 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
   const double bi = valid ? gam[(size_t)b * rows + t] : 0.0;
   const double gi = (guess && valid) ? guess[(size_t)b * rows + t] : 0.0;
   int it_done = 0;
-  const double xi = pcg_run<NX>(R, precond, valid, t, k, N, L, bi, guess != nullptr, gi, tol, max_iter, nwaves,
-                                trace_nu ? trace_nu + (size_t)b * (max_iter + 1) : nullptr,
-                                trace_res ? trace_res + (size_t)b * (max_iter + 1) : nullptr, &it_done);
+  const double xi = pcg_dispatch<NX>(precond, R, valid, t, k, N, L, bi, guess != nullptr, gi, tol, max_iter,
+                                     trace_nu ? trace_nu + (size_t)b * (max_iter + 1) : nullptr,
+                                     trace_res ? trace_res + (size_t)b * (max_iter + 1) : nullptr, &it_done);
   if (valid) lam[(size_t)b * rows + t] = xi;
   if (t == 0) iters[b] = it_done;
 }
@@ -495,7 +593,6 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   if (!active[b]) return;
   extern __shared__ __align__(16) double lds[];
   const int rows = N * NX;
-  const int nwaves = (blockDim.x + 63) >> 6;
   const int t = threadIdx.x;
   const bool valid = t < rows;
   const int k = valid ? t / NX : 0;
@@ -613,12 +710,13 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
     }
   }
   __syncthreads();   // the PCG buffers alias the staging area
+  pcg_lds_clear(lds, N, NX);
   const PcgLds L = pcg_lds(lds, N, NX);
   pcg_precondition<NX>(R, precond, valid, k, i, N, L.piv,
                        Pd_out ? Pd_out + (((size_t)b * N + k) * NX + i) * NX : nullptr);
   int it_done = 0;
-  const double xi = pcg_run<NX>(R, precond, valid, t, k, N, L, bi, false, 0.0, tol, max_iter, nwaves, nullptr,
-                                nullptr, &it_done);
+  const double xi = pcg_dispatch<NX>(precond, R, valid, t, k, N, L, bi, false, 0.0, tol, max_iter, nullptr, nullptr,
+                                     &it_done);
   if (t == 0) iters[b] = it_done;
   // ---- epilogue: dxu = Ghat (g - C^T lambda), operands re-staged into LDS
   __syncthreads();
