@@ -53,6 +53,48 @@ def initial_states(n, B, seed0):
     return q0
 
 
+def shard_seed_base(seed0, rank, B):
+    """Rank r solves problems seed0 + r*B ... seed0 + (r+1)*B - 1: contiguous, disjoint
+    slices of one global workload, so every rank's result equals the
+    single-GPU result for the same problems."""
+    return seed0 + rank * B
+
+
+class Comm:
+    """torch.distributed as plumbing only: a barrier and the max over ranks of the
+    timed region (RCCL on the GPUs; gloo in the CPU tests).  No data-path collective."""
+
+    def __init__(self, world, local_rank, backend="nccl"):
+        self.world = world
+        self.tdist = None
+        if world > 1:
+            import torch
+            import torch.distributed as tdist
+            if backend == "nccl":
+                torch.cuda.set_device(local_rank)
+                self.device = f"cuda:{local_rank}"
+            else:
+                self.device = "cpu"
+            tdist.init_process_group(backend=backend)
+            self.torch, self.tdist = torch, tdist
+
+    def barrier(self):
+        if self.tdist is not None:
+            self.tdist.barrier()
+
+    def max(self, v):
+        if self.tdist is None:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.device)
+        self.tdist.all_reduce(t, op=self.tdist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.tdist is not None:
+            self.tdist.destroy_process_group()
+            self.tdist = None
+
+
 # ------------------------------------------------------------------ byte / flop model (SURVEY §8d)
 def pcg_bytes_per_iter(N, nx):
     return 8 * (2 * (2 * N - 1) * nx * nx + 10 * N * nx)
@@ -133,25 +175,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group(backend="nccl")
-        dist = (torch, tdist)
-
-    def barrier_max(v):
-        if dist is None:
-            return v
-        torch, tdist = dist
-        t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local_rank}")
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        return float(t.item())
-
-    def barrier():
-        if dist is not None:
-            dist[1].barrier()
+    comm = Comm(world, local_rank, "nccl")
 
     from trajoptmpcreference_amd import _native
     from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
@@ -164,7 +188,7 @@ def main():
     ctx.set_cost_quadratic(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
 
     # ---- workload resident in HBM
-    seed_base = a.seed0 + rank * B
+    seed_base = shard_seed_base(a.seed0, rank, B)
     x0 = np.zeros((B, nx, N))
     x0[:, :n, 0] = initial_states(n, B, seed_base)
     u0 = np.zeros((B, nu, N - 1))
@@ -185,16 +209,16 @@ def main():
     ctx.set_options(profile=1)
     ctx.reset_stats()
     counters = np.zeros(4, dtype=np.int64)
-    barrier()
+    comm.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
         counters += np.array(ctx.solve_counters(), dtype=np.int64)
     ctx.synchronize()
-    barrier()
+    comm.barrier()
     t1 = time.perf_counter()
-    elapsed = barrier_max(t1 - t0)
+    elapsed = comm.max(t1 - t0)
     ctx.set_options(profile=0)
 
     kernels = {}
@@ -213,8 +237,7 @@ def main():
     exit_codes, iters = ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=True)
 
     if rank != 0:
-        if dist is not None:
-            dist[1].destroy_process_group()
+        comm.close()
         return
 
     qp = kernels["qp"]
@@ -235,7 +258,7 @@ def main():
                                     "algorithmic_bytes_per_launch": alg_bytes}}
 
     cpu = None
-    if not a.no_cpu_baseline:
+    if not a.no_cpu_baseline and world == 1:
         procs = max(1, min(a.cpu_procs, os.cpu_count() or 1))
         sample = a.cpu_sample if a.cpu_sample > 0 else 2 * procs
         v, wall, res = cpu_baseline(n, N, sample, procs, a.seed0)
@@ -261,8 +284,7 @@ def main():
         "sqp_iters_mean": float(np.mean(iters)),
     }
     print(json.dumps(out))
-    if dist is not None:
-        dist[1].destroy_process_group()
+    comm.close()
 
 
 if __name__ == "__main__":
