@@ -107,6 +107,28 @@ def pcg_flops_per_iter(N, nx, method):
     return spmv + pre + 10 * N * nx
 
 
+def pcg_lds_bytes_per_iter(N, nx, method):
+    # per lane (row): SpMV reads 3 nx doubles; J/BJ/SS preconditioner reads 0 / nx / 4 nx
+    # doubles; 1 / 2 / 4 vector stores -- what the LDS array serves, broadcast or not
+    reads = 3 * nx + {"PCG-J": 0, "PCG-BJ": nx, "PCG-SS": 4 * nx}[method]
+    writes = {"PCG-J": 1, "PCG-BJ": 2, "PCG-SS": 4}[method]
+    return 8 * N * nx * (reads + writes)
+
+
+LDS_PEAK_GBS = 256 * 2.4 * 256   # 256 B/clk/CU (ds_read_b128) x 2.4 GHz x 256 CUs
+
+
+def measured_traffic(kernel_prefix):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+    if not os.path.exists(path):
+        return None
+    for k, v in json.load(open(path))["kernels"].items():
+        if k.startswith(kernel_prefix):
+            return v["hbm_bytes_per_launch"]
+    return None
+
+
 def qp_schur_flops(N, nx, nu):
     # per problem-QP: S blocks (A G A^T, B G B^T, A G), gamma, the diagonal-block inverses and dxu
     per_knot = 2 * (nx * nx * nx + nu * nu * nx + nx * nx * nx + nx * nu * nx + nx * nx * nx) + 2 * nx ** 3
@@ -250,9 +272,18 @@ def main():
     qp_avg_s = qp["avg_ms"] / 1000.0 if qp["avg_ms"] > 0 else float("nan")
     ach_gbs = alg_bytes / qp_avg_s / 1e9
     ach_tf = alg_flops / qp_avg_s / 1e12
+    lds_bytes = per_launch_iters * pcg_lds_bytes_per_iter(N, nx, a.method)
+    ach_lds = lds_bytes / qp_avg_s / 1e9
+    traffic = measured_traffic(f"void tmpc::k_qp<{n}, ")
     roofline = {"kernel": "k_qp (Schur + PCG + dxu, fused)", "bound": "mfma", "achieved": ach_tf,
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                "traffic_source": "profiles/pmc_traffic_latest.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                  "passes, 2 x FETCH + WRITE bytes per k_qp launch (gfx950 correction)",
                 "algorithmic_flops_per_launch": alg_flops, "avg_launch_ms": qp["avg_ms"],
+                "note": "fp64 VALU peak (= fp64 matrix peak on MI355X); the PCG keeps S and P^-1 in "
+                        "registers, so the binding resource is LDS bandwidth + barrier latency (lds_model)",
+                "lds_model": {"achieved": ach_lds, "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": ach_lds / LDS_PEAK_GBS,
+                              "lds_bytes_per_launch": lds_bytes},
                 "streaming_model": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                     "frac": ach_gbs / HBM_PEAK_GBS,
                                     "algorithmic_bytes_per_launch": alg_bytes}}
