@@ -231,13 +231,32 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return readlane_f64(dpp_row_sum(red[lane & 15]), 0);
 }
 
-// the rows of S (and of P_kk^-1) a lane keeps in registers for the whole solve
+// Lane geometry of the one-workgroup-per-problem kernels: RPL rows of S per
+// lane, L = NX / RPL lanes per block row; lane t owns rows i + m L (m < RPL)
+// of block k = t / L.  Two rows per lane halve the LDS traffic of every
+// vector exchange (each block vector a lane reads serves both of its rows).
+template <int NX, int RPL>
+struct PcgLane {
+  static constexpr int L = NX / RPL;
+  int t, k, i;
+  bool valid;
+  __device__ __forceinline__ PcgLane(int t_, int N) {
+    t = t_;
+    valid = t < N * L;
+    k = valid ? t / L : 0;
+    i = valid ? t - k * L : 0;
+  }
+  __device__ __forceinline__ int r(int m) const { return i + m * L; }            // row within block k
+  __device__ __forceinline__ int row(int m) const { return k * NX + i + m * L; }  // row of S
+};
+
+// one row of S (and of P_kk^-1) kept in registers for the whole solve
 template <int NX>
-struct PcgRows {
-  double sd[NX];   // S_kk row i
-  double sl[NX];   // S_{k,k-1} row i   (0 for k = 0)
-  double su[NX];   // S_{k,k+1} row i   (0 for k = N-1)
-  double pr[NX];   // (S_kk)^-1 row i  (J: pr[0] = 1 / S_ii)
+struct PcgRow {
+  double sd[NX];   // S_kk row
+  double sl[NX];   // S_{k,k-1} row   (0 for k = 0)
+  double su[NX];   // S_{k,k+1} row   (0 for k = N-1)
+  double pr[NX];   // (S_kk)^-1 row  (J: pr[0] = 1 / S_ii)
 };
 
 // LDS vectors are [pad NX | N*NX rows | pad NX]: the pads stay zero so the
@@ -246,9 +265,12 @@ struct PcgLds {
   double *pbuf, *rbuf, *wbuf, *tbuf, *xbuf, *red, *piv;
 };
 
-__host__ __device__ inline size_t pcg_vec_doubles(int N, int NX) { return (size_t)(N + 2) * NX; }
+// Fixed stride (the 1024-row maximum plus the pads) so that every buffer is a
+// compile-time offset from one per-lane address: one address VGPR for all
+// vector traffic instead of one per buffer.
+__host__ __device__ constexpr size_t pcg_vec_doubles(int /*N*/, int NX) { return (size_t)1024 + 2 * NX; }
 __host__ __device__ inline size_t pcg_lds_doubles(int N, int NX) {
-  return 5 * pcg_vec_doubles(N, NX) + 32 + (size_t)4 * N * NX;
+  return 5 * pcg_vec_doubles(N, NX) + 32 + (size_t)2 * N * NX;
 }
 
 __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
@@ -260,7 +282,7 @@ __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
   L.tbuf = L.wbuf + v;
   L.xbuf = L.tbuf + v;
   L.red = lds + 5 * v;     // 2 x 16
-  L.piv = L.red + 32;      // 2 x N x 2NX
+  L.piv = L.red + 32;      // 2 x N x NX
   return L;
 }
 
@@ -279,79 +301,128 @@ __device__ __forceinline__ void pcg_lds_clear(double* lds, int N, int NX) {
 }
 
 // compute_preconditioner (PCG.py:166-212): J -> 1/S_ii; BJ and SS -> the
-// diagonal block inverses, Gauss-Jordan with one row per lane and the pivot
-// rows broadcast through LDS (S_kk is negative definite: no pivoting needed).
-template <int NX>
-__device__ __forceinline__ void pcg_precondition(PcgRows<NX>& R, int precond, bool valid, int k, int i, int N,
-                                                 double* piv, double* Pd_row) {
+// diagonal block inverses by in-place Gauss-Jordan (one row per lane slot,
+// pivot rows broadcast through LDS; S_kk is negative definite: no pivoting).
+// In place, the row holds the not-yet-eliminated columns of [S_kk | I] and
+// the already-formed columns of the inverse; the arithmetic is operation for
+// operation that of the augmented [S_kk | I] elimination.
+template <int NX, int RPL>
+__device__ __forceinline__ void pcg_precondition(PcgRow<NX> (&R)[RPL], int precond, const PcgLane<NX, RPL>& ln,
+                                                 int N, double* piv, double* Pd_block) {
   if (precond == PRECOND_J) {
-    double dii = 1.0;
 #pragma unroll
-    for (int j = 0; j < NX; ++j)
-      if (j == i) dii = R.sd[j];
-    if (valid) R.pr[0] = 1.0 / dii;
+    for (int m = 0; m < RPL; ++m) {
+      double dii = 1.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j)
+        if (j == ln.r(m)) dii = R[m].sd[j];
+      if (ln.valid) R[m].pr[0] = 1.0 / dii;
+    }
     return;
   }
-  double aug[2 * NX];
 #pragma unroll
-  for (int j = 0; j < NX; ++j) { aug[j] = R.sd[j]; aug[NX + j] = (j == i) ? 1.0 : 0.0; }
+  for (int m = 0; m < RPL; ++m)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) R[m].pr[j] = R[m].sd[j];
 #pragma unroll
   for (int p = 0; p < NX; ++p) {
-    double* pv = piv + ((p & 1) * N + k) * 2 * NX;
-    if (valid && i == p) {
-      const double d = aug[p];
+    double* pv = piv + ((p & 1) * N + ln.k) * NX;
 #pragma unroll
-      for (int j = 0; j < 2 * NX; ++j) { aug[j] = aug[j] / d; pv[j] = aug[j]; }
+    for (int m = 0; m < RPL; ++m) {
+      if (ln.valid && ln.r(m) == p) {
+        double* a = R[m].pr;
+        const double d = a[p];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+          a[j] = (j == p) ? 1.0 / d : a[j] / d;
+          pv[j] = a[j];
+        }
+      }
     }
     __syncthreads();
-    if (valid && i != p) {
-      const double f = aug[p];
 #pragma unroll
-      for (int j = 0; j < 2 * NX; ++j) aug[j] -= f * pv[j];
+    for (int m = 0; m < RPL; ++m) {
+      if (ln.valid && ln.r(m) != p) {
+        double* a = R[m].pr;
+        const double f = a[p];
+        a[p] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) a[j] -= f * pv[j];
+      }
+    }
+  }
+  if (Pd_block && ln.valid) {
+#pragma unroll
+    for (int m = 0; m < RPL; ++m)
+#pragma unroll
+      for (int j = 0; j < NX; ++j) Pd_block[ln.r(m) * NX + j] = R[m].pr[j];
+  }
+}
+
+// out[m] = (S v) for this lane's rows, each block-vector element read once for
+// all RPL rows.  With one row per lane: three independent chains (latency);
+// with two: one chain per row (the rows interleave, and the VGPR budget of a
+// 2-waves-per-SIMD launch has no room for more accumulators).
+template <int NX, int RPL>
+__device__ __forceinline__ void pcg_spmv(const PcgRow<NX> (&R)[RPL], const double* __restrict__ v, int kb,
+                                         double (&out)[RPL]) {
+  const double* vm = v + kb - NX;
+  constexpr int NC = RPL == 1 ? 3 : 1;
+  double a[NC][RPL];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) a[c][m] = 0.0;
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    const double p0 = vm[j], p1 = vm[NX + j], p2 = vm[2 * NX + j];
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) {
+      a[0][m] += R[m].sl[j] * p0;
+      a[NC > 1 ? 1 : 0][m] += R[m].sd[j] * p1;
+      a[NC > 2 ? 2 : 0][m] += R[m].su[j] * p2;
+    }
+    // two rows per lane: bound the LDS loads in flight (each b128 holds 4
+    // VGPRs; all 18 hoisted would not fit next to the matrix rows): the
+    // accumulators are pinned here, and loads may not cross the fence
+    if (RPL > 1 && (j % 4) == 3) {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) asm volatile("" : "+v"(a[0][m])::"memory");
     }
   }
 #pragma unroll
-  for (int j = 0; j < NX; ++j) R.pr[j] = aug[NX + j];
-  if (Pd_row && valid) {
-#pragma unroll
-    for (int j = 0; j < NX; ++j) Pd_row[j] = R.pr[j];
-  }
+  for (int m = 0; m < RPL; ++m) out[m] = NC == 3 ? (a[0][m] + a[NC > 1 ? 1 : 0][m]) + a[NC > 2 ? 2 : 0][m] : a[0][m];
 }
 
-// (S v) for this lane's row: three independent accumulation chains
-template <int NX>
-__device__ __forceinline__ double pcg_spmv(const PcgRows<NX>& R, const double* __restrict__ v, int kb) {
-  const double* vm = v + kb - NX;
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+// out[m] = P_kk row . v_k
+template <int NX, int RPL>
+__device__ __forceinline__ void pcg_block_dot(const PcgRow<NX> (&R)[RPL], const double* __restrict__ v,
+                                              double (&out)[RPL]) {
+  constexpr int NC = RPL == 1 ? 2 : 1;
+  double a[NC][RPL];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) a[c][m] = 0.0;
 #pragma unroll
   for (int j = 0; j < NX; ++j) {
-    a0 += R.sl[j] * vm[j];
-    a1 += R.sd[j] * vm[NX + j];
-    a2 += R.su[j] * vm[2 * NX + j];
-  }
-  return (a0 + a1) + a2;
-}
-
-template <int NX>
-__device__ __forceinline__ double pcg_block_dot(const double* __restrict__ pr, const double* __restrict__ v) {
-  double a0 = 0.0, a1 = 0.0;
+    const double vj = v[j];
 #pragma unroll
-  for (int j = 0; j < NX; j += 2) {
-    a0 += pr[j] * v[j];
-    if (j + 1 < NX) a1 += pr[j + 1] * v[j + 1];
+    for (int m = 0; m < RPL; ++m) a[j % NC][m] += R[m].pr[j] * vj;
   }
-  return a0 + a1;
+#pragma unroll
+  for (int m = 0; m < RPL; ++m) out[m] = NC == 2 ? a[0][m] + a[NC - 1][m] : a[0][m];
 }
 
 // Diagnostic build only (-DTMPC_PCG_STAMPS, tools/pcg_microbench.py --stamps):
 // per-phase s_memtime cycle totals of the first and last wave of each
 // workgroup replace the |nu| trace; the true-residual trace is disabled.
 #ifdef TMPC_PCG_STAMPS
-#define PCG_STAMP(i)                                          \
-  do {                                                        \
+#define PCG_STAMP(i)                                            \
+  do {                                                          \
     const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
-    st_[i] += n_ - st_prev_;                                  \
-    st_prev_ = n_;                                            \
+    st_[i] += n_ - st_prev_;                                    \
+    st_prev_ = n_;                                              \
   } while (0)
 #else
 #define PCG_STAMP(i) \
@@ -359,88 +430,146 @@ __device__ __forceinline__ double pcg_block_dot(const double* __restrict__ pr, c
   } while (0)
 #endif
 
-// The CG iteration.  Returns this lane's entry of the solution.
-template <int NX, int PRE>
-__device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, bool valid, int t, int k, int N, const PcgLds& L,
-                                          double bi, bool has_guess, double guess_i, double tol, int max_iter,
-                                          double* tn, double* tr, int* iters_out) {
-  const int kb = k * NX;
+// The CG iteration (PCG.pcg, PCG.py:66-111).  x = the lane's entries of the solution.
+template <int NX, int RPL, int PRE>
+__device__ __forceinline__ void pcg_run(const PcgRow<NX> (&R)[RPL], const PcgLane<NX, RPL>& ln, int N,
+                                        const PcgLds& L, const double (&bv)[RPL], const double* guess_v, double tol,
+                                        int max_iter, double* tn, double* tr, int* iters_out, double (&xv)[RPL]) {
+  const int kb = ln.k * NX;
+  const int t = ln.t;
 #ifdef TMPC_PCG_STAMPS
   unsigned long long st_[16] = {}, st_prev_ = __builtin_amdgcn_s_memtime();
   double* const tn_st = tn;
   tn = nullptr;
   tr = nullptr;
 #endif
-  // z = P^-1 r (PCG.py:88-90)
-  auto apply_P = [&](double r_i) -> double {
-    if (PRE == PRECOND_J) return R.pr[0] * r_i;
-    if (valid) L.rbuf[t] = r_i;
-    __syncthreads();
-    PCG_STAMP(5);
-    const double w = pcg_block_dot<NX>(R.pr, L.rbuf + kb);
-    if (PRE == PRECOND_BJ) return w;
-    // SS: z = P_D (r - S_off P_D r)  ==  the symmetric-stair P^-1 r
-    if (valid) L.wbuf[t] = w;
-    __syncthreads();
-    PCG_STAMP(6);
-    const double* wm = L.wbuf + kb - NX;
-    double a0 = 0.0, a1 = 0.0;
+  auto put = [&](double* buf, const double (&v)[RPL]) {
+    if (ln.valid) {
 #pragma unroll
-    for (int j = 0; j < NX; ++j) {
-      a0 += R.sl[j] * wm[j];
-      a1 += R.su[j] * wm[2 * NX + j];
+      for (int m = 0; m < RPL; ++m) buf[ln.row(m)] = v[m];
     }
-    if (valid) L.tbuf[t] = r_i - (a0 + a1);
-    __syncthreads();
-    PCG_STAMP(7);
-    return pcg_block_dot<NX>(R.pr, L.tbuf + kb);
   };
   int rsel = 0;
-  auto reduce = [&](double v) -> double {
-    const double s = block_sum(valid ? v : 0.0, L.red + 16 * rsel);
+  auto reduce = [&](const double (&a)[RPL], const double (&b)[RPL]) -> double {
+    double s = 0.0;
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) s += a[m] * b[m];
+    s = block_sum(ln.valid ? s : 0.0, L.red + 16 * rsel);
     rsel ^= 1;
     return s;
   };
-  // x0 = guess (default zeros, PCG.py:11-12); r = b - A x0 (:76)
-  double xi = 0.0, ri = bi;
-  if (has_guess) {
-    xi = valid ? guess_i : 0.0;
-    if (valid) L.xbuf[t] = xi;
+  // z = P^-1 r (PCG.py:88-90)
+  auto apply_P = [&](const double (&r)[RPL], double (&z)[RPL]) {
+    if (PRE == PRECOND_J) {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) z[m] = R[m].pr[0] * r[m];
+      return;
+    }
+    put(L.rbuf, r);
     __syncthreads();
-    ri = bi - pcg_spmv<NX>(R, L.xbuf, kb);
+    PCG_STAMP(5);
+    double w[RPL];
+    pcg_block_dot<NX, RPL>(R, L.rbuf + kb, w);
+    if (PRE == PRECOND_BJ) {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) z[m] = w[m];
+      return;
+    }
+    // SS: z = P_D (r - S_off P_D r)  ==  the symmetric-stair P^-1 r
+    put(L.wbuf, w);
+    __syncthreads();
+    PCG_STAMP(6);
+    const double* wm = L.wbuf + kb - NX;
+    constexpr int NC = RPL == 1 ? 2 : 1;
+    double a[NC][RPL];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) a[c][m] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const double wl = wm[j], wu = wm[2 * NX + j];
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) {
+        a[0][m] += R[m].sl[j] * wl;
+        a[NC - 1][m] += R[m].su[j] * wu;
+      }
+    }
+    double tv[RPL];
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) tv[m] = r[m] - (NC == 2 ? a[0][m] + a[NC - 1][m] : a[0][m]);
+    put(L.tbuf, tv);
+    __syncthreads();
+    PCG_STAMP(7);
+    pcg_block_dot<NX, RPL>(R, L.tbuf + kb, z);
+  };
+  // x0 = guess (default zeros, PCG.py:11-12); r = b - A x0 (:76).  The iterate x
+  // lives in L.xbuf (lane-private rows): it is only read at the end, so it
+  // costs no VGPRs inside the loop.
+  double rv[RPL], zv[RPL], pv[RPL], av[RPL];
+#pragma unroll
+  for (int m = 0; m < RPL; ++m) {
+    xv[m] = (guess_v && ln.valid) ? guess_v[ln.row(m)] : 0.0;
+    rv[m] = bv[m];
+  }
+  put(L.xbuf, xv);
+  if (guess_v) {
+    __syncthreads();
+    pcg_spmv<NX, RPL>(R, L.xbuf, kb, av);
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) rv[m] = bv[m] - av[m];
     __syncthreads();
   }
-  double zi = apply_P(ri);
-  double pi = zi;
-  double nu = reduce(ri * zi);
+  // With two rows per lane the search direction p also lives only in L.pbuf
+  // (own rows re-read where needed): the VGPR budget of 2 waves per SIMD holds
+  // the 96 matrix doubles per lane and little else.
+  constexpr bool P_IN_LDS = RPL > 1;
+  auto p_own = [&](double (&o)[RPL]) {
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) o[m] = P_IN_LDS ? (ln.valid ? L.pbuf[ln.row(m)] : 0.0) : pv[m];
+  };
+  apply_P(rv, zv);
+#pragma unroll
+  for (int m = 0; m < RPL; ++m) pv[m] = zv[m];
+  double nu = reduce(rv, zv);
   auto true_residual = [&]() -> double {
     // ||b - A x|| (PCG.py:83,95), trace only
-    if (valid) L.xbuf[t] = xi;
     __syncthreads();
-    const double e = bi - pcg_spmv<NX>(R, L.xbuf, kb);
-    return sqrt(reduce(e * e));
+    double e[RPL];
+    pcg_spmv<NX, RPL>(R, L.xbuf, kb, e);
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) e[m] = bv[m] - e[m];
+    return sqrt(reduce(e, e));
   };
   if (tn && t == 0) tn[0] = fabs(nu);
   if (tr) {
     const double rn = true_residual();
     if (t == 0) tr[0] = rn;
   }
+  put(L.pbuf, pv);
   int it_done = max_iter;
   for (int it = 0; it < max_iter; ++it) {
     PCG_STAMP(0);
-    if (valid) L.pbuf[t] = pi;
+    if (!P_IN_LDS) put(L.pbuf, pv);
     __syncthreads();
     PCG_STAMP(1);
-    const double api = pcg_spmv<NX>(R, L.pbuf, kb);
-    const double pap = reduce(pi * api);
-    PCG_STAMP(2);
-    const double alpha = nu / pap;
-    ri = ri - api * alpha;
-    xi = xi + pi * alpha;
+    pcg_spmv<NX, RPL>(R, L.pbuf, kb, av);
+    {
+      double po[RPL];
+      p_own(po);
+      const double pap = reduce(po, av);
+      PCG_STAMP(2);
+      const double alpha = nu / pap;
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) {
+        rv[m] = rv[m] - av[m] * alpha;
+        if (ln.valid) L.xbuf[ln.row(m)] = L.xbuf[ln.row(m)] + po[m] * alpha;
+      }
+    }
     PCG_STAMP(3);
-    zi = apply_P(ri);
+    apply_P(rv, zv);
     PCG_STAMP(8);
-    const double nup = reduce(ri * zi);
+    const double nup = reduce(rv, zv);
     PCG_STAMP(9);
     if (tn && t == 0) tn[it + 1] = fabs(nup);
     if (tr) {
@@ -452,10 +581,20 @@ __device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, bool valid, int 
       break;
     }
     const double beta = nup / nu;
-    pi = zi + pi * beta;
+    if (P_IN_LDS) {
+      if (ln.valid) {
+#pragma unroll
+        for (int m = 0; m < RPL; ++m) L.pbuf[ln.row(m)] = zv[m] + L.pbuf[ln.row(m)] * beta;
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) pv[m] = zv[m] + pv[m] * beta;
+    }
     nu = nup;
     PCG_STAMP(10);
   }
+#pragma unroll
+  for (int m = 0; m < RPL; ++m) xv[m] = ln.valid ? L.xbuf[ln.row(m)] : 0.0;
 #ifdef TMPC_PCG_STAMPS
   if (tn_st && (t == 0 || t == ((int)blockDim.x - 1) / 64 * 64)) {
     double* o = tn_st + (t == 0 ? 0 : 16);
@@ -463,22 +602,30 @@ __device__ __forceinline__ double pcg_run(const PcgRows<NX>& R, bool valid, int 
   }
 #endif
   *iters_out = it_done;
-  return xi;
 }
 
-template <int NX>
-__device__ __forceinline__ double pcg_dispatch(int precond, const PcgRows<NX>& R, bool valid, int t, int k, int N,
-                                               const PcgLds& L, double bi, bool has_guess, double guess_i,
-                                               double tol, int max_iter, double* tn, double* tr, int* iters_out) {
+template <int NX, int RPL>
+__device__ __forceinline__ void pcg_dispatch(int precond, const PcgRow<NX> (&R)[RPL], const PcgLane<NX, RPL>& ln,
+                                             int N, const PcgLds& L, const double (&bv)[RPL], const double* guess_v,
+                                             double tol, int max_iter, double* tn, double* tr, int* iters_out,
+                                             double (&xv)[RPL]) {
   if (precond == PRECOND_J)
-    return pcg_run<NX, PRECOND_J>(R, valid, t, k, N, L, bi, has_guess, guess_i, tol, max_iter, tn, tr, iters_out);
-  if (precond == PRECOND_BJ)
-    return pcg_run<NX, PRECOND_BJ>(R, valid, t, k, N, L, bi, has_guess, guess_i, tol, max_iter, tn, tr, iters_out);
-  return pcg_run<NX, PRECOND_SS>(R, valid, t, k, N, L, bi, has_guess, guess_i, tol, max_iter, tn, tr, iters_out);
+    pcg_run<NX, RPL, PRECOND_J>(R, ln, N, L, bv, guess_v, tol, max_iter, tn, tr, iters_out, xv);
+  else if (precond == PRECOND_BJ)
+    pcg_run<NX, RPL, PRECOND_BJ>(R, ln, N, L, bv, guess_v, tol, max_iter, tn, tr, iters_out, xv);
+  else
+    pcg_run<NX, RPL, PRECOND_SS>(R, ln, N, L, bv, guess_v, tol, max_iter, tn, tr, iters_out, xv);
 }
+
+// Rows per lane for an N x NX block system.  One row per lane up to 768 rows
+// (12 waves, 3 per SIMD): measured fastest for PCG-SS at arm6 N = 64 (two rows
+// per lane halve the LDS traffic but leave 2 waves per SIMD to hide the 9-cycle
+// fp64 FMA latency, and the VGPR budget of 256 then barely holds the matrix
+// rows).  Two rows per lane (<= 8 waves) for 769..1024 rows.
+__host__ __device__ inline int pcg_rpl(int N, int NX) { return (N * NX <= 768 || (NX & 1)) ? 1 : 2; }
 
 // ---- standalone PCG on given blocks (tmpc_pcg_batch: the PCG class)
-template <int NX, int MAXT>
+template <int NX, int RPL, int MAXT>
 __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const double* __restrict__ Sd,
                                               const double* __restrict__ Sl, const double* __restrict__ Su,
                                               const double* __restrict__ gam, const double* __restrict__ guess,
@@ -490,56 +637,61 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
   const int rows = N * NX;
   pcg_lds_clear(lds, N, NX);
   const PcgLds L = pcg_lds(lds, N, NX);
-  const int t = threadIdx.x;
-  const bool valid = t < rows;
-  const int k = valid ? t / NX : 0;
-  const int i = valid ? t - k * NX : 0;
-  const int K = N - 1;
-  PcgRows<NX> R;
+  const PcgLane<NX, RPL> ln(threadIdx.x, N);
+  const int k = ln.k, K = N - 1;
+  PcgRow<NX> R[RPL];
+  double bv[RPL];
 #pragma unroll
-  for (int j = 0; j < NX; ++j) { R.sd[j] = 0.0; R.sl[j] = 0.0; R.su[j] = 0.0; R.pr[j] = 0.0; }
-  if (valid) {
+  for (int m = 0; m < RPL; ++m) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) R[m].sd[j] = R[m].sl[j] = R[m].su[j] = R[m].pr[j] = 0.0;
+    bv[m] = 0.0;
+    if (!ln.valid) continue;
+    const int i = ln.r(m);
     const double* d = Sd + (((size_t)b * N + k) * NX + i) * NX;
 #pragma unroll
-    for (int j = 0; j < NX; ++j) R.sd[j] = d[j];
+    for (int j = 0; j < NX; ++j) R[m].sd[j] = d[j];
     if (k > 0) {
       const double* l = Sl + (((size_t)b * K + (k - 1)) * NX + i) * NX;
 #pragma unroll
-      for (int j = 0; j < NX; ++j) R.sl[j] = l[j];
+      for (int j = 0; j < NX; ++j) R[m].sl[j] = l[j];
     }
     if (k < K) {
       if (Su) {
         const double* up = Su + (((size_t)b * K + k) * NX + i) * NX;
 #pragma unroll
-        for (int j = 0; j < NX; ++j) R.su[j] = up[j];
+        for (int j = 0; j < NX; ++j) R[m].su[j] = up[j];
       } else {
         const double* l = Sl + ((size_t)b * K + k) * NX * NX;
 #pragma unroll
-        for (int j = 0; j < NX; ++j) R.su[j] = l[j * NX + i];
+        for (int j = 0; j < NX; ++j) R[m].su[j] = l[j * NX + i];
       }
     }
+    bv[m] = gam[(size_t)b * rows + ln.row(m)];
   }
-  pcg_precondition<NX>(R, precond, valid, k, i, N, L.piv,
-                       Pd_out ? Pd_out + (((size_t)b * N + k) * NX + i) * NX : nullptr);
-  const double bi = valid ? gam[(size_t)b * rows + t] : 0.0;
-  const double gi = (guess && valid) ? guess[(size_t)b * rows + t] : 0.0;
+  pcg_precondition<NX, RPL>(R, precond, ln, N, L.piv, Pd_out ? Pd_out + ((size_t)b * N + k) * NX * NX : nullptr);
   int it_done = 0;
-  const double xi = pcg_dispatch<NX>(precond, R, valid, t, k, N, L, bi, guess != nullptr, gi, tol, max_iter,
-                                     trace_nu ? trace_nu + (size_t)b * (max_iter + 1) : nullptr,
-                                     trace_res ? trace_res + (size_t)b * (max_iter + 1) : nullptr, &it_done);
-  if (valid) lam[(size_t)b * rows + t] = xi;
-  if (t == 0) iters[b] = it_done;
+  double xv[RPL];
+  pcg_dispatch<NX, RPL>(precond, R, ln, N, L, bv, guess ? guess + (size_t)b * rows : nullptr, tol, max_iter,
+                        trace_nu ? trace_nu + (size_t)b * (max_iter + 1) : nullptr,
+                        trace_res ? trace_res + (size_t)b * (max_iter + 1) : nullptr, &it_done, xv);
+  if (ln.valid) {
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) lam[(size_t)b * rows + ln.row(m)] = xv[m];
+  }
+  if (threadIdx.x == 0) iters[b] = it_done;
 }
 
 // ======================================================================= fused QP kernel
 // One QP of the SQP loop for one problem per workgroup:
 //   prologue  Schur blocks (blockwise form of
-//             solveKKTSystem_Schur :419-424): lane (k, i) computes row i of
-//             S_kk, S_{k,k-1}, S_{k,k+1} and gamma_k[i] straight into registers
+//             solveKKTSystem_Schur :419-424): each lane computes its rows of
+//             S_kk, S_{k,k-1}, S_{k,k+1} and gamma_k straight into registers
 //             from A, B (qp_grad), the defects c (qp_fd) and Ghat (ginv),
 //             all staged once into LDS with coalesced loads;
 //   body      preconditioner + PCG (pcg_precondition / pcg_run);
-//   epilogue  dxu = Ghat (g - C^T lambda) (:449-452).
+//   epilogue  dxu = Ghat (g - C^T lambda) (:449-452), with C^T lambda formed
+//             once per knot in LDS.
 // S and lambda never leave the chip.
 __host__ __device__ inline size_t qp_stage_doubles(int N, int NX, int NU) {
   const size_t K = N - 1;
@@ -548,7 +700,8 @@ __host__ __device__ inline size_t qp_stage_doubles(int N, int NX, int NU) {
 
 // LDS layout of k_qp: [staging area | lambda] is reused by the PCG buffers
 // (which start at 0); the cost gradients g_k = [dx_k^T Q_k, u_k^T R] live past
-// both because they must survive the PCG.
+// both because they must survive the PCG.  In the epilogue the x / u slots of
+// the staging area hold C^T lambda.
 __host__ __device__ inline size_t qp_g_offset(int N, int NX, int NU) {
   const size_t a = qp_stage_doubles(N, NX, NU) + (size_t)N * NX;
   const size_t p = pcg_lds_doubles(N, NX);
@@ -578,7 +731,79 @@ __device__ __forceinline__ void lds_copy(double* dst, const double* __restrict__
   for (int e = threadIdx.x; e < count; e += blockDim.x) dst[e] = src[e];
 }
 
-template <int NJ, int MAXT>
+// Row i of block k of the Schur complement and gamma_k[i] into R (:419-424):
+//   S_kk = -(A G A^T + B G B^T + Ghat_x,k), S_{k,k-1} = A_{k-1} Ghat_x,k-1,
+//   S_{k,k+1} = (A_k Ghat_x,k)^T, gamma_k = c_k + [AB Ghat g]_{k-1} - (Ghat_k g_k)_x
+template <int NJ>
+__device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, const QpStage& S,
+                                               const double* __restrict__ g_lds, double c_ki, int k, int i, int N,
+                                               PcgRow<2 * NJ>& R) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int K = N - 1;
+  const double* Gu = S.G + 2 * NX * NX;
+  const double* Gxk = S.G + (use_QF(C, k, N) ? NX * NX : 0);
+  const double* gk = g_lds + k * (NX + NU);
+  double gam = c_ki;
+  {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) s += Gxk[i * NX + j] * gk[j];
+    gam -= s;
+  }
+  if (k == 0) {
+#pragma unroll
+    for (int j = 0; j < NX; ++j) R.sd[j] = -Gxk[i * NX + j];
+  } else {
+    const int km = k - 1;
+    const double* Gxm = S.G + (use_QF(C, km, N) ? NX * NX : 0);
+    const double* gm = g_lds + km * (NX + NU);
+    const double* A = S.A + km * NX * NX;
+    const double* Bm = S.B + km * NX * NU;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc += A[i * NX + m] * Gxm[m * NX + j];
+      R.sl[j] = acc;
+    }
+    double BG[NU];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NU; ++m) acc += Bm[i * NU + m] * Gu[m * NU + j];
+      BG[j] = acc;
+    }
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc += R.sl[m] * A[j * NX + m];
+#pragma unroll
+      for (int m = 0; m < NU; ++m) acc += BG[m] * Bm[j * NU + m];
+      R.sd[j] = -(acc + Gxk[i * NX + j]);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) s += R.sl[j] * gm[j];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) s += BG[j] * gm[NX + j];
+    gam += s;
+  }
+  if (k < K) {
+    const double* A = S.A + k * NX * NX;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m) acc += A[j * NX + m] * Gxk[m * NX + i];
+      R.su[j] = acc;
+    }
+  }
+  return gam;
+}
+
+template <int NJ, int RPL, int MAXT>
 __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond,
                                              const double* __restrict__ x, const double* __restrict__ u,
                                              const int* __restrict__ active, const double* __restrict__ Ginv,
@@ -593,166 +818,124 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   if (!active[b]) return;
   extern __shared__ __align__(16) double lds[];
   const int rows = N * NX;
-  const int t = threadIdx.x;
-  const bool valid = t < rows;
-  const int k = valid ? t / NX : 0;
-  const int i = valid ? t - k * NX : 0;
+  const PcgLane<NX, RPL> ln(threadIdx.x, N);
+  const int k = ln.k;
   const int K = N - 1;
   const QpStage S = qp_stage(lds, N, NX, NU);
   double* lam_lds = S.u + NU * K;
-  auto stage_in = [&]() {
-    lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
-    lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
-    lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
-    lds_copy(S.x, x + (size_t)b * NX * N, NX * N);
-    lds_copy(S.u, u + (size_t)b * NU * K, NU * K);
-  };
-  const double* Gu = S.G + 2 * NX * NX;
-  stage_in();
+  lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
+  lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
+  lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
+  lds_copy(S.x, x + (size_t)b * NX * N, NX * N);
+  lds_copy(S.u, u + (size_t)b * NU * K, NU * K);
   __syncthreads();
 
-  // cost gradients g_k = [(x_k - xg)^T Q_k, u_k^T R] (QuadraticCost.gradient, TrajoptCost.py:58-69):
-  // lane (k, i) computes entry i (and entry NX + i of the control part for i < NU)
+  // cost gradients g_k = [(x_k - xg)^T Q_k, u_k^T R] (QuadraticCost.gradient, TrajoptCost.py:58-69)
   double* g_lds = lds + qp_g_offset(N, NX, NU);    // [N][NX + NU]
-  if (valid) {
-    const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
+  for (int e = threadIdx.x; e < N * (NX + NU); e += blockDim.x) {
+    const int kk = e / (NX + NU), c = e - kk * (NX + NU);
     double g = 0.0;
+    if (c < NX) {
+      const double* Qk = use_QF(C, kk, N) ? C->QF : C->Q;
 #pragma unroll
-    for (int m = 0; m < NX; ++m) g += (S.x[m * N + k] - C->xg[m]) * Qk[m * NX + i];
-    g_lds[k * (NX + NU) + i] = g;
-    if (i < NU && k < K) {
-      double gu = 0.0;
+      for (int m = 0; m < NX; ++m) g += (S.x[m * N + kk] - C->xg[m]) * Qk[m * NX + c];
+    } else if (kk < K) {
 #pragma unroll
-      for (int m = 0; m < NU; ++m) gu += S.u[m * K + k] * C->R[m * NU + i];
-      g_lds[k * (NX + NU) + NX + i] = gu;
+      for (int m = 0; m < NU; ++m) g += S.u[m * K + kk] * C->R[m * NU + (c - NX)];
     }
+    g_lds[e] = g;
   }
   __syncthreads();
 
-  PcgRows<NX> R;
+  PcgRow<NX> R[RPL];
+  double bv[RPL];
 #pragma unroll
-  for (int j = 0; j < NX; ++j) { R.sd[j] = 0.0; R.sl[j] = 0.0; R.su[j] = 0.0; R.pr[j] = 0.0; }
-  double bi = 0.0;
-  if (valid) {
-    const double* Gxk = S.G + (use_QF(C, k, N) ? NX * NX : 0);
-    const double* gk = g_lds + k * (NX + NU);
-    // gamma_k[i] = c_k[i] + [AB Ghat g]_{k-1} - (Ghat_k g_k)_x[i]
-    double gam = cvec[(size_t)b * N * NX + k * NX + i];
-    {
-      double s = 0.0;
+  for (int m = 0; m < RPL; ++m) {
 #pragma unroll
-      for (int j = 0; j < NX; ++j) s += Gxk[i * NX + j] * gk[j];
-      gam -= s;
-    }
-    if (k == 0) {
-#pragma unroll
-      for (int j = 0; j < NX; ++j) R.sd[j] = -Gxk[i * NX + j];
-    } else {
-      const int km = k - 1;
-      const double* Gxm = S.G + (use_QF(C, km, N) ? NX * NX : 0);
-      const double* gm = g_lds + km * (NX + NU);
-      const double* A = S.A + km * NX * NX;
-      const double* Bm = S.B + km * NX * NU;
-      // S_{k,k-1} row i = (A_{k-1} Ghat_x)[i, :]
-#pragma unroll
-      for (int j = 0; j < NX; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < NX; ++m) acc += A[i * NX + m] * Gxm[m * NX + j];
-        R.sl[j] = acc;
-      }
-      double BG[NU];
-#pragma unroll
-      for (int j = 0; j < NU; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < NU; ++m) acc += Bm[i * NU + m] * Gu[m * NU + j];
-        BG[j] = acc;
-      }
-      // S_kk row i = -(A G A^T + B G B^T + Ghat_x,k)[i, :]
-#pragma unroll
-      for (int j = 0; j < NX; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < NX; ++m) acc += R.sl[m] * A[j * NX + m];
-#pragma unroll
-        for (int m = 0; m < NU; ++m) acc += BG[m] * Bm[j * NU + m];
-        R.sd[j] = -(acc + Gxk[i * NX + j]);
-      }
-      // + (A G g)[i] with g_{k-1} = [dx^T Q, u^T R]
-      double s = 0.0;
-#pragma unroll
-      for (int j = 0; j < NX; ++j) s += R.sl[j] * gm[j];
-#pragma unroll
-      for (int j = 0; j < NU; ++j) s += BG[j] * gm[NX + j];
-      gam += s;
-    }
-    if (k < K) {
-      // S_{k,k+1} row i = S_{k+1,k}^T row i = (A_k Ghat_x,k)[:, i]
-      const double* A = S.A + k * NX * NX;
-#pragma unroll
-      for (int j = 0; j < NX; ++j) {
-        double acc = 0.0;
-#pragma unroll
-        for (int m = 0; m < NX; ++m) acc += A[j * NX + m] * Gxk[m * NX + i];
-        R.su[j] = acc;
-      }
-    }
-    bi = gam;
+    for (int j = 0; j < NX; ++j) R[m].sd[j] = R[m].sl[j] = R[m].su[j] = R[m].pr[j] = 0.0;
+    bv[m] = 0.0;
+    if (!ln.valid) continue;
+    const int i = ln.r(m);
+    bv[m] = qp_schur_row<NJ>(C, S, g_lds, cvec[(size_t)b * N * NX + k * NX + i], k, i, N, R[m]);
     if (Sd_out) {
 #pragma unroll
-      for (int j = 0; j < NX; ++j) Sd_out[(((size_t)b * N + k) * NX + i) * NX + j] = R.sd[j];
+      for (int j = 0; j < NX; ++j) Sd_out[(((size_t)b * N + k) * NX + i) * NX + j] = R[m].sd[j];
       if (k > 0) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) Sl_out[(((size_t)b * K + k - 1) * NX + i) * NX + j] = R.sl[j];
+        for (int j = 0; j < NX; ++j) Sl_out[(((size_t)b * K + k - 1) * NX + i) * NX + j] = R[m].sl[j];
       }
-      gam_out[(size_t)b * rows + t] = gam;
+      gam_out[(size_t)b * rows + ln.row(m)] = bv[m];
     }
   }
   __syncthreads();   // the PCG buffers alias the staging area
   pcg_lds_clear(lds, N, NX);
   const PcgLds L = pcg_lds(lds, N, NX);
-  pcg_precondition<NX>(R, precond, valid, k, i, N, L.piv,
-                       Pd_out ? Pd_out + (((size_t)b * N + k) * NX + i) * NX : nullptr);
+  pcg_precondition<NX, RPL>(R, precond, ln, N, L.piv, Pd_out ? Pd_out + ((size_t)b * N + k) * NX * NX : nullptr);
   int it_done = 0;
-  const double xi = pcg_dispatch<NX>(precond, R, valid, t, k, N, L, bi, false, 0.0, tol, max_iter, nullptr, nullptr,
-                                     &it_done);
-  if (t == 0) iters[b] = it_done;
-  // ---- epilogue: dxu = Ghat (g - C^T lambda), operands re-staged into LDS
+  double xv[RPL];
+  pcg_dispatch<NX, RPL>(precond, R, ln, N, L, bv, nullptr, tol, max_iter, nullptr, nullptr, &it_done, xv);
+  if (threadIdx.x == 0) iters[b] = it_done;
+
+  // ---- epilogue: dxu = Ghat (g - C^T lambda); A, B, Ghat re-staged into LDS
   __syncthreads();
-  stage_in();
-  if (valid) {
-    lam_lds[t] = xi;
-    if (lam_out) lam_out[(size_t)b * rows + t] = xi;
+  lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
+  lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
+  lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
+  if (ln.valid) {
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) {
+      lam_lds[ln.row(m)] = xv[m];
+      if (lam_out) lam_out[(size_t)b * rows + ln.row(m)] = xv[m];
+    }
   }
   __syncthreads();
-  if (valid) {
-    const double* Gxk = S.G + (use_QF(C, k, N) ? NX * NX : 0);
-    const double* lk = lam_lds + k * NX;
-    const double* gk = g_lds + k * (NX + NU);
-    const double* A = S.A + (k < K ? k : 0) * NX * NX;
-    double acc = 0.0;
-#pragma unroll
-    for (int j = 0; j < NX; ++j) {
+  // C^T lambda per knot: x part lambda_k - A_k^T lambda_{k+1} (terminal: lambda_{N-1}),
+  // u part -B_k^T lambda_{k+1}; stored in the (dead) x / u staging slots
+  double* ctl_x = S.x;   // [N][NX]
+  double* ctl_u = S.u;   // [K][NU]
+  for (int e = threadIdx.x; e < N * NX + K * NU; e += blockDim.x) {
+    if (e < N * NX) {
+      const int kk = e / NX, j = e - kk * NX;
       double atl = 0.0;
-      if (k < K) {
+      if (kk < K) {
+        const double* A = S.A + kk * NX * NX;
+        const double* l1 = lam_lds + (kk + 1) * NX;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) atl += A[m * NX + j] * lk[NX + m];
+        for (int m = 0; m < NX; ++m) atl += A[m * NX + j] * l1[m];
       }
-      acc += Gxk[i * NX + j] * (gk[j] - (lk[j] - atl));
+      ctl_x[e] = lam_lds[e] - atl;
+    } else {
+      const int f = e - N * NX;
+      const int kk = f / NU, j = f - kk * NU;
+      const double* Bm = S.B + kk * NX * NU;
+      const double* l1 = lam_lds + (kk + 1) * NX;
+      double btl = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m) btl += Bm[m * NU + j] * l1[m];
+      ctl_u[f] = -btl;
     }
-    dx[((size_t)b * N + k) * NX + i] = acc;
-    if (k < K && i < NU) {
-      const double* Bm = S.B + k * NX * NU;
-      double accu = 0.0;
+  }
+  __syncthreads();
+  const double* Gu = S.G + 2 * NX * NX;
+  for (int e = threadIdx.x; e < N * NX + K * NU; e += blockDim.x) {
+    if (e < N * NX) {
+      const int kk = e / NX, i = e - kk * NX;
+      const double* Gxk = S.G + (use_QF(C, kk, N) ? NX * NX : 0);
+      const double* gk = g_lds + kk * (NX + NU);
+      const double* ck = ctl_x + kk * NX;
+      double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < NU; ++j) {
-        double btl = 0.0;
+      for (int j = 0; j < NX; ++j) acc += Gxk[i * NX + j] * (gk[j] - ck[j]);
+      dx[(size_t)b * N * NX + e] = acc;
+    } else {
+      const int f = e - N * NX;
+      const int kk = f / NU, i = f - kk * NU;
+      const double* gk = g_lds + kk * (NX + NU) + NX;
+      const double* ck = ctl_u + kk * NU;
+      double acc = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) btl += Bm[m * NU + j] * lk[NX + m];
-        accu += Gu[i * NU + j] * (gk[NX + j] - (-btl));
-      }
-      du[((size_t)b * K + k) * NU + i] = accu;
+      for (int j = 0; j < NU; ++j) acc += Gu[i * NU + j] * (gk[j] - ck[j]);
+      du[(size_t)b * K * NU + f] = acc;
     }
   }
 }
@@ -971,13 +1154,14 @@ struct LaunchNJ {
                  double* Pd) {
     constexpr int NX = 2 * NJ;
     const int rows = N * NX;
-    const int threads = ((rows + 63) / 64) * 64;
+    const int rpl = pcg_rpl(N, NX);
+    const int threads = ((rows / rpl + 63) / 64) * 64;
     const size_t lds = qp_lds_doubles(N, NX, NJ) * sizeof(double);
-    if (threads <= 768)
-      hipLaunchKernelGGL((k_qp<NJ, 768>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
+    if (rpl == 1)
+      hipLaunchKernelGGL((k_qp<NJ, 1, 768>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
                          cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
     else
-      hipLaunchKernelGGL((k_qp<NJ, 1024>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
+      hipLaunchKernelGGL((k_qp<NJ, 2, 512>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
                          cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
   }
 };
@@ -985,14 +1169,14 @@ struct LaunchNJ {
 int pcg_set_max_lds() {
   const int bytes = 160 * 1024;
   int err = 0;
-#define SETA(V)                                                                                                 \
-  err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 768>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
-  err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#define SETA(V)                                                                                                    \
+  err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 1, 768>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
+  err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 2, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
   SETA(2) SETA(4) SETA(6) SETA(8) SETA(10) SETA(12) SETA(14) SETA(16)
 #undef SETA
-#define SETQ(V)                                                                                                \
-  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 768>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
-  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#define SETQ(V)                                                                                                   \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1, 768>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 2, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
   SETQ(1) SETQ(2) SETQ(3) SETQ(4) SETQ(5) SETQ(6) SETQ(7)
 #undef SETQ
   return err;
@@ -1003,14 +1187,15 @@ static void launch_pcg_nx(hipStream_t s, int B, int N, int precond, const double
                           const double* Su, const double* gam, const double* guess, double tol, int max_iter,
                           double* lam, int* iters, double* tnu, double* tres, double* Pd) {
   const int rows = N * NX;
-  const int threads = ((rows + 63) / 64) * 64;
+  const int rpl = pcg_rpl(N, NX);
+  const int threads = ((rows / rpl + 63) / 64) * 64;
   const size_t lds = pcg_lds_doubles(N, NX) * sizeof(double);
-  if (threads <= 768)
-    hipLaunchKernelGGL((k_pcg<NX, 768>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess, tol,
-                       max_iter, lam, iters, tnu, tres, Pd);
+  if (rpl == 1)
+    hipLaunchKernelGGL((k_pcg<NX, 1, 768>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess,
+                       tol, max_iter, lam, iters, tnu, tres, Pd);
   else
-    hipLaunchKernelGGL((k_pcg<NX, 1024>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess, tol,
-                       max_iter, lam, iters, tnu, tres, Pd);
+    hipLaunchKernelGGL((k_pcg<NX, 2, 512>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess,
+                       tol, max_iter, lam, iters, tnu, tres, Pd);
 }
 
 int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
