@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--links", type=int, default=6)
     ap.add_argument("--method", default="PCG-SS")
     ap.add_argument("--seed0", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 2 per core)")
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
     ap.add_argument("--cpu-procs", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -291,7 +291,7 @@ def main():
     cpu = None
     if not a.no_cpu_baseline and world == 1:
         procs = max(1, min(a.cpu_procs, os.cpu_count() or 1))
-        sample = a.cpu_sample if a.cpu_sample > 0 else 2 * procs
+        sample = a.cpu_sample if a.cpu_sample > 0 else 40 * procs
         v, wall, res = cpu_baseline(n, N, sample, procs, a.seed0)
         cpu = {"value": v, "unit": "solves/s", "cores": procs, "kind": "port",
                "sample": f"{sample} problems of the same workload (seeds {a.seed0}..{a.seed0 + sample - 1}), "

@@ -39,7 +39,7 @@ extern "C" {
 #define TMPC_ABI_VERSION 1
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). N (dense KKT) is not offered on the GPU. */
-#define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (not yet on GPU: returns error) */
+#define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
 #define TMPC_LINSYS_PCG_J 2  /* PCG, Jacobi preconditioner            PCG.py:168-169 */
 #define TMPC_LINSYS_PCG_BJ 3 /* PCG, block-Jacobi preconditioner      PCG.py:171-179 */
 #define TMPC_LINSYS_PCG_SS 4 /* PCG, symmetric-stair preconditioner   PCG.py:181-212 */

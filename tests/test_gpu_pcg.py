@@ -68,6 +68,23 @@ def test_qp_matches_reference(ctx, name, N, pre):
     assert _rel(r["dxul"][0], d[f"dxul_{pre}"]) < (1e-5 if pre == "J" else 1e-7)
 
 
+@pytest.mark.parametrize("name,N", CASES)
+def test_qp_direct_matches_reference(ctx, name, N):
+    """Method S (solveKKTSystem_Schur use_PCG=False, :441-446): the reference's
+    np.linalg.solve on the dense S vs the GPU block-tridiagonal solve (k_btsolve)."""
+    d = golden(f"qp_{name}_N{N}.npz")
+    m = arm_model(name)
+    ctx.set_model(m)
+    ctx.set_cost_quadratic(*quad_cost_arrays(m.n))
+    r = ctx.qp_batch(d["x"][None], d["u"][None], N, float(d["dt"]), float(d["rho"]), "S")
+    assert _rel(r["S_diag"][0], d["S_diag"]) < 1e-11
+    assert _rel(r["gamma"][0], d["gamma"]) < 1e-11
+    assert int(r["pcg_iters"][0]) == 0
+    nz = r["dxul"][0].size - d["lam_direct"].size
+    assert _rel(r["dxul"][0][nz:], d["lam_direct"]) < 1e-9
+    assert _rel(r["dxul"][0], d["dxul_direct"]) < 1e-9
+
+
 def test_pcg_batch_matches_singles(ctx):
     """Problems are independent: a batch equals the problems solved one by one (bitwise)."""
     d = golden("qp_arm3_N32.npz")

@@ -43,7 +43,7 @@ def _solver(name):
     return TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(n)))
 
 
-@pytest.mark.parametrize("f", [f for f in FILES if _parse(f)[3] != "S"], ids=lambda f: os.path.basename(f))
+@pytest.mark.parametrize("f", FILES, ids=lambda f: os.path.basename(f))
 def test_sqp_matches_reference(f):
     name, N, seed, method = _parse(f)
     d = np.load(f)
@@ -59,7 +59,9 @@ def test_sqp_matches_reference(f):
     assert [t["line_search_iteration"] for t in tr] == list(d["tr_line_search_iteration"].astype(int))
     assert [t["succeeded_line_search"] for t in tr] == list(d["tr_succeeded_line_search"].astype(bool))
     ours = [t["inner_iters"] for t in tr[1:]]
-    if method == "PCG-J":
+    if method == "S":
+        assert ours == [0] * len(ours)   # direct solve: no PCG iterations
+    elif method == "PCG-J":
         assert ours[0] == int(d["pcg_iters"][0])
         assert all(abs(a - int(b)) <= 1 for a, b in zip(ours, d["pcg_iters"]))
     else:
@@ -75,20 +77,22 @@ def test_sqp_matches_reference(f):
     assert float(np.max(np.abs(u - d["u"]))) < rtol * scale
 
 
-@pytest.mark.parametrize("name,N,B", [("arm3", 32, 64), ("arm6fix", 64, 16)])
-def test_sqp_batch_matches_oracle(ctx, name, N, B):
+@pytest.mark.parametrize("name,N,B,method", [("arm3", 32, 64, "PCG-SS"), ("arm6fix", 64, 16, "PCG-SS"),
+                                             ("arm3", 32, 32, "S"), ("arm6fix", 64, 8, "S")])
+def test_sqp_batch_matches_oracle(ctx, name, N, B, method):
     """A batch of §8d problems (seeds 100..100+B) against the oracle, problem by problem."""
     from oracle import sqp as osqp
     m = arm_model(name)
     solver = _solver(name)
     xs, us = zip(*[osqp.initial_problem(m, N, 0.1, 100 + i) for i in range(B)])
-    r = solver.SQP_batch(np.array(xs), np.array(us), N, 0.1, "PCG-SS", {})
+    r = solver.SQP_batch(np.array(xs), np.array(us), N, 0.1, method, {})
     cost = osqp.QuadCost(*quad_cost_arrays(m.n))
     mism = 0
     for i in range(B):
-        o = osqp.sqp(m, cost, xs[i], us[i], N, 0.1, "PCG-SS")
+        o = osqp.sqp(m, cost, xs[i], us[i], N, 0.1, method)
+        ref_pcg = o["pcg_iters"] if method != "S" else [0] * o["sqp_iter"]
         same = (int(r["exit_sqp"][i]) == o["exit_sqp"] and int(r["sqp_iter"][i]) == o["sqp_iter"]
-                and list(r["trace"]["pcg_iters"][i, 1:o["sqp_iter"] + 1]) == o["pcg_iters"])
+                and list(r["trace"]["pcg_iters"][i, 1:o["sqp_iter"] + 1]) == ref_pcg)
         if same:
             scale = max(1.0, float(np.max(np.abs(o["x"]))))
             assert float(np.max(np.abs(r["x"][i] - o["x"]))) < 1e-6 * scale

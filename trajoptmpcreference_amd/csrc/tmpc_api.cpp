@@ -176,8 +176,10 @@ static std::vector<double> alpha_list(const tmpc_options& o) {
   return a;
 }
 
+// 0 = method S (direct block-tridiagonal solve, k_btsolve)
 static int precond_of(int linsys) {
   switch (linsys) {
+    case TMPC_LINSYS_S: return 0;
     case TMPC_LINSYS_PCG_J: return PRECOND_J;
     case TMPC_LINSYS_PCG_BJ: return PRECOND_BJ;
     case TMPC_LINSYS_PCG_SS: return PRECOND_SS;
@@ -204,6 +206,7 @@ static int check_ready(tmpc_ctx* ctx, int B, int N) {
 struct Work {
   double *xs, *qdd, *minv, *cvec, *A, *Bm, *G, *Sd, *Sl, *gam, *lam, *dx, *du, *Pd;
   int* iters;
+  double *U, *Y;   // method S scratch (k_btsolve)
 };
 
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
@@ -228,12 +231,29 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     Timed t(ctx, "ginv");
     LAUNCH_OK(launch_ginv(ctx->stream, nj, ctx->dcost, B, st.rho, st.active, w.G));
   }
+  if (precond == 0) {   // method S: Schur blocks -> direct solve -> dxu
+    {
+      Timed t(ctx, "schur");
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, w.G,
+                          w.A, w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, nullptr, w.Sd, w.Sl, w.gam, nullptr));
+    }
+    {
+      Timed t(ctx, "btsolve");
+      LAUNCH_OK(launch_btsolve(ctx->stream, 2 * nj, B, N, st.active, w.Sd, w.Sl, w.gam, w.U, w.Y, w.lam));
+    }
+    {
+      Timed t(ctx, "dxu");
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, w.G, w.A,
+                          w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, w.lam, nullptr, nullptr, nullptr, nullptr));
+    }
+    return 0;
+  }
   {
     Timed t(ctx, "qp");
-    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, precond, d_x, d_u, st.active, w.G, w.A, w.Bm, w.cvec,
-                        ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx, w.du,
-                        keep_blocks ? w.lam : nullptr, keep_blocks ? w.Sd : nullptr, keep_blocks ? w.Sl : nullptr,
-                        keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr));
+    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, precond, QP_MODE_PCG, d_x, d_u, st.active, w.G, w.A,
+                        w.Bm, w.cvec, ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx,
+                        w.du, keep_blocks ? w.lam : nullptr, keep_blocks ? w.Sd : nullptr,
+                        keep_blocks ? w.Sl : nullptr, keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr));
   }
   return 0;
 }
@@ -250,7 +270,8 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   BUF(double, dx, (size_t)B * N * nx);
   BUF(double, du, (size_t)B * K * nj);
   BUF(int, iters, (size_t)B);
-  w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters};
+  w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters,
+           nullptr, nullptr};
   if (with_blocks) {
     BUF(double, Sdiag, (size_t)B * N * nx * nx);
     BUF(double, Slo, (size_t)B * (K > 0 ? K : 1) * nx * nx);
@@ -262,6 +283,10 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
     w.gam = gam;
     w.lam = lam;
     w.Pd = Pdiag;
+    BUF(double, btU, (size_t)B * (K > 0 ? K : 1) * nx * nx);
+    BUF(double, btY, (size_t)B * N * nx);
+    w.U = btU;
+    w.Y = btY;
   }
   return 0;
 }
@@ -302,7 +327,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   if (rc) return rc;
   const int precond = precond_of(linsys);
   if (precond < 0)
-    return fail(ctx, "linear system method %d is not available on the GPU (use PCG-J/BJ/SS = 2/3/4)", linsys);
+    return fail(ctx, "linear system method %d is not available on the GPU (use S/PCG-J/BJ/SS = 1/2/3/4)", linsys);
   const int nj = ctx->hmodel.n, nx = 2 * nj;
   const bool chain = ctx->hmodel.chain != 0;
   const tmpc_options& o = ctx->opts;
@@ -311,7 +336,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   const int T = (int)al.size();
   const int W = o.max_iter_SQP_DDP + 1;
   Work w;
-  if ((rc = alloc_work(ctx, B, N, w, false))) return rc;
+  if ((rc = alloc_work(ctx, B, N, w, precond == 0))) return rc;
   ProbState st;
   if ((rc = alloc_state(ctx, B, st))) return rc;
   TraceDev tr;
@@ -666,7 +691,7 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   if (S_diag) HIP_OK(hipMemcpy(S_diag, w.Sd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
   if (S_lo) HIP_OK(hipMemcpy(S_lo, w.Sl, sizeof(double) * B * K * nx * nx, hipMemcpyDeviceToHost));
   if (gamma) HIP_OK(hipMemcpy(gamma, w.gam, sizeof(double) * B * N * nx, hipMemcpyDeviceToHost));
-  if (P_diag && precond != PRECOND_J)
+  if (P_diag && precond != PRECOND_J && precond != 0)
     HIP_OK(hipMemcpy(P_diag, w.Pd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
   return 0;
 }

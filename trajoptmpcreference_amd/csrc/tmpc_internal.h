@@ -10,6 +10,7 @@ namespace tmpc {
 
 enum { PRECOND_J = 1, PRECOND_BJ = 2, PRECOND_SS = 3 };
 enum { LS_MODE_INIT = 0, LS_MODE_STEP = 1 };
+enum { QP_MODE_PCG = 0, QP_MODE_SCHUR = 1, QP_MODE_DXU = 2 };
 
 // set_default_options (TrajoptMPCReference.py:91-115) + the fixed merit
 // weight mu = 10 (:545-546)
@@ -73,13 +74,16 @@ int launch_unit_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int K
 int launch_rollout(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, double* x,
                    const double* u);
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G);
-int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, const double* x, const double* u,
+int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, int mode, const double* x,
+              const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
               double* Pd);
 int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
                const double* Su, const double* gam, const double* guess, double tol, int max_iter, double* lam,
                int* iters, double* tnu, double* tres, double* Pd);
+int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const double* Sd, const double* Sl,
+                   const double* gam, double* U, double* Y, double* lam);
 int pcg_set_max_lds();
 void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,

@@ -803,8 +803,12 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
   return gam;
 }
 
+// mode: QP_MODE_PCG   prologue + PCG + epilogue (the fused path);
+//       QP_MODE_SCHUR prologue only: S blocks and gamma to Sd_out / Sl_out / gam_out
+//                     (method S: the direct solve k_btsolve runs next);
+//       QP_MODE_DXU   epilogue only, lambda read from lam_out (method S, after k_btsolve).
 template <int NJ, int RPL, int MAXT>
-__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond,
+__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond, int mode,
                                              const double* __restrict__ x, const double* __restrict__ u,
                                              const int* __restrict__ active, const double* __restrict__ Ginv,
                                              const double* __restrict__ Aall, const double* __restrict__ Ball,
@@ -847,6 +851,12 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   }
   __syncthreads();
 
+  double xv[RPL];
+  if (mode == QP_MODE_DXU) {
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) xv[m] = ln.valid ? lam_out[(size_t)b * rows + ln.row(m)] : 0.0;
+    if (threadIdx.x == 0) iters[b] = 0;
+  } else {
   PcgRow<NX> R[RPL];
   double bv[RPL];
 #pragma unroll
@@ -867,14 +877,18 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
       gam_out[(size_t)b * rows + ln.row(m)] = bv[m];
     }
   }
+  if (mode == QP_MODE_SCHUR) {
+    if (threadIdx.x == 0) iters[b] = 0;
+    return;
+  }
   __syncthreads();   // the PCG buffers alias the staging area
   pcg_lds_clear(lds, N, NX);
   const PcgLds L = pcg_lds(lds, N, NX);
   pcg_precondition<NX, RPL>(R, precond, ln, N, L.piv, Pd_out ? Pd_out + ((size_t)b * N + k) * NX * NX : nullptr);
   int it_done = 0;
-  double xv[RPL];
   pcg_dispatch<NX, RPL>(precond, R, ln, N, L, bv, nullptr, tol, max_iter, nullptr, nullptr, &it_done, xv);
   if (threadIdx.x == 0) iters[b] = it_done;
+  }
 
   // ---- epilogue: dxu = Ghat (g - C^T lambda); A, B, Ghat re-staged into LDS
   __syncthreads();
@@ -885,7 +899,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
 #pragma unroll
     for (int m = 0; m < RPL; ++m) {
       lam_lds[ln.row(m)] = xv[m];
-      if (lam_out) lam_out[(size_t)b * rows + ln.row(m)] = xv[m];
+      if (lam_out && mode == QP_MODE_PCG) lam_out[(size_t)b * rows + ln.row(m)] = xv[m];
     }
   }
   __syncthreads();
@@ -937,6 +951,115 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
       for (int j = 0; j < NU; ++j) acc += Gu[i * NU + j] * (gk[j] - ck[j]);
       du[(size_t)b * K * NU + f] = acc;
     }
+  }
+}
+
+// ======================================================================= method S: direct block-tridiagonal solve
+// solveKKTSystem_Schur with use_PCG = False (TrajoptMPCReference.py:441-446)
+// solves S lambda = gamma by np.linalg.solve on the dense S.  S is exactly
+// block-tridiagonal and negative definite, so the block
+// Thomas recursion needs no pivoting:
+//   D_0 = S_00, e_0 = gamma_0;   D_k = S_kk - S_{k,k-1} U_{k-1},  e_k = gamma_k - S_{k,k-1} y_{k-1}
+//   [U_k | y_k] = D_k^-1 [S_{k,k+1} | e_k]                         (Gauss-Jordan)
+//   lambda_{N-1} = y_{N-1},   lambda_k = y_k - U_k lambda_{k+1}
+// One wave per problem, one lane per column of the augmented block
+// [D_k | S_{k,k+1} | e_k] (2 NX + 1 <= 64 lanes).  The pivot column is
+// broadcast with readlane, so the elimination is register-only; the S_{k,k-1}
+// entries are wave-uniform (scalar loads).  U_k and y_k go to a per-problem
+// scratch for the back substitution.
+template <int NX>
+__global__ void __launch_bounds__(64) k_btsolve(int N, const int* __restrict__ active, const double* __restrict__ Sd,
+                                                const double* __restrict__ Sl, const double* __restrict__ gam,
+                                                double* __restrict__ U, double* __restrict__ Y,
+                                                double* __restrict__ lam) {
+  static_assert(2 * NX + 1 <= 64, "augmented block must fit one wave");
+  const int b = blockIdx.x;
+  if (!active[b]) return;
+  const int t = threadIdx.x;
+  const int K = N - 1;
+  const double* sd = Sd + (size_t)b * N * NX * NX;
+  const double* sl = Sl + (size_t)b * (K > 0 ? K : 1) * NX * NX;
+  const double* gm = gam + (size_t)b * N * NX;
+  double* Ub = U + (size_t)b * (K > 0 ? K : 1) * NX * NX;
+  double* Yb = Y + (size_t)b * N * NX;
+  double a[NX], prev[NX];
+#pragma unroll
+  for (int r = 0; r < NX; ++r) prev[r] = 0.0;
+  for (int k = 0; k < N; ++k) {
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+      double v = 0.0;
+      if (t < NX)
+        v = sd[((size_t)k * NX + r) * NX + t];
+      else if (t < 2 * NX)
+        v = k < K ? sl[((size_t)k * NX + (t - NX)) * NX + r] : 0.0;   // S_{k,k+1}[r][c] = S_{k+1,k}[c][r]
+      else if (t == 2 * NX)
+        v = gm[k * NX + r];
+      a[r] = v;
+    }
+    if (k > 0 && (t < NX || t == 2 * NX)) {
+      const double* L = sl + (size_t)(k - 1) * NX * NX;   // S_{k,k-1}, wave-uniform
+#pragma unroll
+      for (int r = 0; r < NX; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) acc += L[r * NX + m] * prev[m];
+        a[r] -= acc;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < NX; ++p) {
+      double f[NX];
+#pragma unroll
+      for (int r = 0; r < NX; ++r) f[r] = readlane_f64(a[r], p);
+      const double inv = 1.0 / f[p];
+      a[p] *= inv;
+#pragma unroll
+      for (int r = 0; r < NX; ++r)
+        if (r != p) a[r] -= f[r] * a[p];
+    }
+    if (t >= NX && t < 2 * NX && k < K) {
+#pragma unroll
+      for (int r = 0; r < NX; ++r) Ub[((size_t)k * NX + r) * NX + (t - NX)] = a[r];
+    }
+    if (t == 2 * NX) {
+#pragma unroll
+      for (int r = 0; r < NX; ++r) Yb[k * NX + r] = a[r];
+    }
+    // U_k column c moves to lane c for the next D; lane 2 NX keeps y_k
+    const int src = t < NX ? t + NX : t;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+      const int lo = __shfl(__double2loint(a[r]), src, 64);
+      const int hi = __shfl(__double2hiint(a[r]), src, 64);
+      prev[r] = __hiloint2double(hi, lo);
+    }
+  }
+  __threadfence();
+  // back substitution, lane r < NX owns row r of lambda_k
+  double* lb = lam + (size_t)b * N * NX;
+  double lv = (t < NX) ? Yb[K * NX + t] : 0.0;
+  if (t < NX) lb[K * NX + t] = lv;
+  for (int k = K - 1; k >= 0; --k) {
+    double ur[NX];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) ur[c] = t < NX ? Ub[((size_t)k * NX + t) * NX + c] : 0.0;
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < NX; ++c) acc += ur[c] * readlane_f64(lv, c);
+    lv = (t < NX) ? Yb[k * NX + t] - acc : 0.0;
+    if (t < NX) lb[k * NX + t] = lv;
+  }
+}
+
+int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const double* Sd, const double* Sl,
+                   const double* gam, double* U, double* Y, double* lam) {
+  switch (nx) {
+#define CASE_BT(V) \
+  case V: hipLaunchKernelGGL((k_btsolve<V>), dim3(B), dim3(64), 0, s, N, active, Sd, Sl, gam, U, Y, lam); return 0;
+    CASE_BT(2) CASE_BT(4) CASE_BT(6) CASE_BT(8) CASE_BT(10) CASE_BT(12) CASE_BT(14)
+#undef CASE_BT
+    default: return -2;
   }
 }
 
@@ -1148,7 +1271,7 @@ struct LaunchNJ {
   static void ginv(hipStream_t s, const CostDev* C, int B, const double* rho, const int* active, double* G) {
     hipLaunchKernelGGL((k_ginv<NJ>), TMPC_GRID(B * 3 * 16, 64), 0, s, C, B, rho, active, G);
   }
-  static void qp(hipStream_t s, const CostDev* C, int B, int N, int precond, const double* x, const double* u,
+  static void qp(hipStream_t s, const CostDev* C, int B, int N, int precond, int mode, const double* x, const double* u,
                  const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
                  int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
                  double* Pd) {
@@ -1158,11 +1281,11 @@ struct LaunchNJ {
     const int threads = ((rows / rpl + 63) / 64) * 64;
     const size_t lds = qp_lds_doubles(N, NX, NJ) * sizeof(double);
     if (rpl == 1)
-      hipLaunchKernelGGL((k_qp<NJ, 1, 768>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
-                         cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
+      hipLaunchKernelGGL((k_qp<NJ, 1, 768>), dim3(B), dim3(threads), lds, s, C, B, N, precond, mode, x, u, active, G, A,
+                         Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
     else
-      hipLaunchKernelGGL((k_qp<NJ, 2, 512>), dim3(B), dim3(threads), lds, s, C, B, N, precond, x, u, active, G, A, Bm,
-                         cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
+      hipLaunchKernelGGL((k_qp<NJ, 2, 512>), dim3(B), dim3(threads), lds, s, C, B, N, precond, mode, x, u, active, G, A,
+                         Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
   }
 };
 
@@ -1268,13 +1391,14 @@ int launch_unit_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int K
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G) {
   TMPC_DISPATCH_NJ2(nj, ginv(s, C, B, rho, active, G))
 }
-int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, const double* x, const double* u,
+int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, int mode, const double* x,
+              const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
               double* Pd) {
   if (N * 2 * nj > 1024) return -1;
   if (qp_lds_doubles(N, 2 * nj, nj) * sizeof(double) > 160 * 1024) return -3;
-  TMPC_DISPATCH_NJ2(nj, qp(s, C, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd,
+  TMPC_DISPATCH_NJ2(nj, qp(s, C, B, N, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd,
                            Sl, gam, Pd))
 }
 

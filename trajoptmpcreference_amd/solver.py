@@ -135,9 +135,9 @@ class TrajoptMPCReference:
         options = {} if options is None else options
         self.set_default_options(options)
         method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
-        if method in ("N", "S"):
-            raise NotImplementedError("direct KKT / Schur solves (methods N, S) are not on the GPU yet; "
-                                      "use PCG-J, PCG-BJ or PCG-SS")
+        if method == "N":
+            raise NotImplementedError("the dense KKT solve (method N) is not offered on the GPU; "
+                                      "use S, PCG-J, PCG-BJ or PCG-SS")
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
@@ -180,15 +180,13 @@ class TrajoptMPCReference:
         """One QP (formKKTSystemBlocks + solveKKTSystem_Schur, :361-455) -> dxul column.
         xs must equal x[:, 0] (the SQP always passes the initial state)."""
         options = {} if options is None else dict(options)
-        if not use_PCG:
-            raise NotImplementedError("direct Schur solve is not on the GPU yet")
         self.set_default_options(options)
         ptype = options.get("preconditioner_type", "BJ")
+        method = "PCG-" + ptype if use_PCG else "S"
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         if not np.array_equal(np.asarray(xs), x[:, 0]):
             raise NotImplementedError("xs != x[:, 0] is not supported by the batched QP entry point")
-        r = ctx.qp_batch(x[None], np.asarray(u, dtype=np.float64)[None], N, dt, rho, "PCG-" + ptype,
-                         want_blocks=False)
+        r = ctx.qp_batch(x[None], np.asarray(u, dtype=np.float64)[None], N, dt, rho, method, want_blocks=False)
         self.n_inner_iter = int(r["pcg_iters"][0])
         return r["dxul"][0].reshape(-1, 1)
