@@ -16,8 +16,10 @@ inverts it and multiplies dense C G^-1 C^T; S is exactly block-tridiagonal
   dxu_k = Ghat_k (g_k - (C^T lambda)_k),
   (C^T lambda)_k = [lambda_k - A_k^T lambda_{k+1}; -B_k^T lambda_{k+1}]
 
-Only QuadraticCost (TrajoptCost.py:24-104) and no constraints (the reference
-default TrajoptConstraint()) -- the pinned configuration.
+QuadraticCost (TrajoptCost.py:24-104), no constraints (the reference default
+TrajoptConstraint(), the pinned configuration of SURVEY §0) or soft box limits
+(oracle/soft.py: KKT gradient + rank-one Hessian terms, merit cost and D
+terms, and the augmented-Lagrangian outer loop :483-508).
 """
 import copy
 
@@ -71,9 +73,10 @@ def default_options(options=None):
 
 
 # ------------------------------------------------------------------- QP pieces
-def kkt_blocks(model, cost, x, u, xs, N, dt):
+def kkt_blocks(model, cost, x, u, xs, N, dt, soft=None):
     """formKKTSystemBlocks (:200-271), returned blockwise:
-    G (list of n_xu^2 / terminal nx^2), g (list), A, B (N-1), c (N, nx)."""
+    G (list of n_xu^2 / terminal nx^2), g (list), A, B (N-1), c (N, nx).
+    Soft limits add their jacobian to g_k and its outer product to G_k (:220-225, :255-259)."""
     n = model.n
     nx = 2 * n
     X = x[:, :N - 1].T
@@ -85,6 +88,14 @@ def kkt_blocks(model, cost, x, u, xs, N, dt):
     c[1:] = x[:, 1:].T - xkp1
     G = [cost.hessian(False, k) for k in range(N - 1)] + [cost.hessian(True, N - 1)]
     g = [cost.gradient(x[:, k], u[:, k], k) for k in range(N - 1)] + [cost.gradient(x[:, N - 1], None, N - 1)]
+    if soft is not None:
+        nxu = nx + n
+        for k in range(N):
+            uk = u[:, k] if k < N - 1 else None
+            js = soft.jacobians(x[:, k], uk, k, N, nxu if k < N - 1 else nx)
+            if js:
+                g[k] = g[k] + sum(js)
+                G[k] = G[k] + sum(np.outer(j, j) for j in js)
     return G, g, A, B, c
 
 
@@ -195,10 +206,10 @@ def recover_dxu(Gh, g, A, B, lam, nx):
     return np.concatenate(out + [lam])
 
 
-def solve_qp(model, cost, x, u, xs, N, dt, rho, method, options):
+def solve_qp(model, cost, x, u, xs, N, dt, rho, method, options, soft=None):
     """One QP: returns (dxul, pcg_iters or None, extras)."""
     nx = 2 * model.n
-    G, g, A, B, c = kkt_blocks(model, cost, x, u, xs, N, dt)
+    G, g, A, B, c = kkt_blocks(model, cost, x, u, xs, N, dt, soft)
     Gh, Sd, Sl, gam = schur_blocks(G, g, A, B, c, rho, nx)
     Su = np.transpose(Sl, (0, 2, 1))
     gamma = gam.reshape(-1)
@@ -215,12 +226,17 @@ def solve_qp(model, cost, x, u, xs, N, dt, rho, method, options):
 
 
 # ------------------------------------------------------------------- merit pieces
-def total_cost(cost, x, u, N):
-    """totalCost (:296-310), sequential sum as the reference."""
+def total_cost(cost, x, u, N, soft=None):
+    """totalCost (:296-310), sequential sum as the reference (soft terms after the cost terms)."""
     J = 0
     for k in range(N - 1):
         J = J + cost.value(x[:, k], u[:, k], k)
-    return J + cost.value(x[:, N - 1], None, N - 1)
+    J = J + cost.value(x[:, N - 1], None, N - 1)
+    if soft is not None:
+        for k in range(N - 1):
+            J = J + soft.value(x[:, k], u[:, k], k, N)
+        J = J + soft.value(x[:, N - 1], None, N - 1, N)
+    return J
 
 
 def total_violation(model, x, u, xs, N, dt):
@@ -233,85 +249,110 @@ def total_violation(model, x, u, xs, N, dt):
 
 
 # ------------------------------------------------------------------- SQP
-def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None):
-    """TrajoptMPCReference.SQP (:510-760), unconstrained.  Returns a dict."""
+def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None):
+    """TrajoptMPCReference.SQP (:510-760).  Returns a dict.  `soft` (oracle.soft.SoftConstraints)
+    enables the soft-constraint terms and the outer loop; its mu/lambda/phi are updated in place
+    (the reference keeps them in the constraint object)."""
     o = default_options(options)
     nx, nu = 2 * model.n, model.n
     n = nx + nu
     x = np.array(x, dtype=float)
     u = np.array(u, dtype=float)
     xs = copy.deepcopy(x[:, 0])
-    rho = o["rho_init_SQP_DDP"]
-    drho = 1
-    J = total_cost(cost, x, u, N)
-    c = total_violation(model, x, u, xs, N, dt)
-    mu = 10
-    merit = J + mu * c
-    trace = [dict(iteration=0, line_search_iteration=0, alpha=1, rho=rho, J=J, c=c, merit=merit, D=None,
-                  reduction_ratio=None, succeeded_line_search=False)]
-    pcg_iters, dxuls = [], []
-    it = 0
-    exit_sqp = 0
+    outer = 0
+    exit_soft = 0
     while True:
-        dxul, iters, _ = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o)
-        dxul = dxul.reshape(-1, 1)
-        dxuls.append(dxul[:, 0].copy())
-        if iters is not None:
-            pcg_iters.append(iters)
-        alpha = 1
-        error = False
-        ls = 0
+        rho = o["rho_init_SQP_DDP"]
+        drho = 1
+        J = total_cost(cost, x, u, N, soft)
+        c = total_violation(model, x, u, xs, N, dt)
+        mu = 10
+        merit = J + mu * c
+        trace = [dict(outer_iteration=outer, iteration=0, line_search_iteration=0, alpha=1, rho=rho, J=J, c=c,
+                      merit=merit, D=None, reduction_ratio=None, succeeded_line_search=False)]
+        pcg_iters, dxuls = [], []
+        it = 0
+        exit_sqp = 0
         while True:
-            x_new = copy.deepcopy(x)
-            u_new = copy.deepcopy(u)
-            for k in range(N):
-                x_new[:, k] = x_new[:, k] - alpha * dxul[n * k:n * k + nx, 0]
-                if k < N - 1:
-                    u_new[:, k] = u_new[:, k] - alpha * dxul[n * k + nx:n * (k + 1), 0]
-            J_new = total_cost(cost, x_new, u_new, N)
-            c_new = total_violation(model, x_new, u_new, xs, N, dt)
-            D = 0
-            for k in range(N - 1):
-                D += float(cost.gradient(x_new[:, k], u_new[:, k], k) @ dxul[n * k:n * (k + 1), 0])
-            D += float(cost.gradient(x_new[:, N - 1], None, N - 1) @ dxul[n * (N - 1):n * (N - 1) + nx, 0])
-            merit_new = J_new + mu * c_new
-            delta_J = J - J_new
-            delta_merit = merit - merit_new
-            with np.errstate(divide="ignore", invalid="ignore"):
-                ratio = np.float64(delta_merit) / np.float64(alpha * (D - mu * c_new))
-            if (delta_merit >= 0 and ratio >= o["expected_reduction_min_SQP_DDP"]
-                    and ratio <= o["expected_reduction_max_SQP_DDP"]):
-                x, u, J, c, merit = x_new, u_new, J_new, c_new, merit_new
-                drho = min(drho / o["rho_factor_SQP_DDP"], 1 / o["rho_factor_SQP_DDP"])
+            dxul, iters, _ = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o, soft)
+            dxul = dxul.reshape(-1, 1)
+            dxuls.append(dxul[:, 0].copy())
+            if iters is not None:
+                pcg_iters.append(iters)
+            alpha = 1
+            error = False
+            ls = 0
+            while True:
+                x_new = copy.deepcopy(x)
+                u_new = copy.deepcopy(u)
+                for k in range(N):
+                    x_new[:, k] = x_new[:, k] - alpha * dxul[n * k:n * k + nx, 0]
+                    if k < N - 1:
+                        u_new[:, k] = u_new[:, k] - alpha * dxul[n * k + nx:n * (k + 1), 0]
+                J_new = total_cost(cost, x_new, u_new, N, soft)
+                c_new = total_violation(model, x_new, u_new, xs, N, dt)
+                D = 0
+                for k in range(N - 1):
+                    D += float(cost.gradient(x_new[:, k], u_new[:, k], k) @ dxul[n * k:n * (k + 1), 0])
+                    if soft is not None:
+                        for j in soft.jacobians(x_new[:, k], u_new[:, k], k, N, n):
+                            D += float(j.dot(dxul[n * k:n * (k + 1), 0]))
+                D += float(cost.gradient(x_new[:, N - 1], None, N - 1) @ dxul[n * (N - 1):n * (N - 1) + nx, 0])
+                if soft is not None:
+                    for j in soft.jacobians(x_new[:, N - 1], None, N - 1, N, nx):
+                        D += float(j.dot(dxul[n * (N - 1):n * (N - 1) + nx, 0]))
+                merit_new = J_new + mu * c_new
+                delta_J = J - J_new
+                delta_merit = merit - merit_new
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    ratio = np.float64(delta_merit) / np.float64(alpha * (D - mu * c_new))
+                if (delta_merit >= 0 and ratio >= o["expected_reduction_min_SQP_DDP"]
+                        and ratio <= o["expected_reduction_max_SQP_DDP"]):
+                    x, u, J, c, merit = x_new, u_new, J_new, c_new, merit_new
+                    drho = min(drho / o["rho_factor_SQP_DDP"], 1 / o["rho_factor_SQP_DDP"])
+                    rho = max(rho * drho, o["rho_min_SQP_DDP"])
+                    trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=ls, alpha=alpha,
+                                      rho=rho, J=J, c=c, merit=merit, D=D, reduction_ratio=ratio,
+                                      succeeded_line_search=True))
+                    break
+                elif alpha > o["alpha_min_SQP_DDP"]:
+                    alpha *= o["alpha_factor_SQP_DDP"]
+                    ls += 1
+                else:
+                    error = True
+                    trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=ls, alpha=alpha,
+                                      rho=rho, J=J, c=c, merit=merit, D=D, reduction_ratio=ratio,
+                                      succeeded_line_search=False))
+                    break
+            # check_for_exit_or_error (:463-481)
+            exit_flag = False
+            if error:
+                drho = max(drho * o["rho_factor_SQP_DDP"], o["rho_factor_SQP_DDP"])
                 rho = max(rho * drho, o["rho_min_SQP_DDP"])
-                trace.append(dict(iteration=it, line_search_iteration=ls, alpha=alpha, rho=rho, J=J, c=c,
-                                  merit=merit, D=D, reduction_ratio=ratio, succeeded_line_search=True))
-                break
-            elif alpha > o["alpha_min_SQP_DDP"]:
-                alpha *= o["alpha_factor_SQP_DDP"]
-                ls += 1
+                if rho > o["rho_max_SQP_DDP"]:
+                    exit_sqp, exit_flag = 2, True
+            elif delta_J < o["exit_tolerance_SQP_DDP"]:
+                exit_sqp, exit_flag = 1, True
+            if it == o["max_iter_SQP_DDP"] - 1:
+                exit_sqp, exit_flag = 3, True
             else:
-                error = True
-                trace.append(dict(iteration=it, line_search_iteration=ls, alpha=alpha, rho=rho, J=J, c=c,
-                                  merit=merit, D=D, reduction_ratio=ratio, succeeded_line_search=False))
+                it += 1
+            if exit_flag:
                 break
-        # check_for_exit_or_error (:463-481)
-        exit_flag = False
-        if error:
-            drho = max(drho * o["rho_factor_SQP_DDP"], o["rho_factor_SQP_DDP"])
-            rho = max(rho * drho, o["rho_min_SQP_DDP"])
-            if rho > o["rho_max_SQP_DDP"]:
-                exit_sqp, exit_flag = 2, True
-        elif delta_J < o["exit_tolerance_SQP_DDP"]:
-            exit_sqp, exit_flag = 1, True
-        if it == o["max_iter_SQP_DDP"] - 1:
-            exit_sqp, exit_flag = 3, True
+        # check_and_update_soft_constraints (:483-508); without soft limits the max value is 0 < tol
+        done = False
+        max_c = soft.max_value(x, u) if soft is not None else 0
+        if max_c < o["exit_tolerance_softConstraints"]:
+            exit_soft, done = 1, True
+        if outer == o["max_iter_softConstraints"] - 1:
+            exit_soft, done = 2, True
         else:
-            it += 1
-        if exit_flag:
+            outer += 1
+        if not done and soft.update(x, u):
+            exit_soft, done = 3, True
+        if done:
             break
-    # unconstrained outer loop: max soft violation 0 < tol -> exit_soft 1, outer iteration 0 -> 1 (:483-508)
-    return dict(x=x, u=u, exit_sqp=exit_sqp, exit_soft=1, outer_iter=1, sqp_iter=it, trace=trace,
+    return dict(x=x, u=u, exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer, sqp_iter=it, trace=trace,
                 pcg_iters=pcg_iters, dxul=dxuls)
 
 
