@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 1
+#define TMPC_ABI_VERSION 2
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). N (dense KKT) is not offered on the GPU. */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
@@ -52,6 +52,12 @@ extern "C" {
 /* joint types of the model arrays */
 #define TMPC_JOINT_REVOLUTE 0  /* X(q) = X0 + cos(q) Xa + sin(q) Xb */
 #define TMPC_JOINT_PRISMATIC 1 /* X(q) = X0 + q Xa                  */
+
+/* soft box-limit modes (BoxConstraint modes, TrajoptConstraint.py:27-35; the hard modes
+ * ACTIVE_SET / FULL_SET are not offered on the GPU) */
+#define TMPC_LIMIT_NONE 0
+#define TMPC_LIMIT_QUADRATIC_PENALTY 1
+#define TMPC_LIMIT_AUGMENTED_LAGRANGIAN 2
 
 typedef struct tmpc_ctx tmpc_ctx;
 
@@ -72,8 +78,26 @@ typedef struct tmpc_options {
   double expected_reduction_max_SQP_DDP; /* 3      */
   double merit_mu;                       /* 10 (fixed in the reference, :545-546) */
   int32_t profile;                       /* 1: time kernels with HIP events (tmpc_kernel_stats) */
-  int32_t reserved;
+  int32_t max_iter_softConstraints;      /* 10     */
+  double exit_tolerance_softConstraints; /* 1e-6   */
 } tmpc_options;
+
+/* Box limits of TrajoptConstraint (set_joint_limits / set_velocity_limits / set_torque_limits,
+ * TrajoptConstraint.py:190-206) in a soft mode, with the BoxConstraint options (:38-46).
+ * Index 0 = joint (q), 1 = velocity (qd), 2 = torque (u); lb/ub have n entries.
+ * Vector semantics for constraint_size > 1 and the other corrections of SURVEY F6 are
+ * documented in oracle/soft.py. */
+typedef struct tmpc_box_limits {
+  int32_t mode[3];
+  int32_t reserved;
+  double lb[3][8];
+  double ub[3][8];
+  double mu_init[3];    /* quadratic_penalty_mu_init        1e-2 */
+  double mu_factor[3];  /* quadratic_penalty_mu_factor      10   */
+  double mu_max[3];     /* quadratic_penalty_mu_max         1e12 */
+  double phi_init[3];   /* augmentated_lagrangian_phi_init   1e-2 */
+  double phi_factor[3]; /* augmentated_lagrangian_phi_factor 10   */
+} tmpc_box_limits;
 
 /* Per-problem SQP trace, the numeric fields of self.trace (TrajoptMPCReference.py:555-569,691-743).
  * Every member is nullable; each array is [B][max_iter_SQP_DDP + 1]; row 0 is the initial entry,
@@ -114,8 +138,21 @@ int tmpc_set_cost_quadratic(tmpc_ctx* ctx, int nx, int nu, const double* Q, cons
 void tmpc_default_options(tmpc_options* opts);
 int tmpc_set_options(tmpc_ctx* ctx, const tmpc_options* opts);
 
+/* Soft box limits for the following solves (NULL: unconstrained, the reference default
+ * TrajoptConstraint()).  Resets the soft-constraint state. */
+int tmpc_set_box_limits(tmpc_ctx* ctx, const tmpc_box_limits* limits);
+
+/* The per-problem augmented-Lagrangian constants -- the reference keeps them in the
+ * BoxConstraint objects (quadratic_penalty_mu, augmented_lagrangian_lambda / _phi, :21-24)
+ * and SQP updates them in place (:137-166).  Layout [B][N][6 n]: knot k, slot t*2n + e with
+ * t = 0 joint / 1 velocity / 2 torque, e < n the lower-bound half, e >= n the upper half.
+ * set: NULL arrays take the defaults (mu_init, 0, phi_init).  The state persists in the
+ * context across solves of the same (B, N), like the reference object's. */
+int tmpc_set_soft_state(tmpc_ctx* ctx, int B, int N, const double* mu, const double* lam, const double* phi);
+int tmpc_get_soft_state(tmpc_ctx* ctx, int B, int N, double* mu, double* lam, double* phi);
+
 /* Batched TrajoptMPCReference.SQP (TrajoptMPCReference.py:510-760) for B independent problems,
- * unconstrained (TrajoptConstraint() default).  x [B][nx][N] and u [B][nu][N-1] are read as the
+ * with the soft-constraint outer loop (:483-508) when box limits are set.  x [B][nx][N] and u [B][nu][N-1] are read as the
  * initial trajectory and overwritten with the result; per-problem outputs mirror the returned
  * tuple (x, u, exit_sqp, exit_soft, outer_iter, sqp_iter).  trace is nullable. */
 int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* x, double* u,

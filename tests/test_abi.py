@@ -37,7 +37,7 @@ def test_binding_matches_header():
     from trajoptmpcreference_amd import _native
     assert sorted(_native.SIGNATURES) == header_functions()
     lib = _native.load_library()
-    assert lib.tmpc_abi_version() == 1
+    assert lib.tmpc_abi_version() == 2
 
 
 def test_options_struct_layout_and_defaults():
@@ -54,6 +54,14 @@ def test_options_struct_layout_and_defaults():
     assert o.rho_init_SQP_DDP == 1e-3
     assert o.expected_reduction_min_SQP_DDP == 0.05 and o.expected_reduction_max_SQP_DDP == 3
     assert o.merit_mu == 10.0
+    assert o.max_iter_softConstraints == 10 and o.exit_tolerance_softConstraints == 1e-6
+    assert ctypes.sizeof(o) == 12 * 8 + 4 * 4   # 12 doubles, 4 int32, no padding
+
+
+def test_box_limits_struct_size():
+    from trajoptmpcreference_amd import _native
+    # int32 mode[3] + reserved, double lb[3][8], ub[3][8], five double[3] option arrays
+    assert ctypes.sizeof(_native.tmpc_box_limits) == 16 + 2 * 24 * 8 + 15 * 8
 
 
 def test_null_context_is_an_error_not_a_crash():

@@ -36,7 +36,20 @@ class tmpc_options(C.Structure):
         ("expected_reduction_max_SQP_DDP", C.c_double),
         ("merit_mu", C.c_double),
         ("profile", C.c_int32),
-        ("reserved", C.c_int32),
+        ("max_iter_softConstraints", C.c_int32),
+        ("exit_tolerance_softConstraints", C.c_double),
+    ]
+
+
+LIMIT_MODES = {"QUADRATIC_PENALTY": 1, "AUGMENTED_LAGRANGIAN": 2}
+
+
+class tmpc_box_limits(C.Structure):
+    _fields_ = [
+        ("mode", C.c_int32 * 3), ("reserved", C.c_int32),
+        ("lb", (C.c_double * 8) * 3), ("ub", (C.c_double * 8) * 3),
+        ("mu_init", C.c_double * 3), ("mu_factor", C.c_double * 3), ("mu_max", C.c_double * 3),
+        ("phi_init", C.c_double * 3), ("phi_factor", C.c_double * 3),
     ]
 
 
@@ -59,6 +72,9 @@ SIGNATURES = {
     "tmpc_set_cost_quadratic": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp, _dp, C.c_int32]),
     "tmpc_default_options": (None, [C.POINTER(tmpc_options)]),
     "tmpc_set_options": (C.c_int, [C.c_void_p, C.POINTER(tmpc_options)]),
+    "tmpc_set_box_limits": (C.c_int, [C.c_void_p, C.POINTER(tmpc_box_limits)]),
+    "tmpc_set_soft_state": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp]),
+    "tmpc_get_soft_state": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp]),
     "tmpc_sqp_solve_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _ip, _ip, _ip,
                                        _ip, C.POINTER(tmpc_trace)]),
     "tmpc_sqp_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p,
@@ -186,6 +202,45 @@ class Context:
                 raise KeyError(k)
             setattr(self.options, k, v)
         self._check(self.lib.tmpc_set_options(self.h, C.byref(self.options)), "tmpc_set_options")
+
+    def set_box_limits(self, limits):
+        """limits: None, or {type: dict(mode=..., lb=[n], ub=[n], options=...)} with type in
+        joint / velocity / torque (TrajoptConstraint.set_*_limits)."""
+        if not limits:
+            self._check(self.lib.tmpc_set_box_limits(self.h, None), "tmpc_set_box_limits")
+            return
+        L = tmpc_box_limits()
+        n = self.model.n
+        for t, name in enumerate(("joint", "velocity", "torque")):
+            spec = limits.get(name)
+            if spec is None:
+                continue
+            L.mode[t] = LIMIT_MODES[spec["mode"]]
+            lb = np.broadcast_to(np.asarray(spec["lb"], dtype=np.float64), (n,))
+            ub = np.broadcast_to(np.asarray(spec["ub"], dtype=np.float64), (n,))
+            for i in range(n):
+                L.lb[t][i] = float(lb[i])
+                L.ub[t][i] = float(ub[i])
+            o = spec.get("options", {})
+            L.mu_init[t] = o.get("quadratic_penalty_mu_init", 1e-2)
+            L.mu_factor[t] = o.get("quadratic_penalty_mu_factor", 10.0)
+            L.mu_max[t] = o.get("quadratic_penalty_mu_max", 1e12)
+            L.phi_init[t] = o.get("augmentated_lagrangian_phi_init", 1e-2)
+            L.phi_factor[t] = o.get("augmentated_lagrangian_phi_factor", 10.0)
+        self._check(self.lib.tmpc_set_box_limits(self.h, C.byref(L)), "tmpc_set_box_limits")
+
+    def set_soft_state(self, B, N, mu=None, lam=None, phi=None):
+        """[B][N][6n] arrays (None: defaults)."""
+        arrs = [None if a is None else _c64(a) for a in (mu, lam, phi)]
+        self._check(self.lib.tmpc_set_soft_state(self.h, int(B), int(N), *[_ptr(a) for a in arrs]),
+                    "tmpc_set_soft_state")
+
+    def get_soft_state(self, B, N):
+        shape = (B, N, 6 * self.model.n)
+        mu, lam, phi = np.zeros(shape), np.zeros(shape), np.zeros(shape)
+        self._check(self.lib.tmpc_get_soft_state(self.h, int(B), int(N), _ptr(mu), _ptr(lam), _ptr(phi)),
+                    "tmpc_get_soft_state")
+        return mu, lam, phi
 
     # ---------------------------------------------------------------- solves
     def sqp_solve_batch(self, x, u, N, dt, method="PCG-SS", with_trace=True):

@@ -1,13 +1,24 @@
 """TrajoptConstraint / BoxConstraint -- the reference's constraint plugin
 surface (TrajoptConstraint.py:5-387).
 
-This round the GPU solver runs the unconstrained path (the reference default
-``TrajoptConstraint()``, the only configuration whose semantics are pinned:
-SURVEY §0).  The classes keep the reference's constructor and setter
-signatures so callers compose constraints the same way; solving with any
-limit set raises NotImplementedError instead of silently ignoring it.
-Box constraints with corrected vector semantics are the next row of the hot
-path scope.
+Soft modes (QUADRATIC_PENALTY, AUGMENTED_LAGRANGIAN) run on the GPU: the
+solver lowers the limits to ``tmpc_set_box_limits`` and the objects' mu /
+lambda / phi arrays to ``tmpc_set_soft_state``, and stores the updated
+constants back after the solve, as the reference's SQP updates them in place
+(TrajoptMPCReference.py:483-508, TrajoptConstraint.py:137-166).
+
+Semantics are the reference's for constraint_size 1 (the only size its code
+runs) and the elementwise vector generalisation for larger sizes,
+with the corrections documented in oracle/soft.py: joint limits cover all N
+knots, terminal jacobians keep the state part, several soft types sum their
+jacobians (and their per-type outer products in the KKT Hessian).
+
+The hard modes (ACTIVE_SET / FULL_SET) change the row structure of the KKT
+system every iteration; they are not offered on the GPU and raise
+NotImplementedError (as ADMM_PROJECTION exits in the reference).
+
+The host-side value / jacobian / update methods below are the plugin API for
+callers that evaluate constraints themselves; the solve never calls them.
 """
 from typing import List
 
@@ -15,10 +26,11 @@ import numpy as np
 
 HARD_MODES = ("ACTIVE_SET", "FULL_SET")
 SOFT_MODES = ("QUADRATIC_PENALTY", "AUGMENTED_LAGRANGIAN", "ADMM_PROJECTION")
+GPU_SOFT_MODES = ("QUADRATIC_PENALTY", "AUGMENTED_LAGRANGIAN")
 
 
 class BoxConstraint:
-    """lb <= x[:constraint_size] <= ub (TrajoptConstraint.py:5-51)."""
+    """lb <= z <= ub on a constraint_size slice (TrajoptConstraint.py:5-176)."""
 
     def __init__(self, constraint_size: int = 0, num_timesteps: int = 0, upper_bounds: List[float] = (),
                  lower_bounds: List[float] = (), mode: str = "NONE", options=None):
@@ -44,6 +56,10 @@ class BoxConstraint:
         options.setdefault("jacobian_extra_columns_head", 0)
         options.setdefault("jacobian_extra_columns_tail", 0)
         self.options = options
+        T, m = num_timesteps, 2 * constraint_size
+        self.quadratic_penalty_mu = options["quadratic_penalty_mu_init"] * np.ones((m, T))
+        self.augmented_lagrangian_lambda = np.zeros((m, T))
+        self.augmented_lagrangian_phi = options["augmentated_lagrangian_phi_init"] * np.ones((m, T))
 
     def is_hard_constraint_mode(self, mode=None):
         return (self.mode if mode is None else mode) in HARD_MODES
@@ -51,9 +67,76 @@ class BoxConstraint:
     def is_soft_constraint_mode(self, mode=None):
         return (self.mode if mode is None else mode) in SOFT_MODES
 
+    @property
+    def lower(self):
+        return self.bounds[:self.constraint_size]
+
+    @property
+    def upper(self):
+        return self.bounds[self.constraint_size:]
+
+    # ---- plugin API on the host (BoxConstraint.value / jacobian / ..., :53-176)
+    def full_value(self, z):
+        z = np.asarray(z, dtype=np.float64).reshape(-1)[:self.constraint_size]
+        return np.concatenate([z - self.lower, self.upper - z])
+
+    def value(self, z, timestep: int = None, mode: str = None):
+        mode = self.mode if mode is None else mode
+        v = self.full_value(z)
+        if mode == "ACTIVE_SET":
+            return v[v < 0]
+        if mode == "FULL_SET":
+            return v
+        if mode in GPU_SOFT_MODES:
+            if timestep is None:
+                raise ValueError("Need Timestep for Soft Constraint Mode")
+            val = np.sum(self.quadratic_penalty_mu[:, timestep].dot(np.square(v)))
+            if mode == "AUGMENTED_LAGRANGIAN":
+                val = val + self.augmented_lagrangian_lambda[:, timestep] @ v
+            return val
+        raise NotImplementedError("ADMM_PROJECTION is not implemented (the reference exits too, :81-83)")
+
+    def jacobian(self, z, timestep: int = None, mode: str = None):
+        """Soft modes: the jacobian column (head + constraint_size + tail entries)."""
+        mode = self.mode if mode is None else mode
+        v = self.full_value(z)
+        cs = self.constraint_size
+        sign = np.concatenate([np.ones(cs), -np.ones(cs)]) * (v < 0)
+        full = np.zeros((2 * cs, cs))
+        for i in range(2 * cs):
+            full[i, i % cs] = sign[i]
+        head, tail = self.options["jacobian_extra_columns_head"], self.options["jacobian_extra_columns_tail"]
+        full = np.hstack([np.zeros((2 * cs, head)), full, np.zeros((2 * cs, tail))])
+        if mode == "ACTIVE_SET":
+            return full[~np.all(full == 0, axis=1)]
+        if mode == "FULL_SET":
+            return full
+        if timestep is None:
+            raise ValueError("Need Timestep for Soft Constraint Mode")
+        jac = 2 * np.matmul(self.quadratic_penalty_mu[:, timestep] * v, full)
+        if mode == "AUGMENTED_LAGRANGIAN":
+            jac = jac + np.matmul(self.augmented_lagrangian_lambda[:, timestep], full)
+        return jac.reshape(-1, 1)
+
+    def max_soft_constraint_value(self, z_of_t):
+        m = 0
+        for t in range(self.num_timesteps):
+            m = max(m, abs(min(self.full_value(z_of_t[:, t]))))
+        return m
+
+    def shift_soft_constraint_constants(self, shift_steps: int):
+        """Receding-horizon shift (:168-176)."""
+        for arr, init in ((self.quadratic_penalty_mu, self.options["quadratic_penalty_mu_init"]),
+                          (self.augmented_lagrangian_lambda, 0.0),
+                          (self.augmented_lagrangian_phi, self.options["augmentated_lagrangian_phi_init"])):
+            arr[:, :-shift_steps] = arr[:, shift_steps:]
+            arr[:, shift_steps:] = init
+
 
 class TrajoptConstraint:
     """Joint / velocity / torque limits (TrajoptConstraint.py:178-387)."""
+
+    KINDS = ("joint_limits", "velocity_limits", "torque_limits")
 
     def __init__(self, nq: int = 0, nv: int = 0, nu: int = 0, num_timesteps: int = 0):
         self.nq, self.nv, self.nu, self.num_timesteps = nq, nv, nu, num_timesteps
@@ -64,7 +147,8 @@ class TrajoptConstraint:
     def set_joint_limits(self, upper_bounds, lower_bounds, mode, options=None):
         options = {} if options is None else dict(options)
         options["jacobian_extra_columns_tail"] = self.nv + self.nu
-        self.joint_limits = BoxConstraint(self.nq, self.num_timesteps - 1, upper_bounds, lower_bounds, mode, options)
+        # all N knots (the reference sizes joint limits N-1 and then indexes knot N-1: oracle/soft.py)
+        self.joint_limits = BoxConstraint(self.nq, self.num_timesteps, upper_bounds, lower_bounds, mode, options)
 
     def set_velocity_limits(self, upper_bounds, lower_bounds, mode, options=None):
         options = {} if options is None else dict(options)
@@ -77,23 +161,87 @@ class TrajoptConstraint:
         options["jacobian_extra_columns_head"] = self.nq + self.nv
         self.torque_limits = BoxConstraint(self.nu, self.num_timesteps - 1, upper_bounds, lower_bounds, mode, options)
 
+    def limits(self):
+        return [(k, getattr(self, k)) for k in self.KINDS if getattr(self, k) is not None]
+
     def has_any(self) -> bool:
-        return any(c is not None for c in (self.joint_limits, self.velocity_limits, self.torque_limits))
+        return bool(self.limits())
 
     def total_soft_constraints(self, timestep=None):
         total = 0
-        for c in (self.joint_limits, self.velocity_limits, self.torque_limits):
-            if c is not None and c.is_soft_constraint_mode():
-                total += c.num_constraints if timestep is None else c.constraint_size
+        for kind, c in self.limits():
+            if c.is_soft_constraint_mode():
+                if timestep is None:
+                    total += c.num_constraints
+                elif not (kind == "torque_limits" and timestep >= self.num_timesteps - 1):
+                    total += c.constraint_size
         return total
 
     def total_hard_constraints(self, x=None, u=None, timestep=None):
-        if any(c is not None and c.is_hard_constraint_mode()
-               for c in (self.joint_limits, self.velocity_limits, self.torque_limits)):
-            raise NotImplementedError("hard box constraints are not on the GPU path yet (SURVEY §8f row 1)")
+        if any(c.is_hard_constraint_mode() for _, c in self.limits()):
+            raise NotImplementedError("hard box constraints (ACTIVE_SET / FULL_SET) are not offered on the GPU "
+                                      "path; use QUADRATIC_PENALTY or AUGMENTED_LAGRANGIAN")
         return 0
 
     def max_soft_constraint_value(self, x, u):
-        if self.total_soft_constraints() > 0:
-            raise NotImplementedError("soft box constraints are not on the GPU path yet (SURVEY §8f row 1)")
-        return 0
+        m = 0
+        for kind, c in self.limits():
+            if not c.is_soft_constraint_mode():
+                continue
+            if kind == "joint_limits":
+                m = max(m, c.max_soft_constraint_value(np.asarray(x)[:self.nq]))
+            elif kind == "velocity_limits":
+                m = max(m, c.max_soft_constraint_value(np.asarray(x)[self.nq:self.nq + self.nv]))
+            else:
+                m = max(m, c.max_soft_constraint_value(np.asarray(u)))
+        return m
+
+    def shift_soft_constraint_constants(self, shift_steps: int):
+        for _, c in self.limits():
+            c.shift_soft_constraint_constants(shift_steps)
+
+    # ---- lowering to libtmpc
+    def gpu_spec(self):
+        """{joint|velocity|torque: {mode, lb, ub, options}} for Context.set_box_limits."""
+        spec = {}
+        for kind, c in self.limits():
+            if c.mode not in GPU_SOFT_MODES:
+                if c.is_hard_constraint_mode():
+                    self.total_hard_constraints()
+                raise NotImplementedError(f"constraint mode {c.mode} is not implemented (the reference exits)")
+            if c.constraint_size != self.nq:
+                raise ValueError(f"{kind}: constraint_size {c.constraint_size} != n = {self.nq}")
+            spec[kind.split("_")[0]] = dict(mode=c.mode, lb=c.lower.copy(), ub=c.upper.copy(), options=c.options)
+        return spec
+
+    def pack_state(self, N):
+        """The objects' (2n, T) mu / lambda / phi as one problem's [N][6n] soft state."""
+        n = self.nq
+        out = []
+        for attr, fill in (("quadratic_penalty_mu", 1e-2), ("augmented_lagrangian_lambda", 0.0),
+                           ("augmented_lagrangian_phi", 1e-2)):
+            a = np.zeros((N, 6 * n))
+            for t, kind in enumerate(self.KINDS):
+                c = getattr(self, kind)
+                if c is None:
+                    a[:, t * 2 * n:(t + 1) * 2 * n] = fill
+                    continue
+                arr = getattr(c, attr)
+                T = arr.shape[1]
+                a[:T, t * 2 * n:(t + 1) * 2 * n] = arr.T
+                if T < N:
+                    a[T:, t * 2 * n:(t + 1) * 2 * n] = arr[:, -1:].T if T else fill
+            out.append(a)
+        return out
+
+    def unpack_state(self, mu, lam, phi):
+        """Store one problem's [N][6n] soft state back into the objects."""
+        n = self.nq
+        for t, kind in enumerate(self.KINDS):
+            c = getattr(self, kind)
+            if c is None or not c.is_soft_constraint_mode():
+                continue
+            T = c.num_timesteps
+            c.quadratic_penalty_mu[:] = mu[:T, t * 2 * n:(t + 1) * 2 * n].T
+            c.augmented_lagrangian_lambda[:] = lam[:T, t * 2 * n:(t + 1) * 2 * n].T
+            c.augmented_lagrangian_phi[:] = phi[:T, t * 2 * n:(t + 1) * 2 * n].T

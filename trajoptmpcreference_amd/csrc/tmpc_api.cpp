@@ -47,8 +47,11 @@ struct tmpc_ctx {
   bool has_model = false, has_cost = false;
   ModelDev hmodel{};
   CostDev hcost{};
+  ConstrDev hlim{};
   ModelDev* dmodel = nullptr;
   CostDev* dcost = nullptr;
+  ConstrDev* dlim = nullptr;
+  int soft_B = -1, soft_N = -1;   // shape of the valid soft-constraint state (-1: none)
   tmpc_options opts{};
   std::map<std::string, DevBuf> bufs;
   std::map<std::string, Stat> stats;
@@ -207,12 +210,15 @@ struct Work {
   double *xs, *qdd, *minv, *cvec, *A, *Bm, *G, *Sd, *Sl, *gam, *lam, *dx, *du, *Pd;
   int* iters;
   double *U, *Y;   // method S scratch (k_btsolve)
+  double *Gk, *jsoft, *smu, *slam;   // soft limits: per-knot Ghat, jacobian, AL constants
 };
 
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
                   const ProbState& st, Work& w, bool keep_blocks) {
   const int nj = ctx->hmodel.n;
   const bool chain = ctx->hmodel.chain != 0;
+  const bool soft = w.jsoft != nullptr;
+  const double* G = soft ? w.Gk : w.G;
   {
     Timed t(ctx, "qp_fd");
     LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
@@ -227,15 +233,20 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv, w.A,
                              w.Bm));
   }
-  {
+  if (soft) {
+    Timed t(ctx, "ginv");
+    LAUNCH_OK(launch_ginv_soft(ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, st.rho, st.active, d_x, d_u, w.smu,
+                               w.slam, w.Gk, w.jsoft));
+  } else {
     Timed t(ctx, "ginv");
     LAUNCH_OK(launch_ginv(ctx->stream, nj, ctx->dcost, B, st.rho, st.active, w.G));
   }
   if (precond == 0) {   // method S: Schur blocks -> direct solve -> dxu
     {
       Timed t(ctx, "schur");
-      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, w.G,
-                          w.A, w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, nullptr, w.Sd, w.Sl, w.gam, nullptr));
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, G,
+                          w.A, w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, nullptr, w.Sd, w.Sl, w.gam, nullptr,
+                          w.jsoft));
     }
     {
       Timed t(ctx, "btsolve");
@@ -243,17 +254,19 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     }
     {
       Timed t(ctx, "dxu");
-      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, w.G, w.A,
-                          w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, w.lam, nullptr, nullptr, nullptr, nullptr));
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, G, w.A,
+                          w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, w.lam, nullptr, nullptr, nullptr, nullptr,
+                          w.jsoft));
     }
     return 0;
   }
   {
     Timed t(ctx, "qp");
-    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, precond, QP_MODE_PCG, d_x, d_u, st.active, w.G, w.A,
+    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, precond, QP_MODE_PCG, d_x, d_u, st.active, G, w.A,
                         w.Bm, w.cvec, ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx,
                         w.du, keep_blocks ? w.lam : nullptr, keep_blocks ? w.Sd : nullptr,
-                        keep_blocks ? w.Sl : nullptr, keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr));
+                        keep_blocks ? w.Sl : nullptr, keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr,
+                        w.jsoft));
   }
   return 0;
 }
@@ -271,7 +284,7 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   BUF(double, du, (size_t)B * K * nj);
   BUF(int, iters, (size_t)B);
   w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters,
-           nullptr, nullptr};
+           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (with_blocks) {
     BUF(double, Sdiag, (size_t)B * N * nx * nx);
     BUF(double, Slo, (size_t)B * (K > 0 ? K : 1) * nx * nx);
@@ -321,6 +334,18 @@ static int alloc_trace(tmpc_ctx* ctx, int B, int W, TraceDev& tr) {
   return 0;
 }
 
+// soft-constraint state [B][N][6n] (mu, lambda, phi) and the per-knot QP terms
+static int alloc_soft(tmpc_ctx* ctx, int B, int N, double** mu, double** lam, double** phi) {
+  const size_t n = (size_t)B * N * 6 * ctx->hmodel.n;
+  BUF(double, soft_mu, n);
+  BUF(double, soft_lam, n);
+  BUF(double, soft_phi, n);
+  *mu = soft_mu;
+  *lam = soft_lam;
+  *phi = soft_phi;
+  return 0;
+}
+
 static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
                       TraceDev* tr_out) {
   int rc = check_ready(ctx, B, N);
@@ -345,6 +370,26 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   BUF(double, terms, (size_t)B * T * N * 3);
   BUF(int, active_count, 1);
   BUF(unsigned long long, counters, 4);
+  BUF(int, outer_active, B);
+  BUF(int, outer_iter, B);
+  BUF(int, exit_soft, B);
+  const bool soft = ctx->hlim.any != 0;
+  double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
+  if (soft) {
+    if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
+    if (ctx->soft_B != B || ctx->soft_N != N) {
+      launch_soft_init(ctx->stream, ctx->dlim, (size_t)B * N * 6 * nj, 6 * nj, smu, slam, sphi);
+      HIP_OK(hipGetLastError());
+      ctx->soft_B = B;
+      ctx->soft_N = N;
+    }
+    BUF(double, soft_Gk, (size_t)B * N * (nx * nx + nj * nj));
+    BUF(double, soft_j, (size_t)B * N * (nx + nj));
+    w.Gk = soft_Gk;
+    w.jsoft = soft_j;
+    w.smu = smu;
+    w.slam = slam;
+  }
   HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
   std::vector<double> al_h(al);
   al_h.push_back(0.0);  // slot T: alpha = 0 for the initial merit evaluation
@@ -352,30 +397,43 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   // xs = x[:, 0] (:527)
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
-  launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st);
+  launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
+  // soft-constraint outer loop (:531-757): one inner SQP loop per pass for every problem still
+  // in the outer loop, then check_and_update_soft_constraints on the device
+  for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
+  launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
   // initial J, c, merit (:541-548)
-  LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, B, N, 1, dt, alphas + T, d_x, d_u,
-                            w.xs, nullptr, nullptr, st.active, terms));
+  LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
+                            alphas + T, d_x, d_u, w.xs, nullptr, nullptr, st.active, terms));
   HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-  launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, alphas + T, so, terms, d_x, d_u, w.dx, w.du, st,
-                   nullptr, tr, active_count, nullptr);
+  launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
+                   st, nullptr, tr, active_count, nullptr);
   for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
     if ((rc = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false))) return rc;
     {
       Timed t(ctx, "ls_terms");
-      LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, B, N, T, dt, alphas, d_x, d_u,
-                                w.xs, w.dx, w.du, st.active, terms));
+      LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
+                                alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
     }
     HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
     {
       Timed t(ctx, "ls_decide");
-      launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, alphas, so, terms, d_x, d_u, w.dx, w.du, st,
-                       w.iters, tr, active_count, counters);
+      launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
+                       st, w.iters, tr, active_count, counters);
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(hipStreamSynchronize(ctx->stream));
     if (*ctx->h_count == 0) break;
+  }
+  HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
+  launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints, o.max_iter_softConstraints,
+                    d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft, active_count);
+  HIP_OK(hipGetLastError());
+  if (!soft) break;   // unconstrained: exit_soft 1 after one pass, as the reference
+  HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (*ctx->h_count == 0) break;
   }
   unsigned long long hc[4] = {0, 0, 0, 0};
   HIP_OK(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
@@ -412,6 +470,7 @@ int tmpc_create(int device, tmpc_ctx** out) {
   ctx->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&ctx->dmodel, sizeof(ModelDev)) != hipSuccess || hipMalloc(&ctx->dcost, sizeof(CostDev)) != hipSuccess ||
+      hipMalloc(&ctx->dlim, sizeof(ConstrDev)) != hipSuccess || hipMemset(ctx->dlim, 0, sizeof(ConstrDev)) != hipSuccess ||
       hipHostMalloc(&ctx->h_count, sizeof(int)) != hipSuccess) {
     delete ctx;
     return -4;
@@ -435,6 +494,7 @@ void tmpc_destroy(tmpc_ctx* ctx) {
     if (kv.second.ptr) hipFree(kv.second.ptr);
   if (ctx->dmodel) hipFree(ctx->dmodel);
   if (ctx->dcost) hipFree(ctx->dcost);
+  if (ctx->dlim) hipFree(ctx->dlim);
   if (ctx->h_count) hipHostFree(ctx->h_count);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -518,11 +578,76 @@ void tmpc_default_options(tmpc_options* o) {
   o->expected_reduction_max_SQP_DDP = 3;
   o->merit_mu = 10.0;
   o->profile = 0;
+  o->max_iter_softConstraints = 10;
+  o->exit_tolerance_softConstraints = 1e-6;
+}
+
+int tmpc_set_box_limits(tmpc_ctx* ctx, const tmpc_box_limits* L) {
+  if (!ctx) return -1;
+  if (!ctx->has_model) return fail(ctx, "no model: call tmpc_set_model first");
+  ConstrDev c{};
+  if (L) {
+    for (int t = 0; t < 3; ++t) {
+      if (L->mode[t] < TMPC_LIMIT_NONE || L->mode[t] > TMPC_LIMIT_AUGMENTED_LAGRANGIAN)
+        return fail(ctx, "limit %d: mode %d (valid: 0 none, 1 QUADRATIC_PENALTY, 2 AUGMENTED_LAGRANGIAN)", t,
+                    L->mode[t]);
+      c.mode[t] = L->mode[t];
+      if (c.mode[t] != SOFT_NONE) c.any = 1;
+      for (int i = 0; i < NJMAX; ++i) {
+        c.lb[t][i] = L->lb[t][i];
+        c.ub[t][i] = L->ub[t][i];
+      }
+      c.mu_init[t] = L->mu_init[t];
+      c.mu_factor[t] = L->mu_factor[t];
+      c.mu_max[t] = L->mu_max[t];
+      c.phi_init[t] = L->phi_init[t];
+      c.phi_factor[t] = L->phi_factor[t];
+    }
+  }
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMemcpyAsync(ctx->dlim, &c, sizeof(c), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->hlim = c;
+  ctx->soft_B = ctx->soft_N = -1;
+  return 0;
+}
+
+int tmpc_set_soft_state(tmpc_ctx* ctx, int B, int N, const double* mu, const double* lam, const double* phi) {
+  if (!ctx) return -1;
+  if (!ctx->has_model) return fail(ctx, "no model: call tmpc_set_model first");
+  if (B < 1 || N < 2) return fail(ctx, "bad sizes B=%d N=%d", B, N);
+  hipSetDevice(ctx->device);
+  double *smu, *slam, *sphi;
+  int rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi);
+  if (rc) return rc;
+  const size_t n = (size_t)B * N * 6 * ctx->hmodel.n;
+  launch_soft_init(ctx->stream, ctx->dlim, n, 6 * ctx->hmodel.n, smu, slam, sphi);
+  HIP_OK(hipGetLastError());
+  if (mu) HIP_OK(hipMemcpyAsync(smu, mu, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (lam) HIP_OK(hipMemcpyAsync(slam, lam, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (phi) HIP_OK(hipMemcpyAsync(sphi, phi, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->soft_B = B;
+  ctx->soft_N = N;
+  return 0;
+}
+
+int tmpc_get_soft_state(tmpc_ctx* ctx, int B, int N, double* mu, double* lam, double* phi) {
+  if (!ctx) return -1;
+  if (ctx->soft_B != B || ctx->soft_N != N)
+    return fail(ctx, "no soft-constraint state for B=%d N=%d (solve or tmpc_set_soft_state first)", B, N);
+  hipSetDevice(ctx->device);
+  const size_t n = (size_t)B * N * 6 * ctx->hmodel.n;
+  if (mu) HIP_OK(hipMemcpy(mu, ctx->bufs["soft_mu"].ptr, n * sizeof(double), hipMemcpyDeviceToHost));
+  if (lam) HIP_OK(hipMemcpy(lam, ctx->bufs["soft_lam"].ptr, n * sizeof(double), hipMemcpyDeviceToHost));
+  if (phi) HIP_OK(hipMemcpy(phi, ctx->bufs["soft_phi"].ptr, n * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
 }
 
 int tmpc_set_options(tmpc_ctx* ctx, const tmpc_options* o) {
   if (!ctx || !o) return -1;
-  if (o->max_iter_linSys < 1 || o->max_iter_SQP_DDP < 1) return fail(ctx, "max_iter options must be >= 1");
+  if (o->max_iter_linSys < 1 || o->max_iter_SQP_DDP < 1 || o->max_iter_softConstraints < 1)
+    return fail(ctx, "max_iter options must be >= 1");
   if (!(o->alpha_factor_SQP_DDP > 0.0 && o->alpha_factor_SQP_DDP < 1.0))
     return fail(ctx, "alpha_factor_SQP_DDP must be in (0, 1)");
   ctx->opts = *o;
@@ -560,11 +685,8 @@ int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, dou
   HIP_OK(hipMemcpy(u, io_u, un * sizeof(double), hipMemcpyDeviceToHost));
   if (exit_sqp) HIP_OK(hipMemcpy(exit_sqp, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
   if (sqp_iter) HIP_OK(hipMemcpy(sqp_iter, ctx->bufs["st_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
-  // unconstrained: the soft-constraint outer loop runs once and exits with code 1 (:483-508)
-  for (int b = 0; b < B; ++b) {
-    if (exit_soft) exit_soft[b] = 1;
-    if (outer_iter) outer_iter[b] = 1;
-  }
+  if (exit_soft) HIP_OK(hipMemcpy(exit_soft, ctx->bufs["exit_soft"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (outer_iter) HIP_OK(hipMemcpy(outer_iter, ctx->bufs["outer_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
   if (trace) {
     const size_t n = (size_t)B * (ctx->opts.max_iter_SQP_DDP + 1);
 #define CP(field, src, T) \
@@ -665,7 +787,7 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   HIP_OK(hipMemcpyAsync(io_u, u, sizeof(double) * B * nj * K, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(st.rho, rho, sizeof(double) * B, hipMemcpyHostToDevice, ctx->stream));
   launch_init_state(ctx->stream, B, 0.0, ProbState{st.drho, st.drho, st.J, st.c, st.merit, st.iter, st.active,
-                                                   st.need_grad, st.exit_sqp});
+                                                   st.need_grad, st.exit_sqp}, nullptr);
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), io_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
   if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, true))) return rc;

@@ -55,6 +55,58 @@ struct CostDev {            // QuadraticCost (TrajoptCost.py:24-104)
   double xg[NXMAX];
 };
 
+// Soft box limits: BoxConstraint in QUADRATIC_PENALTY / AUGMENTED_LAGRANGIAN
+// mode (TrajoptConstraint.py:53-166) with the vector semantics of
+// oracle/soft.py.  Type t: 0 joint (q), 1 velocity (qd), 2 torque (u).  Per
+// knot the constants mu / lambda / phi have 6 n slots, slot t*2n + e with
+// e < n the lower half (v = z - lb) and e >= n the upper half (v = ub - z).
+// Joint and velocity limits cover knots 0..N-1, torque limits 0..N-2.
+enum { SOFT_NONE = 0, SOFT_QP = 1, SOFT_AL = 2 };
+
+struct ConstrDev {
+  int mode[3];              // SOFT_* per type
+  int any;                  // some type is soft
+  double lb[3][NJMAX], ub[3][NJMAX];
+  double mu_init[3], mu_factor[3], mu_max[3], phi_init[3], phi_factor[3];   // BoxConstraint options (:38-46)
+};
+
+// Value (summed over types, value_soft_constraints :296-310) and the per-type
+// jacobians of one knot.  z = [q; qd; u] (u unused at the terminal knot); the
+// three jacobians have disjoint supports, so jac[3 NJ] holds all of them.
+// Arithmetic as BoxConstraint.value / .jacobian (:53-128).
+template <int NJ>
+__device__ __forceinline__ double soft_knot(const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
+                                            const double* __restrict__ lam, bool terminal, const double (&z)[3 * NJ],
+                                            double (&jac)[3 * NJ]) {
+  double value = 0.0;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int md = Cs->mode[t];
+#pragma unroll
+    for (int i = 0; i < NJ; ++i) jac[t * NJ + i] = 0.0;
+    if (md == SOFT_NONE || (t == 2 && terminal)) continue;
+    double sq = 0.0, lin = 0.0;
+#pragma unroll
+    for (int e = 0; e < 2 * NJ; ++e) {
+      const int i = e < NJ ? e : e - NJ;
+      const double zi = z[t * NJ + i];
+      const double v = e < NJ ? zi - Cs->lb[t][i] : Cs->ub[t][i] - zi;
+      const double m = mu[t * 2 * NJ + e];
+      const double l = lam[t * 2 * NJ + e];
+      sq += m * (v * v);
+      lin += l * v;
+      if (v < 0.0) {
+        const double s = e < NJ ? 1.0 : -1.0;
+        double coef = 2.0 * (m * (v * s));
+        if (md == SOFT_AL) coef += l * s;
+        jac[t * NJ + i] += coef;
+      }
+    }
+    value += md == SOFT_AL ? sq + lin : sq;
+  }
+  return value;
+}
+
 // ----------------------------------------------------------------- helpers
 template <bool CHAIN>
 __device__ __forceinline__ int parent_of(const ModelDev* __restrict__ M, int j) {

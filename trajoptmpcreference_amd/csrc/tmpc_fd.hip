@@ -61,9 +61,13 @@ __global__ void __launch_bounds__(256) k_qp_fd(const ModelDev* __restrict__ M, i
 // totalCost (:296-310), totalHardConstraintViolation (:273-294) and the
 // directional derivative D (:635-648, gradient taken at x_new as the
 // reference does).  Knot lane N-1 carries the terminal cost / D term and the
-// |x_0 - xs| violation term.
-template <int NJ, bool CHAIN>
+// |x_0 - xs| violation term.  SOFT: soft-limit value (slot 3, summed after
+// the cost terms as totalCost does, :303-307) and jacobian . dxu added to D
+// (:633-646).  terms: [B][T][N][4] = cost, violation, D, soft value.
+template <int NJ, bool CHAIN, bool SOFT>
 __global__ void __launch_bounds__(256) k_ls_terms(const ModelDev* __restrict__ M, const CostDev* __restrict__ C,
+                                                  const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
+                                                  const double* __restrict__ lam,
                                                   int B, int N, int T, double dt, const double* __restrict__ alphas,
                                                   const double* __restrict__ x, const double* __restrict__ u,
                                                   const double* __restrict__ xs, const double* __restrict__ dx,
@@ -108,9 +112,11 @@ __global__ void __launch_bounds__(256) k_ls_terms(const ModelDev* __restrict__ M
   }
   double cost = 0.5 * vq;
   double viol = 0.0;
-  double* out = terms + ((size_t)bt * N + k) * 3;
+  double* out = terms + ((size_t)bt * N + k) * 4;
+  double uk[NU], duk[NU];
+#pragma unroll
+  for (int m = 0; m < NU; ++m) uk[m] = duk[m] = 0.0;
   if (k < K) {
-    double uk[NU], duk[NU];
 #pragma unroll
     for (int m = 0; m < NU; ++m) {
       duk[m] = dub ? dub[k * NU + m] : 0.0;
@@ -153,9 +159,26 @@ __global__ void __launch_bounds__(256) k_ls_terms(const ModelDev* __restrict__ M
       viol += fabs(x0 - xs[(size_t)b * NX + m]);
     }
   }
+  double sv = 0.0;
+  if (SOFT) {
+    double z[3 * NJ], jac[3 * NJ];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) z[m] = xk[m];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) z[NX + m] = uk[m];
+    const size_t ko = ((size_t)b * N + k) * 6 * NJ;
+    sv = soft_knot<NJ>(Cs, mu + ko, lam + ko, k == K, z, jac);
+    double Ds = 0.0;
+#pragma unroll
+    for (int m = 0; m < NX; ++m) Ds += jac[m] * dxk[m];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) Ds += jac[NX + m] * duk[m];
+    Dk = Dk + Ds;
+  }
   out[0] = cost;
   out[1] = viol;
   out[2] = Dk;
+  out[3] = sv;
 }
 
 // ======================================================================= kernel-level entry points
@@ -227,11 +250,16 @@ struct LaunchFD {
     hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN>), TMPC_GRID(B * (N - 1), 256), 0, s, M, B, N, dt, x, u, xs, need, qdd,
                        cvec);
   }
-  static void ls_terms(hipStream_t s, const ModelDev* M, const CostDev* C, int B, int N, int T, double dt,
-                       const double* alphas, const double* x, const double* u, const double* xs, const double* dx,
-                       const double* du, const int* active, double* terms) {
-    hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN>), TMPC_GRID(B * T * N, 256), 0, s, M, C, B, N, T, dt, alphas, x, u,
-                       xs, dx, du, active, terms);
+  static void ls_terms(hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
+                       const double* lam, int B, int N, int T, double dt, const double* alphas, const double* x,
+                       const double* u, const double* xs, const double* dx, const double* du, const int* active,
+                       double* terms) {
+    if (mu)
+      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, true>), TMPC_GRID(B * T * N, 256), 0, s, M, C, Cs, mu, lam, B, N, T,
+                         dt, alphas, x, u, xs, dx, du, active, terms);
+    else
+      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, false>), TMPC_GRID(B * T * N, 256), 0, s, M, C, Cs, mu, lam, B, N,
+                         T, dt, alphas, x, u, xs, dx, du, active, terms);
   }
   static void unit_fd(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
                       double* xnext, double* qdd) {
@@ -260,10 +288,11 @@ int launch_qp_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, in
                  const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
   TMPC_DISPATCH_NJ(nj, chain, qp_fd(s, M, B, N, dt, x, u, xs, need, qdd, cvec))
 }
-int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, int B, int N, int T,
-                    double dt, const double* alphas, const double* x, const double* u, const double* xs,
-                    const double* dx, const double* du, const int* active, double* terms) {
-  TMPC_DISPATCH_NJ(nj, chain, ls_terms(s, M, C, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
+int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
+                    const double* mu, const double* lam, int B, int N, int T, double dt, const double* alphas,
+                    const double* x, const double* u, const double* xs, const double* dx, const double* du,
+                    const int* active, double* terms) {
+  TMPC_DISPATCH_NJ(nj, chain, ls_terms(s, M, C, Cs, mu, lam, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
 }
 int launch_unit_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
                    const double* u, double* xnext, double* qdd) {

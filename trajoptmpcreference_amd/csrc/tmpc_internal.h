@@ -63,9 +63,10 @@ int launch_qp_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, 
                    const int* need, double* minv);
 int launch_qp_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, const double* x,
                    const int* need, const double* qdd, const double* minv, double* A, double* Bm);
-int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, int B, int N, int T,
-                    double dt, const double* alphas, const double* x, const double* u, const double* xs,
-                    const double* dx, const double* du, const int* active, double* terms);
+int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
+                    const double* mu, const double* lam, int B, int N, int T, double dt, const double* alphas,
+                    const double* x, const double* u, const double* xs, const double* dx, const double* du,
+                    const int* active, double* terms);
 int launch_unit_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
                    const double* u, double* xnext, double* qdd);
 int launch_unit_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, const double* x, double* minv);
@@ -78,17 +79,26 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-              double* Pd);
+              double* Pd, const double* jsoft);
+int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
+                     const int* active, const double* x, const double* u, const double* mu, const double* lam,
+                     double* Gk, double* jsoft);
 int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
                const double* Su, const double* gam, const double* guess, double tol, int max_iter, double* lam,
                int* iters, double* tnu, double* tres, double* Pd);
 int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const double* Sd, const double* Sl,
                    const double* gam, double* U, double* Y, double* lam);
 int pcg_set_max_lds();
-void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, const double* alphas,
+void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
                       int* active_count, unsigned long long* counters);
-void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st);
+void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active);
+void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
+                       const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
+                       int* outer_iter, int* exit_soft, int* outer_count);
+void launch_outer_init(hipStream_t s, int B, int* outer_active, int* outer_iter, int* exit_soft);
+void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, double* mu, double* lam,
+                      double* phi);
 
 }  // namespace tmpc

@@ -177,6 +177,97 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
   return (k == N - 1) || (C->QF_start >= 0 && k >= C->QF_start);
 }
 
+// Per-knot Ghat_k = (G_k + rho I)^-1 with soft limits: formKKTSystemBlocks adds
+// outer(jac, jac) to the cost Hessian block and jac to its gradient
+// (TrajoptMPCReference.py:220-225, :255-259), then solveKKTSystem_Schur adds rho
+// (:419-422).  The per-type jacobians have disjoint supports on [q | qd | u], so
+// G_k stays block-diagonal in (x, u) and each type's outer product lands in its
+// own diagonal sub-block (oracle/soft.py).  One 16-lane group per (problem,
+// knot, x|u block), one row per lane, Gauss-Jordan as k_ginv.  Also writes the
+// summed jacobian (the g_k increment) to jsoft [B][N][NX + NU].
+// Layout of Gk: [B][N][NX*NX + NU*NU] (x block, then the packed u block).
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
+                                                  int B, int N, const double* __restrict__ rho,
+                                                  const int* __restrict__ active, const double* __restrict__ x,
+                                                  const double* __restrict__ u, const double* __restrict__ mu,
+                                                  const double* __restrict__ lam, double* __restrict__ Gk,
+                                                  double* __restrict__ jsoft) {
+  constexpr int NX = 2 * NJ, NU = NJ, MC = 6 * NJ;
+  const int lane = threadIdx.x & 63;
+  const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int r = lane & 15, base = lane & ~15;
+  const bool in_range = slot < B * N * 2;
+  const int b = in_range ? slot / (2 * N) : 0;
+  const int rem = in_range ? slot - b * 2 * N : 0;
+  const int k = rem >> 1, which = rem & 1;
+  const bool terminal = k == N - 1;
+  const bool act = in_range && active[b] && !(which == 1 && terminal);
+  const int n = which ? NJ : NX;
+  double z[3 * NJ], jac[3 * NJ];
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NU * (N - 1);
+#pragma unroll
+  for (int m = 0; m < NX; ++m) z[m] = act ? xb[m * N + k] : 0.0;
+#pragma unroll
+  for (int m = 0; m < NU; ++m) z[NX + m] = (act && !terminal) ? ub[m * (N - 1) + k] : 0.0;
+  const size_t ko = ((size_t)b * N + k) * MC;
+  soft_knot<NJ>(Cs, mu + ko, lam + ko, terminal, z, jac);
+  const double* src = which ? C->R : (use_QF(C, k, N) ? C->QF : C->Q);
+  const double rh = act ? rho[b] : 0.0;
+  double a[NX], inv[NX];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) {
+    double outer = 0.0;
+    if (which == 0) {
+#pragma unroll
+      for (int rr = 0; rr < NX; ++rr)
+        if (rr == r && (rr / NJ) == (c / NJ)) outer = jac[rr] * jac[c];
+    } else {
+#pragma unroll
+      for (int rr = 0; rr < NU; ++rr)
+        if (rr == r && c < NU) outer = jac[NX + rr] * jac[NX + c];
+    }
+    a[c] = (act && r < n && c < n) ? (src[r * n + c] + outer) + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
+    inv[c] = (r == c) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int p = 0; p < NX; ++p) {
+    double pa[NX], pi[NX];
+#pragma unroll
+    for (int c = 0; c < NX; ++c) {
+      pa[c] = __shfl(a[c], base + p, 64);
+      pi[c] = __shfl(inv[c], base + p, 64);
+    }
+    const double piv = pa[p];
+    if (r == p) {
+#pragma unroll
+      for (int c = 0; c < NX; ++c) { a[c] = a[c] / piv; inv[c] = inv[c] / piv; }
+    } else {
+      const double f = a[p];
+#pragma unroll
+      for (int c = 0; c < NX; ++c) { a[c] -= f * (pa[c] / piv); inv[c] -= f * (pi[c] / piv); }
+    }
+  }
+  if (!in_range || !active[b] || r >= n) return;
+  if (act) {
+    double* out = Gk + ((size_t)b * N + k) * (NX * NX + NU * NU) + (which ? NX * NX : 0);
+#pragma unroll
+    for (int c = 0; c < NX; ++c)
+      if (c < n) out[r * n + c] = inv[c];
+  }
+  double jr = 0.0;
+#pragma unroll
+  for (int m = 0; m < NX; ++m)
+    if (m == (which ? NX + r : r)) jr = jac[m];
+  if (which) {
+#pragma unroll
+    for (int m = 0; m < NU; ++m)
+      if (m == r) jr = terminal ? 0.0 : jac[NX + m];
+  }
+  jsoft[((size_t)b * N + k) * (NX + NU) + (which ? NX : 0) + r] = jr;
+}
+
 // ======================================================================= block-tridiagonal PCG
 // One workgroup per problem, one lane per row of S (PCG.pcg, PCG.py:66-111).
 //
@@ -734,14 +825,27 @@ __device__ __forceinline__ void lds_copy(double* dst, const double* __restrict__
 // Row i of block k of the Schur complement and gamma_k[i] into R (:419-424):
 //   S_kk = -(A G A^T + B G B^T + Ghat_x,k), S_{k,k-1} = A_{k-1} Ghat_x,k-1,
 //   S_{k,k+1} = (A_k Ghat_x,k)^T, gamma_k = c_k + [AB Ghat g]_{k-1} - (Ghat_k g_k)_x
-template <int NJ>
+// Ghat blocks: the three distinct cost blocks staged in LDS (QuadraticCost,
+// no soft limits), or per knot from HBM (PK: soft limits, k_ginv_soft layout)
+template <int NJ, bool PK>
+struct GhatSrc {
+  static constexpr int NX = 2 * NJ, NU = NJ, GS = NX * NX + NU * NU;
+  const double* base;
+  __device__ __forceinline__ const double* x(const CostDev* C, int k, int N) const {
+    return PK ? base + (size_t)k * GS : base + (use_QF(C, k, N) ? NX * NX : 0);
+  }
+  __device__ __forceinline__ const double* u(int k) const {
+    return PK ? base + (size_t)k * GS + NX * NX : base + 2 * NX * NX;
+  }
+};
+
+template <int NJ, bool PK>
 __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, const QpStage& S,
-                                               const double* __restrict__ g_lds, double c_ki, int k, int i, int N,
-                                               PcgRow<2 * NJ>& R) {
+                                               const GhatSrc<NJ, PK>& Gh, const double* __restrict__ g_lds,
+                                               double c_ki, int k, int i, int N, PcgRow<2 * NJ>& R) {
   constexpr int NX = 2 * NJ, NU = NJ;
   const int K = N - 1;
-  const double* Gu = S.G + 2 * NX * NX;
-  const double* Gxk = S.G + (use_QF(C, k, N) ? NX * NX : 0);
+  const double* Gxk = Gh.x(C, k, N);
   const double* gk = g_lds + k * (NX + NU);
   double gam = c_ki;
   {
@@ -755,7 +859,8 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
     for (int j = 0; j < NX; ++j) R.sd[j] = -Gxk[i * NX + j];
   } else {
     const int km = k - 1;
-    const double* Gxm = S.G + (use_QF(C, km, N) ? NX * NX : 0);
+    const double* Gxm = Gh.x(C, km, N);
+    const double* Gu = Gh.u(km);
     const double* gm = g_lds + km * (NX + NU);
     const double* A = S.A + km * NX * NX;
     const double* Bm = S.B + km * NX * NU;
@@ -807,8 +912,8 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
 //       QP_MODE_SCHUR prologue only: S blocks and gamma to Sd_out / Sl_out / gam_out
 //                     (method S: the direct solve k_btsolve runs next);
 //       QP_MODE_DXU   epilogue only, lambda read from lam_out (method S, after k_btsolve).
-template <int NJ, int RPL, int MAXT>
-__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond, int mode,
+template <int NJ, int RPL, int MAXT, bool PK, int MODE>
+__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond,
                                              const double* __restrict__ x, const double* __restrict__ u,
                                              const int* __restrict__ active, const double* __restrict__ Ginv,
                                              const double* __restrict__ Aall, const double* __restrict__ Ball,
@@ -816,7 +921,8 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
                                              int* __restrict__ iters, double* __restrict__ dx,
                                              double* __restrict__ du, double* __restrict__ lam_out,
                                              double* __restrict__ Sd_out, double* __restrict__ Sl_out,
-                                             double* __restrict__ gam_out, double* __restrict__ Pd_out) {
+                                             double* __restrict__ gam_out, double* __restrict__ Pd_out,
+                                             const double* __restrict__ jsoft) {
   constexpr int NX = 2 * NJ, NU = NJ;
   const int b = blockIdx.x;
   if (!active[b]) return;
@@ -829,7 +935,8 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   double* lam_lds = S.u + NU * K;
   lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
   lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
-  lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
+  if (!PK) lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
+  const GhatSrc<NJ, PK> Gh{PK ? Ginv + (size_t)b * N * GhatSrc<NJ, PK>::GS : S.G};
   lds_copy(S.x, x + (size_t)b * NX * N, NX * N);
   lds_copy(S.u, u + (size_t)b * NU * K, NU * K);
   __syncthreads();
@@ -847,12 +954,13 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
 #pragma unroll
       for (int m = 0; m < NU; ++m) g += S.u[m * K + kk] * C->R[m * NU + (c - NX)];
     }
+    if (PK) g = g + jsoft[(size_t)b * N * (NX + NU) + e];   // soft-limit jacobian (:220-225)
     g_lds[e] = g;
   }
   __syncthreads();
 
   double xv[RPL];
-  if (mode == QP_MODE_DXU) {
+  if constexpr (MODE == QP_MODE_DXU) {
 #pragma unroll
     for (int m = 0; m < RPL; ++m) xv[m] = ln.valid ? lam_out[(size_t)b * rows + ln.row(m)] : 0.0;
     if (threadIdx.x == 0) iters[b] = 0;
@@ -866,7 +974,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
     bv[m] = 0.0;
     if (!ln.valid) continue;
     const int i = ln.r(m);
-    bv[m] = qp_schur_row<NJ>(C, S, g_lds, cvec[(size_t)b * N * NX + k * NX + i], k, i, N, R[m]);
+    bv[m] = qp_schur_row<NJ, PK>(C, S, Gh, g_lds, cvec[(size_t)b * N * NX + k * NX + i], k, i, N, R[m]);
     if (Sd_out) {
 #pragma unroll
       for (int j = 0; j < NX; ++j) Sd_out[(((size_t)b * N + k) * NX + i) * NX + j] = R[m].sd[j];
@@ -877,7 +985,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
       gam_out[(size_t)b * rows + ln.row(m)] = bv[m];
     }
   }
-  if (mode == QP_MODE_SCHUR) {
+  if constexpr (MODE == QP_MODE_SCHUR) {
     if (threadIdx.x == 0) iters[b] = 0;
     return;
   }
@@ -894,12 +1002,12 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   __syncthreads();
   lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
   lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
-  lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
+  if (!PK) lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
   if (ln.valid) {
 #pragma unroll
     for (int m = 0; m < RPL; ++m) {
       lam_lds[ln.row(m)] = xv[m];
-      if (lam_out && mode == QP_MODE_PCG) lam_out[(size_t)b * rows + ln.row(m)] = xv[m];
+      if (lam_out && MODE == QP_MODE_PCG) lam_out[(size_t)b * rows + ln.row(m)] = xv[m];
     }
   }
   __syncthreads();
@@ -930,11 +1038,10 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
     }
   }
   __syncthreads();
-  const double* Gu = S.G + 2 * NX * NX;
   for (int e = threadIdx.x; e < N * NX + K * NU; e += blockDim.x) {
     if (e < N * NX) {
       const int kk = e / NX, i = e - kk * NX;
-      const double* Gxk = S.G + (use_QF(C, kk, N) ? NX * NX : 0);
+      const double* Gxk = Gh.x(C, kk, N);
       const double* gk = g_lds + kk * (NX + NU);
       const double* ck = ctl_x + kk * NX;
       double acc = 0.0;
@@ -944,6 +1051,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
     } else {
       const int f = e - N * NX;
       const int kk = f / NU, i = f - kk * NU;
+      const double* Gu = Gh.u(kk);
       const double* gk = g_lds + kk * (NX + NU) + NX;
       const double* ck = ctl_u + kk * NU;
       double acc = 0.0;
@@ -1068,7 +1176,7 @@ int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const
 // alpha schedule (:712-718), reduce_regularization (:457-461) and
 // check_for_exit_or_error (:463-481), applies the accepted step and records
 // the trace row (:691-705 / :729-743).
-__global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, int T, int mode,
+__global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, int T, int mode, int soft,
                                                   const double* __restrict__ alphas, SolverOpts o,
                                                   const double* __restrict__ terms, double* __restrict__ x,
                                                   double* __restrict__ u, const double* __restrict__ dx,
@@ -1082,14 +1190,18 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
   __shared__ int s_choice;
   const int t = threadIdx.x;
   if (t < T) {
-    const double* tm = terms + ((size_t)b * T + t) * N * 3;
+    const double* tm = terms + ((size_t)b * T + t) * N * 4;
     double J = 0.0, c = 0.0, D = 0.0;
-    for (int k = 0; k < N - 1; ++k) J = J + tm[k * 3 + 0];
-    J = J + tm[(N - 1) * 3 + 0];
-    c = tm[(N - 1) * 3 + 1];
-    for (int k = 0; k < N - 1; ++k) c = c + tm[k * 3 + 1];
-    for (int k = 0; k < N - 1; ++k) D += tm[k * 3 + 2];
-    D += tm[(N - 1) * 3 + 2];
+    for (int k = 0; k < N - 1; ++k) J = J + tm[k * 4 + 0];
+    J = J + tm[(N - 1) * 4 + 0];
+    if (soft) {   // totalCost adds the soft values after the cost terms (:303-307)
+      for (int k = 0; k < N - 1; ++k) J = J + tm[k * 4 + 3];
+      J = J + tm[(N - 1) * 4 + 3];
+    }
+    c = tm[(N - 1) * 4 + 1];
+    for (int k = 0; k < N - 1; ++k) c = c + tm[k * 4 + 1];
+    for (int k = 0; k < N - 1; ++k) D += tm[k * 4 + 2];
+    D += tm[(N - 1) * 4 + 2];
     sJ[t] = J;
     sC[t] = c;
     sD[t] = D;
@@ -1196,9 +1308,13 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
   }
 }
 
-__global__ void k_init_state(int B, double rho_init, ProbState st) {
+__global__ void k_init_state(int B, double rho_init, ProbState st, const int* __restrict__ outer_active) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  if (outer_active && !outer_active[b]) {
+    st.active[b] = 0;
+    return;
+  }
   st.rho[b] = rho_init;
   st.drho[b] = 1.0;
   st.iter[b] = 0;
@@ -1274,18 +1390,35 @@ struct LaunchNJ {
   static void qp(hipStream_t s, const CostDev* C, int B, int N, int precond, int mode, const double* x, const double* u,
                  const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
                  int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-                 double* Pd) {
+                 double* Pd, const double* jsoft) {
     constexpr int NX = 2 * NJ;
     const int rows = N * NX;
     const int rpl = pcg_rpl(N, NX);
     const int threads = ((rows / rpl + 63) / 64) * 64;
     const size_t lds = qp_lds_doubles(N, NX, NJ) * sizeof(double);
-    if (rpl == 1)
-      hipLaunchKernelGGL((k_qp<NJ, 1, 768>), dim3(B), dim3(threads), lds, s, C, B, N, precond, mode, x, u, active, G, A,
-                         Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
-    else
-      hipLaunchKernelGGL((k_qp<NJ, 2, 512>), dim3(B), dim3(threads), lds, s, C, B, N, precond, mode, x, u, active, G, A,
-                         Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, Sl, gam, Pd);
+#define TMPC_QP_ARGS s, C, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, \
+                     Sl, gam, Pd, jsoft
+#define TMPC_QP_LAUNCH(PKV, MODEV)                                                                        \
+    if (rpl == 1)                                                                                          \
+      hipLaunchKernelGGL((k_qp<NJ, 1, 768, PKV, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);        \
+    else                                                                                                   \
+      hipLaunchKernelGGL((k_qp<NJ, 2, 512, PKV, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);
+    // soft limits (jsoft != null): per-knot Ghat from HBM
+    if (mode == QP_MODE_PCG) {
+      if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_PCG) } else { TMPC_QP_LAUNCH(false, QP_MODE_PCG) }
+    } else if (mode == QP_MODE_SCHUR) {
+      if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_SCHUR) } else { TMPC_QP_LAUNCH(false, QP_MODE_SCHUR) }
+    } else {
+      if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_DXU) } else { TMPC_QP_LAUNCH(false, QP_MODE_DXU) }
+    }
+#undef TMPC_QP_LAUNCH
+#undef TMPC_QP_ARGS
+  }
+  static void ginv_soft(hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
+                        const int* active, const double* x, const double* u, const double* mu, const double* lam,
+                        double* Gk, double* jsoft) {
+    hipLaunchKernelGGL((k_ginv_soft<NJ>), TMPC_GRID(B * N * 2 * 16, 64), 0, s, C, Cs, B, N, rho, active, x, u, mu,
+                       lam, Gk, jsoft);
   }
 };
 
@@ -1297,11 +1430,17 @@ int pcg_set_max_lds() {
   err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 2, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
   SETA(2) SETA(4) SETA(6) SETA(8) SETA(10) SETA(12) SETA(14) SETA(16)
 #undef SETA
-#define SETQ(V)                                                                                                   \
-  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1, 768>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
-  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 2, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#define SETQ2(V, P, MD)                                                                                  \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1, 768, P, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  bytes);                                                              \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 2, 512, P, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  bytes);
+#define SETQ1(V, P) SETQ2(V, P, QP_MODE_PCG) SETQ2(V, P, QP_MODE_SCHUR) SETQ2(V, P, QP_MODE_DXU)
+#define SETQ(V) SETQ1(V, false) SETQ1(V, true)
   SETQ(1) SETQ(2) SETQ(3) SETQ(4) SETQ(5) SETQ(6) SETQ(7)
 #undef SETQ
+#undef SETQ1
+#undef SETQ2
   return err;
 }
 
@@ -1334,16 +1473,141 @@ int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* S
   }
 }
 
-void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, const double* alphas,
+void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
                       int* active_count, unsigned long long* counters) {
-  hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, B, N, NX, NU, T, mode, alphas, o, terms, x, u, dx, du,
+  hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u, dx, du,
                      st, pcg_iters, tr, active_count, counters);
 }
 
-void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st) {
-  hipLaunchKernelGGL(k_init_state, TMPC_GRID(B, 256), 0, s, B, rho_init, st);
+void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active) {
+  hipLaunchKernelGGL(k_init_state, TMPC_GRID(B, 256), 0, s, B, rho_init, st, outer_active);
+}
+
+// ======================================================================= soft-constraint outer loop
+// check_and_update_soft_constraints (TrajoptMPCReference.py:483-508) for one
+// problem per 64-lane workgroup, after its inner SQP loop exited:
+//   max_c = max over types and knots of |min(v)|  (max_soft_constraint_value, :130-135)
+//   exit 1 if max_c < tol; exit 2 at the last outer iteration (else outer_iter += 1);
+//   otherwise update_soft_constraint_constants (:137-166) elementwise and exit 3
+//   when no constant changed (all mu at their limit).
+// Unconstrained problems (no soft type) take the reference's path: max_c = 0 -> exit 1.
+__device__ __forceinline__ double soft_v(const ConstrDev* Cs, int t, int e, int n, double z) {
+  const int i = e < n ? e : e - n;
+  return e < n ? z - Cs->lb[t][i] : Cs->ub[t][i] - z;
+}
+
+__global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__ Cs, int B, int N, int NJ,
+                                                   double tol, int max_iter, const double* __restrict__ x,
+                                                   const double* __restrict__ u, double* __restrict__ mu,
+                                                   double* __restrict__ lam, double* __restrict__ phi,
+                                                   int* __restrict__ outer_active, int* __restrict__ outer_iter,
+                                                   int* __restrict__ exit_soft, int* __restrict__ outer_count) {
+  const int b = blockIdx.x;
+  if (!outer_active[b]) return;
+  const int t0 = threadIdx.x;
+  const int NX = 2 * NJ, K = N - 1, MC = 6 * NJ;
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NJ * K;
+  auto zval = [&](int t, int i, int k) -> double {
+    return t == 2 ? ub[i * K + k] : xb[(t * NJ + i) * N + k];
+  };
+  // max_c over (type, knot) pairs
+  double mx = 0.0;
+  for (int p = t0; p < 3 * N; p += 64) {
+    const int t = p / N, k = p - t * N;
+    if (Cs->mode[t] == SOFT_NONE || (t == 2 && k == K)) continue;
+    double mn = 0.0;
+    for (int e = 0; e < 2 * NJ; ++e) {
+      const double v = soft_v(Cs, t, e, NJ, zval(t, e < NJ ? e : e - NJ, k));
+      mn = e == 0 ? v : fmin(mn, v);
+    }
+    mx = fmax(mx, fabs(mn));
+  }
+  __shared__ double smax[64];
+  __shared__ int s_exit, s_changed;
+  smax[t0] = mx;
+  if (t0 == 0) s_changed = 0;
+  __syncthreads();
+  if (t0 == 0) {
+    double m = 0.0;
+    for (int i = 0; i < 64; ++i) m = fmax(m, smax[i]);
+    int ex = 0;
+    if (m < tol) ex = 1;
+    const int it = outer_iter[b];
+    if (it == max_iter - 1) ex = 2;
+    else outer_iter[b] = it + 1;
+    s_exit = ex;
+  }
+  __syncthreads();
+  if (s_exit == 0) {
+    for (int p = t0; p < N * MC; p += 64) {
+      const int k = p / MC, sl = p - k * MC;
+      const int t = sl / (2 * NJ), e = sl - t * 2 * NJ;
+      if (Cs->mode[t] == SOFT_NONE || (t == 2 && k == K)) continue;
+      const double v = soft_v(Cs, t, e, NJ, zval(t, e < NJ ? e : e - NJ, k));
+      const size_t o = ((size_t)b * N + k) * MC + sl;
+      if (v < 0.0 && !(fabs(v) < phi[o])) {
+        if (mu[o] < Cs->mu_max[t]) {
+          s_changed = 1;
+          mu[o] = fmin(Cs->mu_max[t], mu[o] * Cs->mu_factor[t]);
+        }
+      } else if (v < 0.0) {
+        s_changed = 1;
+        lam[o] += mu[o] * v;
+        phi[o] /= Cs->phi_factor[t];
+      }
+    }
+  }
+  __syncthreads();
+  if (t0 == 0) {
+    int ex = s_exit;
+    if (ex == 0 && !s_changed) ex = 3;
+    if (ex) {
+      exit_soft[b] = ex;
+      outer_active[b] = 0;
+    } else {
+      atomicAdd(outer_count, 1);
+    }
+  }
+}
+
+void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
+                       const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
+                       int* outer_iter, int* exit_soft, int* outer_count) {
+  hipLaunchKernelGGL(k_soft_outer, dim3(B), dim3(64), 0, s, Cs, B, N, nj, tol, max_iter, x, u, mu, lam, phi,
+                     outer_active, outer_iter, exit_soft, outer_count);
+}
+
+// BoxConstraint.__init__ (:21-24): mu = mu_init, lambda = 0, phi = phi_init
+__global__ void k_soft_init(const ConstrDev* __restrict__ Cs, size_t total, int MC, double* __restrict__ mu,
+                            double* __restrict__ lam, double* __restrict__ phi) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int t = (int)(i % MC) / (MC / 3);
+  mu[i] = Cs->mu_init[t];
+  lam[i] = 0.0;
+  phi[i] = Cs->phi_init[t];
+}
+
+__global__ void k_outer_init(int B, int* __restrict__ outer_active, int* __restrict__ outer_iter,
+                             int* __restrict__ exit_soft) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  outer_active[b] = 1;
+  outer_iter[b] = 0;
+  exit_soft[b] = 0;
+}
+
+void launch_outer_init(hipStream_t s, int B, int* outer_active, int* outer_iter, int* exit_soft) {
+  hipLaunchKernelGGL(k_outer_init, TMPC_GRID(B, 256), 0, s, B, outer_active, outer_iter, exit_soft);
+}
+
+void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, double* mu, double* lam,
+                      double* phi) {
+  hipLaunchKernelGGL(k_soft_init, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, Cs, total, MC, mu, lam,
+                     phi);
 }
 
 // dispatch tables over the joint count and the chain specialisation
@@ -1395,11 +1659,16 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-              double* Pd) {
+              double* Pd, const double* jsoft) {
   if (N * 2 * nj > 1024) return -1;
   if (qp_lds_doubles(N, 2 * nj, nj) * sizeof(double) > 160 * 1024) return -3;
   TMPC_DISPATCH_NJ2(nj, qp(s, C, B, N, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd,
-                           Sl, gam, Pd))
+                           Sl, gam, Pd, jsoft))
+}
+int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
+                     const int* active, const double* x, const double* u, const double* mu, const double* lam,
+                     double* Gk, double* jsoft) {
+  TMPC_DISPATCH_NJ2(nj, ginv_soft(s, C, Cs, B, N, rho, active, x, u, mu, lam, Gk, jsoft))
 }
 
 }  // namespace tmpc

@@ -48,6 +48,8 @@ _OPTION_MAP = {
     "rho_init_SQP_DDP": "rho_init_SQP_DDP",
     "expected_reduction_min_SQP_DDP": "expected_reduction_min_SQP_DDP",
     "expected_reduction_max_SQP_DDP": "expected_reduction_max_SQP_DDP",
+    "max_iter_softConstraints": "max_iter_softConstraints",
+    "exit_tolerance_softConstraints": "exit_tolerance_softConstraints",
 }
 
 
@@ -120,18 +122,22 @@ class TrajoptMPCReference:
                                       "device implementation)")
         if not isinstance(self.cost, QuadraticCost):
             raise NotImplementedError("the GPU solver supports QuadraticCost (UrdfCost is SURVEY §8f row 4)")
-        if self.other_constraints.has_any():
-            raise NotImplementedError("box constraints are not on the GPU path yet (SURVEY §8f row 1)")
+        spec = self.other_constraints.gpu_spec()   # raises for the hard modes
         if options.get("overloading"):
             raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
         ctx = self.plant._ctx()
         c = self.cost
         ctx.set_cost_quadratic(c.Q, c.QF, c.R, c.xg, c.QF_start)
         ctx.set_options(**{v: options[k] for k, v in _OPTION_MAP.items()})
+        ctx.set_box_limits(spec)
         return ctx
 
-    def SQP_batch(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.PCG_SS, options=None):
-        """B problems at once: x [B][nx][N], u [B][nu][N-1] -> dict of per-problem results."""
+    def SQP_batch(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.PCG_SS, options=None,
+                  soft_state=None):
+        """B problems at once: x [B][nx][N], u [B][nu][N-1] -> dict of per-problem results.
+        With soft limits every problem starts from the constraint objects' mu / lambda / phi
+        (or from soft_state = (mu, lam, phi), each [B][N][6n]); the final per-problem
+        constants are returned as r["soft_state"]."""
         options = {} if options is None else options
         self.set_default_options(options)
         method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
@@ -143,7 +149,19 @@ class TrajoptMPCReference:
         u = np.asarray(u, dtype=np.float64)
         if x.ndim != 3 or u.ndim != 3 or x.shape[2] != N or u.shape[2] != N - 1 or x.shape[0] != u.shape[0]:
             raise ValueError(f"expected x [B][nx][{N}] and u [B][nu][{N - 1}], got {x.shape} and {u.shape}")
-        return ctx.sqp_solve_batch(x, u, N, dt, method)
+        B = x.shape[0]
+        soft = self.other_constraints.has_any()
+        if soft:
+            if self.other_constraints.num_timesteps != N:
+                raise ValueError(f"TrajoptConstraint was built for {self.other_constraints.num_timesteps} knots, "
+                                 f"solving with N = {N}")
+            if soft_state is None:
+                soft_state = [np.broadcast_to(a, (B,) + a.shape) for a in self.other_constraints.pack_state(N)]
+            ctx.set_soft_state(B, N, *soft_state)
+        r = ctx.sqp_solve_batch(x, u, N, dt, method)
+        if soft:
+            r["soft_state"] = ctx.get_soft_state(B, N)
+        return r
 
     def SQP(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.N, options=None):
         """TrajoptMPCReference.SQP (:510-760) for one problem."""
@@ -154,10 +172,16 @@ class TrajoptMPCReference:
         it = int(r["sqp_iter"][0])
         t = r["trace"]
         rows = min(it + 1, t["alpha"].shape[1])
+        # the trace is that of the last outer pass, whose index is outer_iter unless the outer
+        # loop exited with code 1 or 3 (which increment the counter first, :490-499)
+        ex_soft, outer = int(r["exit_soft"][0]), int(r["outer_iter"][0])
+        last_pass = outer if ex_soft == 2 else outer - 1
+        if "soft_state" in r:
+            self.other_constraints.unpack_state(*[a[0] for a in r["soft_state"]])
         self.trace = []
         for i in range(rows):
             self.trace.append({
-                "outer_iteration": 0,
+                "outer_iteration": last_pass,
                 "iteration": int(t["iteration"][0, i]),
                 "line_search_iteration": int(t["line_search_iteration"][0, i]),
                 "alpha": float(t["alpha"][0, i]) if i else 1,
