@@ -164,6 +164,17 @@ int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, dou
 int tmpc_sqp_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
                                 int32_t* exit_sqp, int32_t* sqp_iter);
 
+/* Batched iLQR (the reference has only the MPCSolverMethods.iLQR enum value,
+ * TrajoptMPCReference.py:21-27): Riccati backward sweep + closed-loop forward rollouts with the
+ * SQP's *_SQP_DDP options, rho schedule and exit codes, and the soft-constraint outer loop when box
+ * limits are set.  Algorithm: oracle/ilqr.py.  x is replaced by the rollout of u from x[:, 0]
+ * before the first iteration.  exit_code: 1 converged (dJ < tol), 2 rho > rho_max, 3 max_iter.
+ * trace as tmpc_sqp_solve_batch (c = 0, merit = J, D = dV1 of the backward sweep). */
+int tmpc_ilqr_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, double* x, double* u, int32_t* exit_code,
+                          int32_t* exit_soft, int32_t* outer_iter, int32_t* iters, tmpc_trace* trace);
+int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u,
+                                 int32_t* exit_code, int32_t* iters);
+
 /* Euler rollout x_{k+1} = f(x_k, u_k) from x[:, 0] (device pointers), the §8d initial trajectory. */
 int tmpc_rollout_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, const double* d_u);
 

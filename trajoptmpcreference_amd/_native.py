@@ -79,6 +79,10 @@ SIGNATURES = {
                                        _ip, C.POINTER(tmpc_trace)]),
     "tmpc_sqp_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p,
                                               C.c_void_p, _ip, _ip]),
+    "tmpc_ilqr_solve_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, _dp, _dp, _ip, _ip, _ip, _ip,
+                                        C.POINTER(tmpc_trace)]),
+    "tmpc_ilqr_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p,
+                                               _ip, _ip]),
     "tmpc_rollout_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p]),
     "tmpc_fd_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
     "tmpc_fd_grad_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
@@ -243,28 +247,50 @@ class Context:
         return mu, lam, phi
 
     # ---------------------------------------------------------------- solves
+    def _trace_arrays(self, B):
+        W = int(self.options.max_iter_SQP_DDP) + 1
+        arrays = {}
+        for name, dt_ in [("iteration", np.int32), ("line_search_iteration", np.int32), ("alpha", np.float64),
+                          ("rho", np.float64), ("J", np.float64), ("c", np.float64), ("merit", np.float64),
+                          ("D", np.float64), ("reduction_ratio", np.float64),
+                          ("succeeded_line_search", np.int32), ("pcg_iters", np.int32)]:
+            arrays[name] = np.zeros((B, W), dtype=dt_)
+        return arrays, tmpc_trace(**{k: _ptr(v) for k, v in arrays.items()})
+
     def sqp_solve_batch(self, x, u, N, dt, method="PCG-SS", with_trace=True):
         """x [B][nx][N], u [B][nu][N-1] -> dict of results (arrays per problem)."""
         x = _c64(x).copy()
         u = _c64(u).copy()
         B = x.shape[0]
-        W = int(self.options.max_iter_SQP_DDP) + 1
         out = {k: np.zeros(B, dtype=np.int32) for k in ("exit_sqp", "exit_soft", "outer_iter", "sqp_iter")}
-        tr = None
-        arrays = {}
-        if with_trace:
-            for name, dt_ in [("iteration", np.int32), ("line_search_iteration", np.int32), ("alpha", np.float64),
-                              ("rho", np.float64), ("J", np.float64), ("c", np.float64), ("merit", np.float64),
-                              ("D", np.float64), ("reduction_ratio", np.float64),
-                              ("succeeded_line_search", np.int32), ("pcg_iters", np.int32)]:
-                arrays[name] = np.zeros((B, W), dtype=dt_)
-            tr = tmpc_trace(**{k: _ptr(v) for k, v in arrays.items()})
+        arrays, tr = self._trace_arrays(B) if with_trace else ({}, None)
         self._check(self.lib.tmpc_sqp_solve_batch(
             self.h, B, int(N), float(dt), LINSYS[method], _ptr(x), _ptr(u), _ptr(out["exit_sqp"]),
             _ptr(out["exit_soft"]), _ptr(out["outer_iter"]), _ptr(out["sqp_iter"]),
             C.byref(tr) if tr is not None else None), "tmpc_sqp_solve_batch")
         out.update(x=x, u=u, trace=arrays)
         return out
+
+    def ilqr_solve_batch(self, x, u, N, dt, with_trace=True):
+        """Batched iLQR (oracle/ilqr.py): x [B][nx][N] (only x[:, :, 0] is read), u [B][nu][N-1]."""
+        x = _c64(x).copy()
+        u = _c64(u).copy()
+        B = x.shape[0]
+        out = {k: np.zeros(B, dtype=np.int32) for k in ("exit_code", "exit_soft", "outer_iter", "iter")}
+        arrays, tr = self._trace_arrays(B) if with_trace else ({}, None)
+        self._check(self.lib.tmpc_ilqr_solve_batch(
+            self.h, B, int(N), float(dt), _ptr(x), _ptr(u), _ptr(out["exit_code"]), _ptr(out["exit_soft"]),
+            _ptr(out["outer_iter"]), _ptr(out["iter"]), C.byref(tr) if tr is not None else None),
+            "tmpc_ilqr_solve_batch")
+        out.update(x=x, u=u, trace=arrays)
+        return out
+
+    def ilqr_solve_batch_device(self, B, N, dt, d_x, d_u, want_status=False):
+        ex = np.zeros(B, dtype=np.int32) if want_status else None
+        it = np.zeros(B, dtype=np.int32) if want_status else None
+        self._check(self.lib.tmpc_ilqr_solve_batch_device(self.h, B, int(N), float(dt), d_x, d_u, _ptr(ex), _ptr(it)),
+                    "tmpc_ilqr_solve_batch_device")
+        return ex, it
 
     def fd_batch(self, x, u, dt=0.0, want_minv=True):
         x, u = _c64(x), _c64(u)

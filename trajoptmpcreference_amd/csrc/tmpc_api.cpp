@@ -447,6 +447,111 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   return 0;
 }
 
+// ------------------------------------------------------------------ iLQR driver (oracle/ilqr.py)
+static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u, TraceDev* tr_out) {
+  int rc = check_ready(ctx, B, N);
+  if (rc) return rc;
+  const int nj = ctx->hmodel.n, nx = 2 * nj, K = N - 1;
+  const bool chain = ctx->hmodel.chain != 0;
+  const tmpc_options& o = ctx->opts;
+  const SolverOpts so = solver_opts(o);
+  const std::vector<double> al = alpha_list(o);
+  const int T = (int)al.size();
+  const int W = o.max_iter_SQP_DDP + 1;
+  Work w;
+  if ((rc = alloc_work(ctx, B, N, w, false))) return rc;
+  ProbState st;
+  if ((rc = alloc_state(ctx, B, st))) return rc;
+  TraceDev tr;
+  if ((rc = alloc_trace(ctx, B, W, tr))) return rc;
+  BUF(double, alphas, T);
+  BUF(double, il_K, (size_t)B * K * nj * nx);
+  BUF(double, il_d, (size_t)B * K * nj);
+  BUF(double, il_dV, (size_t)B * 2);
+  BUF(int, il_ok, B);
+  BUF(double, il_xt, (size_t)B * T * nx * N);
+  BUF(double, il_ut, (size_t)B * T * nj * K);
+  BUF(double, il_J, (size_t)B * T);
+  BUF(int, active_count, 1);
+  BUF(int, outer_active, B);
+  BUF(int, outer_iter, B);
+  BUF(int, exit_soft, B);
+  const bool soft = ctx->hlim.any != 0;
+  double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
+  if (soft) {
+    if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
+    if (ctx->soft_B != B || ctx->soft_N != N) {
+      launch_soft_init(ctx->stream, ctx->dlim, (size_t)B * N * 6 * nj, 6 * nj, smu, slam, sphi);
+      HIP_OK(hipGetLastError());
+      ctx->soft_B = B;
+      ctx->soft_N = N;
+    }
+  }
+  HIP_OK(hipMemcpyAsync(alphas, al.data(), al.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  // iLQR iterates are rollouts: start from the rollout of u from x[:, 0]
+  LAUNCH_OK(launch_rollout(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, d_u));
+  HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
+                          hipMemcpyDeviceToDevice, ctx->stream));
+  launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
+  for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
+    launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
+    HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
+    LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
+                                  1, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
+    launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st,
+                       tr, active_count);
+    for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
+      {
+        Timed t(ctx, "qp_fd");
+        LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
+                               w.cvec));
+      }
+      {
+        Timed t(ctx, "qp_minv");
+        LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
+      }
+      {
+        Timed t(ctx, "qp_grad");
+        LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv,
+                                 w.A, w.Bm));
+      }
+      {
+        Timed t(ctx, "ilqr_backward");
+        LAUNCH_OK(launch_ilqr_backward(ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, d_x, d_u, st.rho, st.active,
+                                       w.A, w.Bm, smu, slam, il_K, il_d, il_dV, il_ok));
+      }
+      {
+        Timed t(ctx, "ilqr_forward");
+        LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T,
+                                      dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
+      }
+      HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
+      {
+        Timed t(ctx, "ilqr_decide");
+        launch_ilqr_decide(ctx->stream, B, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u,
+                           st, tr, active_count);
+        HIP_OK(hipGetLastError());
+      }
+      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+      HIP_OK(hipStreamSynchronize(ctx->stream));
+      if (*ctx->h_count == 0) break;
+    }
+    HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
+    launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
+                      o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
+                      active_count);
+    HIP_OK(hipGetLastError());
+    if (!soft) break;
+    HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    if (*ctx->h_count == 0) break;
+  }
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  resolve_timings(ctx);
+  if (tr_out) *tr_out = tr;
+  return 0;
+}
+
 // ======================================================================= C ABI
 extern "C" {
 
@@ -704,6 +809,58 @@ int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, dou
     CP(pcg_iters, pcg_iters, int)
 #undef CP
   }
+  return 0;
+}
+
+int tmpc_ilqr_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, double* x, double* u, int32_t* exit_code,
+                          int32_t* exit_soft, int32_t* outer_iter, int32_t* iters, tmpc_trace* trace) {
+  if (!ctx) return -1;
+  int rc = check_ready(ctx, B, N);
+  if (rc) return rc;
+  if (!x || !u) return fail(ctx, "null x/u");
+  hipSetDevice(ctx->device);
+  const int nx = ctx->hcost.nx, nu = ctx->hcost.nu;
+  const size_t xn = (size_t)B * nx * N, un = (size_t)B * nu * (N - 1);
+  BUF(double, io_x, xn);
+  BUF(double, io_u, un);
+  HIP_OK(hipMemcpyAsync(io_x, x, xn * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(io_u, u, un * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  TraceDev tr;
+  if ((rc = ilqr_device(ctx, B, N, dt, io_x, io_u, &tr))) return rc;
+  HIP_OK(hipMemcpy(x, io_x, xn * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(u, io_u, un * sizeof(double), hipMemcpyDeviceToHost));
+  if (exit_code) HIP_OK(hipMemcpy(exit_code, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (iters) HIP_OK(hipMemcpy(iters, ctx->bufs["st_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (exit_soft) HIP_OK(hipMemcpy(exit_soft, ctx->bufs["exit_soft"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (outer_iter) HIP_OK(hipMemcpy(outer_iter, ctx->bufs["outer_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (trace) {
+    const size_t n = (size_t)B * (ctx->opts.max_iter_SQP_DDP + 1);
+#define CP(field, src, T) \
+  if (trace->field) HIP_OK(hipMemcpy(trace->field, tr.src, n * sizeof(T), hipMemcpyDeviceToHost));
+    CP(iteration, iteration, int)
+    CP(line_search_iteration, ls_iter, int)
+    CP(alpha, alpha, double)
+    CP(rho, rho, double)
+    CP(J, J, double)
+    CP(c, c, double)
+    CP(merit, merit, double)
+    CP(D, D, double)
+    CP(reduction_ratio, ratio, double)
+    CP(succeeded_line_search, accepted, int)
+    CP(pcg_iters, pcg_iters, int)
+#undef CP
+  }
+  return 0;
+}
+
+int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u,
+                                 int32_t* exit_code, int32_t* iters) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  int rc = ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr);
+  if (rc) return rc;
+  if (exit_code) HIP_OK(hipMemcpy(exit_code, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (iters) HIP_OK(hipMemcpy(iters, ctx->bufs["st_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
   return 0;
 }
 

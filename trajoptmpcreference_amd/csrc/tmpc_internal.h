@@ -97,6 +97,17 @@ void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& s
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
                        const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
                        int* outer_iter, int* exit_soft, int* outer_count);
+int launch_ilqr_backward(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
+                         const double* u, const double* rho, const int* active, const double* A, const double* Bm,
+                         const double* mu, const double* lam, double* K, double* d, double* dV, int* ok);
+int launch_ilqr_forward(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
+                        const double* mu, const double* lam, int B, int N, int T, double dt, int init,
+                        const double* alphas, const double* x, const double* u, const double* K, const double* d,
+                        const int* active, const int* ok, double* xt, double* ut, double* Jt);
+void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,
+                        const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
+                        const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
+                        int* active_count);
 void launch_outer_init(hipStream_t s, int B, int* outer_active, int* outer_iter, int* exit_soft);
 void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, double* mu, double* lam,
                       double* phi);

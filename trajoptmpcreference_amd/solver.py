@@ -171,7 +171,9 @@ class TrajoptMPCReference:
         method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
         it = int(r["sqp_iter"][0])
         t = r["trace"]
-        rows = min(it + 1, t["alpha"].shape[1])
+        # one row per SQP iteration run plus the initial row; the iteration counter is not
+        # incremented by the max_iter exit (check_for_exit_or_error :475-479)
+        rows = min(it + 1 + (int(r["exit_sqp"][0]) == 3), t["alpha"].shape[1])
         # the trace is that of the last outer pass, whose index is outer_iter unless the outer
         # loop exited with code 1 or 3 (which increment the counter first, :490-499)
         ex_soft, outer = int(r["exit_soft"][0]), int(r["outer_iter"][0])
@@ -199,6 +201,58 @@ class TrajoptMPCReference:
         self.exit_sqp = int(r["exit_sqp"][0])
         self.exit_soft = int(r["exit_soft"][0])
         return (r["x"][0], r["u"][0], self.exit_sqp, self.exit_soft, int(r["outer_iter"][0]), it)
+
+    # ------------------------------------------------------------------ iLQR (MPCSolverMethods.iLQR)
+    def iLQR_batch(self, x, u, N: int, dt: float, options=None, soft_state=None):
+        """Batched iLQR (algorithm in oracle/ilqr.py -- the reference defines only
+        the MPCSolverMethods.iLQR enum value).  Same plugins, *_SQP_DDP options, rho schedule, exit
+        codes and soft-constraint outer loop as SQP_batch; x is replaced by the rollout of u from
+        x[:, :, 0]."""
+        options = {} if options is None else options
+        self.set_default_options(options)
+        ctx = self._context(options)
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        if x.ndim != 3 or u.ndim != 3 or x.shape[2] != N or u.shape[2] != N - 1 or x.shape[0] != u.shape[0]:
+            raise ValueError(f"expected x [B][nx][{N}] and u [B][nu][{N - 1}], got {x.shape} and {u.shape}")
+        B = x.shape[0]
+        soft = self.other_constraints.has_any()
+        if soft:
+            if soft_state is None:
+                soft_state = [np.broadcast_to(a, (B,) + a.shape) for a in self.other_constraints.pack_state(N)]
+            ctx.set_soft_state(B, N, *soft_state)
+        r = ctx.ilqr_solve_batch(x, u, N, dt)
+        if soft:
+            r["soft_state"] = ctx.get_soft_state(B, N)
+        return r
+
+    def iLQR(self, x, u, N: int, dt: float, options=None):
+        """One problem: returns (x, u, exit_code, exit_soft, outer_iter, iter) like SQP, trace in self.trace."""
+        r = self.iLQR_batch(np.asarray(x, dtype=np.float64)[None], np.asarray(u, dtype=np.float64)[None], N, dt,
+                            options)
+        it = int(r["iter"][0])
+        t = r["trace"]
+        ex_soft, outer = int(r["exit_soft"][0]), int(r["outer_iter"][0])
+        last_pass = outer if ex_soft == 2 else outer - 1
+        if "soft_state" in r:
+            self.other_constraints.unpack_state(*[a[0] for a in r["soft_state"]])
+        self.trace = []
+        for i in range(min(it + 1 + (int(r["exit_code"][0]) == 3), t["alpha"].shape[1])):
+            self.trace.append({
+                "outer_iteration": last_pass,
+                "iteration": int(t["iteration"][0, i]),
+                "line_search_iteration": int(t["line_search_iteration"][0, i]),
+                "alpha": float(t["alpha"][0, i]) if i else 1,
+                "rho": float(t["rho"][0, i]),
+                "J": float(t["J"][0, i]),
+                "dV1": None if i == 0 or np.isnan(t["D"][0, i]) else float(t["D"][0, i]),
+                "reduction_ratio": None if i == 0 or np.isnan(t["reduction_ratio"][0, i])
+                else float(t["reduction_ratio"][0, i]),
+                "succeeded_line_search": bool(t["succeeded_line_search"][0, i]),
+            })
+        self.exit_sqp = int(r["exit_code"][0])
+        self.exit_soft = ex_soft
+        return (r["x"][0], r["u"][0], self.exit_sqp, self.exit_soft, outer, it)
 
     def solveKKTSystem_Schur(self, x, u, xs, N, dt, rho=0.0, use_PCG=True, options=None):
         """One QP (formKKTSystemBlocks + solveKKTSystem_Schur, :361-455) -> dxul column.
