@@ -38,7 +38,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
     ap.add_argument("--N", type=int, default=64)
     ap.add_argument("--links", type=int, default=6)
-    ap.add_argument("--method", default="PCG-SS")
+    ap.add_argument("--method", default="PCG-SS", help="SQP linear-system method: PCG-SS / PCG-BJ / PCG-J / S")
+    ap.add_argument("--solver", default="sqp", choices=["sqp", "ilqr"],
+                    help="sqp: the BASELINE metric; ilqr: BASELINE config 3 (same workload, iLQR)")
     ap.add_argument("--seed0", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
     ap.add_argument("--cpu-procs", type=int, default=16)
@@ -192,6 +194,46 @@ def kkt_residual_check(ctx, model, n):
             "pcg_iters_build": int(r["pcg_iters"][0]), "pcg_iters_ref": int(d["iters_SS"])}
 
 
+def ilqr_backward_flops_per_knot(nx, nu):
+    # V_xx [A B], A^T P, B^T [P R], Q_ux^T [K d] products + the per-lane Cholesky solves
+    return 2 * (2 * nx ** 3 + 2 * nx * nx * nu + nu * nu * nx + nx * nx * nu) + 2 * (nx + 1) * nu * nu
+
+
+def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant, counters, exit_codes, iters):
+    """Bench line for the non-headline paths (iLQR = BASELINE config 3, SQP with method S)."""
+    if comm.world > 1 and int(os.environ.get("RANK", "0")) != 0:
+        comm.close()
+        return
+    nx, nu = 2 * n, n
+    value = B * a.steps * world / elapsed
+    roofline = None
+    if a.solver == "ilqr":
+        bw = kernels.get("ilqr_backward")
+        if bw:
+            # algorithmic flops per backward launch: problem-iterations in the launch x (N-1) knots
+            per_launch = int(counters[0]) / max(1, bw["launches"])
+            flops = per_launch * (N - 1) * ilqr_backward_flops_per_knot(nx, nu)
+            ach = flops / (bw["avg_ms"] / 1e3) / 1e12
+            roofline = {"kernel": "k_ilqr_backward", "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
+                        "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
+                        "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
+    out = {
+        "metric": f"MPC solves/sec (arm{n}.urdf, N={N}, {'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method})",
+        "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": 1000.0 * elapsed / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
+        "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} {a.solver.upper()} "
+                               f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU",
+                   "global_batch": B * world, "N": N, "parallelism": f"shard{world}"},
+        "roofline": roofline, "cpu_baseline": None, "kernels": kernels, "dominant_kernel": dominant,
+        "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(exit_codes, return_counts=True))},
+        "iters_mean": float(np.mean(iters)), "iters_max": int(np.max(iters)),
+    }
+    print(json.dumps(out))
+    comm.close()
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -220,10 +262,15 @@ def main():
     ctx.h2d(d_u0, u0)
     ctx.rollout_device(B, N, dt, d_x0, d_u0)
 
+    def solve(want_status=False):
+        if a.solver == "ilqr":
+            return ctx.ilqr_solve_batch_device(B, N, dt, d_x, d_u, want_status=want_status)
+        return ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=want_status)
+
     def step():
         ctx.d2d(d_x, d_x0, xb)
         ctx.d2d(d_u, d_u0, ub)
-        ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method)
+        solve()
 
     for _ in range(a.warmup):
         step()
@@ -244,9 +291,11 @@ def main():
     ctx.set_options(profile=0)
 
     kernels = {}
-    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "ls_terms", "ls_decide"]:
+    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "schur", "btsolve", "dxu", "ls_terms", "ls_decide",
+                 "ilqr_backward", "ilqr_forward", "ilqr_decide"]:
         cnt, ms = ctx.kernel_stats(name)
-        kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt if cnt else 0.0}
+        if cnt:
+            kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
     dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
 
     total_solves = B * a.steps * world
@@ -256,12 +305,14 @@ def main():
     # ---- status of one solve (exit codes / iteration counts) for the record
     ctx.d2d(d_x, d_x0, xb)
     ctx.d2d(d_u, d_u0, ub)
-    exit_codes, iters = ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=True)
+    exit_codes, iters = solve(want_status=True)
 
     if rank != 0:
         comm.close()
         return
 
+    if a.solver == "ilqr" or a.method == "S":
+        return report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant, counters, exit_codes, iters)
     qp = kernels["qp"]
     n_pcg_iters = int(counters[1])
     n_qps = int(counters[0])

@@ -367,7 +367,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   TraceDev tr;
   if ((rc = alloc_trace(ctx, B, W, tr))) return rc;
   BUF(double, alphas, T + 1);
-  BUF(double, terms, (size_t)B * T * N * 3);
+  BUF(double, terms, (size_t)B * T * N * 4);   // [B][T][N][cost, violation, D, soft value]
   BUF(int, active_count, 1);
   BUF(unsigned long long, counters, 4);
   BUF(int, outer_active, B);
@@ -476,6 +476,8 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   BUF(int, outer_active, B);
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
+  BUF(unsigned long long, counters, 4);
+  HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
   const bool soft = ctx->hlim.any != 0;
   double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
   if (soft) {
@@ -499,7 +501,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
                                   1, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
     launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st,
-                       tr, active_count);
+                       tr, active_count, nullptr);
     for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
       {
         Timed t(ctx, "qp_fd");
@@ -529,7 +531,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
       {
         Timed t(ctx, "ilqr_decide");
         launch_ilqr_decide(ctx->stream, B, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u,
-                           st, tr, active_count);
+                           st, tr, active_count, counters);
         HIP_OK(hipGetLastError());
       }
       HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -546,7 +548,11 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     HIP_OK(hipStreamSynchronize(ctx->stream));
     if (*ctx->h_count == 0) break;
   }
+  unsigned long long hc[4] = {0, 0, 0, 0};
+  HIP_OK(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
+  for (int i = 0; i < 3; ++i) ctx->last_counters[i] = (int64_t)hc[i];
+  ctx->last_counters[3] = (int64_t)T;
   resolve_timings(ctx);
   if (tr_out) *tr_out = tr;
   return 0;

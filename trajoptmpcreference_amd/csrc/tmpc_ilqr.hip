@@ -381,7 +381,8 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
                                                     const int* __restrict__ okb, const double* __restrict__ xt,
                                                     const double* __restrict__ ut, double* __restrict__ x,
                                                     double* __restrict__ u, ProbState st, TraceDev tr,
-                                                    int* __restrict__ active_count) {
+                                                    int* __restrict__ active_count,
+                                                    unsigned long long* __restrict__ counters) {
   const int b = blockIdx.x;
   if (!st.active[b]) return;
   __shared__ int s_choice;
@@ -423,6 +424,11 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
       const bool error = choice < 0;
       const int it = st.iter[b];
       const size_t e = (size_t)b * W + it + 1;
+      if (counters) {
+        // [0] problem-iterations, [2] iterations with a fresh dynamics gradient
+        atomicAdd(&counters[0], 1ull);
+        atomicAdd(&counters[2], (unsigned long long)st.need_grad[b]);
+      }
       if (!error) {
         st.J[b] = Jn;
         st.merit[b] = Jn;
@@ -520,9 +526,9 @@ int launch_ilqr_forward(hipStream_t s, int nj, bool chain, const ModelDev* M, co
 void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
-                        int* active_count) {
+                        int* active_count, unsigned long long* counters) {
   hipLaunchKernelGGL(k_ilqr_decide, dim3(B), dim3(64), 0, s, B, N, NX, NU, T, init, alphas, o, Jt, dV, ok, xt, ut, x,
-                     u, st, tr, active_count);
+                     u, st, tr, active_count, counters);
 }
 
 }  // namespace tmpc

@@ -107,7 +107,7 @@ int launch_ilqr_forward(hipStream_t s, int nj, bool chain, const ModelDev* M, co
 void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
-                        int* active_count);
+                        int* active_count, unsigned long long* counters);
 void launch_outer_init(hipStream_t s, int B, int* outer_active, int* outer_iter, int* exit_soft);
 void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, double* mu, double* lam,
                       double* phi);
