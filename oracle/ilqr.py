@@ -72,8 +72,10 @@ def derivatives(cost, x, u, N, soft=None):
     return lx, lu, lxx, luu
 
 
-def backward(A, B, lx, lu, lxx, luu, rho):
-    """Riccati sweep; returns (K, d, dV1, dV2, ok)."""
+def backward(A, B, lx, lu, lxx, luu, rho, solve="cholesky"):
+    """Riccati sweep; returns (K, d, dV1, dV2, ok).  solve = "lu" solves for [K | d] with
+    np.linalg.solve instead of the Cholesky factor: the same algorithm with different
+    rounding, used by the tests to tell rounding-sensitive problems from real mismatches."""
     N = len(lx)
     nu = lu[0].shape[0]
     Vx = lx[N - 1].copy()
@@ -93,7 +95,7 @@ def backward(A, B, lx, lu, lxx, luu, rho):
         except np.linalg.LinAlgError:
             return None, None, 0.0, 0.0, False
         rhs = np.hstack([Qux, Qu[:, None]])
-        sol = np.linalg.solve(L.T, np.linalg.solve(L, rhs))
+        sol = np.linalg.solve(L.T, np.linalg.solve(L, rhs)) if solve == "cholesky" else np.linalg.solve(Quu, rhs)
         K[k] = -sol[:, :-1]
         d[k] = -sol[:, -1]
         dV1 += d[k] @ Qu
@@ -115,7 +117,7 @@ def forward(model, x, u, K, d, alpha, dt):
     return xn, un
 
 
-def ilqr(model, cost, x, u, N, dt, options=None, soft=None):
+def ilqr(model, cost, x, u, N, dt, options=None, soft=None, solve="cholesky"):
     """Returns dict(x, u, exit_code, exit_soft, outer_iter, iter, trace)."""
     o = default_options(options)
     x = rollout(model, np.array(x, dtype=float)[:, 0], np.array(u, dtype=float), dt)
@@ -133,7 +135,7 @@ def ilqr(model, cost, x, u, N, dt, options=None, soft=None):
         while True:
             A, B = rbd.euler_gradient(model, x[:, :N - 1].T, u.T, dt)
             lx, lu, lxx, luu = derivatives(cost, x, u, N, soft)
-            K, d, dV1, dV2, ok = backward(A, B, lx, lu, lxx, luu, rho)
+            K, d, dV1, dV2, ok = backward(A, B, lx, lu, lxx, luu, rho, solve)
             error = not ok
             delta_J = 0.0
             if ok:

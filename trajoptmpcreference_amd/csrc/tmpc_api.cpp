@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -52,6 +53,7 @@ struct tmpc_ctx {
   CostDev* dcost = nullptr;
   ConstrDev* dlim = nullptr;
   int soft_B = -1, soft_N = -1;   // shape of the valid soft-constraint state (-1: none)
+  int model_id = 0;               // compiled model (tmpc_models.h) equal to the set model; 0 = runtime model
   tmpc_options opts{};
   std::map<std::string, DevBuf> bufs;
   std::map<std::string, Stat> stats;
@@ -221,16 +223,16 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   const double* G = soft ? w.Gk : w.G;
   {
     Timed t(ctx, "qp_fd");
-    LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
+    LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
                            w.cvec));
   }
   {
     Timed t(ctx, "qp_minv");
-    LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
+    LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
   }
   {
     Timed t(ctx, "qp_grad");
-    LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv, w.A,
+    LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv, w.A,
                              w.Bm));
   }
   if (soft) {
@@ -403,7 +405,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
   launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
   // initial J, c, merit (:541-548)
-  LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
+  LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
                             alphas + T, d_x, d_u, w.xs, nullptr, nullptr, st.active, terms));
   HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
   launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
@@ -412,7 +414,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     if ((rc = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false))) return rc;
     {
       Timed t(ctx, "ls_terms");
-      LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
+      LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
                                 alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
     }
     HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
@@ -491,30 +493,30 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   }
   HIP_OK(hipMemcpyAsync(alphas, al.data(), al.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   // iLQR iterates are rollouts: start from the rollout of u from x[:, 0]
-  LAUNCH_OK(launch_rollout(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, d_u));
+  LAUNCH_OK(launch_rollout(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
   for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
     launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
     HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-    LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
+    LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
                                   1, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
     launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st,
                        tr, active_count, nullptr);
     for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
       {
         Timed t(ctx, "qp_fd");
-        LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
+        LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
                                w.cvec));
       }
       {
         Timed t(ctx, "qp_minv");
-        LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
+        LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
       }
       {
         Timed t(ctx, "qp_grad");
-        LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv,
+        LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv,
                                  w.A, w.Bm));
       }
       {
@@ -524,7 +526,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
       }
       {
         Timed t(ctx, "ilqr_forward");
-        LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T,
+        LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T,
                                       dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
       }
       HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
@@ -643,6 +645,10 @@ int tmpc_set_model(tmpc_ctx* ctx, int n, const int32_t* parent, const int32_t* j
     if (parent[j] >= 0) m.subtree[parent[j]] |= m.subtree[j];
   }
   m.chain = chain ? 1 : 0;
+  // per-robot compiled kernels when the model is one of the bundled ones (tools/gen_models.py);
+  // TMPC_GENERIC_MODEL=1 forces the runtime-coefficient kernels
+  const char* gen = getenv("TMPC_GENERIC_MODEL");
+  ctx->model_id = (gen && gen[0] == '1') ? 0 : match_static_model(m);
   hipSetDevice(ctx->device);
   HIP_OK(hipMemcpyAsync(ctx->dmodel, &m, sizeof(m), hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -874,7 +880,7 @@ int tmpc_rollout_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model");
   hipSetDevice(ctx->device);
-  LAUNCH_OK(launch_rollout(ctx->stream, ctx->hmodel.n, ctx->hmodel.chain != 0, ctx->dmodel, B, N, dt, d_x, d_u));
+  LAUNCH_OK(launch_rollout(ctx->stream, ctx->hmodel.n, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -893,8 +899,8 @@ int tmpc_fd_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const double
   BUF(double, u_minv, (size_t)K * nj * nj);
   HIP_OK(hipMemcpyAsync(u_x, x, sizeof(double) * K * nx, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(u_u, u, sizeof(double) * K * nj, hipMemcpyHostToDevice, ctx->stream));
-  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->dmodel, K, dt, u_x, u_u, u_xn, u_qdd));
-  if (Minv) LAUNCH_OK(launch_unit_minv(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->dmodel, K, u_x, u_minv));
+  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, K, dt, u_x, u_u, u_xn, u_qdd));
+  if (Minv) LAUNCH_OK(launch_unit_minv(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, K, u_x, u_minv));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (xnext) HIP_OK(hipMemcpy(xnext, u_xn, sizeof(double) * K * nx, hipMemcpyDeviceToHost));
   if (qdd) HIP_OK(hipMemcpy(qdd, u_qdd, sizeof(double) * K * nj, hipMemcpyDeviceToHost));
@@ -919,9 +925,9 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
   BUF(double, u_dqdd, (size_t)K * nj * 3 * nj);
   HIP_OK(hipMemcpyAsync(u_x, x, sizeof(double) * K * nx, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(u_u, u, sizeof(double) * K * nj, hipMemcpyHostToDevice, ctx->stream));
-  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, chain, ctx->dmodel, K, 0.0, u_x, u_u, nullptr, u_qdd));
-  LAUNCH_OK(launch_unit_minv(ctx->stream, nj, chain, ctx->dmodel, K, u_x, u_minv));
-  LAUNCH_OK(launch_unit_grad(ctx->stream, nj, chain, ctx->dmodel, K, dt, u_x, u_qdd, u_minv, u_A, u_B, u_dqdd));
+  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, 0.0, u_x, u_u, nullptr, u_qdd));
+  LAUNCH_OK(launch_unit_minv(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, u_x, u_minv));
+  LAUNCH_OK(launch_unit_grad(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, dt, u_x, u_qdd, u_minv, u_A, u_B, u_dqdd));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (A) HIP_OK(hipMemcpy(A, u_A, sizeof(double) * K * nx * nx, hipMemcpyDeviceToHost));
   if (Bo) HIP_OK(hipMemcpy(Bo, u_B, sizeof(double) * K * nx * nj, hipMemcpyDeviceToHost));

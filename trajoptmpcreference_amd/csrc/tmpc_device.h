@@ -107,18 +107,62 @@ __device__ __forceinline__ double soft_knot(const ConstrDev* __restrict__ Cs, co
   return value;
 }
 
-// ----------------------------------------------------------------- helpers
-template <bool CHAIN>
-__device__ __forceinline__ int parent_of(const ModelDev* __restrict__ M, int j) {
+// The per-lane dynamics kernels read the model's coefficients (X0 / Xa / Xb /
+// I: ~9 KB) with wave-uniform addresses.  From global memory they become
+// scalar loads that the fully unrolled recursions hoist far ahead of use, and
+// the SGPR file overflows into v_writelane / v_readlane spill traffic (15.6k
+// v_readlane per k_qp_grad lane vs 5.5k fp64 FMAs).  Staging the model in LDS
+// removes the spills but exposes an LDS round trip per coefficient: measured
+// on MI355X (arm6, B = 4096) it is 3.5x / 10x slower for k_qp_grad /
+// k_ls_terms (1 wave per SIMD, nothing hides the latency) and 1.2x faster for
+// k_ilqr_forward, whose knot loop is not unrolled; only the latter uses it.
+__device__ __forceinline__ const ModelDev* stage_model(const ModelDev* __restrict__ Mg, ModelDev* sM) {
+  constexpr int W = (int)(sizeof(ModelDev) / sizeof(unsigned long long));
+  static_assert(sizeof(ModelDev) % sizeof(unsigned long long) == 0, "ModelDev must be 8-byte sized");
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(Mg);
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(sM);
+  for (int i = threadIdx.x; i < W; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  return sM;
+}
+
+// ----------------------------------------------------------------- model access
+// The dynamics routines take the model as `const MT& M` and read it as
+// `M->field`:
+//   ModelRef  the runtime model (ModelDev in HBM, from tmpc_set_model): every
+//             coefficient is a wave-uniform load;
+//   Arm<N>    a compile-time model (tmpc_models.h, generated from the bundled
+//             URDFs the way GRiD generates per-robot code): the same fields as
+//             static constexpr arrays, so coefficients fold to literals and the
+//             structural zeros of X(q), I and S drop out at compile time.
+// The compile-time path performs the same floating-point operations on the
+// nonzero terms (a skipped term is acc + x * 0 = acc), so both paths agree for
+// finite inputs.
+struct ModelRef {
+  static constexpr bool STATIC = false;
+  const ModelDev* p;
+  __device__ __forceinline__ const ModelDev* operator->() const { return p; }
+  static ModelRef make(const ModelDev* q) { return ModelRef{q}; }
+};
+
+// true unless `a` is a structural zero of a compile-time model
+template <class MT>
+__device__ __forceinline__ constexpr bool nz(double a) {
+  return !MT::STATIC || a != 0.0;
+}
+
+template <bool CHAIN, class MT>
+__device__ __forceinline__ int parent_of(const MT& M, int j) {
   return CHAIN ? j - 1 : M->parent[j];
 }
 
-template <bool CHAIN>
-__device__ __forceinline__ bool in_subtree(const ModelDev* __restrict__ M, int j, int s) {
+template <bool CHAIN, class MT>
+__device__ __forceinline__ bool in_subtree(const MT& M, int j, int s) {
   return CHAIN ? (s >= j) : ((M->subtree[j] >> s) & 1u);
 }
 
-__device__ __forceinline__ void joint_cs(const ModelDev* __restrict__ M, int j, double q, double& c, double& s) {
+template <class MT>
+__device__ __forceinline__ void joint_cs(const MT& M, int j, double q, double& c, double& s) {
   if (M->jtype[j] == 0) {
     sincos(q, &s, &c);
   } else {
@@ -131,63 +175,113 @@ __device__ __forceinline__ void joint_cs(const ModelDev* __restrict__ M, int j, 
 // (which would keep 36 doubles per joint live for the whole kernel).
 __device__ __forceinline__ void opaque(double& c, double& s) { asm volatile("" : "+v"(c), "+v"(s)); }
 
+// entry e of X_j(q) = X0 + cos(q) Xa + sin(q) Xb; false for a structural zero
+template <class MT>
+__device__ __forceinline__ bool xent(const MT& M, int j, int e, double c, double s, double& x) {
+  const double a0 = M->X0[j][e], a1 = M->Xa[j][e], a2 = M->Xb[j][e];
+  if (!MT::STATIC) {
+    x = a0 + c * a1 + s * a2;
+    return true;
+  }
+  if (a0 == 0.0 && a1 == 0.0 && a2 == 0.0) return false;
+  double t = a0;
+  if (a1 != 0.0) t = a0 != 0.0 ? __fma_rn(c, a1, a0) : c * a1;
+  if (a2 != 0.0) t = (a0 != 0.0 || a1 != 0.0) ? __fma_rn(s, a2, t) : s * a2;
+  x = t;
+  return true;
+}
+
 // y = X v, rows formed on the fly
-__device__ __forceinline__ void mvX(const ModelDev* __restrict__ M, int j, double c, double s, const double v[6],
-                                    double y[6]) {
+template <class MT>
+__device__ __forceinline__ void mvX(const MT& M, int j, double c, double s, const double v[6], double y[6]) {
   opaque(c, s);
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     double acc = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const double x = M->X0[j][r * 6 + k] + c * M->Xa[j][r * 6 + k] + s * M->Xb[j][r * 6 + k];
-      acc += x * v[k];
+      double x;
+      if (xent(M, j, r * 6 + k, c, s, x)) acc += x * v[k];
     }
     y[r] = acc;
   }
 }
 
 // y += X^T f, columns formed on the fly
-__device__ __forceinline__ void add_mtvX(const ModelDev* __restrict__ M, int j, double c, double s,
-                                         const double f[6], double y[6]) {
+template <class MT>
+__device__ __forceinline__ void add_mtvX(const MT& M, int j, double c, double s, const double f[6], double y[6]) {
   opaque(c, s);
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     double acc = 0.0;
+    bool any = false;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      const double x = M->X0[j][r * 6 + k] + c * M->Xa[j][r * 6 + k] + s * M->Xb[j][r * 6 + k];
-      acc += x * f[r];
+      double x;
+      if (xent(M, j, r * 6 + k, c, s, x)) {
+        acc += x * f[r];
+        any = true;
+      }
     }
-    y[k] += acc;
+    if (any) y[k] += acc;
   }
 }
 
-// o = I v, I a uniform model matrix
-__device__ __forceinline__ void mvI(const double* __restrict__ I, const double v[6], double o[6]) {
+// o = I_j v
+template <class MT>
+__device__ __forceinline__ void mvI(const MT& M, int j, const double v[6], double o[6]) {
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     double acc = 0.0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) acc += I[r * 6 + k] * v[k];
+    for (int k = 0; k < 6; ++k)
+      if (nz<MT>(M->I[j][r * 6 + k])) acc += M->I[j][r * 6 + k] * v[k];
     o[r] = acc;
   }
 }
 
-// crm(w) S for a 0/1 subspace vector S (mxS, RBDReference.py:57-62)
-__device__ __forceinline__ void crmS(const double w[6], const double* __restrict__ S, double o[6]) {
-  o[0] = -w[2] * S[1] + w[1] * S[2];
-  o[1] = w[2] * S[0] - w[0] * S[2];
-  o[2] = -w[1] * S[0] + w[0] * S[1];
-  o[3] = -w[5] * S[1] + w[4] * S[2] - w[2] * S[4] + w[1] * S[5];
-  o[4] = w[5] * S[0] - w[3] * S[2] + w[2] * S[3] - w[0] * S[5];
-  o[5] = -w[4] * S[0] + w[3] * S[1] - w[1] * S[3] + w[0] * S[4];
+// crm(w) S_j for a 0/1 subspace vector S (mxS, RBDReference.py:57-62)
+template <class MT>
+__device__ __forceinline__ void crmS(const double w[6], const MT& M, int j, double o[6]) {
+#define S_(i) M->S[j][i]
+  if (!MT::STATIC) {
+    o[0] = -w[2] * S_(1) + w[1] * S_(2);
+    o[1] = w[2] * S_(0) - w[0] * S_(2);
+    o[2] = -w[1] * S_(0) + w[0] * S_(1);
+    o[3] = -w[5] * S_(1) + w[4] * S_(2) - w[2] * S_(4) + w[1] * S_(5);
+    o[4] = w[5] * S_(0) - w[3] * S_(2) + w[2] * S_(3) - w[0] * S_(5);
+    o[5] = -w[4] * S_(0) + w[3] * S_(1) - w[1] * S_(3) + w[0] * S_(4);
+    return;
+  }
+  // S is a unit vector: each output has at most one term, and the products are exact
+#define T_(acc, sign, wi, si) \
+  if (S_(si) != 0.0) acc += (sign) * w[wi] * S_(si);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0;
+  T_(a0, -1.0, 2, 1) T_(a0, 1.0, 1, 2)
+  T_(a1, 1.0, 2, 0) T_(a1, -1.0, 0, 2)
+  T_(a2, -1.0, 1, 0) T_(a2, 1.0, 0, 1)
+  T_(a3, -1.0, 5, 1) T_(a3, 1.0, 4, 2) T_(a3, -1.0, 2, 4) T_(a3, 1.0, 1, 5)
+  T_(a4, 1.0, 5, 0) T_(a4, -1.0, 3, 2) T_(a4, 1.0, 2, 3) T_(a4, -1.0, 0, 5)
+  T_(a5, -1.0, 4, 0) T_(a5, 1.0, 3, 1) T_(a5, -1.0, 1, 3) T_(a5, 1.0, 0, 4)
+#undef T_
+#undef S_
+  o[0] = a0; o[1] = a1; o[2] = a2; o[3] = a3; o[4] = a4; o[5] = a5;
 }
 
-__device__ __forceinline__ double dotS(const double* __restrict__ S, const double v[6]) {
+// S_j . v
+template <class MT>
+__device__ __forceinline__ double dotS(const MT& M, int j, const double v[6]) {
   double acc = 0.0;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) acc += S[k] * v[k];
+  for (int k = 0; k < 6; ++k)
+    if (nz<MT>(M->S[j][k])) acc += M->S[j][k] * v[k];
+  return acc;
+}
+
+__device__ __forceinline__ double dot6(const double a[6], const double b[6]) {
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) acc += a[k] * b[k];
   return acc;
 }
 
@@ -206,56 +300,71 @@ __device__ __forceinline__ constexpr int sidx(int r, int c) {
   return r <= c ? r * 6 - (r * (r - 1)) / 2 + (c - r) : c * 6 - (c * (c - 1)) / 2 + (r - c);
 }
 
-// out = X^T A X for symmetric A (21 entries).  Column-at-a-time so that only
-// two 6-vectors of X and one of A X are live (X columns are recomputed).
-__device__ __forceinline__ void Xcol(const ModelDev* __restrict__ M, int j, double c, double s, int k, double x[6]) {
+// column k of X_j (structural-zero mask in nzm)
+template <class MT>
+__device__ __forceinline__ void Xcol(const MT& M, int j, double c, double s, int k, double x[6], bool nzm[6]) {
 #pragma unroll
-  for (int r = 0; r < 6; ++r) x[r] = M->X0[j][r * 6 + k] + c * M->Xa[j][r * 6 + k] + s * M->Xb[j][r * 6 + k];
+  for (int r = 0; r < 6; ++r) {
+    nzm[r] = xent(M, j, r * 6 + k, c, s, x[r]);
+    if (!nzm[r]) x[r] = 0.0;
+  }
 }
 
-__device__ __forceinline__ void XtAX(const ModelDev* __restrict__ M, int j, double c, double s, const double A[21],
-                                     double out[21]) {
+// out = X^T A X for symmetric A (21 entries).  Column-at-a-time so that only
+// two 6-vectors of X and one of A X are live (X columns are recomputed).
+template <class MT>
+__device__ __forceinline__ void XtAX(const MT& M, int j, double c, double s, const double A[21], double out[21]) {
   opaque(c, s);
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     double xk[6], z[6];
-    Xcol(M, j, c, s, k, xk);
+    bool nk[6];
+    Xcol(M, j, c, s, k, xk, nk);
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       double acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < 6; ++m) acc += A[sidx(r, m)] * xk[m];
+      for (int m = 0; m < 6; ++m)
+        if (nk[m]) acc += A[sidx(r, m)] * xk[m];
       z[r] = acc;
     }
 #pragma unroll
     for (int r = 0; r <= k; ++r) {
       double xr[6];
+      bool nr[6];
       if (r == k) {
 #pragma unroll
-        for (int m = 0; m < 6; ++m) xr[m] = xk[m];
+        for (int m = 0; m < 6; ++m) {
+          xr[m] = xk[m];
+          nr[m] = nk[m];
+        }
       } else {
-        Xcol(M, j, c, s, r, xr);
+        Xcol(M, j, c, s, r, xr, nr);
       }
       double acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < 6; ++m) acc += xr[m] * z[m];
+      for (int m = 0; m < 6; ++m)
+        if (nr[m]) acc += xr[m] * z[m];
       out[sidx(r, k)] = acc;
     }
   }
 }
 
 // y1 = X v1, y2 = X v2 sharing the formation of each X row
-__device__ __forceinline__ void mvX2(const ModelDev* __restrict__ M, int j, double c, double s, const double v1[6],
-                                     const double v2[6], double y1[6], double y2[6]) {
+template <class MT>
+__device__ __forceinline__ void mvX2(const MT& M, int j, double c, double s, const double v1[6], const double v2[6],
+                                     double y1[6], double y2[6]) {
   opaque(c, s);
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     double a1 = 0.0, a2 = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const double x = M->X0[j][r * 6 + k] + c * M->Xa[j][r * 6 + k] + s * M->Xb[j][r * 6 + k];
-      a1 += x * v1[k];
-      a2 += x * v2[k];
+      double x;
+      if (xent(M, j, r * 6 + k, c, s, x)) {
+        a1 += x * v1[k];
+        a2 += x * v2[k];
+      }
     }
     y1[r] = a1;
     y2[r] = a2;
@@ -268,9 +377,9 @@ __device__ __forceinline__ void mvX2(const ModelDev* __restrict__ M, int j, doub
 // M^-1 tau (qd = 0, no gravity).  Velocities are recomputed in pass 3
 // instead of being kept from pass 1, so at most ~8 doubles per joint are
 // stored across passes.
-template <int NJ, bool CHAIN, bool UNIT = false>
-__device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const double cq[NJ], const double sq[NJ],
-                                       const double qd[NJ], const double tau[NJ], double qdd[NJ]) {
+template <int NJ, bool CHAIN, bool UNIT = false, class MT>
+__device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const double sq[NJ], const double qd[NJ],
+                                       const double tau[NJ], double qdd[NJ]) {
   double v[NJ][6];
   // pass 1: velocities
   if (!UNIT) {
@@ -284,7 +393,8 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
         mvX(M, j, cq[j], sq[j], v[p], v[j]);
       }
 #pragma unroll
-      for (int i = 0; i < 6; ++i) v[j][i] += M->S[j][i] * qd[j];
+      for (int i = 0; i < 6; ++i)
+        if (nz<MT>(M->S[j][i])) v[j][i] += M->S[j][i] * qd[j];
     }
   }
   // pass 2: articulated inertias / bias forces, leaf to root
@@ -303,16 +413,17 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
-      for (int k = r; k < 6; ++k) IA[sidx(r, k)] = M->I[j][r * 6 + k] + chIA[j][sidx(r, k)];
+      for (int k = r; k < 6; ++k)
+        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? M->I[j][r * 6 + k] + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
     double pA[6], cj[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) pA[i] = chpA[j][i];
     if (!UNIT) {
       double Iv[6];
-      mvI(M->I[j], v[j], Iv);
+      mvI(M, j, v[j], Iv);
       add_fxv(v[j], Iv, pA);
       double cc[6];
-      crmS(v[j], M->S[j], cc);
+      crmS(v[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) cj[i] = qd[j] * cc[i];
     } else {
@@ -323,11 +434,12 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
     for (int r = 0; r < 6; ++r) {
       double acc = 0.0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) acc += IA[sidx(r, k)] * M->S[j][k];
+      for (int k = 0; k < 6; ++k)
+        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * M->S[j][k];
       U[j][r] = acc;
     }
-    Dd[j] = dotS(M->S[j], U[j]);
-    uu[j] = tau[j] - dotS(M->S[j], pA);
+    Dd[j] = dotS(M, j, U[j]);
+    uu[j] = tau[j] - dotS(M, j, pA);
     const int p = parent_of<CHAIN>(M, j);
     if (p >= 0) {
       const double dinv = 1.0 / Dd[j];
@@ -373,15 +485,17 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
         mvX2(M, j, cq[j], sq[j], v3[p], a[p], v3[j], a[j]);
       }
 #pragma unroll
-      for (int i = 0; i < 6; ++i) v3[j][i] += M->S[j][i] * qd[j];
+      for (int i = 0; i < 6; ++i)
+        if (nz<MT>(M->S[j][i])) v3[j][i] += M->S[j][i] * qd[j];
       double cc[6];
-      crmS(v3[j], M->S[j], cc);
+      crmS(v3[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) a[j][i] += qd[j] * cc[i];
     }
-    qdd[j] = (uu[j] - dotS(U[j], a[j])) / Dd[j];
+    qdd[j] = (uu[j] - dot6(U[j], a[j])) / Dd[j];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) a[j][i] += M->S[j][i] * qdd[j];
+    for (int i = 0; i < 6; ++i)
+      if (nz<MT>(M->S[j][i])) a[j][i] += M->S[j][i] * qdd[j];
   }
 }
 
@@ -390,9 +504,9 @@ __device__ __forceinline__ void fd_aba(const ModelDev* __restrict__ M, const dou
 // before symmetrising, :908-930) following minv_bpass / minv_fpass
 // restricted to column `col` (F[:, :, col] is per column; IA, U, Dinv are
 // recomputed per lane).
-template <int NJ, bool CHAIN>
-__device__ __forceinline__ void minv_column(const ModelDev* __restrict__ M, const double cq[NJ], const double sq[NJ],
-                                            int col, double mcol[NJ]) {
+template <int NJ, bool CHAIN, class MT>
+__device__ __forceinline__ void minv_column(const MT& M, const double cq[NJ], const double sq[NJ], int col,
+                                            double mcol[NJ]) {
   double chIA[NJ][21];
   double Fc[NJ][6];      // F[j][:, col]
   double U[NJ][6], Dinv[NJ];
@@ -411,18 +525,20 @@ __device__ __forceinline__ void minv_column(const ModelDev* __restrict__ M, cons
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
-      for (int k = r; k < 6; ++k) IA[sidx(r, k)] = M->I[j][r * 6 + k] + chIA[j][sidx(r, k)];
+      for (int k = r; k < 6; ++k)
+        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? M->I[j][r * 6 + k] + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       double acc = 0.0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) acc += IA[sidx(r, k)] * M->S[j][k];
+      for (int k = 0; k < 6; ++k)
+        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * M->S[j][k];
       U[j][r] = acc;
     }
-    Dinv[j] = 1.0 / dotS(M->S[j], U[j]);
+    Dinv[j] = 1.0 / dotS(M, j, U[j]);
     const bool mine = in_subtree<CHAIN>(M, j, col);
     if (j == col) mcol[j] = Dinv[j];
-    if (mine) mcol[j] -= Dinv[j] * dotS(M->S[j], Fc[j]);
+    if (mine) mcol[j] -= Dinv[j] * dotS(M, j, Fc[j]);
     const int p = parent_of<CHAIN>(M, j);
     if (p >= 0) {
       if (mine) {
@@ -451,12 +567,12 @@ __device__ __forceinline__ void minv_column(const ModelDev* __restrict__ M, cons
       double XF[6];
       mvX(M, j, cq[j], sq[j], Ff[p], XF);   // X F[p][:, col]
       // (U^T X) F[p][:, col] == U^T (X F[p][:, col])
-      mcol[j] -= Dinv[j] * dotS(U[j], XF);
+      mcol[j] -= Dinv[j] * dot6(U[j], XF);
 #pragma unroll
-      for (int r = 0; r < 6; ++r) Ff[j][r] = M->S[j][r] * mcol[j] + XF[r];
+      for (int r = 0; r < 6; ++r) Ff[j][r] = nz<MT>(M->S[j][r]) ? M->S[j][r] * mcol[j] + XF[r] : XF[r];
     } else {
 #pragma unroll
-      for (int r = 0; r < 6; ++r) Ff[j][r] = M->S[j][r] * mcol[j];
+      for (int r = 0; r < 6; ++r) Ff[j][r] = nz<MT>(M->S[j][r]) ? M->S[j][r] * mcol[j] : 0.0;
     }
   }
 }
@@ -465,17 +581,16 @@ __device__ __forceinline__ void minv_column(const ModelDev* __restrict__ M, cons
 // d c / d q_col (colqd = false) or d c / d qd_col (colqd = true) at (q, qd, qdd):
 // rnea_grad forward passes (:561-690) and backward passes (:692-771) for ONE
 // column, fused with the RNEA passes that produce v, a and the accumulated f.
-template <int NJ, bool CHAIN>
-__device__ __forceinline__ void rnea_grad_column(const ModelDev* __restrict__ M, const double cq[NJ],
-                                                 const double sq[NJ], const double qd[NJ], const double qdd[NJ],
-                                                 int col, bool colqd, double dc[NJ]) {
+template <int NJ, bool CHAIN, class MT>
+__device__ __forceinline__ void rnea_grad_column(const MT& M, const double cq[NJ], const double sq[NJ],
+                                                 const double qd[NJ], const double qdd[NJ], int col, bool colqd,
+                                                 double dc[NJ]) {
   double v[NJ][6], a[NJ][6], f[NJ][6];
   double dv[NJ][6], da[NJ][6], df[NJ][6];
   const double g[6] = {0.0, 0.0, 0.0, 0.0, 0.0, -M->gravity};
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int p = parent_of<CHAIN>(M, j);
-    const double* S = M->S[j];
     // ---- RNEA forward (with qdd)
     double Xvp[6], Xap[6];
     if (p < 0) {
@@ -487,16 +602,20 @@ __device__ __forceinline__ void rnea_grad_column(const ModelDev* __restrict__ M,
       mvX(M, j, cq[j], sq[j], a[p], Xap);
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) v[j][i] = Xvp[i] + S[i] * qd[j];
+    for (int i = 0; i < 6; ++i) v[j][i] = nz<MT>(M->S[j][i]) ? Xvp[i] + M->S[j][i] * qd[j] : Xvp[i];
     {
       double cc[6];
-      crmS(v[j], S, cc);
+      crmS(v[j], M, j, cc);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) a[j][i] = Xap[i] + qd[j] * cc[i] + S[i] * qdd[j];
+      for (int i = 0; i < 6; ++i) {
+        double t = Xap[i] + qd[j] * cc[i];
+        if (nz<MT>(M->S[j][i])) t += M->S[j][i] * qdd[j];
+        a[j][i] = t;
+      }
     }
     double Iv[6];
-    mvI(M->I[j], a[j], f[j]);
-    mvI(M->I[j], v[j], Iv);
+    mvI(M, j, a[j], f[j]);
+    mvI(M, j, v[j], Iv);
     add_fxv(v[j], Iv, f[j]);
     // ---- derivative forward pass for this column
     if (p >= 0) {
@@ -510,45 +629,45 @@ __device__ __forceinline__ void rnea_grad_column(const ModelDev* __restrict__ M,
       if (!colqd) {
         if (p >= 0) {
           double cc[6];
-          crmS(Xvp, S, cc);
+          crmS(Xvp, M, j, cc);
 #pragma unroll
           for (int i = 0; i < 6; ++i) dv[j][i] += cc[i];
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) dv[j][i] += S[i];
+        for (int i = 0; i < 6; ++i)
+          if (nz<MT>(M->S[j][i])) dv[j][i] += M->S[j][i];
       }
     }
     {
       double cc[6];
-      crmS(dv[j], S, cc);
+      crmS(dv[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) da[j][i] += qd[j] * cc[i];
     }
     if (j == col) {
       double cc[6];
-      crmS(colqd ? v[j] : Xap, S, cc);  // mxS(S, v) or mxS(S, X a_parent) / mxS(S, X g)
+      crmS(colqd ? v[j] : Xap, M, j, cc);  // mxS(S, v) or mxS(S, X a_parent) / mxS(S, X g)
 #pragma unroll
       for (int i = 0; i < 6; ++i) da[j][i] += cc[i];
     }
-    mvI(M->I[j], da[j], df[j]);
+    mvI(M, j, da[j], df[j]);
     add_fxv(dv[j], Iv, df[j]);
     double Idv[6];
-    mvI(M->I[j], dv[j], Idv);
+    mvI(M, j, dv[j], Idv);
     add_fxv(v[j], Idv, df[j]);
   }
   // ---- fused backward passes
 #pragma unroll
   for (int j = NJ - 1; j >= 0; --j) {
-    const double* S = M->S[j];
-    dc[j] = dotS(S, df[j]);
+    dc[j] = dotS(M, j, df[j]);
     const int p = parent_of<CHAIN>(M, j);
     if (p >= 0) {
       add_mtvX(M, j, cq[j], sq[j], df[j], df[p]);
       if (!colqd && j == col) {
         // delta = X^T fxS(S, f) = -X^T (crm(f) S)
         double cc[6];
-        crmS(f[j], S, cc);
+        crmS(f[j], M, j, cc);
 #pragma unroll
         for (int i = 0; i < 6; ++i) cc[i] = -cc[i];
         add_mtvX(M, j, cq[j], sq[j], cc, df[p]);

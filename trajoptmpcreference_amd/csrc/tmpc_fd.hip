@@ -16,8 +16,8 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
 // evaluated at, TrajoptPlant.py:313) and the dynamics defect
 // c_{k+1} = x_{k+1} - f(x_k, u_k) (formKKTSystemBlocks :227-231); lane k = 0
 // also writes c_0 = x_0 - xs (:213-214).
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_qp_fd(const ModelDev* __restrict__ M, int B, int N, double dt,
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(256) k_qp_fd(MT M, int B, int N, double dt,
                                                const double* __restrict__ x, const double* __restrict__ u,
                                                const double* __restrict__ xs, const int* __restrict__ need,
                                                double* __restrict__ qdd_out, double* __restrict__ cvec) {
@@ -64,8 +64,8 @@ __global__ void __launch_bounds__(256) k_qp_fd(const ModelDev* __restrict__ M, i
 // |x_0 - xs| violation term.  SOFT: soft-limit value (slot 3, summed after
 // the cost terms as totalCost does, :303-307) and jacobian . dxu added to D
 // (:633-646).  terms: [B][T][N][4] = cost, violation, D, soft value.
-template <int NJ, bool CHAIN, bool SOFT>
-__global__ void __launch_bounds__(256) k_ls_terms(const ModelDev* __restrict__ M, const CostDev* __restrict__ C,
+template <int NJ, bool CHAIN, bool SOFT, class MT>
+__global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restrict__ C,
                                                   const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                   const double* __restrict__ lam,
                                                   int B, int N, int T, double dt, const double* __restrict__ alphas,
@@ -182,8 +182,8 @@ __global__ void __launch_bounds__(256) k_ls_terms(const ModelDev* __restrict__ M
 }
 
 // ======================================================================= kernel-level entry points
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_unit_fd(const ModelDev* __restrict__ M, int K, double dt,
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(256) k_unit_fd(MT M, int K, double dt,
                                                  const double* __restrict__ x, const double* __restrict__ u,
                                                  double* __restrict__ xnext, double* __restrict__ qdd_out) {
   constexpr int NX = 2 * NJ;
@@ -209,8 +209,8 @@ __global__ void __launch_bounds__(256) k_unit_fd(const ModelDev* __restrict__ M,
 }
 
 // sequential Euler rollout, one lane per problem (workload setup: §8d)
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(64) k_rollout(const ModelDev* __restrict__ M, int B, int N, double dt,
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(64) k_rollout(MT M, int B, int N, double dt,
                                                 double* __restrict__ x, const double* __restrict__ u) {
   constexpr int NX = 2 * NJ;
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -243,11 +243,11 @@ __global__ void __launch_bounds__(64) k_rollout(const ModelDev* __restrict__ M, 
 
 #define TMPC_GRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
 
-template <int NJ, bool CHAIN>
+template <int NJ, bool CHAIN, class MT>
 struct LaunchFD {
   static void qp_fd(hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const double* u,
                     const double* xs, const int* need, double* qdd, double* cvec) {
-    hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN>), TMPC_GRID(B * (N - 1), 256), 0, s, M, B, N, dt, x, u, xs, need, qdd,
+    hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), B, N, dt, x, u, xs, need, qdd,
                        cvec);
   }
   static void ls_terms(hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
@@ -255,50 +255,54 @@ struct LaunchFD {
                        const double* u, const double* xs, const double* dx, const double* du, const int* active,
                        double* terms) {
     if (mu)
-      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, true>), TMPC_GRID(B * T * N, 256), 0, s, M, C, Cs, mu, lam, B, N, T,
+      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, true, MT>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, lam, B, N, T,
                          dt, alphas, x, u, xs, dx, du, active, terms);
     else
-      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, false>), TMPC_GRID(B * T * N, 256), 0, s, M, C, Cs, mu, lam, B, N,
+      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, false, MT>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, lam, B, N,
                          T, dt, alphas, x, u, xs, dx, du, active, terms);
   }
   static void unit_fd(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
                       double* xnext, double* qdd) {
-    hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN>), TMPC_GRID(K, 256), 0, s, M, K, dt, x, u, xnext, qdd);
+    hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
   }
   static void rollout(hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u) {
-    hipLaunchKernelGGL((k_rollout<NJ, CHAIN>), TMPC_GRID(B, 64), 0, s, M, B, N, dt, x, u);
+    hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT>), TMPC_GRID(B, 64), 0, s, MT::make(M), B, N, dt, x, u);
   }
 };
 
 // dispatch tables over the joint count and the chain specialisation
-#define TMPC_DISPATCH_NJ(nj, chain, CALL)                                          \
-  switch (nj) {                                                                    \
-    case 1: if (chain) LaunchFD<1, true>::CALL; else LaunchFD<1, false>::CALL; break;  \
-    case 2: if (chain) LaunchFD<2, true>::CALL; else LaunchFD<2, false>::CALL; break;  \
-    case 3: if (chain) LaunchFD<3, true>::CALL; else LaunchFD<3, false>::CALL; break;  \
-    case 4: if (chain) LaunchFD<4, true>::CALL; else LaunchFD<4, false>::CALL; break;  \
-    case 5: if (chain) LaunchFD<5, true>::CALL; else LaunchFD<5, false>::CALL; break;  \
-    case 6: if (chain) LaunchFD<6, true>::CALL; else LaunchFD<6, false>::CALL; break;  \
-    case 7: if (chain) LaunchFD<7, true>::CALL; else LaunchFD<7, false>::CALL; break;  \
-    default: return -2;                                                            \
-  }                                                                                \
+#define TMPC_DISPATCH_NJ(nj, chain, CALL)                                                              \
+  switch (mid) {                                                                                       \
+    TMPC_STATIC_MODEL_CASES(LaunchFD, CALL)                                                            \
+    default: break;                                                                                    \
+  }                                                                                                    \
+  switch (nj) {                                                                                        \
+    case 1: if (chain) LaunchFD<1, true, ModelRef>::CALL; else LaunchFD<1, false, ModelRef>::CALL; break;  \
+    case 2: if (chain) LaunchFD<2, true, ModelRef>::CALL; else LaunchFD<2, false, ModelRef>::CALL; break;  \
+    case 3: if (chain) LaunchFD<3, true, ModelRef>::CALL; else LaunchFD<3, false, ModelRef>::CALL; break;  \
+    case 4: if (chain) LaunchFD<4, true, ModelRef>::CALL; else LaunchFD<4, false, ModelRef>::CALL; break;  \
+    case 5: if (chain) LaunchFD<5, true, ModelRef>::CALL; else LaunchFD<5, false, ModelRef>::CALL; break;  \
+    case 6: if (chain) LaunchFD<6, true, ModelRef>::CALL; else LaunchFD<6, false, ModelRef>::CALL; break;  \
+    case 7: if (chain) LaunchFD<7, true, ModelRef>::CALL; else LaunchFD<7, false, ModelRef>::CALL; break;  \
+    default: return -2;                                                                                \
+  }                                                                                                    \
   return 0;
 
-int launch_qp_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, const double* x,
+int launch_qp_fd(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
                  const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
   TMPC_DISPATCH_NJ(nj, chain, qp_fd(s, M, B, N, dt, x, u, xs, need, qdd, cvec))
 }
-int launch_ls_terms(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
+int launch_ls_terms(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
                     const double* mu, const double* lam, int B, int N, int T, double dt, const double* alphas,
                     const double* x, const double* u, const double* xs, const double* dx, const double* du,
                     const int* active, double* terms) {
   TMPC_DISPATCH_NJ(nj, chain, ls_terms(s, M, C, Cs, mu, lam, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
 }
-int launch_unit_fd(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
+int launch_unit_fd(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
                    const double* u, double* xnext, double* qdd) {
   TMPC_DISPATCH_NJ(nj, chain, unit_fd(s, M, K, dt, x, u, xnext, qdd))
 }
-int launch_rollout(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, double* x,
+int launch_rollout(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
                    const double* u) {
   TMPC_DISPATCH_NJ(nj, chain, rollout(s, M, B, N, dt, x, u))
 }

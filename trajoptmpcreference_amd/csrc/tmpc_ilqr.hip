@@ -262,8 +262,8 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
 // trajectories are kept ([B][T][nx][N], [B][T][nu][N-1]) so the decision kernel
 // copies the accepted one.  Cost sums in totalCost's order (:296-310): the
 // QuadraticCost terms, then the soft values.
-template <int NJ, bool CHAIN, bool SOFT>
-__global__ void __launch_bounds__(64) k_ilqr_forward(const ModelDev* __restrict__ M, const CostDev* __restrict__ C,
+template <int NJ, bool CHAIN, bool SOFT, class MT>
+__global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __restrict__ C,
                                                      const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                      const double* __restrict__ lam, int B, int N, int T, double dt,
                                                      int init, const double* __restrict__ alphas,
@@ -272,6 +272,10 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(const ModelDev* __restrict_
                                                      const int* __restrict__ active, const int* __restrict__ ok,
                                                      double* __restrict__ xt, double* __restrict__ ut,
                                                      double* __restrict__ Jt) {
+  // the runtime model is staged in LDS (tmpc_device.h, stage_model); compiled models need no data
+  __shared__ ModelDev sM;
+  MT M = Mg;
+  if constexpr (!MT::STATIC) M = ModelRef{stage_model(Mg.p, &sM)};
   constexpr int NX = 2 * NJ, NU = NJ;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * T) return;
@@ -475,7 +479,7 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
 // ======================================================================= launchers
 #define TMPC_GRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
 
-template <int NJ, bool CHAIN>
+template <int NJ, bool CHAIN, class MT>
 struct LaunchIlqr {
   static void backward(hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                        const double* u, const double* rho, const int* active, const double* A, const double* Bm,
@@ -488,34 +492,39 @@ struct LaunchIlqr {
                       const double* x, const double* u, const double* K, const double* d, const int* active,
                       const int* ok, double* xt, double* ut, double* Jt) {
     if (mu)
-      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, true>), TMPC_GRID(B * T, 64), 0, s, M, C, Cs, mu, lam, B, N, T,
+      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, true, MT>), TMPC_GRID(B * T, 64), 0, s, MT::make(M), C, Cs, mu, lam, B, N, T,
                          dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
     else
-      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, false>), TMPC_GRID(B * T, 64), 0, s, M, C, Cs, mu, lam, B, N, T,
+      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, false, MT>), TMPC_GRID(B * T, 64), 0, s, MT::make(M), C, Cs, mu, lam, B, N, T,
                          dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
   }
 };
 
-#define TMPC_DISPATCH_ILQR(nj, chain, CALL)                                                \
-  switch (nj) {                                                                            \
-    case 1: if (chain) LaunchIlqr<1, true>::CALL; else LaunchIlqr<1, false>::CALL; break;  \
-    case 2: if (chain) LaunchIlqr<2, true>::CALL; else LaunchIlqr<2, false>::CALL; break;  \
-    case 3: if (chain) LaunchIlqr<3, true>::CALL; else LaunchIlqr<3, false>::CALL; break;  \
-    case 4: if (chain) LaunchIlqr<4, true>::CALL; else LaunchIlqr<4, false>::CALL; break;  \
-    case 5: if (chain) LaunchIlqr<5, true>::CALL; else LaunchIlqr<5, false>::CALL; break;  \
-    case 6: if (chain) LaunchIlqr<6, true>::CALL; else LaunchIlqr<6, false>::CALL; break;  \
-    case 7: if (chain) LaunchIlqr<7, true>::CALL; else LaunchIlqr<7, false>::CALL; break;  \
-    default: return -2;                                                                    \
-  }                                                                                        \
+#define TMPC_DISPATCH_ILQR(nj, chain, CALL)                                                              \
+  switch (mid) {                                                                                       \
+    TMPC_STATIC_MODEL_CASES(LaunchIlqr, CALL)                                                            \
+    default: break;                                                                                    \
+  }                                                                                                    \
+  switch (nj) {                                                                                        \
+    case 1: if (chain) LaunchIlqr<1, true, ModelRef>::CALL; else LaunchIlqr<1, false, ModelRef>::CALL; break;  \
+    case 2: if (chain) LaunchIlqr<2, true, ModelRef>::CALL; else LaunchIlqr<2, false, ModelRef>::CALL; break;  \
+    case 3: if (chain) LaunchIlqr<3, true, ModelRef>::CALL; else LaunchIlqr<3, false, ModelRef>::CALL; break;  \
+    case 4: if (chain) LaunchIlqr<4, true, ModelRef>::CALL; else LaunchIlqr<4, false, ModelRef>::CALL; break;  \
+    case 5: if (chain) LaunchIlqr<5, true, ModelRef>::CALL; else LaunchIlqr<5, false, ModelRef>::CALL; break;  \
+    case 6: if (chain) LaunchIlqr<6, true, ModelRef>::CALL; else LaunchIlqr<6, false, ModelRef>::CALL; break;  \
+    case 7: if (chain) LaunchIlqr<7, true, ModelRef>::CALL; else LaunchIlqr<7, false, ModelRef>::CALL; break;  \
+    default: return -2;                                                                                \
+  }                                                                                                    \
   return 0;
 
 int launch_ilqr_backward(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                          const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                          const double* mu, const double* lam, double* K, double* d, double* dV, int* ok) {
+  const int mid = 0;
   TMPC_DISPATCH_ILQR(nj, true, backward(s, C, Cs, B, N, x, u, rho, active, A, Bm, mu, lam, K, d, dV, ok))
 }
 
-int launch_ilqr_forward(hipStream_t s, int nj, bool chain, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
+int launch_ilqr_forward(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
                         const double* mu, const double* lam, int B, int N, int T, double dt, int init,
                         const double* alphas, const double* x, const double* u, const double* K, const double* d,
                         const int* active, const int* ok, double* xt, double* ut, double* Jt) {

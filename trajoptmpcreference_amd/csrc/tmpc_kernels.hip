@@ -25,8 +25,8 @@ namespace tmpc {
 // lane = (knot, col), col < NJ; writes the full symmetric matrix (column col
 // above the diagonal and row col left of it, :908-930).  x is [K][NX] rows
 // with row stride `xstride` per knot and element stride `estride`.
-template <int NJ, bool CHAIN>
-__device__ __forceinline__ void minv_lane_store(const ModelDev* __restrict__ M, const double q[NJ], int col,
+template <int NJ, bool CHAIN, class MT>
+__device__ __forceinline__ void minv_lane_store(const MT& M, const double q[NJ], int col,
                                                 double* __restrict__ Mo) {
   double cq[NJ], sq[NJ], mc[NJ];
 #pragma unroll
@@ -41,8 +41,8 @@ __device__ __forceinline__ void minv_lane_store(const ModelDev* __restrict__ M, 
   }
 }
 
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_qp_minv(const ModelDev* __restrict__ M, int B, int N,
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(256) k_qp_minv(MT M, int B, int N,
                                                  const double* __restrict__ x, const int* __restrict__ need,
                                                  double* __restrict__ minv_out) {
   constexpr int NX = 2 * NJ;
@@ -64,8 +64,8 @@ __global__ void __launch_bounds__(256) k_qp_minv(const ModelDev* __restrict__ M,
 // lane = (b, k, col), col < 2 NJ.  dqdd[:, col] = -Minv dc[:, col]
 // (TrajoptPlant.py:313-316); A = I + dt [[0, I], [dqdd_q, dqdd_qd]],
 // B = dt [[0], [Minv]] (TrajoptPlant.py:100-108).
-template <int NJ, bool CHAIN>
-__device__ __forceinline__ void grad_lane_store(const ModelDev* __restrict__ M, double dt, const double q[NJ],
+template <int NJ, bool CHAIN, class MT>
+__device__ __forceinline__ void grad_lane_store(const MT& M, double dt, const double q[NJ],
                                                 const double qd[NJ], const double qdd[NJ],
                                                 const double* __restrict__ Mi, int col, double* __restrict__ A,
                                                 double* __restrict__ Bm, double* __restrict__ dqdd) {
@@ -95,8 +95,8 @@ __device__ __forceinline__ void grad_lane_store(const ModelDev* __restrict__ M, 
   }
 }
 
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_qp_grad(const ModelDev* __restrict__ M, int B, int N, double dt,
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(256) k_qp_grad(MT M, int B, int N, double dt,
                                                  const double* __restrict__ x, const int* __restrict__ need,
                                                  const double* __restrict__ qdd_in, const double* __restrict__ minv_in,
                                                  double* __restrict__ Aout, double* __restrict__ Bout) {
@@ -1325,8 +1325,8 @@ __global__ void k_init_state(int B, double rho_init, ProbState st, const int* __
 
 // ======================================================================= kernel-level entry points
 // [K][nx] / [K][nu] row layout, one lane per knot (or per knot and column)
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_unit_minv(const ModelDev* __restrict__ M, int K, const double* __restrict__ x,
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(256) k_unit_minv(MT M, int K, const double* __restrict__ x,
                                                    double* __restrict__ minv_out) {
   constexpr int NX = 2 * NJ;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1338,8 +1338,8 @@ __global__ void __launch_bounds__(256) k_unit_minv(const ModelDev* __restrict__ 
   minv_lane_store<NJ, CHAIN>(M, q, col, minv_out + (size_t)k * NJ * NJ);
 }
 
-template <int NJ, bool CHAIN>
-__global__ void __launch_bounds__(256) k_unit_grad(const ModelDev* __restrict__ M, int K, double dt,
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(256) k_unit_grad(MT M, int K, double dt,
                                                    const double* __restrict__ x, const double* __restrict__ qdd_in,
                                                    const double* __restrict__ minv_in, double* __restrict__ Aout,
                                                    double* __restrict__ Bout, double* __restrict__ dqdd) {
@@ -1362,22 +1362,22 @@ __global__ void __launch_bounds__(256) k_unit_grad(const ModelDev* __restrict__ 
 // ======================================================================= launchers
 #define TMPC_GRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
 
-template <int NJ, bool CHAIN>
+template <int NJ, bool CHAIN, class MT>
 struct Launch {
   static void qp_minv(hipStream_t s, const ModelDev* M, int B, int N, const double* x, const int* need, double* minv) {
-    hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, M, B, N, x, need, minv);
+    hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), B, N, x, need, minv);
   }
   static void qp_grad(hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const int* need,
                       const double* qdd, const double* minv, double* A, double* Bm) {
-    hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, M, B, N, dt, x, need,
+    hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), B, N, dt, x, need,
                        qdd, minv, A, Bm);
   }
   static void unit_minv(hipStream_t s, const ModelDev* M, int K, const double* x, double* minv) {
-    hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN>), TMPC_GRID(K * NJ, 256), 0, s, M, K, x, minv);
+    hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
   }
   static void unit_grad(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* qdd,
                         const double* minv, double* A, double* Bm, double* dqdd) {
-    hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN>), TMPC_GRID(K * 2 * NJ, 256), 0, s, M, K, dt, x, qdd, minv, A, Bm,
+    hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN, MT>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd, minv, A, Bm,
                        dqdd);
   }
 };
@@ -1611,17 +1611,21 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
 }
 
 // dispatch tables over the joint count and the chain specialisation
-#define TMPC_DISPATCH_NJ(nj, chain, CALL)                                          \
-  switch (nj) {                                                                    \
-    case 1: if (chain) Launch<1, true>::CALL; else Launch<1, false>::CALL; break;  \
-    case 2: if (chain) Launch<2, true>::CALL; else Launch<2, false>::CALL; break;  \
-    case 3: if (chain) Launch<3, true>::CALL; else Launch<3, false>::CALL; break;  \
-    case 4: if (chain) Launch<4, true>::CALL; else Launch<4, false>::CALL; break;  \
-    case 5: if (chain) Launch<5, true>::CALL; else Launch<5, false>::CALL; break;  \
-    case 6: if (chain) Launch<6, true>::CALL; else Launch<6, false>::CALL; break;  \
-    case 7: if (chain) Launch<7, true>::CALL; else Launch<7, false>::CALL; break;  \
-    default: return -2;                                                            \
-  }                                                                                \
+#define TMPC_DISPATCH_NJ(nj, chain, CALL)                                                              \
+  switch (mid) {                                                                                       \
+    TMPC_STATIC_MODEL_CASES(Launch, CALL)                                                            \
+    default: break;                                                                                    \
+  }                                                                                                    \
+  switch (nj) {                                                                                        \
+    case 1: if (chain) Launch<1, true, ModelRef>::CALL; else Launch<1, false, ModelRef>::CALL; break;  \
+    case 2: if (chain) Launch<2, true, ModelRef>::CALL; else Launch<2, false, ModelRef>::CALL; break;  \
+    case 3: if (chain) Launch<3, true, ModelRef>::CALL; else Launch<3, false, ModelRef>::CALL; break;  \
+    case 4: if (chain) Launch<4, true, ModelRef>::CALL; else Launch<4, false, ModelRef>::CALL; break;  \
+    case 5: if (chain) Launch<5, true, ModelRef>::CALL; else Launch<5, false, ModelRef>::CALL; break;  \
+    case 6: if (chain) Launch<6, true, ModelRef>::CALL; else Launch<6, false, ModelRef>::CALL; break;  \
+    case 7: if (chain) Launch<7, true, ModelRef>::CALL; else Launch<7, false, ModelRef>::CALL; break;  \
+    default: return -2;                                                                                \
+  }                                                                                                    \
   return 0;
 
 #define TMPC_DISPATCH_NJ2(nj, CALL)          \
@@ -1637,18 +1641,18 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
   }                                                                                \
   return 0;
 
-int launch_qp_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, const double* x,
+int launch_qp_minv(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, const double* x,
                    const int* need, double* minv) {
   TMPC_DISPATCH_NJ(nj, chain, qp_minv(s, M, B, N, x, need, minv))
 }
-int launch_qp_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int B, int N, double dt, const double* x,
+int launch_qp_grad(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
                    const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
   TMPC_DISPATCH_NJ(nj, chain, qp_grad(s, M, B, N, dt, x, need, qdd, minv, A, Bm))
 }
-int launch_unit_minv(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, const double* x, double* minv) {
+int launch_unit_minv(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, const double* x, double* minv) {
   TMPC_DISPATCH_NJ(nj, chain, unit_minv(s, M, K, x, minv))
 }
-int launch_unit_grad(hipStream_t s, int nj, bool chain, const ModelDev* M, int K, double dt, const double* x,
+int launch_unit_grad(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
                      const double* qdd, const double* minv, double* A, double* Bm, double* dqdd) {
   TMPC_DISPATCH_NJ(nj, chain, unit_grad(s, M, K, dt, x, qdd, minv, A, Bm, dqdd))
 }
