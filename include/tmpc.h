@@ -175,6 +175,20 @@ int tmpc_ilqr_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, double* x, dou
 int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u,
                                  int32_t* exit_code, int32_t* iters);
 
+/* Receding-horizon MPC loop for B problems (the reference has only the hooks --
+ * shift_QF_start, shift_soft_constraint_constants -- and no loop, F1; algorithm: oracle/mpc.py).
+ * Per step: solve the horizon (solver = TMPC_LINSYS_* for SQP, or TMPC_SOLVER_ILQR) warm-started
+ * from (x, u); apply u[:, 0] to the plant (one Euler step); shift x, u by one knot (last kept) with
+ * x[:, 0] = the new state; QF_start -= 1 (floor 0) when set; soft-limit constants shifted.
+ * Outputs: the executed states x_exec [B][nx][steps+1] and controls u_exec [B][nu][steps], per-step
+ * exit codes and iteration counts [B][steps] (all nullable); x, u hold the final shifted horizon.
+ * Horizons up to N * nx = 1024 for SQP; iLQR has no horizon limit. */
+#define TMPC_SOLVER_ILQR 16
+int tmpc_mpc_batch(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps, double* x, double* u,
+                   double* x_exec, double* u_exec, int32_t* exit_codes, int32_t* iters);
+int tmpc_mpc_batch_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps, double* d_x, double* d_u,
+                          double* d_x_exec, double* d_u_exec, int32_t* d_exit_codes, int32_t* d_iters);
+
 /* Euler rollout x_{k+1} = f(x_k, u_k) from x[:, 0] (device pointers), the §8d initial trajectory. */
 int tmpc_rollout_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, const double* d_u);
 

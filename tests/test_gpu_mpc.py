@@ -1,0 +1,83 @@
+"""GPU parity: the receding-horizon MPC loop (oracle/mpc.py --
+the reference calls runMPCExample but never defines it, so the loop is this
+build's definition, checked against the oracle).  Per step the exit code and
+iteration count must be identical, the executed states / controls within
+1e-6 relative; QF_start and the soft-limit constants shift as the reference's
+hooks do."""
+import numpy as np
+import pytest
+
+from conftest import arm_model, quad_cost_arrays
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(n, N, QF_start=None, spec=None):
+    from trajoptmpcreference_amd import (QuadraticCost, TrajoptConstraint, TrajoptMPCReference, URDFPlant,
+                                         planar_arm_urdf)
+    plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(n)})
+    Q, QF, R, xg = quad_cost_arrays(n)
+    con = TrajoptConstraint(n, n, n, N)
+    for kind, (lb, ub, mode) in (spec or {}).items():
+        getattr(con, f"set_{kind}_limits")(ub, lb, mode)
+    return TrajoptMPCReference(plant, QuadraticCost(Q, QF, R, xg, QF_start), con)
+
+
+@pytest.mark.parametrize("method", ["iLQR", "QP-PCG-SS", "QP-S"])
+def test_mpc_matches_oracle(method):
+    from oracle import mpc as ompc
+    from oracle import sqp as osqp
+    m = arm_model("arm3")
+    N, B, steps = 16, 4, 3
+    solver = _setup(3, N, QF_start=12)
+    xs, us = zip(*[osqp.initial_problem(m, N, 0.1, 700 + i) for i in range(B)])
+    r = solver.MPC_batch(np.array(xs), np.array(us), N, 0.1, method, {"max_iter_SQP_DDP": 8}, mpc_steps=steps)
+    assert solver.cost.QF_start == 12 - steps
+    for i in range(B):
+        cost = osqp.QuadCost(*quad_cost_arrays(3), QF_start=12)
+        o = ompc.mpc(m, cost, xs[i], us[i], N, 0.1, "iLQR" if method == "iLQR" else method[3:], steps,
+                     {"max_iter_SQP_DDP": 8})
+        assert list(r["exit_codes"][i]) == list(o["exit_codes"]), i
+        assert list(r["iters"][i]) == list(o["iters"]), i
+        assert np.allclose(r["x_exec"][i], o["x_exec"], rtol=1e-6, atol=1e-8)
+        assert np.allclose(r["u_exec"][i], o["u_exec"], rtol=1e-6, atol=1e-8)
+        assert np.allclose(r["x"][i], o["x"], rtol=1e-6, atol=1e-8)
+
+
+def test_mpc_soft_limits_shift_like_the_reference():
+    from oracle import mpc as ompc
+    from oracle import sqp as osqp
+    from oracle.soft import SoftConstraints, SoftLimit
+    m = arm_model("arm3")
+    N, B, steps = 12, 3, 2
+    spec = {"torque": ([-0.7] * 3, [0.7] * 3, "AUGMENTED_LAGRANGIAN")}
+    solver = _setup(3, N, spec=spec)
+    opts = {"max_iter_SQP_DDP": 6, "max_iter_softConstraints": 3}
+    xs, us = zip(*[osqp.initial_problem(m, N, 0.1, 710 + i) for i in range(B)])
+    r = solver.MPC_batch(np.array(xs), np.array(us), N, 0.1, "QP-S", dict(opts), mpc_steps=steps)
+    for i in range(B):
+        lim = SoftLimit("torque", 3, N, [-0.7] * 3, [0.7] * 3, "AUGMENTED_LAGRANGIAN")
+        o = ompc.mpc(m, osqp.QuadCost(*quad_cost_arrays(3)), xs[i], us[i], N, 0.1, "S", steps, dict(opts),
+                     SoftConstraints([lim]))
+        assert list(r["exit_codes"][i]) == list(o["exit_codes"]), i
+        assert np.allclose(r["x_exec"][i], o["x_exec"], rtol=1e-6, atol=1e-8)
+        assert np.array_equal(r["soft_state"][0][i, :N - 1, 12:18].T, lim.mu)
+
+
+def test_ilqr_long_horizon_n128():
+    """iLQR has no horizon limit (the MPC config is arm6 N = 128).  Compared at convergence:
+    intermediate iterates of a 128-step closed-loop rollout amplify rounding differences along the
+    horizon (two CPU restatements differ there too), the converged trajectory does not."""
+    from oracle import ilqr as oilqr
+    from oracle import sqp as osqp
+    m = arm_model("arm6fix")
+    N = 128
+    solver = _setup(6, N)
+    x, u = osqp.initial_problem(m, N, 0.05, 3)
+    r = solver.iLQR_batch(x[None], u[None], N, 0.05, {})
+    runs = [oilqr.ilqr(m, osqp.QuadCost(*quad_cost_arrays(6)), x, u, N, 0.05, {}, solve=s) for s in ("cholesky", "lu")]
+    got = (int(r["exit_code"][0]), int(r["iter"][0]))
+    match = [o for o in runs if (o["exit_code"], o["iter"]) == got]
+    assert match, (got, [(o["exit_code"], o["iter"]) for o in runs])
+    assert got[0] == 1
+    assert np.allclose(r["x"][0], match[0]["x"], rtol=1e-6, atol=1e-7)

@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TMPC_LIBRARY") or os.path.join(_HERE, "libtmpc.so")
 
 LINSYS = {"S": 1, "PCG-J": 2, "PCG-BJ": 3, "PCG-SS": 4}
+SOLVER_ILQR = 16
 PRECOND = {"J": 1, "BJ": 2, "SS": 3}
 
 _dp = C.POINTER(C.c_double)
@@ -83,6 +84,10 @@ SIGNATURES = {
                                         C.POINTER(tmpc_trace)]),
     "tmpc_ilqr_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p,
                                                _ip, _ip]),
+    "tmpc_mpc_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, _dp, _dp, _dp, _dp,
+                                 _ip, _ip]),
+    "tmpc_mpc_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "tmpc_rollout_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p]),
     "tmpc_fd_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
     "tmpc_fd_grad_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
@@ -284,6 +289,26 @@ class Context:
             "tmpc_ilqr_solve_batch")
         out.update(x=x, u=u, trace=arrays)
         return out
+
+    def mpc_batch(self, x, u, N, dt, solver, steps):
+        """Receding-horizon loop (oracle/mpc.py); solver = "iLQR" or an SQP method name."""
+        x = _c64(x).copy()
+        u = _c64(u).copy()
+        B, nx, _ = x.shape
+        nu = u.shape[1]
+        xe = np.zeros((B, nx, steps + 1))
+        ue = np.zeros((B, nu, steps))
+        codes = np.zeros((B, steps), dtype=np.int32)
+        iters = np.zeros((B, steps), dtype=np.int32)
+        sid = SOLVER_ILQR if solver == "iLQR" else LINSYS[solver]
+        self._check(self.lib.tmpc_mpc_batch(self.h, B, int(N), float(dt), sid, int(steps), _ptr(x), _ptr(u), _ptr(xe),
+                                            _ptr(ue), _ptr(codes), _ptr(iters)), "tmpc_mpc_batch")
+        return dict(x=x, u=u, x_exec=xe, u_exec=ue, exit_codes=codes, iters=iters)
+
+    def mpc_batch_device(self, B, N, dt, solver, steps, d_x, d_u, d_xe, d_ue, d_codes, d_iters):
+        sid = SOLVER_ILQR if solver == "iLQR" else LINSYS[solver]
+        self._check(self.lib.tmpc_mpc_batch_device(self.h, B, int(N), float(dt), sid, int(steps), d_x, d_u, d_xe, d_ue,
+                                                   d_codes, d_iters), "tmpc_mpc_batch_device")
 
     def ilqr_solve_batch_device(self, B, N, dt, d_x, d_u, want_status=False):
         ex = np.zeros(B, dtype=np.int32) if want_status else None

@@ -192,7 +192,7 @@ static int precond_of(int linsys) {
   }
 }
 
-static int check_ready(tmpc_ctx* ctx, int B, int N) {
+static int check_ready(tmpc_ctx* ctx, int B, int N, bool qp = true) {
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model: call tmpc_set_model first");
   if (!ctx->has_cost) return fail(ctx, "no cost: call tmpc_set_cost_quadratic first");
@@ -201,7 +201,7 @@ static int check_ready(tmpc_ctx* ctx, int B, int N) {
                 ctx->hmodel.n);
   if (B < 1) return fail(ctx, "batch size must be >= 1 (got %d)", B);
   if (N < 2) return fail(ctx, "N must be >= 2 (got %d)", N);
-  if (N * ctx->hcost.nx > 1024)
+  if (qp && N * ctx->hcost.nx > 1024)
     return fail(ctx, "N * nx = %d exceeds 1024 rows (one PCG workgroup per problem); larger horizons are not "
                 "supported yet", N * ctx->hcost.nx);
   return 0;
@@ -451,7 +451,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
 
 // ------------------------------------------------------------------ iLQR driver (oracle/ilqr.py)
 static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u, TraceDev* tr_out) {
-  int rc = check_ready(ctx, B, N);
+  int rc = check_ready(ctx, B, N, false);
   if (rc) return rc;
   const int nj = ctx->hmodel.n, nx = 2 * nj, K = N - 1;
   const bool chain = ctx->hmodel.chain != 0;
@@ -827,7 +827,7 @@ int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, dou
 int tmpc_ilqr_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, double* x, double* u, int32_t* exit_code,
                           int32_t* exit_soft, int32_t* outer_iter, int32_t* iters, tmpc_trace* trace) {
   if (!ctx) return -1;
-  int rc = check_ready(ctx, B, N);
+  int rc = check_ready(ctx, B, N, false);
   if (rc) return rc;
   if (!x || !u) return fail(ctx, "null x/u");
   hipSetDevice(ctx->device);
@@ -873,6 +873,80 @@ int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double*
   if (rc) return rc;
   if (exit_code) HIP_OK(hipMemcpy(exit_code, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
   if (iters) HIP_OK(hipMemcpy(iters, ctx->bufs["st_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// ------------------------------------------------------------------ receding-horizon MPC (oracle/mpc.py)
+static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps, double* d_x, double* d_u,
+                      double* d_xe, double* d_ue, int* d_codes, int* d_iters) {
+  const bool ilqr = solver == TMPC_SOLVER_ILQR;
+  int rc = check_ready(ctx, B, N, !ilqr);
+  if (rc) return rc;
+  if (steps < 1) return fail(ctx, "steps must be >= 1");
+  if (!ilqr && precond_of(solver) < 0) return fail(ctx, "solver %d: use TMPC_LINSYS_* or TMPC_SOLVER_ILQR", solver);
+  const int nj = ctx->hmodel.n, nx = 2 * nj;
+  const bool chain = ctx->hmodel.chain != 0;
+  // executed state 0 = x[:, 0]
+  HIP_OK(hipMemcpy2DAsync(d_xe, (size_t)(steps + 1) * sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double),
+                          (size_t)B * nx, hipMemcpyDeviceToDevice, ctx->stream));
+  for (int s = 0; s < steps; ++s) {
+    rc = ilqr ? ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr) : sqp_device(ctx, B, N, dt, solver, d_x, d_u, nullptr);
+    if (rc) return rc;
+    HIP_OK(hipMemcpy2DAsync(d_codes + s, (size_t)steps * sizeof(int), ctx->bufs["st_exit"].ptr, sizeof(int),
+                            sizeof(int), B, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_OK(hipMemcpy2DAsync(d_iters + s, (size_t)steps * sizeof(int), ctx->bufs["st_iter"].ptr, sizeof(int),
+                            sizeof(int), B, hipMemcpyDeviceToDevice, ctx->stream));
+    {
+      Timed t(ctx, "mpc_shift");
+      LAUNCH_OK(launch_mpc_shift(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, s, steps, d_x, d_u,
+                                 d_xe, d_ue));
+    }
+    // QuadraticCost.shift_QF_start(-1) (TrajoptCost.py:100-104)
+    if (ctx->hcost.QF_start >= 0) {
+      ctx->hcost.QF_start = ctx->hcost.QF_start > 0 ? ctx->hcost.QF_start - 1 : 0;
+      HIP_OK(hipMemcpyAsync(ctx->dcost, &ctx->hcost, sizeof(CostDev), hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (ctx->hlim.any) {
+      launch_soft_shift(ctx->stream, ctx->dlim, B, N, nj, (double*)ctx->bufs["soft_mu"].ptr,
+                        (double*)ctx->bufs["soft_lam"].ptr, (double*)ctx->bufs["soft_phi"].ptr);
+      HIP_OK(hipGetLastError());
+    }
+  }
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int tmpc_mpc_batch_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps, double* d_x, double* d_u,
+                          double* d_x_exec, double* d_u_exec, int32_t* d_exit_codes, int32_t* d_iters) {
+  if (!ctx) return -1;
+  hipSetDevice(ctx->device);
+  return mpc_device(ctx, B, N, dt, solver, steps, d_x, d_u, d_x_exec, d_u_exec, d_exit_codes, d_iters);
+}
+
+int tmpc_mpc_batch(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps, double* x, double* u,
+                   double* x_exec, double* u_exec, int32_t* exit_codes, int32_t* iters) {
+  if (!ctx) return -1;
+  int rc = check_ready(ctx, B, N, solver != TMPC_SOLVER_ILQR);
+  if (rc) return rc;
+  if (!x || !u || steps < 1) return fail(ctx, "null x/u or steps < 1");
+  hipSetDevice(ctx->device);
+  const int nx = ctx->hcost.nx, nu = ctx->hcost.nu;
+  const size_t xn = (size_t)B * nx * N, un = (size_t)B * nu * (N - 1);
+  BUF(double, mpc_x, xn);
+  BUF(double, mpc_u, un);
+  BUF(double, mpc_xe, (size_t)B * nx * (steps + 1));
+  BUF(double, mpc_ue, (size_t)B * nu * steps);
+  BUF(int, mpc_codes, (size_t)B * steps);
+  BUF(int, mpc_iters, (size_t)B * steps);
+  HIP_OK(hipMemcpyAsync(mpc_x, x, xn * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(mpc_u, u, un * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = mpc_device(ctx, B, N, dt, solver, steps, mpc_x, mpc_u, mpc_xe, mpc_ue, mpc_codes, mpc_iters))) return rc;
+  HIP_OK(hipMemcpy(x, mpc_x, xn * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(u, mpc_u, un * sizeof(double), hipMemcpyDeviceToHost));
+  if (x_exec) HIP_OK(hipMemcpy(x_exec, mpc_xe, sizeof(double) * B * nx * (steps + 1), hipMemcpyDeviceToHost));
+  if (u_exec) HIP_OK(hipMemcpy(u_exec, mpc_ue, sizeof(double) * B * nu * steps, hipMemcpyDeviceToHost));
+  if (exit_codes) HIP_OK(hipMemcpy(exit_codes, mpc_codes, sizeof(int) * B * steps, hipMemcpyDeviceToHost));
+  if (iters) HIP_OK(hipMemcpy(iters, mpc_iters, sizeof(int) * B * steps, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -241,6 +241,54 @@ __global__ void __launch_bounds__(64) k_rollout(MT M, int B, int N, double dt,
   }
 }
 
+// ======================================================================= MPC step (oracle/mpc.py)
+// One 64-lane workgroup per problem after a horizon solve: apply the first
+// control to the plant, x_next = integrator(x_0, u_0) (TrajoptPlant.py:92-99),
+// record it, and shift the trajectory by one knot for the warm start
+// (x_k <- x_{k+1}, u_k <- u_{k+1}, last knot kept, x_0 <- x_next).
+template <int NJ, bool CHAIN, class MT>
+__global__ void __launch_bounds__(64) k_mpc_shift(MT M, int B, int N, double dt, int step, int steps,
+                                                  double* __restrict__ x, double* __restrict__ u,
+                                                  double* __restrict__ xe, double* __restrict__ ue) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int K = N - 1;
+  double* xb = x + (size_t)b * NX * N;
+  double* ub = u + (size_t)b * NU * K;
+  __shared__ double xn[NX];
+  if (t == 0) {
+    double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      q[j] = xb[j * N];
+      qd[j] = xb[(NJ + j) * N];
+      uu[j] = ub[j * K];
+      joint_cs(M, j, q[j], cq[j], sq[j]);
+    }
+    fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      xn[j] = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
+      xn[NJ + j] = __dadd_rn(qd[j], __dmul_rn(dt, qdd[j]));
+    }
+#pragma unroll
+    for (int m = 0; m < NX; ++m) xe[((size_t)b * NX + m) * (steps + 1) + step + 1] = xn[m];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) ue[((size_t)b * NU + m) * steps + step] = uu[m];
+  }
+  __syncthreads();
+  // shift each state / control row (rows are contiguous in the [nx][N] layout)
+  for (int m = t; m < NX; m += 64) {
+    double* row = xb + m * N;
+    for (int k = 0; k < N - 1; ++k) row[k] = row[k + 1];
+    row[0] = xn[m];
+  }
+  for (int m = t; m < NU; m += 64) {
+    double* row = ub + m * K;
+    for (int k = 0; k < K - 1; ++k) row[k] = row[k + 1];
+  }
+}
+
 #define TMPC_GRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
 
 template <int NJ, bool CHAIN, class MT>
@@ -264,6 +312,11 @@ struct LaunchFD {
   static void unit_fd(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
                       double* xnext, double* qdd) {
     hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
+  }
+  static void mpc_shift(hipStream_t s, const ModelDev* M, int B, int N, double dt, int step, int steps, double* x,
+                        double* u, double* xe, double* ue) {
+    hipLaunchKernelGGL((k_mpc_shift<NJ, CHAIN, MT>), dim3(B), dim3(64), 0, s, MT::make(M), B, N, dt, step, steps, x,
+                       u, xe, ue);
   }
   static void rollout(hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u) {
     hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT>), TMPC_GRID(B, 64), 0, s, MT::make(M), B, N, dt, x, u);
@@ -305,6 +358,11 @@ int launch_unit_fd(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M
 int launch_rollout(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
                    const double* u) {
   TMPC_DISPATCH_NJ(nj, chain, rollout(s, M, B, N, dt, x, u))
+}
+
+int launch_mpc_shift(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, int step,
+                     int steps, double* x, double* u, double* xe, double* ue) {
+  TMPC_DISPATCH_NJ(nj, chain, mpc_shift(s, M, B, N, dt, step, steps, x, u, xe, ue))
 }
 
 }  // namespace tmpc

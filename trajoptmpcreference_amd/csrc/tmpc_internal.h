@@ -109,6 +109,10 @@ void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int 
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
                         int* active_count, unsigned long long* counters);
+int launch_mpc_shift(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, int step,
+                     int steps, double* x, double* u, double* xe, double* ue);
+void launch_soft_shift(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double* mu, double* lam,
+                       double* phi);
 void launch_outer_init(hipStream_t s, int B, int* outer_active, int* outer_iter, int* exit_soft);
 void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, double* mu, double* lam,
                       double* phi);

@@ -1591,6 +1591,30 @@ __global__ void k_soft_init(const ConstrDev* __restrict__ Cs, size_t total, int 
   phi[i] = Cs->phi_init[t];
 }
 
+// BoxConstraint.shift_soft_constraint_constants(1) (TrajoptConstraint.py:168-176) on the
+// [B][N][6n] state: arr[:, :-1] = arr[:, 1:]; arr[:, 1:] = init (the reference's semantics:
+// every knot after the first returns to its initial value).  Torque limits span N-1 knots.
+__global__ void k_soft_shift(const ConstrDev* __restrict__ Cs, int B, int N, int NJ, double* __restrict__ mu,
+                             double* __restrict__ lam, double* __restrict__ phi) {
+  const int MC = 6 * NJ;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * MC) return;
+  const int b = i / MC, sl = i - b * MC, t = sl / (2 * NJ);
+  const int T = t == 2 ? N - 1 : N;
+  double* arrs[3] = {mu, lam, phi};
+  const double init[3] = {Cs->mu_init[t], 0.0, Cs->phi_init[t]};
+  for (int a = 0; a < 3; ++a) {
+    double* v = arrs[a] + (size_t)b * N * MC + sl;
+    if (T > 1) v[0] = v[MC];
+    for (int k = 1; k < T; ++k) v[(size_t)k * MC] = init[a];
+  }
+}
+
+void launch_soft_shift(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double* mu, double* lam,
+                       double* phi) {
+  hipLaunchKernelGGL(k_soft_shift, TMPC_GRID(B * 6 * nj, 256), 0, s, Cs, B, N, nj, mu, lam, phi);
+}
+
 __global__ void k_outer_init(int B, int* __restrict__ outer_active, int* __restrict__ outer_iter,
                              int* __restrict__ exit_soft) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;

@@ -254,6 +254,50 @@ class TrajoptMPCReference:
         self.exit_soft = ex_soft
         return (r["x"][0], r["u"][0], self.exit_sqp, self.exit_soft, outer, it)
 
+    # ------------------------------------------------------------------ receding-horizon MPC
+    def MPC_batch(self, x, u, N: int, dt: float, SOLVER_METHOD=MPCSolverMethods.QP_PCG_SS, options=None,
+                  mpc_steps: int = 1, soft_state=None):
+        """Receding-horizon loop for B problems (algorithm in oracle/mpc.py -- the
+        reference calls runMPCExample but never defines it, F1).  Each step solves the horizon with
+        SQP (QP-S / QP-PCG-*) or iLQR warm-started from the shifted previous solution, applies u[:, 0]
+        for one Euler step and shifts; the cost's QF_start and the soft-limit constants shift as the
+        reference's hooks do (TrajoptCost.py:100-104, TrajoptConstraint.py:168-176).  Returns the
+        executed states [B][nx][steps+1] / controls [B][nu][steps] and per-step exit codes / iterations."""
+        options = {} if options is None else options
+        self.set_default_options(options)
+        m = SOLVER_METHOD.value if isinstance(SOLVER_METHOD, MPCSolverMethods) else str(SOLVER_METHOD)
+        if m == "iLQR":
+            solver = "iLQR"
+        elif m.startswith("QP-") and m[3:] in ("S", "PCG-J", "PCG-BJ", "PCG-SS"):
+            solver = m[3:]
+        else:
+            raise NotImplementedError(f"MPC solver {m}: use iLQR, QP-S, QP-PCG-J, QP-PCG-BJ or QP-PCG-SS")
+        ctx = self._context(options)
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        if x.ndim != 3 or u.ndim != 3 or x.shape[2] != N or u.shape[2] != N - 1 or x.shape[0] != u.shape[0]:
+            raise ValueError(f"expected x [B][nx][{N}] and u [B][nu][{N - 1}], got {x.shape} and {u.shape}")
+        B = x.shape[0]
+        soft = self.other_constraints.has_any()
+        if soft:
+            if soft_state is None:
+                soft_state = [np.broadcast_to(a, (B,) + a.shape) for a in self.other_constraints.pack_state(N)]
+            ctx.set_soft_state(B, N, *soft_state)
+        r = ctx.mpc_batch(x, u, N, dt, solver, int(mpc_steps))
+        if soft:
+            r["soft_state"] = ctx.get_soft_state(B, N)
+        if self.cost.QF_start is not None:
+            self.cost.QF_start = max(self.cost.QF_start - int(mpc_steps), 0)
+        return r
+
+    def MPC(self, x, u, N: int, dt: float, SOLVER_METHOD=MPCSolverMethods.QP_PCG_SS, options=None, mpc_steps: int = 1):
+        """One problem: returns (x_exec [nx][steps+1], u_exec [nu][steps], exit_codes, iters)."""
+        r = self.MPC_batch(np.asarray(x, dtype=np.float64)[None], np.asarray(u, dtype=np.float64)[None], N, dt,
+                           SOLVER_METHOD, options, mpc_steps)
+        if "soft_state" in r:
+            self.other_constraints.unpack_state(*[a[0] for a in r["soft_state"]])
+        return r["x_exec"][0], r["u_exec"][0], r["exit_codes"][0], r["iters"][0]
+
     def solveKKTSystem_Schur(self, x, u, xs, N, dt, rho=0.0, use_PCG=True, options=None):
         """One QP (formKKTSystemBlocks + solveKKTSystem_Schur, :361-455) -> dxul column.
         xs must equal x[:, 0] (the SQP always passes the initial state)."""
