@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--method", default="PCG-SS", help="SQP linear-system method: PCG-SS / PCG-BJ / PCG-J / S")
     ap.add_argument("--solver", default="sqp", choices=["sqp", "ilqr"],
                     help="sqp: the BASELINE metric; ilqr: BASELINE config 3 (same workload, iLQR)")
+    ap.add_argument("--mpc-steps", type=int, default=0,
+                    help="> 0: BASELINE config 5, one step = a receding-horizon loop of this many horizon solves "
+                         "(use with --N 128 --solver ilqr --batch 8192)")
     ap.add_argument("--seed0", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
     ap.add_argument("--cpu-procs", type=int, default=16)
@@ -205,9 +208,9 @@ def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant
         comm.close()
         return
     nx, nu = 2 * n, n
-    value = B * a.steps * world / elapsed
-    roofline = None
-    if a.solver == "ilqr":
+    value = B * a.steps * world * max(1, a.mpc_steps) / elapsed
+    roofline = None   # MPC mode: the work counters cover only the last horizon solve
+    if a.solver == "ilqr" and a.mpc_steps == 0:
         bw = kernels.get("ilqr_backward")
         if bw:
             # algorithmic flops per backward launch: problem-iterations in the launch x (N-1) knots
@@ -218,8 +221,11 @@ def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant
                         "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
                         "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
                         "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
+    name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
+    if a.mpc_steps > 0:
+        name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
     out = {
-        "metric": f"MPC solves/sec (arm{n}.urdf, N={N}, {'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method})",
+        "metric": f"MPC solves/sec (arm{n}.urdf, N={N}, {name})",
         "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": 1000.0 * elapsed / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
@@ -262,7 +268,22 @@ def main():
     ctx.h2d(d_u0, u0)
     ctx.rollout_device(B, N, dt, d_x0, d_u0)
 
+    if a.mpc_steps > 0:
+        K1 = a.mpc_steps
+        d_xe, d_ue = ctx.alloc(B * nx * (K1 + 1) * 8), ctx.alloc(B * nu * K1 * 8)
+        d_codes, d_iters = ctx.alloc(B * K1 * 4), ctx.alloc(B * K1 * 4)
+
     def solve(want_status=False):
+        if a.mpc_steps > 0:
+            ctx.mpc_batch_device(B, N, dt, "iLQR" if a.solver == "ilqr" else a.method, a.mpc_steps, d_x, d_u, d_xe,
+                                 d_ue, d_codes, d_iters)
+            if want_status:
+                codes = np.zeros((B, a.mpc_steps), dtype=np.int32)
+                its = np.zeros((B, a.mpc_steps), dtype=np.int32)
+                ctx.d2h(codes, d_codes)
+                ctx.d2h(its, d_iters)
+                return codes.reshape(-1), its.reshape(-1)
+            return None, None
         if a.solver == "ilqr":
             return ctx.ilqr_solve_batch_device(B, N, dt, d_x, d_u, want_status=want_status)
         return ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=want_status)
@@ -298,7 +319,7 @@ def main():
             kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
     dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
 
-    total_solves = B * a.steps * world
+    total_solves = B * a.steps * world * max(1, a.mpc_steps)
     value = total_solves / elapsed
     ms_per_step = 1000.0 * elapsed / a.steps
 
@@ -311,7 +332,7 @@ def main():
         comm.close()
         return
 
-    if a.solver == "ilqr" or a.method == "S":
+    if a.solver == "ilqr" or a.method == "S" or a.mpc_steps > 0:
         return report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant, counters, exit_codes, iters)
     qp = kernels["qp"]
     n_pcg_iters = int(counters[1])
