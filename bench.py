@@ -30,6 +30,17 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector (= fp64 matrix) spec
 
 
+# Soft box-constraint presets (TrajoptConstraint.set_*_limits; |u| <= 0.5 and |q| <= 1.0 are
+# active on part of the §8d workload: its unconstrained optima reach |u| ~ 1.5, |q| ~ 1).
+LIMIT_PRESETS = {
+    "none": {},
+    "torque-al": {"torque": dict(mode="AUGMENTED_LAGRANGIAN", lb=-0.5, ub=0.5)},
+    "torque-qp": {"torque": dict(mode="QUADRATIC_PENALTY", lb=-0.5, ub=0.5)},
+    "torque-joint-al": {"torque": dict(mode="AUGMENTED_LAGRANGIAN", lb=-0.5, ub=0.5),
+                        "joint": dict(mode="AUGMENTED_LAGRANGIAN", lb=-1.0, ub=1.0)},
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,6 +55,9 @@ def parse():
     ap.add_argument("--mpc-steps", type=int, default=0,
                     help="> 0: BASELINE config 5, one step = a receding-horizon loop of this many horizon solves "
                          "(use with --N 128 --solver ilqr --batch 8192)")
+    ap.add_argument("--limits", default="none", choices=sorted(LIMIT_PRESETS),
+                    help="soft box constraints: torque-al = BASELINE config 3 (with --solver ilqr), "
+                         "torque-joint-al = config 4 (SQP-PCG with torque + joint limits)")
     ap.add_argument("--seed0", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
     ap.add_argument("--cpu-procs", type=int, default=16)
@@ -222,6 +236,8 @@ def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant
                         "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
                         "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
     name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
+    if a.limits != "none":
+        name += f", soft box constraints {a.limits}"
     if a.mpc_steps > 0:
         name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
     out = {
@@ -230,7 +246,8 @@ def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant
         "ms_per_step": 1000.0 * elapsed / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
         "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} {a.solver.upper()} "
-                               f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU",
+                               f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU"
+                               + ("" if a.limits == "none" else f", limits {a.limits}"),
                    "global_batch": B * world, "N": N, "parallelism": f"shard{world}"},
         "roofline": roofline, "cpu_baseline": None, "kernels": kernels, "dominant_kernel": dominant,
         "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(exit_codes, return_counts=True))},
@@ -256,6 +273,8 @@ def main():
     ctx = _native.Context(local_rank)
     ctx.set_model(model)
     ctx.set_cost_quadratic(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
+    limits = LIMIT_PRESETS[a.limits]
+    ctx.set_box_limits(limits)
 
     # ---- workload resident in HBM
     seed_base = shard_seed_base(a.seed0, rank, B)
@@ -291,6 +310,8 @@ def main():
     def step():
         ctx.d2d(d_x, d_x0, xb)
         ctx.d2d(d_u, d_u0, ub)
+        if limits:
+            ctx.set_soft_state(B, N)   # every step starts from the initial mu / lambda / phi
         solve()
 
     for _ in range(a.warmup):
@@ -326,13 +347,15 @@ def main():
     # ---- status of one solve (exit codes / iteration counts) for the record
     ctx.d2d(d_x, d_x0, xb)
     ctx.d2d(d_u, d_u0, ub)
+    if limits:
+        ctx.set_soft_state(B, N)
     exit_codes, iters = solve(want_status=True)
 
     if rank != 0:
         comm.close()
         return
 
-    if a.solver == "ilqr" or a.method == "S" or a.mpc_steps > 0:
+    if a.solver == "ilqr" or a.method == "S" or a.mpc_steps > 0 or limits:
         return report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant, counters, exit_codes, iters)
     qp = kernels["qp"]
     n_pcg_iters = int(counters[1])

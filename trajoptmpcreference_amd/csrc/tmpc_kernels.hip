@@ -121,54 +121,84 @@ __global__ void __launch_bounds__(256) k_qp_grad(MT M, int B, int N, double dt,
 }
 
 // ======================================================================= G-block inverses
+// lanes outside ROW_MASK read 0
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_get(double v) {
+  int lo, hi;
+  if (ROW_MASK == 0xf) {
+    lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+    hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+  } else {
+    lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  }
+  return __hiloint2double(hi, lo);
+}
+
+// In-place Gauss-Jordan inverse of an SPD matrix (no pivoting needed), one
+// 16-lane DPP row per matrix, lane r holding row r in a[]: pivot row p is
+// broadcast with DPP row_newbcast:p (a VALU move, no LDS round trip), its
+// reciprocal taken once.  Exact for diagonal inputs.  All 64 lanes must run it.
+template <int P, int NX>
+__device__ __forceinline__ void gj_pivot(double (&a)[NX], int r) {
+  double pr[NX];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) pr[c] = dpp_get<0x150 + P, 0xf>(a[c]);
+  const double rp = 1.0 / pr[P];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) pr[c] *= rp;
+  const double f = a[P];
+  if (r == P) {
+#pragma unroll
+    for (int c = 0; c < NX; ++c) a[c] = pr[c];
+    a[P] = rp;
+  } else {
+#pragma unroll
+    for (int c = 0; c < NX; ++c) a[c] = fma(-f, pr[c], a[c]);
+    a[P] = -f * rp;
+  }
+}
+
+template <int P, int NX>
+struct GjSweep {
+  static __device__ __forceinline__ void run(double (&a)[NX], int r) {
+    gj_pivot<P, NX>(a, r);
+    GjSweep<P + 1, NX>::run(a, r);
+  }
+};
+template <int NX>
+struct GjSweep<NX, NX> {
+  static __device__ __forceinline__ void run(double (&)[NX], int) {}
+};
+
 // Ghat = (G_k + rho I)^-1 for the three distinct cost Hessian blocks of
 // QuadraticCost (Q, QF, R; TrajoptCost.py:71-83); solveKKTSystem_Schur
 // adds rho in place and inverts (TrajoptMPCReference.py:419-422).
-// Gauss-Jordan on an SPD matrix (no pivoting needed; exact for diagonal
-// inputs), one 16-lane group per matrix, one row per lane, pivot rows
-// broadcast with wave shuffles.
+// One 16-lane group per matrix, one row per lane (GjSweep).
 template <int NJ>
 __global__ void __launch_bounds__(64) k_ginv(const CostDev* __restrict__ C, int B, const double* __restrict__ rho,
                                              const int* __restrict__ active, double* __restrict__ Ginv) {
   constexpr int NX = 2 * NJ;
   const int lane = threadIdx.x & 63;
   const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;   // one matrix per 16 lanes
-  const int r = lane & 15, base = lane & ~15;
+  const int r = lane & 15;
   const bool in_range = slot < B * 3;
   const int b = in_range ? slot / 3 : 0, which = in_range ? slot - 3 * b : 0;
   const bool act = in_range && active[b];
   const int n = which == 2 ? NJ : NX;
   const double* src = which == 0 ? C->Q : (which == 1 ? C->QF : C->R);
+  if (!__any(act)) return;   // wave-uniform exit
   const double rh = act ? rho[b] : 0.0;
-  double a[NX], inv[NX];
+  double a[NX];
 #pragma unroll
-  for (int c = 0; c < NX; ++c) {
+  for (int c = 0; c < NX; ++c)
     a[c] = (act && r < n && c < n) ? src[r * n + c] + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
-    inv[c] = (r == c) ? 1.0 : 0.0;
-  }
-#pragma unroll
-  for (int p = 0; p < NX; ++p) {
-    double pa[NX], pi[NX];
-#pragma unroll
-    for (int c = 0; c < NX; ++c) {
-      pa[c] = __shfl(a[c], base + p, 64);
-      pi[c] = __shfl(inv[c], base + p, 64);
-    }
-    const double piv = pa[p];
-    if (r == p) {
-#pragma unroll
-      for (int c = 0; c < NX; ++c) { a[c] = a[c] / piv; inv[c] = inv[c] / piv; }
-    } else {
-      const double f = a[p];
-#pragma unroll
-      for (int c = 0; c < NX; ++c) { a[c] -= f * (pa[c] / piv); inv[c] -= f * (pi[c] / piv); }
-    }
-  }
+  GjSweep<0, NX>::run(a, r);
   if (act && r < n) {
     double* out = Ginv + ((size_t)b * 3 + which) * NX * NX;
 #pragma unroll
     for (int c = 0; c < NX; ++c)
-      if (c < n) out[r * n + c] = inv[c];
+      if (c < n) out[r * n + c] = a[c];
   }
 }
 
@@ -196,13 +226,14 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
   constexpr int NX = 2 * NJ, NU = NJ, MC = 6 * NJ;
   const int lane = threadIdx.x & 63;
   const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-  const int r = lane & 15, base = lane & ~15;
+  const int r = lane & 15;
   const bool in_range = slot < B * N * 2;
   const int b = in_range ? slot / (2 * N) : 0;
   const int rem = in_range ? slot - b * 2 * N : 0;
   const int k = rem >> 1, which = rem & 1;
   const bool terminal = k == N - 1;
   const bool act = in_range && active[b] && !(which == 1 && terminal);
+  if (!__any(in_range && active[b])) return;   // wave-uniform exit
   const int n = which ? NJ : NX;
   double z[3 * NJ], jac[3 * NJ];
   const double* xb = x + (size_t)b * NX * N;
@@ -215,7 +246,7 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
   soft_knot<NJ>(Cs, mu + ko, lam + ko, terminal, z, jac);
   const double* src = which ? C->R : (use_QF(C, k, N) ? C->QF : C->Q);
   const double rh = act ? rho[b] : 0.0;
-  double a[NX], inv[NX];
+  double a[NX];
 #pragma unroll
   for (int c = 0; c < NX; ++c) {
     double outer = 0.0;
@@ -229,32 +260,14 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
         if (rr == r && c < NU) outer = jac[NX + rr] * jac[NX + c];
     }
     a[c] = (act && r < n && c < n) ? (src[r * n + c] + outer) + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
-    inv[c] = (r == c) ? 1.0 : 0.0;
   }
-#pragma unroll
-  for (int p = 0; p < NX; ++p) {
-    double pa[NX], pi[NX];
-#pragma unroll
-    for (int c = 0; c < NX; ++c) {
-      pa[c] = __shfl(a[c], base + p, 64);
-      pi[c] = __shfl(inv[c], base + p, 64);
-    }
-    const double piv = pa[p];
-    if (r == p) {
-#pragma unroll
-      for (int c = 0; c < NX; ++c) { a[c] = a[c] / piv; inv[c] = inv[c] / piv; }
-    } else {
-      const double f = a[p];
-#pragma unroll
-      for (int c = 0; c < NX; ++c) { a[c] -= f * (pa[c] / piv); inv[c] -= f * (pi[c] / piv); }
-    }
-  }
+  GjSweep<0, NX>::run(a, r);
   if (!in_range || !active[b] || r >= n) return;
   if (act) {
     double* out = Gk + ((size_t)b * N + k) * (NX * NX + NU * NU) + (which ? NX * NX : 0);
 #pragma unroll
     for (int c = 0; c < NX; ++c)
-      if (c < n) out[r * n + c] = inv[c];
+      if (c < n) out[r * n + c] = a[c];
   }
   double jr = 0.0;
 #pragma unroll
@@ -275,20 +288,7 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
 // shuffles cost an LDS round trip per step) and one LDS fan-in of the
 // per-wave totals, reduced again by DPP: a fixed tree, so the result is
 // deterministic and identical for a problem whatever its batch neighbours.
-// lanes outside ROW_MASK read 0
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ double dpp_get(double v) {
-  int lo, hi;
-  if (ROW_MASK == 0xf) {
-    lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
-    hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
-  } else {
-    lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
-    hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
-  }
-  return __hiloint2double(hi, lo);
-}
-
+// dpp_get: see the G-block inverses above
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
