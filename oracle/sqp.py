@@ -86,7 +86,10 @@ def kkt_blocks(model, cost, x, u, xs, N, dt, soft=None):
     c = np.zeros((N, nx))
     c[0] = x[:, 0] - xs
     c[1:] = x[:, 1:].T - xkp1
-    G = [cost.hessian(False, k) for k in range(N - 1)] + [cost.hessian(True, N - 1)]
+    if getattr(cost, "state_hessian", False):     # UrdfCost: hessian depends on x_k (TrajoptCost.py:482-519)
+        G = [cost.hessian(False, k, x[:, k]) for k in range(N - 1)] + [cost.hessian(True, N - 1, x[:, N - 1])]
+    else:
+        G = [cost.hessian(False, k) for k in range(N - 1)] + [cost.hessian(True, N - 1)]
     g = [cost.gradient(x[:, k], u[:, k], k) for k in range(N - 1)] + [cost.gradient(x[:, N - 1], None, N - 1)]
     if soft is not None:
         nxu = nx + n

@@ -198,6 +198,97 @@ def gen_qp(name, N, seed=0, dt=0.1, rho=1e-3):
     print(f"[golden] qp {name} N={N}: iters J/BJ/SS = {rec['iters_J']}/{rec['iters_BJ']}/{rec['iters_SS']}", flush=True)
 
 
+# ---------------------------------------------------------------- UrdfCost
+EE_Q = np.eye(4)
+EE_QF = 100.0 * np.eye(4)
+EE_R = 0.1 * np.eye(2)
+
+
+def make_ee_cost(plant, xg, QF_start=None):
+    _setup_reference()
+    from TrajoptCost import UrdfCost
+    return UrdfCost(plant, EE_Q.copy(), EE_QF.copy(), EE_R.copy(), np.array(xg, dtype=float), QF_start=QF_start)
+
+
+def gen_ee_points(K=24, seed=77):
+    """UrdfCost value / gradient / hessian and the RBDReference EE kinematics at random arm2 states."""
+    plant = make_plant("arm2")
+    cost = make_ee_cost(plant, [-1.0, 1.5, 0.0, 0.0], QF_start=20)
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(-2.0, 2.0, (K, 4))
+    U = rng.uniform(-3.0, 3.0, (K, 2))
+    ks = rng.integers(0, 30, K)
+    term = (np.arange(K) % 4) == 3
+    rec = {k: [] for k in ["pos", "J", "Jtot", "dx", "value", "grad", "hess"]}
+    rbd = plant.rbdReference
+    for i in range(K):
+        x, u, k = X[i], (None if term[i] else U[i]), int(ks[i])
+        rec["pos"].append(np.asarray(rbd.end_effector_positions(x[:2], cost.offsets), dtype=float).reshape(2))
+        rec["J"].append(np.asarray(rbd.Jacobian(x[:2], cost.offsets), dtype=float))
+        rec["Jtot"].append(np.asarray(rbd.jacobian_tot_state(x[:2], x[2:], cost.offsets), dtype=float))
+        rec["dx"].append(np.asarray(cost.delta_x(x), dtype=float).reshape(4))
+        rec["value"].append(float(np.asarray(cost.value(x, u, k)).reshape(())))
+        g = np.zeros(6)
+        gv = np.asarray(cost.gradient(x, u, k), dtype=float).reshape(-1)
+        g[:gv.size] = gv
+        rec["grad"].append(g)
+        h = np.zeros((6, 6))
+        hv = np.asarray(cost.hessian(x, u, k), dtype=float)
+        h[:hv.shape[0], :hv.shape[1]] = hv
+        rec["hess"].append(h)
+    np.savez_compressed(os.path.join(OUT, "ee_arm2_points.npz"), X=X, U=U, k=ks, terminal=term, QF_start=20,
+                        xg=np.array([-1.0, 1.5, 0.0, 0.0]), **{k: np.array(v) for k, v in rec.items()})
+    print(f"[golden] ee points arm2 K={K}")
+
+
+def run_ee_sqp(args):
+    """examples/twolinks.py (type_cost='urdf', PCG-SS, N=10, dt=0.1, x=u=0, expected_reduction_min=-100):
+    the configuration data/4 (xg=[-1,1.5,0,0]) and data/3 (xg=[-1.18,-1.58,0,0]) were recorded with."""
+    tag, xg, method = args
+    _setup_reference()
+    from TrajoptMPCReference import TrajoptMPCReference, SQPSolverMethods
+    from overloading import matrix_
+    matrix_.iteration = 0
+    matrix_.soft_constraint_iteration = 0
+    matrix_.line_search_iteration = 0
+    plant = make_plant("arm2")
+    cost = make_ee_cost(plant, xg)
+    N, dt = 10, 0.1
+    x0, u0 = np.zeros((4, N)), np.zeros((2, N - 1))
+    solver = TrajoptMPCReference(plant, cost)
+    m = {"S": SQPSolverMethods.S, "PCG-SS": SQPSolverMethods.PCG_SS, "PCG-BJ": SQPSolverMethods.PCG_BJ}[method]
+    opts = {"expected_reduction_min_SQP_DDP": -100, "RETURN_TRACE_SQP": True, "overloading": False}
+    import io
+    import contextlib
+    t0 = time.time()
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(copy.deepcopy(x0), copy.deepcopy(u0), N, dt, m,
+                                                                     opts)
+    wall = time.time() - t0
+    tr = solver.trace
+    keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
+            "succeeded_line_search"]
+    rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(t[k]) for t in tr]) for k in keys}
+    pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, f"ee_sqp_arm2_N10_{tag}_{method}.npz"),
+                        x0=x0, u0=u0, x=np.asarray(x), u=np.asarray(u), dt=dt, xg=np.array(xg, dtype=float),
+                        expected_reduction_min=-100.0, exit_sqp=exit_sqp, exit_soft=exit_soft,
+                        outer_iter=outer_iter, sqp_iter=sqp_iter, pcg_iters=pcg_iters, wall_s=wall, **rec)
+    return f"[golden] ee sqp {tag} {method}: exit={exit_sqp} iters={sqp_iter} pcg={list(pcg_iters)} wall={wall:.1f}s"
+
+
+def gen_ee_recorded():
+    """The recorded twolinks runs' final trajectories (data/4, data/3 CSVs: data, read as text)."""
+    out = {}
+    for tag in ("4", "3"):
+        for nm in ("final_traj", "final_input"):
+            path = os.path.join(REF, "data", tag, nm + ".csv")
+            if os.path.exists(path):
+                out[f"d{tag}_{nm}"] = np.loadtxt(path, delimiter=",", skiprows=1)[:, 1:]
+    np.savez_compressed(os.path.join(OUT, "ee_arm2_recorded.npz"), **out)
+    print(f"[golden] ee recorded: {sorted(out)}")
+
+
 # ---------------------------------------------------------------- full SQP
 def run_sqp(args):
     name, N, seed, method, dt = args
@@ -319,6 +410,14 @@ def main():
         jobs.sort(key=lambda j: -j[1] * (2 if j[0].startswith("arm6") else 1))
         with mp.get_context("fork").Pool(min(8, len(jobs))) as pool:
             for msg in pool.imap_unordered(run_sqp, jobs):
+                print(msg, flush=True)
+    if a.only in (None, "ee"):
+        gen_ee_points()
+        gen_ee_recorded()
+        jobs = [("d4", [-1.0, 1.5, 0.0, 0.0], "PCG-SS"), ("d3", [-1.18, -1.58, 0.0, 0.0], "PCG-SS"),
+                ("d4", [-1.0, 1.5, 0.0, 0.0], "S")]
+        with mp.get_context("fork").Pool(len(jobs)) as pool:
+            for msg in pool.imap_unordered(run_ee_sqp, jobs):
                 print(msg, flush=True)
     if a.only in (None, "soft"):
         jobs = [("QUADRATIC_PENALTY", "PCG-SS", 8, 2.0, 0, 0.1), ("AUGMENTED_LAGRANGIAN", "PCG-SS", 8, 2.0, 0, 0.1),

@@ -112,6 +112,10 @@ class _Joint:
     Xa: np.ndarray = None
     Xb: np.ndarray = None
     S: np.ndarray = None
+    # homogeneous 4x4 transform H(q) = H0 + a(q)*Ha + b(q)*Hb (Joint.py:91-95)
+    H0: np.ndarray = None
+    Ha: np.ndarray = None
+    Hb: np.ndarray = None
 
 
 @dataclass
@@ -129,6 +133,9 @@ class RobotModel:
     damping: np.ndarray                    # (n,)
     subtree: list = field(default_factory=list)   # sorted subtree ids (Robot.py:67-68)
     joint_names: list = field(default_factory=list)
+    H0: np.ndarray = None                  # (n, 4, 4) homogeneous transform coefficients
+    Ha: np.ndarray = None                  #   H(q) = H0 + cos q Ha + sin q Hb (revolute)
+    Hb: np.ndarray = None                  #   H(q) = H0 + q Ha (prismatic)
 
     @property
     def nq(self):
@@ -138,6 +145,18 @@ class RobotModel:
         if self.jtype[j] == JTYPE_REVOLUTE:
             return self.X0[j] + math.cos(q) * self.Xa[j] + math.sin(q) * self.Xb[j]
         return self.X0[j] + q * self.Xa[j]
+
+    def H(self, j: int, q: float) -> np.ndarray:
+        """Robot.get_Xmat_hom_Func_by_id (Joint.py:105-106)."""
+        if self.jtype[j] == JTYPE_REVOLUTE:
+            return self.H0[j] + math.cos(q) * self.Ha[j] + math.sin(q) * self.Hb[j]
+        return self.H0[j] + q * self.Ha[j]
+
+    def dH(self, j: int, q: float) -> np.ndarray:
+        """Robot.get_dXmat_hom_Func_by_id: d/dq of H (Joint.py:97,111-112)."""
+        if self.jtype[j] == JTYPE_REVOLUTE:
+            return -math.sin(q) * self.Ha[j] + math.cos(q) * self.Hb[j]
+        return self.Ha[j].copy()
 
     def is_serial_chain(self) -> bool:
         return all(int(self.parent[j]) == j - 1 for j in range(self.n))
@@ -190,6 +209,35 @@ def _joint_transform(j: _Joint):
     return snap(X0), snap(Xa), snap(Xb), S
 
 
+def _hom(R3, t3):
+    H = np.zeros((4, 4))
+    H[:3, :3] = R3
+    H[:3, 3] = t3
+    return H
+
+
+def _joint_hom(j: _Joint):
+    """Homogeneous transform coefficients (Joint.py:91-95): rotation (Rfree(q) E)^T,
+    translation = free translation + origin xyz, snapped like nsimplify(tolerance=1e-6)."""
+    E = _rx(j.rpy[0]) @ _ry(j.rpy[1]) @ _rz(j.rpy[2])
+    xyz = np.array(j.xyz, dtype=float)
+    zero = np.zeros(3)
+    if j.jtype == "revolute":
+        C0, Ca, Cb = (C[:3, :3] for C in _axis_coeffs(_axis_index(j.axis)))
+        H0, Ha, Hb = _hom((C0 @ E).T, xyz), _hom((Ca @ E).T, zero), _hom((Cb @ E).T, zero)
+        H0[3, 3] = 1.0
+    elif j.jtype == "prismatic":
+        e = np.zeros(3)
+        e[_axis_index(j.axis)] = 1.0
+        H0, Ha, Hb = _hom(E.T, xyz), _hom(np.zeros((3, 3)), e), np.zeros((4, 4))
+        H0[3, 3] = 1.0
+    else:
+        H0, Ha, Hb = _hom(E.T, xyz), np.zeros((4, 4)), np.zeros((4, 4))
+        H0[3, 3] = 1.0
+    snap = np.vectorize(lambda v: _snap(float(v), 10 ** 6))
+    return snap(H0), snap(Ha), snap(Hb)
+
+
 def _axis_index(axis):
     # the reference tests axis[2]==1, then axis[1]==1, then axis[0]==1 (Joint.py:56-80)
     for idx in (2, 1, 0):
@@ -232,6 +280,8 @@ def parse_urdf(path_or_text: str) -> RobotModel:
                    rpy=tuple(_floats(o.get("rpy") if o is not None else None)),
                    damping=float(dyn.get("damping")) if dyn is not None else 0.0)
         j.X0, j.Xa, j.Xb, j.S = _joint_transform(j)
+        if j.jtype in ("revolute", "prismatic", "fixed"):
+            j.H0, j.Ha, j.Hb = _joint_hom(j)
         joints.append(j)
 
     # fold fixed joints (URDFParser.py:323-345)
@@ -242,6 +292,7 @@ def parse_urdf(path_or_text: str) -> RobotModel:
             if gc.parent == j.child:
                 gc.parent = j.parent
                 gc.X0, gc.Xa, gc.Xb = gc.X0 @ j.X0, gc.Xa @ j.X0, gc.Xb @ j.X0
+                gc.H0, gc.Ha, gc.Hb = j.H0 @ gc.H0, j.H0 @ gc.Ha, j.H0 @ gc.Hb
         Xf = j.X0
         link_I[j.parent] = link_I[j.parent] + Xf.T @ link_I[j.child] @ Xf
         joints.remove(j)
@@ -281,7 +332,10 @@ def parse_urdf(path_or_text: str) -> RobotModel:
         Xb=np.array([by_name[nm].Xb for nm in order]),
         I=np.array([link_I[by_name[nm].child] for nm in order]),
         damping=np.array([by_name[nm].damping for nm in order]),
-        subtree=[sorted(s) for s in subtree], joint_names=list(order))
+        subtree=[sorted(s) for s in subtree], joint_names=list(order),
+        H0=np.array([by_name[nm].H0 for nm in order]),
+        Ha=np.array([by_name[nm].Ha for nm in order]),
+        Hb=np.array([by_name[nm].Hb for nm in order]))
 
 
 def planar_arm_urdf(n_links: int, mass: float = 0.1, length: float = 1.0) -> str:
