@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 2
+#define TMPC_ABI_VERSION 3
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). N (dense KKT) is not offered on the GPU. */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
@@ -134,6 +134,15 @@ int tmpc_set_model(tmpc_ctx* ctx, int n, const int32_t* parent, const int32_t* j
 /* QuadraticCost(Q, QF, R, xg, QF_start) (TrajoptCost.py:24-47); QF_start < 0 means None. */
 int tmpc_set_cost_quadratic(tmpc_ctx* ctx, int nx, int nu, const double* Q, const double* QF, const double* R,
                             const double* xg, int32_t QF_start);
+
+/* UrdfCost(plant, Q, QF, R, xg, QF_start) (TrajoptCost.py:371-569): the quadratic form acts on the
+ * end-effector task state [p(q); J(q) qd] (RBDReference.py:123-148, 313-387), Gauss-Newton hessian
+ * (hess_mode 0, :490-492).  2-link arms only (nx = 4, nu = 2), as the reference.  H0 / Ha / Hb:
+ * [2][4][4] row-major coefficients of each joint's homogeneous transform
+ * H_j(q) = H0 + cos q Ha + sin q Hb (Joint.py:91-97).  Supported by tmpc_sqp_solve_batch[_device];
+ * iLQR, the MPC loop and tmpc_qp_batch reject it. */
+int tmpc_set_cost_ee(tmpc_ctx* ctx, int nx, int nu, const double* Q, const double* QF, const double* R,
+                     const double* xg, int32_t QF_start, const double* H0, const double* Ha, const double* Hb);
 
 void tmpc_default_options(tmpc_options* opts);
 int tmpc_set_options(tmpc_ctx* ctx, const tmpc_options* opts);

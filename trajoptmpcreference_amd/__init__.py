@@ -7,13 +7,13 @@ interfaces; compute: hand-written gfx950 HIP kernels in libtmpc.so behind a
 ctypes C ABI (include/tmpc.h).  No CPU fallback.
 """
 from .constraint import BoxConstraint, TrajoptConstraint
-from .cost import QuadraticCost, TrajoptCost
+from .cost import QuadraticCost, TrajoptCost, UrdfCost
 from .pcg import PCG
 from .plant import TrajoptPlant, URDFPlant
 from .solver import MPCSolverMethods, SQPSolverMethods, TrajoptMPCReference
 from .urdf import RobotModel, parse_urdf, planar_arm_urdf
 
 __all__ = [
-    "BoxConstraint", "TrajoptConstraint", "QuadraticCost", "TrajoptCost", "PCG", "TrajoptPlant", "URDFPlant",
+    "BoxConstraint", "TrajoptConstraint", "QuadraticCost", "TrajoptCost", "UrdfCost", "PCG", "TrajoptPlant", "URDFPlant",
     "MPCSolverMethods", "SQPSolverMethods", "TrajoptMPCReference", "RobotModel", "parse_urdf", "planar_arm_urdf",
 ]

@@ -71,6 +71,7 @@ SIGNATURES = {
     "tmpc_last_error": (C.c_char_p, [C.c_void_p]),
     "tmpc_set_model": (C.c_int, [C.c_void_p, C.c_int, _ip, _ip, _ip, _dp, _dp, _dp, _dp, C.c_double]),
     "tmpc_set_cost_quadratic": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp, _dp, C.c_int32]),
+    "tmpc_set_cost_ee": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp, _dp, C.c_int32, _dp, _dp, _dp]),
     "tmpc_default_options": (None, [C.POINTER(tmpc_options)]),
     "tmpc_set_options": (C.c_int, [C.c_void_p, C.POINTER(tmpc_options)]),
     "tmpc_set_box_limits": (C.c_int, [C.c_void_p, C.POINTER(tmpc_box_limits)]),
@@ -204,6 +205,16 @@ class Context:
         self._check(self.lib.tmpc_set_cost_quadratic(self.h, self.nx, self.nu, _ptr(Q), _ptr(QF), _ptr(R), _ptr(xg),
                                                      -1 if QF_start is None else int(QF_start)),
                     "tmpc_set_cost_quadratic")
+
+    def set_cost_ee(self, Q, QF, R, xg, QF_start, H0, Ha, Hb):
+        """UrdfCost (TrajoptCost.py:371-569): H0/Ha/Hb are the 2 joints' homogeneous
+        transform coefficients (RobotModel.H0/Ha/Hb[:2])."""
+        Q, QF, R, xg = _c64(Q), _c64(QF), _c64(R), _c64(xg).reshape(-1)
+        H0, Ha, Hb = _c64(H0), _c64(Ha), _c64(Hb)
+        self.nx, self.nu = Q.shape[0], R.shape[0]
+        self._check(self.lib.tmpc_set_cost_ee(self.h, self.nx, self.nu, _ptr(Q), _ptr(QF), _ptr(R), _ptr(xg),
+                                              -1 if QF_start is None else int(QF_start), _ptr(H0), _ptr(Ha),
+                                              _ptr(Hb)), "tmpc_set_cost_ee")
 
     def set_options(self, **kw):
         for k, v in kw.items():

@@ -83,3 +83,67 @@ class QuadraticCost(TrajoptCost):
         self.QF_start += shift
         self.QF_start = max(self.QF_start, 0)
         return self.QF_start
+
+
+class UrdfCost(QuadraticCost):
+    """End-effector cost (TrajoptCost.py:371-569): the quadratic form acts on the
+    task state y = [p(q); J(q) qd] of the leaf's offset point [0, 1, 0, 1]
+    (RBDReference.py:123-148, 313-387) instead of on x.  Hessian: hess_mode 0,
+    (Q Jt)^T Jt (:490-492).  Like the reference it is defined for
+    2-link arms only.  The GPU solver evaluates it on the device (ee_eval in
+    csrc/tmpc_device.h); these host hooks serve callers that evaluate costs
+    themselves."""
+
+    OFFSET = np.array([0.0, 1.0, 0.0, 1.0])
+
+    def __init__(self, plant, Q_in, QF_in, R_in, xg_in, QF_start=None, overloading=False):
+        super().__init__(Q_in, QF_in, R_in, xg_in, QF_start)
+        self.plant = plant
+        self.n = plant.get_num_pos()
+        m = plant.model
+        if self.n != 2 or m.H0 is None or not m.is_serial_chain():
+            raise ValueError("UrdfCost is defined for 2-link serial arms only (RBDReference.py:262-265; SURVEY F5)")
+        if overloading:
+            raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
+        self.hess_mode = 0
+
+    def _kin(self, q):
+        m = self.plant.model
+        H = [m.H(j, q[j]) for j in range(2)]
+        dH = [m.dH(j, q[j]) for j in range(2)]
+        pos = (H[0] @ H[1] @ self.OFFSET)[:2]
+        J = np.column_stack(((dH[0] @ H[1] @ self.OFFSET)[:2], (H[0] @ dH[1] @ self.OFFSET)[:2]))
+        return pos, J
+
+    def jacobian_tot_state(self, q, qd):
+        """RBDReference.py:313-331 with the hand-coded dJdq pattern (:252-259)."""
+        _, J = self._kin(q)
+        dJdq = np.array([[-J[1, 0], -J[1, 1]], [-J[1, 1], -J[1, 1]], [-J[0, 0], -J[0, 1]], [J[0, 1], J[0, 1]]])
+        J2 = (dJdq @ qd).reshape(2, 2)
+        return np.vstack((np.hstack((J, np.zeros((2, 2)))), np.hstack((J2, J))))
+
+    def delta_x(self, x):
+        x = np.asarray(x, dtype=np.float64)
+        pos, J = self._kin(x[:2])
+        return np.concatenate((pos, J @ x[2:])) - self.xg
+
+    def value(self, x, u=None, timestep=None, iter_1=0, iter_2=0, iter_3=0):
+        dx = self.delta_x(x)
+        cost = 0.5 * (dx @ (self.get_currQ(u, timestep) @ dx))
+        if u is not None:
+            u = np.asarray(u)
+            cost += 0.5 * (u @ (self.R @ u))
+        return cost
+
+    def gradient(self, x, u=None, timestep=None, iter_1=0, iter_2=0, iter_3=0):
+        x = np.asarray(x, dtype=np.float64)
+        top = (self.delta_x(x) @ self.get_currQ(u, timestep)) @ self.jacobian_tot_state(x[:2], x[2:])
+        return top if u is None else np.hstack((top, np.asarray(u) @ self.R))
+
+    def hessian(self, x, u=None, timestep=None, iter_1=0, iter_2=0, iter_3=0):
+        x = np.asarray(x, dtype=np.float64)
+        Jt = self.jacobian_tot_state(x[:2], x[2:])
+        hx = (self.get_currQ(u, timestep) @ Jt).T @ Jt
+        if u is None:
+            return hx
+        return np.vstack((np.hstack((hx, np.zeros((4, 2)))), np.hstack((np.zeros((2, 4)), self.R))))

@@ -376,8 +376,10 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
   const bool soft = ctx->hlim.any != 0;
+  // UrdfCost has a state-dependent Hessian: it takes the per-knot Ghat path of the soft limits
+  const bool perknot = soft || ctx->hcost.kind == COST_EE;
   double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
-  if (soft) {
+  if (perknot) {
     if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
     if (ctx->soft_B != B || ctx->soft_N != N) {
       launch_soft_init(ctx->stream, ctx->dlim, (size_t)B * N * 6 * nj, 6 * nj, smu, slam, sphi);
@@ -453,6 +455,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
 static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u, TraceDev* tr_out) {
   int rc = check_ready(ctx, B, N, false);
   if (rc) return rc;
+  if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "iLQR supports QuadraticCost only (UrdfCost: use SQP)");
   const int nj = ctx->hmodel.n, nx = 2 * nj, K = N - 1;
   const bool chain = ctx->hmodel.chain != 0;
   const tmpc_options& o = ctx->opts;
@@ -678,6 +681,32 @@ int tmpc_set_cost_quadratic(tmpc_ctx* ctx, int nx, int nu, const double* Q, cons
   return 0;
 }
 
+int tmpc_set_cost_ee(tmpc_ctx* ctx, int nx, int nu, const double* Q, const double* QF, const double* R,
+                     const double* xg, int32_t QF_start, const double* H0, const double* Ha, const double* Hb) {
+  if (!ctx) return -1;
+  if (nx != 4 || nu != 2)
+    return fail(ctx, "UrdfCost is defined for 2-link arms only (nx=4, nu=2; got nx=%d, nu=%d)", nx, nu);
+  if (!Q || !QF || !R || !xg || !H0 || !Ha || !Hb) return fail(ctx, "null cost array");
+  CostDev c{};
+  c.nx = nx;
+  c.nu = nu;
+  c.kind = COST_EE;
+  c.QF_start = QF_start < 0 ? -1 : QF_start;
+  memcpy(c.Q, Q, sizeof(double) * nx * nx);
+  memcpy(c.QF, QF, sizeof(double) * nx * nx);
+  memcpy(c.R, R, sizeof(double) * nu * nu);
+  memcpy(c.xg, xg, sizeof(double) * nx);
+  memcpy(c.eeH0, H0, sizeof(double) * 32);
+  memcpy(c.eeHa, Ha, sizeof(double) * 32);
+  memcpy(c.eeHb, Hb, sizeof(double) * 32);
+  hipSetDevice(ctx->device);
+  HIP_OK(hipMemcpyAsync(ctx->dcost, &c, sizeof(c), hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->hcost = c;
+  ctx->has_cost = true;
+  return 0;
+}
+
 void tmpc_default_options(tmpc_options* o) {
   if (!o) return;
   memset(o, 0, sizeof(*o));
@@ -882,6 +911,7 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
   const bool ilqr = solver == TMPC_SOLVER_ILQR;
   int rc = check_ready(ctx, B, N, !ilqr);
   if (rc) return rc;
+  if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "the MPC loop supports QuadraticCost only");
   if (steps < 1) return fail(ctx, "steps must be >= 1");
   if (!ilqr && precond_of(solver) < 0) return fail(ctx, "solver %d: use TMPC_LINSYS_* or TMPC_SOLVER_ILQR", solver);
   const int nj = ctx->hmodel.n, nx = 2 * nj;
@@ -1015,6 +1045,7 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   if (!ctx) return -1;
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
+  if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "tmpc_qp_batch supports QuadraticCost only");
   const int precond = precond_of(linsys);
   if (precond < 0) return fail(ctx, "linear system method %d is not available on the GPU", linsys);
   if (!rho || !x || !u) return fail(ctx, "null input");

@@ -45,15 +45,107 @@ struct ModelDev {
   double I[NJMAX][36];
 };
 
-struct CostDev {            // QuadraticCost (TrajoptCost.py:24-104)
+enum { COST_QUADRATIC = 0, COST_EE = 1 };
+
+struct CostDev {            // QuadraticCost (TrajoptCost.py:24-104) or UrdfCost (:371-569)
   int nx, nu;
   int QF_start;             // -1 = None
-  int pad;
+  int kind;                 // COST_*
   double Q[NXMAX * NXMAX];
   double QF[NXMAX * NXMAX];
   double R[NJMAX * NJMAX];
   double xg[NXMAX];
+  // COST_EE: homogeneous joint transforms H_j(q) = H0 + cos q Ha + sin q Hb (Joint.py:91-97),
+  // row-major 4x4, joints 0 and 1 of the 2-link chain
+  double eeH0[2][16], eeHa[2][16], eeHb[2][16];
 };
+
+// UrdfCost task-space terms at one knot (2-link arms only, as the reference: SURVEY F5).
+//   y = [p(q); J(q) qd] - xg          delta_x           TrajoptCost.py:425-435
+//   p = (H_0 H_1 o)[0:2], o = [0,1,0,1]  end_effector_positions  RBDReference.py:123-148
+//   J[:, d] = (chain with dH_d) o [0:2]  Jacobian               RBDReference.py:334-387
+//   Jt = [[J, 0], [reshape(dJdq qd), J]] with the hand-coded dJdq pattern (:252-259, :313-331)
+// Returns 0.5 y^T Q y (value, :415) and writes grad = (y^T Q) Jt (:449) and Jt.
+template <int NJ>
+__device__ __forceinline__ double ee_eval(const CostDev* __restrict__ C, const double* __restrict__ Qk,
+                                          const double* xk, double* grad, double* Jt) {
+  constexpr int NX = 2 * NJ;
+  if constexpr (NJ != 2) {
+    for (int m = 0; m < NX; ++m) grad[m] = 0.0;
+    for (int m = 0; m < NX * NX; ++m) Jt[m] = 0.0;
+    return 0.0;
+  } else {
+    double H[2][16], dH[2][16];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      double s, c;
+      sincos(xk[j], &s, &c);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        H[j][e] = C->eeH0[j][e] + c * C->eeHa[j][e] + s * C->eeHb[j][e];
+        dH[j][e] = -s * C->eeHa[j][e] + c * C->eeHb[j][e];
+      }
+    }
+    // o = [0, 1, 0, 1]: M o = column 1 + column 3
+    double v1[4], w1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v1[r] = H[1][r * 4 + 1] + H[1][r * 4 + 3];
+      w1[r] = dH[1][r * 4 + 1] + dH[1][r * 4 + 3];
+    }
+    double p[2], J[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      double a = 0.0, b = 0.0, d = 0.0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        a += H[0][r * 4 + m] * v1[m];
+        b += dH[0][r * 4 + m] * v1[m];
+        d += H[0][r * 4 + m] * w1[m];
+      }
+      p[r] = a;
+      J[r][0] = b;
+      J[r][1] = d;
+    }
+    const double qd0 = xk[2], qd1 = xk[3];
+    const double J2[2][2] = {{-J[1][0] * qd0 - J[1][1] * qd1, -J[1][1] * qd0 - J[1][1] * qd1},
+                             {-J[0][0] * qd0 - J[0][1] * qd1, J[0][1] * qd0 + J[0][1] * qd1}};
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        Jt[r * 4 + c] = J[r][c];
+        Jt[r * 4 + 2 + c] = 0.0;
+        Jt[(2 + r) * 4 + c] = J2[r][c];
+        Jt[(2 + r) * 4 + 2 + c] = J[r][c];
+      }
+    double y[4];
+    y[0] = p[0] - C->xg[0];
+    y[1] = p[1] - C->xg[1];
+    y[2] = (J[0][0] * qd0 + J[0][1] * qd1) - C->xg[2];
+    y[3] = (J[1][0] * qd0 + J[1][1] * qd1) - C->xg[3];
+    double v = 0.0, gq[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double qy = 0.0, yq = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        qy += Qk[r * 4 + c] * y[c];
+        yq += y[c] * Qk[c * 4 + r];
+      }
+      v += y[r] * qy;
+      gq[r] = yq;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double g = 0.0;
+#pragma unroll
+      for (int l = 0; l < 4; ++l) g += gq[l] * Jt[l * 4 + c];
+      grad[c] = g;
+    }
+    return 0.5 * v;
+  }
+}
 
 // Soft box limits: BoxConstraint in QUADRATIC_PENALTY / AUGMENTED_LAGRANGIAN
 // mode (TrajoptConstraint.py:53-166) with the vector semantics of

@@ -94,11 +94,19 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
     xk[m] = dxb ? xb[m * N + k] - al * dxk[m] : xb[m * N + k];
   }
   const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
+  double cost, Dk = 0.0;
+  if (C->kind == COST_EE) {
+    // UrdfCost value and gradient at the trial point (TrajoptCost.py:402-458)
+    double gx[NX], Jt[NX * NX];
+    cost = ee_eval<NJ>(C, Qk, xk, gx, Jt);
+#pragma unroll
+    for (int m = 0; m < NX; ++m) Dk += gx[m] * dxk[m];
+  } else {
   double d[NX];
 #pragma unroll
   for (int m = 0; m < NX; ++m) d[m] = xk[m] - C->xg[m];
   // value: 0.5 dx^T (Q dx) [+ 0.5 u^T (R u)]; gradient: [dx^T Q, u^T R]
-  double vq = 0.0, Dk = 0.0;
+  double vq = 0.0;
 #pragma unroll
   for (int r = 0; r < NX; ++r) {
     double qd = 0.0, gq = 0.0;
@@ -110,7 +118,8 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
     vq += d[r] * qd;
     Dk += gq * dxk[r];
   }
-  double cost = 0.5 * vq;
+  cost = 0.5 * vq;
+  }
   double viol = 0.0;
   double* out = terms + ((size_t)bt * N + k) * 4;
   double uk[NU], duk[NU];

@@ -246,6 +246,36 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
   soft_knot<NJ>(Cs, mu + ko, lam + ko, terminal, z, jac);
   const double* src = which ? C->R : (use_QF(C, k, N) ? C->QF : C->Q);
   const double rh = act ? rho[b] : 0.0;
+  // UrdfCost: state-dependent x block (Q Jt)^T Jt (hess_mode 0, TrajoptCost.py:490-492)
+  // and its gradient (y^T Q) Jt (:449) joins the soft jacobian in jsoft
+  const bool ee = C->kind == COST_EE && which == 0;
+  double eg[NX], hrow[NX];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) eg[c] = hrow[c] = 0.0;
+  if (ee) {
+    double Jt[NX * NX], qj[NX];
+    ee_eval<NJ>(C, src, z, eg, Jt);
+#pragma unroll
+    for (int l = 0; l < NX; ++l) {   // (Q Jt)[l][r]
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NX; ++m) {
+        double jm = 0.0;
+#pragma unroll
+        for (int rr = 0; rr < NX; ++rr)
+          if (rr == r) jm = Jt[m * NX + rr];
+        acc += src[l * NX + m] * jm;
+      }
+      qj[l] = acc;
+    }
+#pragma unroll
+    for (int c = 0; c < NX; ++c) {
+      double acc = 0.0;
+#pragma unroll
+      for (int l = 0; l < NX; ++l) acc += qj[l] * Jt[l * NX + c];
+      hrow[c] = acc;
+    }
+  }
   double a[NX];
 #pragma unroll
   for (int c = 0; c < NX; ++c) {
@@ -259,7 +289,8 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
       for (int rr = 0; rr < NU; ++rr)
         if (rr == r && c < NU) outer = jac[NX + rr] * jac[NX + c];
     }
-    a[c] = (act && r < n && c < n) ? (src[r * n + c] + outer) + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
+    const double h = ee ? hrow[c] : src[(r < n ? r : 0) * n + c];
+    a[c] = (act && r < n && c < n) ? (h + outer) + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
   }
   GjSweep<0, NX>::run(a, r);
   if (!in_range || !active[b] || r >= n) return;
@@ -273,6 +304,11 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
 #pragma unroll
   for (int m = 0; m < NX; ++m)
     if (m == (which ? NX + r : r)) jr = jac[m];
+  if (ee) {
+#pragma unroll
+    for (int m = 0; m < NX; ++m)
+      if (m == r) jr = eg[m] + jr;
+  }
   if (which) {
 #pragma unroll
     for (int m = 0; m < NU; ++m)
@@ -947,6 +983,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
     const int kk = e / (NX + NU), c = e - kk * (NX + NU);
     double g = 0.0;
     if (c < NX) {
+      if (C->kind == COST_EE) { g_lds[e] = PK ? jsoft[(size_t)b * N * (NX + NU) + e] : 0.0; continue; }   // in jsoft
       const double* Qk = use_QF(C, kk, N) ? C->QF : C->Q;
 #pragma unroll
       for (int m = 0; m < NX; ++m) g += (S.x[m * N + kk] - C->xg[m]) * Qk[m * NX + c];

@@ -14,7 +14,7 @@ import numpy as np
 
 from . import _native
 from .constraint import TrajoptConstraint
-from .cost import QuadraticCost, TrajoptCost
+from .cost import QuadraticCost, TrajoptCost, UrdfCost
 from .plant import TrajoptPlant, URDFPlant
 
 
@@ -121,13 +121,17 @@ class TrajoptMPCReference:
             raise NotImplementedError("the GPU solver needs a URDFPlant (custom TrajoptPlant subclasses have no "
                                       "device implementation)")
         if not isinstance(self.cost, QuadraticCost):
-            raise NotImplementedError("the GPU solver supports QuadraticCost (UrdfCost is SURVEY §8f row 4)")
+            raise NotImplementedError("the GPU solver supports QuadraticCost and UrdfCost")
         spec = self.other_constraints.gpu_spec()   # raises for the hard modes
         if options.get("overloading"):
             raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
         ctx = self.plant._ctx()
         c = self.cost
-        ctx.set_cost_quadratic(c.Q, c.QF, c.R, c.xg, c.QF_start)
+        if isinstance(c, UrdfCost):
+            m = self.plant.model
+            ctx.set_cost_ee(c.Q, c.QF, c.R, c.xg, c.QF_start, m.H0[:2], m.Ha[:2], m.Hb[:2])
+        else:
+            ctx.set_cost_quadratic(c.Q, c.QF, c.R, c.xg, c.QF_start)
         ctx.set_options(**{v: options[k] for k, v in _OPTION_MAP.items()})
         ctx.set_box_limits(spec)
         return ctx
