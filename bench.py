@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--limits", default="none", choices=sorted(LIMIT_PRESETS),
                     help="soft box constraints: torque-al = BASELINE config 3 (with --solver ilqr), "
                          "torque-joint-al = config 4 (SQP-PCG with torque + joint limits)")
+    ap.add_argument("--cost", default="quadratic", choices=["quadratic", "ee"],
+                    help="ee: UrdfCost (SURVEY 8f row 4; 2-link only) with examples/twolinks.py's Q, QF, R, "
+                         "xg = [-1, 1.5, 0, 0]; use with --links 2")
     ap.add_argument("--seed0", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
     ap.add_argument("--cpu-procs", type=int, default=16)
@@ -238,6 +241,8 @@ def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant
     name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
     if a.limits != "none":
         name += f", soft box constraints {a.limits}"
+    if a.cost == "ee":
+        name += ", UrdfCost end-effector cost (twolinks.py goal)"
     if a.mpc_steps > 0:
         name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
     out = {
@@ -247,7 +252,8 @@ def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant
         "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
         "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} {a.solver.upper()} "
                                f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU"
-                               + ("" if a.limits == "none" else f", limits {a.limits}"),
+                               + ("" if a.limits == "none" else f", limits {a.limits}")
+                               + (", UrdfCost" if a.cost == "ee" else ""),
                    "global_batch": B * world, "N": N, "parallelism": f"shard{world}"},
         "roofline": roofline, "cpu_baseline": None, "kernels": kernels, "dominant_kernel": dominant,
         "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(exit_codes, return_counts=True))},
@@ -272,7 +278,13 @@ def main():
     model = parse_urdf(planar_arm_urdf(n))
     ctx = _native.Context(local_rank)
     ctx.set_model(model)
-    ctx.set_cost_quadratic(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
+    if a.cost == "ee":
+        if n != 2:
+            raise SystemExit("--cost ee needs --links 2 (UrdfCost is 2-link only, SURVEY F5)")
+        ctx.set_cost_ee(np.eye(4), 100 * np.eye(4), 0.1 * np.eye(2), np.array([-1.0, 1.5, 0.0, 0.0]), None,
+                        model.H0[:2], model.Ha[:2], model.Hb[:2])
+    else:
+        ctx.set_cost_quadratic(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
     limits = LIMIT_PRESETS[a.limits]
     ctx.set_box_limits(limits)
 
@@ -355,7 +367,7 @@ def main():
         comm.close()
         return
 
-    if a.solver == "ilqr" or a.method == "S" or a.mpc_steps > 0 or limits:
+    if a.solver == "ilqr" or a.method == "S" or a.mpc_steps > 0 or limits or a.cost != "quadratic":
         return report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant, counters, exit_codes, iters)
     qp = kernels["qp"]
     n_pcg_iters = int(counters[1])

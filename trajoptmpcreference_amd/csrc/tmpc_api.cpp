@@ -372,6 +372,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   BUF(double, terms, (size_t)B * T * N * 4);   // [B][T][N][cost, violation, D, soft value]
   BUF(int, active_count, 1);
   BUF(unsigned long long, counters, 4);
+  BUF(unsigned long long, prob_counters, (size_t)B * 3);   // per-problem tallies of k_ls_decide
   BUF(int, outer_active, B);
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
@@ -395,6 +396,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     w.slam = slam;
   }
   HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
+  HIP_OK(hipMemsetAsync(prob_counters, 0, (size_t)B * 3 * sizeof(unsigned long long), ctx->stream));
   std::vector<double> al_h(al);
   al_h.push_back(0.0);  // slot T: alpha = 0 for the initial merit evaluation
   HIP_OK(hipMemcpyAsync(alphas, al_h.data(), al_h.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
@@ -423,7 +425,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     {
       Timed t(ctx, "ls_decide");
       launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
-                       st, w.iters, tr, active_count, counters);
+                       st, w.iters, tr, active_count, prob_counters);
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -439,6 +441,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (*ctx->h_count == 0) break;
   }
+  launch_sum_counters(ctx->stream, B, prob_counters, counters);
   unsigned long long hc[4] = {0, 0, 0, 0};
   HIP_OK(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));

@@ -90,6 +90,7 @@ int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* S
 int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const double* Sd, const double* Sl,
                    const double* gam, double* U, double* Y, double* lam);
 int pcg_set_max_lds();
+void launch_sum_counters(hipStream_t s, int B, const unsigned long long* pc, unsigned long long* out);
 void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,

@@ -1280,10 +1280,13 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
       const int it = st.iter[b];
       const size_t e = (size_t)b * W + it + 1;
       if (counters) {
+        // per-problem tallies [B][3], summed once per solve by k_sum_counters (one global
+        // atomic per problem and iteration serialised thousands of blocks on one L2 line):
         // [0] problem-QPs solved, [1] PCG iterations, [2] QPs with a fresh dynamics gradient
-        atomicAdd(&counters[0], 1ull);
-        atomicAdd(&counters[1], (unsigned long long)(pcg_iters ? pcg_iters[b] : 0));
-        atomicAdd(&counters[2], (unsigned long long)st.need_grad[b]);
+        unsigned long long* pc = counters + (size_t)b * 3;
+        pc[0] += 1ull;
+        pc[1] += (unsigned long long)(pcg_iters ? pcg_iters[b] : 0);
+        pc[2] += (unsigned long long)st.need_grad[b];
       }
       const bool error = choice < 0;
       double deltaJ = 0.0;
@@ -1319,7 +1322,7 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
       st.drho[b] = drho;
       st.need_grad[b] = (error || done) ? 0 : 1;
       if (done) st.active[b] = 0;
-      else atomicAdd(active_count, 1);
+      else *active_count = 1;   // the host only tests for zero
       s_choice = choice;
     }
   }
@@ -1341,8 +1344,26 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
       ub[e] = ub[e] - al * dub[k * NU + m];
     }
   } else if (choice == -2 && t == 0) {
-    atomicAdd(active_count, 1);
+    *active_count = 1;
   }
+}
+
+// Sum the per-problem tallies of k_ls_decide into out[0..2] (256 atomics per solve).
+__global__ void __launch_bounds__(256) k_sum_counters(int B, const unsigned long long* __restrict__ pc,
+                                                      unsigned long long* __restrict__ out) {
+  unsigned long long s0 = 0, s1 = 0, s2 = 0;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    s0 += pc[(size_t)b * 3];
+    s1 += pc[(size_t)b * 3 + 1];
+    s2 += pc[(size_t)b * 3 + 2];
+  }
+  atomicAdd(&out[0], s0);
+  atomicAdd(&out[1], s1);
+  atomicAdd(&out[2], s2);
+}
+
+void launch_sum_counters(hipStream_t s, int B, const unsigned long long* pc, unsigned long long* out) {
+  hipLaunchKernelGGL(k_sum_counters, dim3(1), dim3(256), 0, s, B, pc, out);
 }
 
 __global__ void k_init_state(int B, double rho_init, ProbState st, const int* __restrict__ outer_active) {
