@@ -85,3 +85,26 @@ def test_ee_sqp_reproduces_recorded_runs(tag, xg):
     # |x| reaches 4.7 on data/3; the reference run today is itself 2.0e-6 away from it
     assert np.max(np.abs(r["x"] - rec[f"d{tag}_final_traj"])) < 1e-5
     assert np.max(np.abs(r["u"] - rec[f"d{tag}_final_input"])) < 1e-5
+
+
+def test_host_urdfcost_hooks_match_reference():
+    """The drop-in's host UrdfCost (trajoptmpcreference_amd/cost.py) -- the plugin hooks
+    callers evaluate themselves, e.g. exampleHelpers.py:101-111 -- against the same
+    reference evaluations (no GPU needed: URDFPlant only parses the model)."""
+    from trajoptmpcreference_amd import URDFPlant, UrdfCost, planar_arm_urdf
+    d = golden("ee_arm2_points.npz")
+    plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(2)})
+    cost = UrdfCost(plant, np.eye(4), 100.0 * np.eye(4), 0.1 * np.eye(2), d["xg"], int(d["QF_start"]))
+    for i, x in enumerate(d["X"]):
+        term = bool(d["terminal"][i])
+        u = None if term else d["U"][i]
+        k = int(d["k"][i])
+        nz = 4 if term else 6
+        assert np.allclose(cost.delta_x(x), d["dx"][i], rtol=0, atol=1e-12)
+        assert np.allclose(cost.jacobian_tot_state(x[:2], x[2:]), d["Jtot"][i], rtol=0, atol=1e-12)
+        assert abs(cost.value(x, u, k, iter_1=1, iter_2=0, iter_3=2) - d["value"][i]) <= 1e-12 * max(1.0, abs(d["value"][i]))
+        assert _rel(cost.gradient(x, u, k), d["grad"][i][:nz]) < 1e-12
+        assert _rel(cost.hessian(x, u, k), d["hess"][i][:nz, :nz]) < 1e-12
+    with pytest.raises(ValueError, match="2-link"):
+        UrdfCost(URDFPlant(options={"path_to_urdf": planar_arm_urdf(3)}), np.eye(6), np.eye(6), np.eye(3),
+                 np.zeros(6))
