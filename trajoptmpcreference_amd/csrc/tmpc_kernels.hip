@@ -820,9 +820,11 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
 //   epilogue  dxu = Ghat (g - C^T lambda) (:449-452), with C^T lambda formed
 //             once per knot in LDS.
 // S and lambda never leave the chip.
+// A_k / B_k are read from HBM (L2-resident, shared by the NX lanes of a knot), not staged:
+// that keeps k_qp's LDS under 80 KB so two problems' workgroups share a CU.
 __host__ __device__ inline size_t qp_stage_doubles(int N, int NX, int NU) {
   const size_t K = N - 1;
-  return K * NX * NX + K * NX * NU + 3 * (size_t)NX * NX + (size_t)NX * N + (size_t)NU * K;
+  return 3 * (size_t)NX * NX + (size_t)NX * N + (size_t)NU * K;
 }
 
 // LDS layout of k_qp: [staging area | lambda] is reused by the PCG buffers
@@ -840,15 +842,15 @@ __host__ __device__ inline size_t qp_lds_doubles(int N, int NX, int NU) {
 }
 
 struct QpStage {
-  double *A, *B, *G, *x, *u;
+  const double *A, *B;      // global (this problem's A_k, B_k)
+  double *G, *x, *u;        // LDS
 };
 
-__device__ __forceinline__ QpStage qp_stage(double* lds, int N, int NX, int NU) {
-  const int K = N - 1;
+__device__ __forceinline__ QpStage qp_stage(double* lds, int N, int NX, int NU, const double* A, const double* B) {
   QpStage S;
-  S.A = lds;
-  S.B = S.A + (size_t)K * NX * NX;
-  S.G = S.B + (size_t)K * NX * NU;
+  S.A = A;
+  S.B = B;
+  S.G = lds;
   S.x = S.G + 3 * NX * NX;
   S.u = S.x + NX * N;
   return S;
@@ -967,10 +969,8 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   const PcgLane<NX, RPL> ln(threadIdx.x, N);
   const int k = ln.k;
   const int K = N - 1;
-  const QpStage S = qp_stage(lds, N, NX, NU);
+  const QpStage S = qp_stage(lds, N, NX, NU, Aall + (size_t)b * K * NX * NX, Ball + (size_t)b * K * NX * NU);
   double* lam_lds = S.u + NU * K;
-  lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
-  lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
   if (!PK) lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
   const GhatSrc<NJ, PK> Gh{PK ? Ginv + (size_t)b * N * GhatSrc<NJ, PK>::GS : S.G};
   lds_copy(S.x, x + (size_t)b * NX * N, NX * N);
@@ -1035,10 +1035,8 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   if (threadIdx.x == 0) iters[b] = it_done;
   }
 
-  // ---- epilogue: dxu = Ghat (g - C^T lambda); A, B, Ghat re-staged into LDS
+  // ---- epilogue: dxu = Ghat (g - C^T lambda); Ghat re-staged into LDS
   __syncthreads();
-  lds_copy(S.A, Aall + (size_t)b * K * NX * NX, K * NX * NX);
-  lds_copy(S.B, Ball + (size_t)b * K * NX * NU, K * NX * NU);
   if (!PK) lds_copy(S.G, Ginv + (size_t)b * 3 * NX * NX, 3 * NX * NX);
   if (ln.valid) {
 #pragma unroll
