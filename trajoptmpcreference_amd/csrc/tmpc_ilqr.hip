@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
       tr.iteration[e] = 0; tr.ls_iter[e] = 0; tr.alpha[e] = 1.0; tr.rho[e] = st.rho[b];
       tr.J[e] = J; tr.c[e] = 0.0; tr.merit[e] = J; tr.D[e] = __builtin_nan(""); tr.ratio[e] = __builtin_nan("");
       tr.accepted[e] = 0; tr.pcg_iters[e] = 0;
-      atomicAdd(active_count, 1);
+      *active_count = 1;   // the host only tests for zero
       s_choice = -1;
     } else {
       const double J = st.J[b];
@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
       st.drho[b] = drho;
       st.need_grad[b] = (error || done) ? 0 : 1;
       if (done) st.active[b] = 0;
-      else atomicAdd(active_count, 1);
+      else *active_count = 1;
       s_choice = choice;
     }
   }
