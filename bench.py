@@ -9,10 +9,19 @@ every problem's exit) of B independent problems of the §8d workload:
 Inputs are resident in HBM before the timed region (each step restores the
 initial trajectories with a device-to-device copy, inside the timed region).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-one process per GPU, each rank solves its own B problems (seeds offset by
-rank * B) -- independent problems, no data-path collective, weak scaling.
-torch.distributed is used only for the barrier and the max-over-ranks time.
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N,
+or any launcher that sets RANK / WORLD_SIZE / LOCAL_RANK): one process per GPU,
+rank r solves global problems [r B, (r+1) B) -- independent problems, no
+collective inside a solve, weak scaling.  RCCL over xGMI through libtmpc's
+tmpc_comm_* C ABI (trajoptmpcreference_amd/dist.py; no PyTorch) broadcasts the
+initial states from rank 0, times the region with a barrier and the max over
+ranks, and gathers every problem's exit code / iteration count to rank 0.
+
+Checks carried in the line (rank 0): the CPU leg (oracle NumPy restatement,
+`cpu_baseline`) solves the first S problems of the same workload and
+`parity` compares them with the GPU's exit codes, SQP iteration counts and
+per-QP PCG iteration counts; `kkt_residual` is SURVEY §8d's residual against
+the reference's own first QP.
 """
 import argparse
 import json
@@ -26,8 +35,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector (= fp64 matrix) spec
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md: 8.0 TB/s)
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector (= fp64 matrix) peak
+LDS_PEAK_GBS = 256 * 2.4 * 256   # 256 B/clk/CU (ds_read_b64/b128) x 2.4 GHz x 256 CUs
 
 
 # Soft box-constraint presets (TrajoptConstraint.set_*_limits; |u| <= 0.5 and |q| <= 1.0 are
@@ -41,7 +51,7 @@ LIMIT_PRESETS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -65,7 +75,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
     ap.add_argument("--cpu-procs", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def initial_states(n, B, seed0):
@@ -75,86 +85,52 @@ def initial_states(n, B, seed0):
     return q0
 
 
-def shard_seed_base(seed0, rank, B):
-    """Rank r solves problems seed0 + r*B ... seed0 + (r+1)*B - 1: contiguous, disjoint
-    slices of one global workload, so every rank's result equals the
-    single-GPU result for the same problems."""
-    return seed0 + rank * B
+# ------------------------------------------------------------------ flop / byte models
+def f_pcg_survey(N, nx):
+    """f_pcg = 2*3*nx^2*N*2 + ~10*N*nx flop per PCG iteration (SpMV with the three
+    S blocks of every block row and a three-block P^-1 apply, plus the vector work)."""
+    return 2 * 3 * nx * nx * N * 2 + 10 * N * nx
 
 
-class Comm:
-    """torch.distributed as plumbing only: a barrier and the max over ranks of the
-    timed region (RCCL on the GPUs; gloo in the CPU tests).  No data-path collective."""
-
-    def __init__(self, world, local_rank, backend="nccl"):
-        self.world = world
-        self.tdist = None
-        if world > 1:
-            import torch
-            import torch.distributed as tdist
-            if backend == "nccl":
-                torch.cuda.set_device(local_rank)
-                self.device = f"cuda:{local_rank}"
-            else:
-                self.device = "cpu"
-            tdist.init_process_group(backend=backend)
-            self.torch, self.tdist = torch, tdist
-
-    def barrier(self):
-        if self.tdist is not None:
-            self.tdist.barrier()
-
-    def max(self, v):
-        if self.tdist is None:
-            return v
-        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.device)
-        self.tdist.all_reduce(t, op=self.tdist.ReduceOp.MAX)
-        return float(t.item())
-
-    def close(self):
-        if self.tdist is not None:
-            self.tdist.destroy_process_group()
-            self.tdist = None
-
-
-# ------------------------------------------------------------------ byte / flop model (SURVEY §8d)
-def pcg_bytes_per_iter(N, nx):
-    return 8 * (2 * (2 * N - 1) * nx * nx + 10 * N * nx)
-
-
-def pcg_flops_per_iter(N, nx, method):
-    # SpMV with S (3 blocks per block row) + preconditioner apply + dots/axpys
+def pcg_flops_impl(N, nx, method):
+    """What k_qp executes per PCG iteration: SpMV over the 3N-2 stored S blocks; the
+    preconditioner as implemented (SS: z = P_D (r - S_off P_D r), 4N-2 block products)."""
     spmv = 2 * (3 * N - 2) * nx * nx
-    pre = {"PCG-J": N * nx, "PCG-BJ": 2 * N * nx * nx, "PCG-SS": 2 * (N + 2 * (N - 1) + N) * nx * nx}[method]
+    pre = {"PCG-J": N * nx, "PCG-BJ": 2 * N * nx * nx, "PCG-SS": 2 * (N + 2 * (N - 1) + N) * nx * nx,
+           "PCG-0": 0}[method]
     return spmv + pre + 10 * N * nx
 
 
+def b_pcg_survey(N, nx):
+    """SURVEY §8(d) streaming model: b_pcg = 8 (2 (2N-1) nx^2 + 10 N nx) B per PCG iteration."""
+    return 8 * (2 * (2 * N - 1) * nx * nx + 10 * N * nx)
+
+
 def pcg_lds_bytes_per_iter(N, nx, method):
-    # per lane (row): SpMV reads 3 nx doubles; J/BJ/SS preconditioner reads 0 / nx / 4 nx
-    # doubles; 1 / 2 / 4 vector stores -- what the LDS array serves, broadcast or not
-    reads = 3 * nx + {"PCG-J": 0, "PCG-BJ": nx, "PCG-SS": 4 * nx}[method]
-    writes = {"PCG-J": 1, "PCG-BJ": 2, "PCG-SS": 4}[method]
+    """LDS bytes the array serves per PCG iteration (k_qp, one row per lane): SpMV reads 3 nx
+    doubles per row; SS rebuilds its r block (2 nx) and reads w (2 nx) and t (nx); BJ 2 nx; plus
+    the per-row vector stores (Ap, r, w, t, p for SS)."""
+    reads = 3 * nx + {"PCG-J": 0, "PCG-0": 0, "PCG-BJ": 2 * nx, "PCG-SS": 5 * nx}[method]
+    writes = {"PCG-J": 1, "PCG-0": 1, "PCG-BJ": 3, "PCG-SS": 5}[method]
     return 8 * N * nx * (reads + writes)
-
-
-LDS_PEAK_GBS = 256 * 2.4 * 256   # 256 B/clk/CU (ds_read_b128) x 2.4 GHz x 256 CUs
-
-
-def measured_traffic(kernel_prefix):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_summary.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
-    if not os.path.exists(path):
-        return None
-    for k, v in json.load(open(path))["kernels"].items():
-        if k.startswith(kernel_prefix):
-            return v["hbm_bytes_per_launch"]
-    return None
 
 
 def qp_schur_flops(N, nx, nu):
     # per problem-QP: S blocks (A G A^T, B G B^T, A G), gamma, the diagonal-block inverses and dxu
     per_knot = 2 * (nx * nx * nx + nu * nu * nx + nx * nx * nx + nx * nu * nx + nx * nx * nx) + 2 * nx ** 3
     return N * per_knot
+
+
+def measured_traffic(kernel_prefix):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    for k, v in d["kernels"].items():
+        if k.startswith(kernel_prefix):
+            return v["hbm_bytes_per_launch"], d.get("source")
+    return None, None
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle = restatement)
@@ -167,7 +143,8 @@ def _cpu_solve(args):
     x, u = osqp.initial_problem(m, N, 0.1, seed)
     cost = osqp.QuadCost(np.eye(2 * n), 100 * np.eye(2 * n), 0.1 * np.eye(n), np.zeros(2 * n))
     r = osqp.sqp(m, cost, x, u, N, 0.1, "PCG-SS")
-    return r["exit_sqp"], r["sqp_iter"]
+    return dict(exit_sqp=int(r["exit_sqp"]), sqp_iter=int(r["sqp_iter"]), pcg_iters=list(r["pcg_iters"]),
+                x=r["x"], u=r["u"])
 
 
 def cpu_baseline(n, N, sample, procs, seed0):
@@ -180,8 +157,25 @@ def cpu_baseline(n, N, sample, procs, seed0):
     return sample / wall, wall, res
 
 
+def parity_check(gpu, cpu):
+    """GPU vs oracle on the same problems: exit code, SQP iterations and the per-QP PCG counts must be
+    identical (integer parity); trajectories are compared relative to their magnitude."""
+    mism, worst = [], 0.0
+    for i, c in enumerate(cpu):
+        ex, it = int(gpu["exit_sqp"][i]), int(gpu["sqp_iter"][i])
+        nq = it + (1 if ex == 3 else 0)
+        pcg = [int(v) for v in gpu["trace"]["pcg_iters"][i, 1:nq + 1]]
+        if ex != c["exit_sqp"] or it != c["sqp_iter"] or pcg != c["pcg_iters"]:
+            mism.append(i)
+        for a, b in ((gpu["x"][i], c["x"]), (gpu["u"][i], c["u"])):
+            worst = max(worst, float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b)))))
+    return {"checked": len(cpu), "mismatches": len(mism), "mismatched_problems": mism[:16],
+            "compared": "exit_sqp, sqp_iter, per-QP PCG iteration counts (exact); final x, u",
+            "max_traj_rel_diff": worst}
+
+
 # ------------------------------------------------------------------ KKT residual vs the reference (golden QP)
-def kkt_residual_check(ctx, model, n):
+def kkt_residual_check(ctx, n):
     """|r_build - r_ref| for the first QP of arm6 N=64 seed 0, r = ||[G+rho I, C^T; C, 0] dxul - [g; c]||_inf
     computed identically on both sides; the reference's r comes from tests/golden."""
     path = os.path.join(ROOT, "tests", "golden", "qp_arm6fix_N64.npz")
@@ -219,64 +213,55 @@ def ilqr_backward_flops_per_knot(nx, nu):
     return 2 * (2 * nx ** 3 + 2 * nx * nx * nu + nu * nu * nx + nx * nx * nu) + 2 * (nx + 1) * nu * nu
 
 
-def report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant, counters, exit_codes, iters):
-    """Bench line for the non-headline paths (iLQR = BASELINE config 3, SQP with method S)."""
-    if comm.world > 1 and int(os.environ.get("RANK", "0")) != 0:
-        comm.close()
-        return
-    nx, nu = 2 * n, n
-    value = B * a.steps * world * max(1, a.mpc_steps) / elapsed
-    roofline = None   # MPC mode: the work counters cover only the last horizon solve
-    if a.solver == "ilqr" and a.mpc_steps == 0:
-        bw = kernels.get("ilqr_backward")
-        if bw:
-            # algorithmic flops per backward launch: problem-iterations in the launch x (N-1) knots
-            per_launch = int(counters[0]) / max(1, bw["launches"])
-            flops = per_launch * (N - 1) * ilqr_backward_flops_per_knot(nx, nu)
-            ach = flops / (bw["avg_ms"] / 1e3) / 1e12
-            roofline = {"kernel": "k_ilqr_backward", "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
-                        "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
-                        "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
-    name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
-    if a.limits != "none":
-        name += f", soft box constraints {a.limits}"
-    if a.cost == "ee":
-        name += ", UrdfCost end-effector cost (twolinks.py goal)"
-    if a.mpc_steps > 0:
-        name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
-    out = {
-        "metric": f"MPC solves/sec (arm{n}.urdf, N={N}, {name})",
-        "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": 1000.0 * elapsed / a.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
-        "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} {a.solver.upper()} "
-                               f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU"
-                               + ("" if a.limits == "none" else f", limits {a.limits}")
-                               + (", UrdfCost" if a.cost == "ee" else ""),
-                   "global_batch": B * world, "N": N, "parallelism": f"shard{world}"},
-        "roofline": roofline, "cpu_baseline": None, "kernels": kernels, "dominant_kernel": dominant,
-        "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(exit_codes, return_counts=True))},
-        "iters_mean": float(np.mean(iters)), "iters_max": int(np.max(iters)),
-    }
-    print(json.dumps(out))
-    comm.close()
+def sqp_roofline(a, N, nx, nu, kernels, counters):
+    """Roofline of the dominant kernel k_qp (Schur + PCG + dxu fused, one workgroup per problem).
+    frac uses SURVEY §8(d)'s algorithmic flops (f_pcg per PCG iteration); the kernel keeps S and
+    P^-1 in registers, so it is bound by fp64 VALU issue, LDS bandwidth and barrier latency, not
+    by HBM: hbm_frac (PMC bytes) is reported beside it."""
+    qp = kernels["qp"]
+    per_launch_iters = int(counters[1]) / max(1, qp["launches"])
+    per_launch_qps = int(counters[0]) / max(1, qp["launches"])
+    avg_s = qp["avg_ms"] / 1000.0
+    flops = per_launch_iters * f_pcg_survey(N, nx)
+    ach = flops / avg_s / 1e12
+    impl = per_launch_iters * pcg_flops_impl(N, nx, a.method) + per_launch_qps * qp_schur_flops(N, nx, nu)
+    lds_bytes = per_launch_iters * pcg_lds_bytes_per_iter(N, nx, a.method)
+    traffic, src = measured_traffic(f"void tmpc::k_qp<{nx // 2}, ")
+    out = {"kernel": "k_qp (Schur + PCG + dxu, fused)", "bound": "fp64-valu", "achieved": ach,
+           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": traffic,
+           "avg_launch_ms": qp["avg_ms"], "pcg_iters_per_launch": per_launch_iters,
+           "flops_basis": "SURVEY 8(d) f_pcg = 2*3*nx^2*N*2 + 10*N*nx flop per PCG iteration "
+                          f"({f_pcg_survey(N, nx)} at N={N}, nx={nx}) x PCG iterations per launch",
+           "algorithmic_flops_per_launch": flops,
+           "impl_flops": {"per_launch": impl, "tflops": impl / avg_s / 1e12,
+                          "frac": impl / avg_s / 1e12 / FP64_PEAK_TFLOPS,
+                          "basis": "flops k_qp executes: SpMV over 3N-2 blocks, SS as 4N-2 block products, "
+                                   "plus the Schur prologue / dxu epilogue"},
+           "lds_model": {"achieved_GBps": lds_bytes / avg_s / 1e9, "peak_GBps": LDS_PEAK_GBS,
+                         "frac": lds_bytes / avg_s / 1e9 / LDS_PEAK_GBS, "lds_bytes_per_launch": lds_bytes},
+           "note": "bound label: the contract's enum has no fp64-VALU/LDS value; S and P^-1 stay in registers "
+                   "so HBM is not the binding resource (hbm_frac)"}
+    if traffic:
+        gbs = traffic / avg_s / 1e9
+        out.update(hbm_GBps=gbs, hbm_frac=gbs / HBM_PEAK_GBS, traffic_source=src)
+    sb = per_launch_iters * b_pcg_survey(N, nx)
+    out["streaming_model"] = {"bytes_per_launch": sb, "GBps": sb / avg_s / 1e9,
+                              "note": "SURVEY 8(d) b_pcg: bytes a design streaming S and P^-1 from HBM every "
+                                      "PCG iteration would move; this design never does"}
+    return out
 
 
 def main():
     a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    comm = Comm(world, local_rank, "nccl")
-
-    from trajoptmpcreference_amd import _native
+    from trajoptmpcreference_amd import _native, dist
     from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
 
+    rank, world, local_rank = dist.env_ranks()
     n, N, B, dt = a.links, a.N, a.batch, 0.1
     nx, nu = 2 * n, n
     model = parse_urdf(planar_arm_urdf(n))
     ctx = _native.Context(local_rank)
+    comm = dist.make_comm(ctx, rank, world)
     ctx.set_model(model)
     if a.cost == "ee":
         if n != 2:
@@ -288,10 +273,10 @@ def main():
     limits = LIMIT_PRESETS[a.limits]
     ctx.set_box_limits(limits)
 
-    # ---- workload resident in HBM
-    seed_base = shard_seed_base(a.seed0, rank, B)
+    # ---- workload: rank 0 draws every rank's start states, RCCL broadcast, own slice resident in HBM
+    q0 = dist.scatter_from_root(comm, rank, B, lambda count: initial_states(n, count, a.seed0), (n,))
     x0 = np.zeros((B, nx, N))
-    x0[:, :n, 0] = initial_states(n, B, seed_base)
+    x0[:, :n, 0] = q0
     u0 = np.zeros((B, nu, N - 1))
     xb, ub = x0.nbytes, u0.nbytes
     d_x0, d_u0, d_x, d_u = ctx.alloc(xb), ctx.alloc(ub), ctx.alloc(xb), ctx.alloc(ub)
@@ -356,73 +341,103 @@ def main():
     value = total_solves / elapsed
     ms_per_step = 1000.0 * elapsed / a.steps
 
-    # ---- status of one solve (exit codes / iteration counts) for the record
+    # ---- status of one solve (exit codes / iteration counts), gathered from every rank over RCCL
     ctx.d2d(d_x, d_x0, xb)
     ctx.d2d(d_u, d_u0, ub)
     if limits:
         ctx.set_soft_state(B, N)
     exit_codes, iters = solve(want_status=True)
+    g = dist.gather_summaries(comm, exit_codes=exit_codes.astype(np.int32), iters=iters.astype(np.int32))
+    exit_all, iters_all = g["exit_codes"], g["iters"]
+
+    # ---- PCIe-inclusive rate: the same batch through the host-array entry point (H2D + solve + D2H)
+    pcie = None
+    if a.solver == "sqp" and a.mpc_steps == 0 and not limits and a.cost == "quadratic":
+        xh = np.empty((B, nx, N))
+        ctx.d2h(xh, d_x0)
+        ctx.synchronize()
+        tp = time.perf_counter()
+        ctx.sqp_solve_batch(xh, u0, N, dt, a.method, with_trace=False)
+        tp = time.perf_counter() - tp
+        pcie = {"value": B / tp, "unit": "solves/s", "ms_per_solve_batch": 1000.0 * tp,
+                "note": "tmpc_sqp_solve_batch with host x/u (H2D, solve, D2H of x, u and the status arrays), "
+                        "one batch, this GPU; `value` above is the HBM-resident rate"}
+    comm.barrier()
 
     if rank != 0:
         comm.close()
         return
 
-    if a.solver == "ilqr" or a.method == "S" or a.mpc_steps > 0 or limits or a.cost != "quadratic":
-        return report_other(a, comm, ctx, model, n, N, B, world, elapsed, kernels, dominant, counters, exit_codes, iters)
-    qp = kernels["qp"]
-    n_pcg_iters = int(counters[1])
-    n_qps = int(counters[0])
-    per_launch_iters = n_pcg_iters / max(1, qp["launches"])
-    per_launch_qps = n_qps / max(1, qp["launches"])
-    alg_bytes = per_launch_iters * pcg_bytes_per_iter(N, nx)
-    alg_flops = per_launch_iters * pcg_flops_per_iter(N, nx, a.method) + per_launch_qps * qp_schur_flops(N, nx, nu)
-    qp_avg_s = qp["avg_ms"] / 1000.0 if qp["avg_ms"] > 0 else float("nan")
-    ach_gbs = alg_bytes / qp_avg_s / 1e9
-    ach_tf = alg_flops / qp_avg_s / 1e12
-    lds_bytes = per_launch_iters * pcg_lds_bytes_per_iter(N, nx, a.method)
-    ach_lds = lds_bytes / qp_avg_s / 1e9
-    traffic = measured_traffic(f"void tmpc::k_qp<{n}, ")
-    roofline = {"kernel": "k_qp (Schur + PCG + dxu, fused)", "bound": "mfma", "achieved": ach_tf,
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
-                "traffic_source": "profiles/pmc_traffic_latest.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                                  "passes, 2 x FETCH + WRITE bytes per k_qp launch (gfx950 correction)",
-                "algorithmic_flops_per_launch": alg_flops, "avg_launch_ms": qp["avg_ms"],
-                "note": "fp64 VALU peak (= fp64 matrix peak on MI355X); the PCG keeps S and P^-1 in "
-                        "registers, so the binding resource is LDS bandwidth + barrier latency (lds_model)",
-                "lds_model": {"achieved": ach_lds, "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": ach_lds / LDS_PEAK_GBS,
-                              "lds_bytes_per_launch": lds_bytes},
-                "streaming_model": {"bound": "hbm", "achieved": ach_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                    "frac": ach_gbs / HBM_PEAK_GBS,
-                                    "algorithmic_bytes_per_launch": alg_bytes}}
+    name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
+    headline = a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and not limits and \
+        a.cost == "quadratic"
+    if a.limits != "none":
+        name += f", soft box constraints {a.limits}"
+    if a.cost == "ee":
+        name += ", UrdfCost end-effector cost (twolinks.py goal)"
+    if a.mpc_steps > 0:
+        name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
+    out = {
+        "metric": ("MPC solves/sec (arm6.urdf, N=64, SQP-PCG) at 1/2/4/8 GPUs; KKT residual vs ref" if headline
+                   else f"MPC solves/sec (arm{n}.urdf, N={N}, {name})"),
+        "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
+        "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} {a.solver.upper()} "
+                               f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU"
+                               + ("" if a.limits == "none" else f", limits {a.limits}")
+                               + (", UrdfCost" if a.cost == "ee" else ""),
+                   "global_batch": B * world, "N": N, "method": a.method if a.solver == "sqp" else "iLQR",
+                   "parallelism": f"shard{world} (RCCL broadcast of start states, gather of results)"},
+    }
+    roofline = None
+    if a.solver == "sqp" and a.method.startswith("PCG") and a.mpc_steps == 0 and "qp" in kernels:
+        roofline = sqp_roofline(a, N, nx, nu, kernels, counters)
+    elif a.solver == "ilqr" and a.mpc_steps == 0 and "ilqr_backward" in kernels:
+        bw = kernels["ilqr_backward"]
+        per_launch = int(counters[0]) / max(1, bw["launches"])
+        flops = per_launch * (N - 1) * ilqr_backward_flops_per_knot(nx, nu)
+        ach = flops / (bw["avg_ms"] / 1e3) / 1e12
+        roofline = {"kernel": "k_ilqr_backward", "bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
+                    "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
+                    "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
+    out["roofline"] = roofline
 
-    cpu = None
-    if not a.no_cpu_baseline and world == 1:
+    cpu, par = None, None
+    if headline and not a.no_cpu_baseline and world == 1:
         procs = max(1, min(a.cpu_procs, os.cpu_count() or 1))
-        sample = a.cpu_sample if a.cpu_sample > 0 else 40 * procs
+        sample = min(B, a.cpu_sample if a.cpu_sample > 0 else 40 * procs)
         v, wall, res = cpu_baseline(n, N, sample, procs, a.seed0)
         cpu = {"value": v, "unit": "solves/s", "cores": procs, "kind": "port",
                "sample": f"{sample} problems of the same workload (seeds {a.seed0}..{a.seed0 + sample - 1}), "
                          f"oracle NumPy restatement (no SymPy), {procs} processes x 1 BLAS thread, {wall:.1f} s"}
-
-    kkt = kkt_residual_check(ctx, model, n)
-    out = {
-        "metric": "MPC solves/sec (arm6.urdf, N=64, SQP-PCG) at 1/2/4/8 GPUs; KKT residual vs ref",
-        "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
-        "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} SQP {a.method}, batch {B} per GPU",
-                   "global_batch": B * world, "N": N, "method": a.method, "parallelism": f"shard{world}"},
-        "roofline": roofline,
-        "cpu_baseline": cpu,
-        "kkt_residual": kkt,
-        "kernels": kernels, "dominant_kernel": dominant,
-        "work": {"problem_qps_per_step": int(counters[0]) / a.steps, "pcg_iters_per_step": n_pcg_iters / a.steps,
-                 "grad_evals_per_step": int(counters[2]) / a.steps, "ls_trials_per_qp": int(counters[3]) // max(1, a.steps)},
-        "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(exit_codes, return_counts=True))},
-        "sqp_iters_mean": float(np.mean(iters)),
-    }
+        # the GPU's own results for those problems (rank 0's first `sample` problems), with trace
+        gr = ctx.sqp_solve_batch(x0_host(ctx, d_x0, B, nx, N)[:sample], u0[:sample], N, dt, a.method)
+        par = parity_check(gr, res)
+    out["cpu_baseline"] = cpu
+    if headline:
+        out["parity"] = par
+        out["kkt_residual"] = kkt_residual_check(ctx, n)
+        out["pcie_inclusive"] = pcie
+        out["work"] = {"problem_qps_per_step": int(counters[0]) / a.steps,
+                       "pcg_iters_per_step": int(counters[1]) / a.steps,
+                       "grad_evals_per_step": int(counters[2]) / a.steps,
+                       "ls_trials_per_qp": int(counters[3]) // max(1, a.steps)}
+    out["kernels"] = kernels
+    out["dominant_kernel"] = dominant
+    out["exit_codes"] = {str(k): int(v) for k, v in zip(*np.unique(exit_all, return_counts=True))}
+    out["iters_mean"] = float(np.mean(iters_all))
+    out["iters_max"] = int(np.max(iters_all))
+    out["problems_gathered"] = int(exit_all.size)
     print(json.dumps(out))
     comm.close()
+
+
+def x0_host(ctx, d_x0, B, nx, N):
+    x = np.empty((B, nx, N))
+    ctx.d2h(x, d_x0)
+    return x
 
 
 if __name__ == "__main__":

@@ -36,18 +36,21 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 3
+#define TMPC_ABI_VERSION 4
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). N (dense KKT) is not offered on the GPU. */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
 #define TMPC_LINSYS_PCG_J 2  /* PCG, Jacobi preconditioner            PCG.py:168-169 */
 #define TMPC_LINSYS_PCG_BJ 3 /* PCG, block-Jacobi preconditioner      PCG.py:171-179 */
 #define TMPC_LINSYS_PCG_SS 4 /* PCG, symmetric-stair preconditioner   PCG.py:181-212 */
+#define TMPC_LINSYS_PCG_0 5  /* PCG, no preconditioner ('0', identity) PCG.py:114-118 (no SQPSolverMethods member;
+                                reachable through solveKKTSystem_Schur's options['preconditioner_type']) */
 
 /* preconditioner ids for tmpc_pcg_batch (PCG options['preconditioner_type']) */
 #define TMPC_PRECOND_J 1
 #define TMPC_PRECOND_BJ 2
 #define TMPC_PRECOND_SS 3
+#define TMPC_PRECOND_NONE 4  /* '0' */
 
 /* joint types of the model arrays */
 #define TMPC_JOINT_REVOLUTE 0  /* X(q) = X0 + cos(q) Xa + sin(q) Xb */
@@ -80,6 +83,12 @@ typedef struct tmpc_options {
   int32_t profile;                       /* 1: time kernels with HIP events (tmpc_kernel_stats) */
   int32_t max_iter_softConstraints;      /* 10     */
   double exit_tolerance_softConstraints; /* 1e-6   */
+  /* PCG warm start (options['guess'] -> PCG.update_guess, TrajoptMPCReference.py:439-440; the reference's
+   * SQP never forwards it, :512-519, so 0 is the reference behaviour): 1 = each QP's PCG starts from the
+   * previous QP's lambda of the same problem, and in tmpc_mpc_batch the first QP of an MPC step starts
+   * from the previous step's last lambda shifted by one knot (oracle/mpc.py). */
+  int32_t pcg_warm_start;                /* 0      */
+  int32_t reserved0;
 } tmpc_options;
 
 /* Box limits of TrajoptConstraint (set_joint_limits / set_velocity_limits / set_torque_limits,
@@ -216,12 +225,13 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
 
 /* One QP of the SQP loop for B problems: formKKTSystemBlocks + solveKKTSystem_Schur with PCG
  * (TrajoptMPCReference.py:200-271,415-455) at the given trajectories and regularisation rho[B].
+ * guess [B][N nx] (nullable) is the PCG initial iterate, options['guess'] of solveKKTSystem_Schur (:439-440).
  * dxul [B][n_xu(N-1)+nx + nx N] in the reference's interleaved order [x0,u0,x1,...,x_{N-1}; lambda].
  * S_diag [B][N][nx][nx], S_lo [B][N-1][nx][nx] (= S_{k+1,k}), gamma [B][N nx], P_diag [B][N][nx][nx]
  * are optional (nullable) copies of the intermediate blocks. */
 int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
-                  const double* u, double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma,
-                  double* P_diag);
+                  const double* u, const double* guess, double* dxul, int32_t* pcg_iters, double* S_diag,
+                  double* S_lo, double* gamma, double* P_diag);
 
 /* PCG(S, gamma, nx, N, options={'preconditioner_type': J|BJ|SS, exit_tolerance, max_iter}).solve()
  * (GBD-PCG-Python/PCG.py:66-111) on B block-tridiagonal systems given by their blocks:
@@ -250,6 +260,24 @@ int tmpc_reset_stats(tmpc_ctx* ctx);
 /* Work counters of the last SQP solve on this context: [0] problem-QPs solved, [1] total PCG
  * iterations, [2] QPs that recomputed the dynamics gradient, [3] line-search trials per QP. */
 int tmpc_solve_counters(tmpc_ctx* ctx, int64_t* counters);
+
+/* ---- multi-GPU: one process per GPU, RCCL over xGMI ----
+ * The reference has no distributed path (independent problems in a multiprocessing.Pool,
+ * examples/test_multiple.py:123-128).  Problems shard by contiguous batch slices with no exchange
+ * inside a solve; the communicator carries the initial states broadcast from rank 0 and the
+ * per-problem summaries gathered back.  Rank 0 calls tmpc_comm_get_unique_id and shares the id
+ * out of band (bench.py: a file next to the launcher's rendezvous) before every rank calls
+ * tmpc_comm_create.  Buffers are device memory; every call is synchronous on the ctx stream. */
+#define TMPC_COMM_ID_BYTES 128
+typedef struct tmpc_comm tmpc_comm;
+int tmpc_comm_get_unique_id(uint8_t* id /* [TMPC_COMM_ID_BYTES] */);
+int tmpc_comm_create(tmpc_ctx* ctx, int nranks, int rank, const uint8_t* id, tmpc_comm** out);
+void tmpc_comm_destroy(tmpc_comm* comm);
+int tmpc_comm_size(const tmpc_comm* comm, int* nranks, int* rank);
+int tmpc_comm_broadcast(tmpc_comm* comm, void* d_buf, size_t bytes, int root);      /* in place */
+int tmpc_comm_allgather(tmpc_comm* comm, const void* d_send, void* d_recv, size_t bytes_per_rank);
+int tmpc_comm_allreduce_max_f64(tmpc_comm* comm, double* d_buf, size_t count);     /* in place */
+int tmpc_comm_barrier(tmpc_comm* comm);
 
 #ifdef __cplusplus
 }

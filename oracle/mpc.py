@@ -40,8 +40,10 @@ def shift_soft(soft):
             arr[:, 1:] = init
 
 
-def mpc(model, cost, x, u, N, dt, method, steps, options=None, soft=None):
-    """method: "iLQR" or an SQP linear-system method ("S", "PCG-SS", ...)."""
+def mpc(model, cost, x, u, N, dt, method, steps, options=None, soft=None, pcg_warm_start=False):
+    """method: "iLQR" or an SQP linear-system method ("S", "PCG-SS", ...).
+    pcg_warm_start: every PCG starts from the previous QP's lambda; the first QP of a step from the
+    previous step's last lambda shifted by one knot (lambda_k <- lambda_{k+1}, last block kept)."""
     x = np.array(x, dtype=float)
     u = np.array(u, dtype=float)
     nx, nu = x.shape[0], u.shape[0]
@@ -50,12 +52,13 @@ def mpc(model, cost, x, u, N, dt, method, steps, options=None, soft=None):
     codes = np.zeros(steps, dtype=np.int64)
     iters = np.zeros(steps, dtype=np.int64)
     xe[:, 0] = x[:, 0]
+    warm = {"lam": None} if pcg_warm_start and method.startswith("PCG") else None
     for s in range(steps):
         if method == "iLQR":
             r = oilqr.ilqr(model, cost, x, u, N, dt, options, soft)
             codes[s], iters[s] = r["exit_code"], r["iter"]
         else:
-            r = osqp.sqp(model, cost, x, u, N, dt, method, options, soft)
+            r = osqp.sqp(model, cost, x, u, N, dt, method, options, soft, warm)
             codes[s], iters[s] = r["exit_sqp"], r["sqp_iter"]
         x, u = r["x"], r["u"]
         x_next = rbd.euler(model, x[:, 0][None], u[:, 0][None], dt)[0]
@@ -67,4 +70,7 @@ def mpc(model, cost, x, u, N, dt, method, steps, options=None, soft=None):
         if cost.QF_start is not None:
             cost.QF_start = max(cost.QF_start - 1, 0)
         shift_soft(soft)
+        if warm is not None and warm["lam"] is not None:
+            L = warm["lam"].reshape(N, nx)
+            warm["lam"] = np.concatenate([L[1:], L[-1:]]).reshape(-1)
     return dict(x_exec=xe, u_exec=ue, exit_codes=codes, iters=iters, x=x, u=u)

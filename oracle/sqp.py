@@ -136,6 +136,8 @@ def preconditioner(Sd, Sl, Su, ptype):
     N, b, _ = Sd.shape
     Pl = np.zeros((N - 1, b, b))
     Pu = np.zeros((N - 1, b, b))
+    if ptype == "0":   # identity (PCG.py:114-118)
+        return np.array([np.eye(b) for _ in range(N)]), Pl, Pu
     if ptype == "J":
         Pd = np.array([np.linalg.inv(np.diag(np.diag(Sd[k]))) for k in range(N)])
         return Pd, Pl, Pu
@@ -166,15 +168,15 @@ def block_tridiag_mv(Dg, Lo, Up, v):
     return out.reshape(-1)
 
 
-def pcg(Sd, Sl, Su, b, Pd, Pl, Pu, tol=1e-6, max_iter=100):
-    """PCG.pcg (PCG.py:66-111): x0 = 0, exit on |nu'| < tol.
+def pcg(Sd, Sl, Su, b, Pd, Pl, Pu, tol=1e-6, max_iter=100, guess=None):
+    """PCG.pcg (PCG.py:66-111): x0 = guess (default 0, :11-12), exit on |nu'| < tol.
     Returns (x, trace_nu (abs), trace_res, iterations)."""
     def A(v):
         return block_tridiag_mv(Sd, Sl, Su, v)
 
     def P(v):
         return block_tridiag_mv(Pd, Pl, Pu, v)
-    x = np.zeros_like(b)
+    x = np.zeros_like(b) if guess is None else np.array(guess, dtype=float).reshape(-1)
     r = b - A(x)
     rt = P(r)
     p = rt
@@ -209,8 +211,9 @@ def recover_dxu(Gh, g, A, B, lam, nx):
     return np.concatenate(out + [lam])
 
 
-def solve_qp(model, cost, x, u, xs, N, dt, rho, method, options, soft=None):
-    """One QP: returns (dxul, pcg_iters or None, extras)."""
+def solve_qp(model, cost, x, u, xs, N, dt, rho, method, options, soft=None, guess=None):
+    """One QP: returns (dxul, pcg_iters or None, extras).  guess: PCG initial iterate
+    (options['guess'] of solveKKTSystem_Schur, :439-440)."""
     nx = 2 * model.n
     G, g, A, B, c = kkt_blocks(model, cost, x, u, xs, N, dt, soft)
     Gh, Sd, Sl, gam = schur_blocks(G, g, A, B, c, rho, nx)
@@ -222,10 +225,11 @@ def solve_qp(model, cost, x, u, xs, N, dt, rho, method, options, soft=None):
     elif method.startswith("PCG-"):
         Pd, Pl, Pu = preconditioner(Sd, Sl, Su, method[4:])
         lam, _, _, iters = pcg(Sd, Sl, Su, gamma, Pd, Pl, Pu, options["exit_tolerance_linSys"],
-                               options["max_iter_linSys"])
+                               options["max_iter_linSys"], guess)
     else:
         raise ValueError(f"oracle supports S / PCG-J / PCG-BJ / PCG-SS, got {method}")
-    return recover_dxu(Gh, g, A, B, lam, nx), iters, dict(G=G, g=g, A=A, B=B, c=c, Sd=Sd, Sl=Sl, gamma=gamma)
+    return recover_dxu(Gh, g, A, B, lam, nx), iters, dict(G=G, g=g, A=A, B=B, c=c, Sd=Sd, Sl=Sl, gamma=gamma,
+                                                          lam=lam)
 
 
 # ------------------------------------------------------------------- merit pieces
@@ -252,10 +256,13 @@ def total_violation(model, x, u, xs, N, dt):
 
 
 # ------------------------------------------------------------------- SQP
-def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None):
+def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm=None):
     """TrajoptMPCReference.SQP (:510-760).  Returns a dict.  `soft` (oracle.soft.SoftConstraints)
     enables the soft-constraint terms and the outer loop; its mu/lambda/phi are updated in place
-    (the reference keeps them in the constraint object)."""
+    (the reference keeps them in the constraint object).
+    `warm` (build option pcg_warm_start, include/tmpc.h): a dict whose "lam" (None = zeros) is each
+    QP's PCG initial iterate and receives that QP's lambda -- the reference never forwards a guess
+    from SQP (:512-519), so warm=None is the reference behaviour."""
     o = default_options(options)
     nx, nu = 2 * model.n, model.n
     n = nx + nu
@@ -277,7 +284,10 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None):
         it = 0
         exit_sqp = 0
         while True:
-            dxul, iters, _ = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o, soft)
+            guess = None if warm is None else warm.get("lam")
+            dxul, iters, ex = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o, soft, guess)
+            if warm is not None and iters is not None:
+                warm["lam"] = ex["lam"].copy()
             dxul = dxul.reshape(-1, 1)
             dxuls.append(dxul[:, 0].copy())
             if iters is not None:

@@ -179,7 +179,7 @@ def gen_qp(name, N, seed=0, dt=0.1, rho=1e-3):
     l_direct = np.linalg.solve(S, gamma)
     rec["lam_direct"] = l_direct[:, 0]
     rec["dxul_direct"] = np.vstack((np.matmul(invG, g - np.matmul(C.T, l_direct)), l_direct))[:, 0]
-    for p in ["J", "BJ", "SS"]:
+    for p in ["J", "BJ", "SS", "0"]:
         opts = {"exit_tolerance": 1e-6, "max_iter": 100, "DEBUG_MODE": False, "RETURN_TRACE": False,
                 "preconditioner_type": p}
         pcg = PCG(S, gamma, nx, N, options=opts)
@@ -194,8 +194,24 @@ def gen_qp(name, N, seed=0, dt=0.1, rho=1e-3):
         # KKT residual computed the §8d way on the reference's own iterate
         KKT = np.block([[G, C.T], [C, np.zeros((C.shape[0], C.shape[0]))]])
         rec[f"kkt_res_{p}"] = np.max(np.abs(KKT @ rec[f"dxul_{p}"] - np.concatenate([g[:, 0], c[:, 0]])))
+    # options['guess'] -> PCG.update_guess (TrajoptMPCReference.py:439-440): a perturbed iterate as the
+    # initial x of the SS and BJ solves
+    rng = np.random.default_rng(4321)
+    guess = rec["lam_SS"] * (1.0 + 0.1 * rng.standard_normal(rec["lam_SS"].shape))
+    rec["guess"] = guess
+    for p in ["BJ", "SS"]:
+        opts = {"exit_tolerance": 1e-6, "max_iter": 100, "DEBUG_MODE": False, "RETURN_TRACE": False,
+                "preconditioner_type": p}
+        pcg = PCG(S, gamma, nx, N, options=opts)
+        pcg.update_guess(guess.copy())
+        lam, (tr_nu, tr_res) = pcg.solve()
+        rec[f"lam_{p}_guess"] = lam[:, 0]
+        rec[f"trace_nu_{p}_guess"] = np.array(tr_nu)
+        rec[f"iters_{p}_guess"] = len(tr_nu) - 1
+        rec[f"dxul_{p}_guess"] = np.vstack((np.matmul(invG, g - np.matmul(C.T, lam)), lam))[:, 0]
     np.savez_compressed(os.path.join(OUT, f"qp_{name}_N{N}.npz"), **rec)
-    print(f"[golden] qp {name} N={N}: iters J/BJ/SS = {rec['iters_J']}/{rec['iters_BJ']}/{rec['iters_SS']}", flush=True)
+    print(f"[golden] qp {name} N={N}: iters J/BJ/SS/0 = {rec['iters_J']}/{rec['iters_BJ']}/{rec['iters_SS']}/"
+          f"{rec['iters_0']}, guess BJ/SS = {rec['iters_BJ_guess']}/{rec['iters_SS_guess']}", flush=True)
 
 
 # ---------------------------------------------------------------- UrdfCost

@@ -37,7 +37,7 @@ def test_binding_matches_header():
     from trajoptmpcreference_amd import _native
     assert sorted(_native.SIGNATURES) == header_functions()
     lib = _native.load_library()
-    assert lib.tmpc_abi_version() == 3
+    assert lib.tmpc_abi_version() == 4
 
 
 def test_options_struct_layout_and_defaults():
@@ -55,7 +55,8 @@ def test_options_struct_layout_and_defaults():
     assert o.expected_reduction_min_SQP_DDP == 0.05 and o.expected_reduction_max_SQP_DDP == 3
     assert o.merit_mu == 10.0
     assert o.max_iter_softConstraints == 10 and o.exit_tolerance_softConstraints == 1e-6
-    assert ctypes.sizeof(o) == 12 * 8 + 4 * 4   # 12 doubles, 4 int32, no padding
+    assert o.pcg_warm_start == 0   # the reference never forwards a PCG guess from SQP (:512-519)
+    assert ctypes.sizeof(o) == 12 * 8 + 6 * 4   # 12 doubles, 6 int32, no padding
 
 
 def test_box_limits_struct_size():

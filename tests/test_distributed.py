@@ -1,6 +1,13 @@
-"""CPU, world_size 2 over gloo: the multi-GPU path of bench.py (one process per
-GPU, contiguous disjoint problem slices, barrier + max over ranks of the timed
-region, no data-path collective) run with the gloo backend."""
+"""CPU, world_size 2: the multi-GPU path of bench.py (trajoptmpcreference_amd/dist.py) --
+rank 0 draws every rank's start states and broadcasts them, each rank solves its
+contiguous slice, the per-problem summaries are gathered in rank order and the
+timed region is the max over ranks.
+
+On the GPUs the collectives are RCCL through libtmpc (dist.make_comm ->
+_native.Comm); here the same dist functions run over a gloo-backed stand-in
+with the same four methods, and the per-rank "solver" is the oracle (real SQP
+solves, oracle-sized) -- so the test checks the sharding logic end to end:
+sharded results equal the single-process results bitwise."""
 import multiprocessing as mp
 import os
 import socket
@@ -8,6 +15,7 @@ import socket
 import numpy as np
 
 import bench
+from trajoptmpcreference_amd import dist
 
 
 def _free_port():
@@ -16,47 +24,125 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, B, n, seed0, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
-    try:
-        comm = bench.Comm(world, rank, backend="gloo")
-        comm.barrier()
-        q0 = bench.initial_states(n, B, bench.shard_seed_base(seed0, rank, B))
+class GlooComm:
+    """Test-side stand-in for _native.Comm (broadcast / allgather / max / barrier) over gloo."""
+
+    def __init__(self, world, rank):
         import torch
-        parts = [torch.zeros(B, n, dtype=torch.float64) for _ in range(world)]
-        comm.tdist.all_gather(parts, torch.from_numpy(q0))   # test-side check only
-        elapsed = comm.max(0.25 + rank)                       # rank-dependent "time"
+        import torch.distributed as tdist
+        tdist.init_process_group(backend="gloo", world_size=world, rank=rank)
+        self.torch, self.tdist, self.world, self.rank = torch, tdist, world, rank
+
+    def barrier(self):
+        self.tdist.barrier()
+
+    def broadcast(self, arr, root=0):
+        t = self.torch.from_numpy(np.ascontiguousarray(arr).copy())
+        self.tdist.broadcast(t, src=root)
+        return t.numpy()
+
+    def allgather(self, arr):
+        t = self.torch.from_numpy(np.ascontiguousarray(arr))
+        parts = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.tdist.all_gather(parts, t)
+        return np.stack([p.numpy() for p in parts])
+
+    def max(self, v):
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+        self.tdist.all_reduce(t, op=self.tdist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        self.tdist.destroy_process_group()
+
+
+def _solve_slice(q0, n, N, dt):
+    """The per-rank solve: oracle SQP-PCG-SS on each problem of the slice."""
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    m = parse_urdf(planar_arm_urdf(n))
+    cost = osqp.QuadCost(np.eye(2 * n), 100 * np.eye(2 * n), 0.1 * np.eye(n), np.zeros(2 * n))
+    ex, it, xs = [], [], []
+    for q in q0:
+        x = np.zeros((2 * n, N))
+        x[:n, 0] = q
+        u = np.zeros((n, N - 1))
+        from oracle import rbd
+        for k in range(N - 1):
+            x[:, k + 1] = rbd.euler(m, x[:, k][None], u[:, k][None], dt)[0]
+        r = osqp.sqp(m, cost, x, u, N, dt, "PCG-SS")
+        ex.append(r["exit_sqp"])
+        it.append(r["sqp_iter"])
+        xs.append(r["x"])
+    return np.array(ex, dtype=np.int32), np.array(it, dtype=np.int32), np.array(xs)
+
+
+def _worker(rank, world, port, B, n, N, seed0, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), OMP_NUM_THREADS="1")
+    try:
+        comm = GlooComm(world, rank)
+        assert dist.env_ranks() == (rank, world, rank)
+        q0 = dist.scatter_from_root(comm, rank, B, lambda count: bench.initial_states(n, count, seed0), (n,))
+        comm.barrier()
+        ex, it, xs = _solve_slice(q0, n, N, 0.1)
+        g = dist.gather_summaries(comm, exit_codes=ex, iters=it, x=xs)
+        elapsed = comm.max(0.25 + rank)   # rank-dependent "time"
         comm.barrier()
         comm.close()
-        q.put((rank, np.concatenate([p.numpy() for p in parts]), elapsed))
+        q.put((rank, q0, g, elapsed))
     except Exception as e:  # surface the failure in the parent
-        q.put((rank, repr(e), None))
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
 
 
-def test_two_rank_sharding_and_max_time():
-    world, B, n, seed0 = 2, 5, 6, 11
+def test_two_rank_sharded_solves_equal_single_process():
+    world, B, n, N, seed0 = 2, 2, 2, 8, 11
     ctx = mp.get_context("fork")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, B, n, seed0, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, n, N, seed0, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=120) for _ in range(world)]
+    out = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
-    ref = bench.initial_states(n, world * B, seed0)
-    for rank, gathered, elapsed in out:
-        assert not isinstance(gathered, str), gathered
-        # the ranks' slices tile the single-process workload exactly, in rank order
-        assert np.array_equal(gathered, ref)
+    q_all = bench.initial_states(n, world * B, seed0)
+    ex_ref, it_ref, x_ref = _solve_slice(q_all, n, N, 0.1)
+    for rank, q0, g, elapsed in out:
+        assert not isinstance(q0, str), q0
+        lo, hi = dist.shard_range(rank, B)
+        # the broadcast start states are the single-process workload's slice for this rank
+        assert np.array_equal(q0, q_all[lo:hi])
+        # gathered results, in rank order, equal the single-process solves bitwise
+        assert np.array_equal(g["exit_codes"], ex_ref)
+        assert np.array_equal(g["iters"], it_ref)
+        assert np.array_equal(g["x"], x_ref)
         # every rank sees the slowest rank's time
         assert elapsed == 1.25
 
 
 def test_single_rank_comm_is_a_no_op():
-    c = bench.Comm(1, 0)
+    c = dist.LocalComm()
     c.barrier()
     assert c.max(3.5) == 3.5
+    a = np.arange(6.0).reshape(3, 2)
+    assert np.array_equal(c.broadcast(a), a)
+    assert c.allgather(a).shape == (1, 3, 2)
+    g = dist.gather_summaries(c, e=np.array([1, 2], dtype=np.int32))
+    assert np.array_equal(g["e"], [1, 2])
+    q0 = dist.scatter_from_root(c, 0, 4, lambda count: bench.initial_states(3, count, 5), (3,))
+    assert np.array_equal(q0, bench.initial_states(3, 4, 5))
+    assert dist.shard_range(3, 100) == (300, 400)
     c.close()
-    assert bench.shard_seed_base(7, 3, 100) == 307
+
+
+def test_unique_id_file_exchange(tmp_path, monkeypatch):
+    """Rank 0 publishes the RCCL id atomically; another rank reads exactly those bytes (the
+    id itself comes from libtmpc on the GPU box: faked here)."""
+    path = tmp_path / "uid"
+    monkeypatch.setenv("TMPC_COMM_ID_FILE", str(path))
+    fake = bytes(range(128))
+    monkeypatch.setattr(dist._native, "comm_unique_id", lambda: fake)
+    assert dist.exchange_unique_id(0) == fake
+    assert dist.exchange_unique_id(1, timeout_s=5) == fake

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--stamps", action="store_true", help="library built with -DTMPC_PCG_STAMPS")
     a = ap.parse_args()
     from trajoptmpcreference_amd import _native
-    lib = a.lib or _native.LIB_PATH
+    lib = os.path.abspath(a.lib) if a.lib else _native.LIB_PATH
     _native.load_library(lib)
     ctx = _native.Context(0)
     ctx.set_options(profile=1)

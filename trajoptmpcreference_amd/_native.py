@@ -13,9 +13,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TMPC_LIBRARY") or os.path.join(_HERE, "libtmpc.so")
 
-LINSYS = {"S": 1, "PCG-J": 2, "PCG-BJ": 3, "PCG-SS": 4}
+LINSYS = {"S": 1, "PCG-J": 2, "PCG-BJ": 3, "PCG-SS": 4, "PCG-0": 5}
 SOLVER_ILQR = 16
-PRECOND = {"J": 1, "BJ": 2, "SS": 3}
+PRECOND = {"J": 1, "BJ": 2, "SS": 3, "0": 4}
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -39,6 +39,8 @@ class tmpc_options(C.Structure):
         ("profile", C.c_int32),
         ("max_iter_softConstraints", C.c_int32),
         ("exit_tolerance_softConstraints", C.c_double),
+        ("pcg_warm_start", C.c_int32),
+        ("reserved0", C.c_int32),
     ]
 
 
@@ -92,8 +94,8 @@ SIGNATURES = {
     "tmpc_rollout_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p]),
     "tmpc_fd_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
     "tmpc_fd_grad_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
-    "tmpc_qp_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _dp, _dp, _ip, _dp, _dp,
-                                _dp, _dp]),
+    "tmpc_qp_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _dp, _dp, _dp, _ip, _dp,
+                                _dp, _dp, _dp]),
     "tmpc_pcg_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, C.c_double,
                                  C.c_int, _dp, _ip, _dp, _dp, _dp]),
     "tmpc_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
@@ -105,7 +107,16 @@ SIGNATURES = {
     "tmpc_kernel_stats": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "tmpc_reset_stats": (C.c_int, [C.c_void_p]),
     "tmpc_solve_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+    "tmpc_comm_get_unique_id": (C.c_int, [C.c_void_p]),
+    "tmpc_comm_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
+    "tmpc_comm_destroy": (None, [C.c_void_p]),
+    "tmpc_comm_size": (C.c_int, [C.c_void_p, _ip, _ip]),
+    "tmpc_comm_broadcast": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]),
+    "tmpc_comm_allgather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    "tmpc_comm_allreduce_max_f64": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    "tmpc_comm_barrier": (C.c_int, [C.c_void_p]),
 }
+COMM_ID_BYTES = 128
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -183,6 +194,17 @@ class Context:
         except Exception:
             pass
 
+    def _check_traj(self, x, u, N):
+        """x [B][nx][N], u [B][nu][N-1] with nx / nu of the loaded model: the library copies
+        B*nx*N and B*nu*(N-1) doubles in and out of these buffers."""
+        if self.model is None:
+            raise NativeError("no model: call set_model first")
+        n = self.model.n
+        if x.ndim != 3 or u.ndim != 3 or x.shape[0] != u.shape[0] or x.shape[1:] != (2 * n, N) \
+                or u.shape[1:] != (n, N - 1):
+            raise ValueError(f"expected x [B][{2 * n}][{N}] and u [B][{n}][{N - 1}] for a {n}-joint model, "
+                             f"got {x.shape} and {u.shape}")
+
     def _check(self, rc, what):
         if rc != 0:
             msg = self.lib.tmpc_last_error(self.h)
@@ -252,6 +274,10 @@ class Context:
     def set_soft_state(self, B, N, mu=None, lam=None, phi=None):
         """[B][N][6n] arrays (None: defaults)."""
         arrs = [None if a is None else _c64(a) for a in (mu, lam, phi)]
+        shape = (int(B), int(N), 6 * self.model.n)
+        for a in arrs:
+            if a is not None and a.shape != shape:
+                raise ValueError(f"soft-constraint state must be {shape}, got {a.shape}")
         self._check(self.lib.tmpc_set_soft_state(self.h, int(B), int(N), *[_ptr(a) for a in arrs]),
                     "tmpc_set_soft_state")
 
@@ -277,6 +303,7 @@ class Context:
         """x [B][nx][N], u [B][nu][N-1] -> dict of results (arrays per problem)."""
         x = _c64(x).copy()
         u = _c64(u).copy()
+        self._check_traj(x, u, N)
         B = x.shape[0]
         out = {k: np.zeros(B, dtype=np.int32) for k in ("exit_sqp", "exit_soft", "outer_iter", "sqp_iter")}
         arrays, tr = self._trace_arrays(B) if with_trace else ({}, None)
@@ -291,6 +318,7 @@ class Context:
         """Batched iLQR (oracle/ilqr.py): x [B][nx][N] (only x[:, :, 0] is read), u [B][nu][N-1]."""
         x = _c64(x).copy()
         u = _c64(u).copy()
+        self._check_traj(x, u, N)
         B = x.shape[0]
         out = {k: np.zeros(B, dtype=np.int32) for k in ("exit_code", "exit_soft", "outer_iter", "iter")}
         arrays, tr = self._trace_arrays(B) if with_trace else ({}, None)
@@ -305,6 +333,7 @@ class Context:
         """Receding-horizon loop (oracle/mpc.py); solver = "iLQR" or an SQP method name."""
         x = _c64(x).copy()
         u = _c64(u).copy()
+        self._check_traj(x, u, N)
         B, nx, _ = x.shape
         nu = u.shape[1]
         xe = np.zeros((B, nx, steps + 1))
@@ -350,10 +379,14 @@ class Context:
                     "tmpc_fd_grad_batch")
         return A, Bm, dq
 
-    def qp_batch(self, x, u, N, dt, rho, method="PCG-SS", want_blocks=True):
+    def qp_batch(self, x, u, N, dt, rho, method="PCG-SS", want_blocks=True, guess=None):
+        """guess [B][N nx]: the PCG initial iterate (solveKKTSystem_Schur's options['guess'])."""
         x, u = _c64(x), _c64(u)
+        self._check_traj(x, u, N)
         B, nx, _ = x.shape
         nu = u.shape[1]
+        if guess is not None:
+            guess = _c64(guess).reshape(B, N * nx)
         rho = _c64(np.broadcast_to(np.asarray(rho, dtype=np.float64), (B,)))
         L = (nx + nu) * (N - 1) + nx + nx * N
         dxul = np.zeros((B, L))
@@ -363,7 +396,7 @@ class Context:
         g = np.zeros((B, N * nx)) if want_blocks else None
         Pd = np.zeros((B, N, nx, nx)) if want_blocks else None
         self._check(self.lib.tmpc_qp_batch(self.h, B, int(N), float(dt), LINSYS[method], _ptr(rho), _ptr(x), _ptr(u),
-                                           _ptr(dxul), _ptr(iters), _ptr(Sd), _ptr(Sl), _ptr(g), _ptr(Pd)),
+                                           _ptr(guess), _ptr(dxul), _ptr(iters), _ptr(Sd), _ptr(Sl), _ptr(g), _ptr(Pd)),
                     "tmpc_qp_batch")
         return dict(dxul=dxul, pcg_iters=iters, S_diag=Sd, S_lo=Sl, gamma=g, P_diag=Pd)
 
@@ -430,6 +463,83 @@ class Context:
 
     def reset_stats(self):
         self._check(self.lib.tmpc_reset_stats(self.h), "tmpc_reset_stats")
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (rank 0, before the id is shared with the other ranks)."""
+    lib = load_library()
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    if lib.tmpc_comm_get_unique_id(buf) != 0:
+        raise NativeError("tmpc_comm_get_unique_id failed (RCCL)")
+    return bytes(buf)
+
+
+class Comm:
+    """RCCL communicator over the GPUs of a node (tmpc_comm_*, include/tmpc.h): one rank per
+    process / GPU.  Host-array helpers stage through device memory of the context."""
+
+    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"RCCL unique id must be {COMM_ID_BYTES} bytes")
+        self.ctx, self.lib = ctx, ctx.lib
+        self.world, self.rank = int(nranks), int(rank)
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        ctx._check(self.lib.tmpc_comm_create(ctx.h, self.world, self.rank, buf, C.byref(h)), "tmpc_comm_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tmpc_comm_destroy(self.h)
+            self.h = None
+
+    def barrier(self):
+        self.ctx._check(self.lib.tmpc_comm_barrier(self.h), "tmpc_comm_barrier")
+
+    def broadcast_device(self, d_ptr, nbytes, root=0):
+        self.ctx._check(self.lib.tmpc_comm_broadcast(self.h, d_ptr, int(nbytes), int(root)), "tmpc_comm_broadcast")
+
+    def allgather_device(self, d_send, d_recv, nbytes_per_rank):
+        self.ctx._check(self.lib.tmpc_comm_allgather(self.h, d_send, d_recv, int(nbytes_per_rank)),
+                        "tmpc_comm_allgather")
+
+    def broadcast(self, arr, root=0):
+        """Host array (same shape / dtype on every rank) broadcast from root, returned."""
+        arr = np.ascontiguousarray(arr)
+        d = self.ctx.alloc(max(8, arr.nbytes))
+        try:
+            self.ctx.h2d(d, arr)
+            self.broadcast_device(d, arr.nbytes, root)
+            out = np.empty_like(arr)
+            self.ctx.d2h(out, d)
+        finally:
+            self.ctx.free(d)
+        return out
+
+    def allgather(self, arr):
+        """Host array per rank -> [world, *arr.shape] on every rank (rank order)."""
+        arr = np.ascontiguousarray(arr)
+        ds, dr = self.ctx.alloc(max(8, arr.nbytes)), self.ctx.alloc(max(8, arr.nbytes * self.world))
+        try:
+            self.ctx.h2d(ds, arr)
+            self.allgather_device(ds, dr, arr.nbytes)
+            out = np.empty((self.world,) + arr.shape, dtype=arr.dtype)
+            self.ctx.d2h(out, dr)
+        finally:
+            self.ctx.free(ds)
+            self.ctx.free(dr)
+        return out
+
+    def max(self, v: float) -> float:
+        a = np.array([float(v)])
+        d = self.ctx.alloc(8)
+        try:
+            self.ctx.h2d(d, a)
+            self.ctx._check(self.lib.tmpc_comm_allreduce_max_f64(self.h, d, 1), "tmpc_comm_allreduce_max_f64")
+            self.ctx.d2h(a, d)
+        finally:
+            self.ctx.free(d)
+        return float(a[0])
 
 
 _default_ctx = {}

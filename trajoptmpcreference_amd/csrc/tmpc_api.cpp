@@ -73,6 +73,20 @@ static int fail(tmpc_ctx* c, const char* fmt, ...) {
   return -1;
 }
 
+namespace tmpc {
+int ctx_fail(tmpc_ctx* ctx, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return -1;
+}
+int ctx_device(const tmpc_ctx* ctx) { return ctx->device; }
+hipStream_t ctx_stream(const tmpc_ctx* ctx) { return ctx->stream; }
+}  // namespace tmpc
+
 #define HIP_OK(call)                                                                        \
   do {                                                                                      \
     hipError_t e_ = (call);                                                                 \
@@ -188,6 +202,7 @@ static int precond_of(int linsys) {
     case TMPC_LINSYS_PCG_J: return PRECOND_J;
     case TMPC_LINSYS_PCG_BJ: return PRECOND_BJ;
     case TMPC_LINSYS_PCG_SS: return PRECOND_SS;
+    case TMPC_LINSYS_PCG_0: return PRECOND_NONE;
     default: return -1;
   }
 }
@@ -213,6 +228,8 @@ struct Work {
   int* iters;
   double *U, *Y;   // method S scratch (k_btsolve)
   double *Gk, *jsoft, *smu, *slam;   // soft limits: per-knot Ghat, jacobian, AL constants
+  const double* guess;               // PCG initial iterate [B][N nx] (nullable)
+  double* lam_keep;                  // where the PCG path stores lambda (nullable; warm start)
 };
 
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
@@ -248,7 +265,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
       Timed t(ctx, "schur");
       LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, G,
                           w.A, w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, nullptr, w.Sd, w.Sl, w.gam, nullptr,
-                          w.jsoft));
+                          w.jsoft, nullptr));
     }
     {
       Timed t(ctx, "btsolve");
@@ -258,7 +275,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
       Timed t(ctx, "dxu");
       LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, G, w.A,
                           w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, w.lam, nullptr, nullptr, nullptr, nullptr,
-                          w.jsoft));
+                          w.jsoft, nullptr));
     }
     return 0;
   }
@@ -266,9 +283,9 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     Timed t(ctx, "qp");
     LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, precond, QP_MODE_PCG, d_x, d_u, st.active, G, w.A,
                         w.Bm, w.cvec, ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx,
-                        w.du, keep_blocks ? w.lam : nullptr, keep_blocks ? w.Sd : nullptr,
+                        w.du, keep_blocks ? w.lam : w.lam_keep, keep_blocks ? w.Sd : nullptr,
                         keep_blocks ? w.Sl : nullptr, keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr,
-                        w.jsoft));
+                        w.jsoft, w.guess));
   }
   return 0;
 }
@@ -286,7 +303,7 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   BUF(double, du, (size_t)B * K * nj);
   BUF(int, iters, (size_t)B);
   w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters,
-           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (with_blocks) {
     BUF(double, Sdiag, (size_t)B * N * nx * nx);
     BUF(double, Slo, (size_t)B * (K > 0 ? K : 1) * nx * nx);
@@ -348,8 +365,9 @@ static int alloc_soft(tmpc_ctx* ctx, int B, int N, double** mu, double** lam, do
   return 0;
 }
 
+// keep_warm: the PCG warm-start buffer already holds this batch's starting lambdas (MPC loop)
 static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
-                      TraceDev* tr_out) {
+                      TraceDev* tr_out, bool keep_warm = false) {
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
   const int precond = precond_of(linsys);
@@ -394,6 +412,14 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     w.jsoft = soft_j;
     w.smu = smu;
     w.slam = slam;
+  }
+  if (o.pcg_warm_start && precond != 0) {
+    // PCG warm start: each QP starts from the problem's previous lambda (in place: a workgroup reads
+    // its guess before it writes its lambda)
+    BUF(double, lam_warm, (size_t)B * N * nx);
+    if (!keep_warm) HIP_OK(hipMemsetAsync(lam_warm, 0, (size_t)B * N * nx * sizeof(double), ctx->stream));
+    w.guess = lam_warm;
+    w.lam_keep = lam_warm;
   }
   HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
   HIP_OK(hipMemsetAsync(prob_counters, 0, (size_t)B * 3 * sizeof(unsigned long long), ctx->stream));
@@ -655,6 +681,7 @@ int tmpc_set_model(tmpc_ctx* ctx, int n, const int32_t* parent, const int32_t* j
   // TMPC_GENERIC_MODEL=1 forces the runtime-coefficient kernels
   const char* gen = getenv("TMPC_GENERIC_MODEL");
   ctx->model_id = (gen && gen[0] == '1') ? 0 : match_static_model(m);
+  ctx->soft_B = ctx->soft_N = -1;   // the soft-constraint state is sized per model (6 n slots per knot)
   hipSetDevice(ctx->device);
   HIP_OK(hipMemcpyAsync(ctx->dmodel, &m, sizeof(m), hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -923,8 +950,18 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
   HIP_OK(hipMemcpy2DAsync(d_xe, (size_t)(steps + 1) * sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double),
                           (size_t)B * nx, hipMemcpyDeviceToDevice, ctx->stream));
   for (int s = 0; s < steps; ++s) {
-    rc = ilqr ? ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr) : sqp_device(ctx, B, N, dt, solver, d_x, d_u, nullptr);
+    rc = ilqr ? ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr)
+              : sqp_device(ctx, B, N, dt, solver, d_x, d_u, nullptr, /*keep_warm=*/s > 0);
     if (rc) return rc;
+    if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0) {
+      // the next step's first PCG starts from this step's last lambda shifted by one knot
+      // (lambda_k <- lambda_{k+1}, last block kept), as x and u are shifted (oracle/mpc.py)
+      double* lw = (double*)ctx->bufs["lam_warm"].ptr;
+      BUF(double, lam_tmp, (size_t)B * N * nx);
+      const size_t row = (size_t)N * nx * sizeof(double), blk = (size_t)nx * sizeof(double);
+      HIP_OK(hipMemcpyAsync(lam_tmp, lw, (size_t)B * row, hipMemcpyDeviceToDevice, ctx->stream));
+      HIP_OK(hipMemcpy2DAsync(lw, row, (char*)lam_tmp + blk, row, row - blk, B, hipMemcpyDeviceToDevice, ctx->stream));
+    }
     HIP_OK(hipMemcpy2DAsync(d_codes + s, (size_t)steps * sizeof(int), ctx->bufs["st_exit"].ptr, sizeof(int),
                             sizeof(int), B, hipMemcpyDeviceToDevice, ctx->stream));
     HIP_OK(hipMemcpy2DAsync(d_iters + s, (size_t)steps * sizeof(int), ctx->bufs["st_iter"].ptr, sizeof(int),
@@ -1043,8 +1080,8 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
 }
 
 int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
-                  const double* u, double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma,
-                  double* P_diag) {
+                  const double* u, const double* guess, double* dxul, int32_t* pcg_iters, double* S_diag,
+                  double* S_lo, double* gamma, double* P_diag) {
   if (!ctx) return -1;
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
@@ -1067,6 +1104,11 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
                                                    st.need_grad, st.exit_sqp}, nullptr);
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), io_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
+  if (guess && precond != 0) {
+    BUF(double, io_guess, (size_t)B * N * nx);
+    HIP_OK(hipMemcpyAsync(io_guess, guess, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
+    w.guess = io_guess;
+  }
   if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, true))) return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
   resolve_timings(ctx);
@@ -1102,8 +1144,8 @@ int tmpc_pcg_batch(tmpc_ctx* ctx, int B, int N, int nx, int precond, const doubl
   if (!ctx) return -1;
   if (B < 1 || N < 1 || nx < 1) return fail(ctx, "bad sizes B=%d N=%d nx=%d", B, N, nx);
   if (N * nx > 1024) return fail(ctx, "N * nx = %d exceeds 1024 rows", N * nx);
-  if (precond != PRECOND_J && precond != PRECOND_BJ && precond != PRECOND_SS)
-    return fail(ctx, "preconditioner %d: valid are J=1, BJ=2, SS=3 (PCG.py:52-55)", precond);
+  if (precond != PRECOND_J && precond != PRECOND_BJ && precond != PRECOND_SS && precond != PRECOND_NONE)
+    return fail(ctx, "preconditioner %d: valid are J=1, BJ=2, SS=3, 0=4 (PCG.py:52-55)", precond);
   if (max_iter < 0) return fail(ctx, "max_iter must be >= 0");
   if (!S_diag || !gamma || (N > 1 && !S_lo)) return fail(ctx, "null input");
   hipSetDevice(ctx->device);

@@ -7,9 +7,17 @@
 #include "tmpc_device.h"
 #include "tmpc_models.h"
 
+struct tmpc_ctx;
+
 namespace tmpc {
 
-enum { PRECOND_J = 1, PRECOND_BJ = 2, PRECOND_SS = 3 };
+// context accessors for the other translation units (tmpc_comm.cpp)
+int ctx_fail(tmpc_ctx* ctx, const char* fmt, ...);
+int ctx_device(const tmpc_ctx* ctx);
+hipStream_t ctx_stream(const tmpc_ctx* ctx);
+
+// PRECOND_NONE: the identity preconditioner '0' (PCG.py:114-118)
+enum { PRECOND_J = 1, PRECOND_BJ = 2, PRECOND_SS = 3, PRECOND_NONE = 4 };
 enum { LS_MODE_INIT = 0, LS_MODE_STEP = 1 };
 enum { QP_MODE_PCG = 0, QP_MODE_SCHUR = 1, QP_MODE_DXU = 2 };
 
@@ -80,7 +88,7 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-              double* Pd, const double* jsoft);
+              double* Pd, const double* jsoft, const double* guess);
 int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
                      const int* active, const double* x, const double* u, const double* mu, const double* lam,
                      double* Gk, double* jsoft);

@@ -348,16 +348,6 @@ __device__ __forceinline__ double wave_sum(double v) {
   return readlane_f64(v, 63);
 }
 
-// Workgroup sum, uniform in every lane.  `red` is one of two 16-slot halves
-// used alternately by consecutive calls (slots of absent waves hold 0).
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  return readlane_f64(dpp_row_sum(red[lane & 15]), 0);
-}
-
 // Lane geometry of the one-workgroup-per-problem kernels: RPL rows of S per
 // lane, L = NX / RPL lanes per block row; lane t owns rows i + m L (m < RPL)
 // of block k = t / L.  Two rows per lane halve the LDS traffic of every
@@ -387,9 +377,12 @@ struct PcgRow {
 };
 
 // LDS vectors are [pad NX | N*NX rows | pad NX]: the pads stay zero so the
-// block-tridiagonal products need no edge branches.
+// block-tridiagonal products need no edge branches.  r is double-buffered
+// (rbuf[it & 1]): in the same phase every lane reads the old r of its block
+// while the owners write the new one.
+constexpr int PCG_NVEC = 7;
 struct PcgLds {
-  double *pbuf, *rbuf, *wbuf, *tbuf, *xbuf, *red, *piv;
+  double *pbuf, *rbuf[2], *abuf, *wbuf, *tbuf, *xbuf, *red, *piv;
 };
 
 // Fixed stride (the 1024-row maximum plus the pads) so that every buffer is a
@@ -397,19 +390,21 @@ struct PcgLds {
 // vector traffic instead of one per buffer.
 __host__ __device__ constexpr size_t pcg_vec_doubles(int /*N*/, int NX) { return (size_t)1024 + 2 * NX; }
 __host__ __device__ inline size_t pcg_lds_doubles(int N, int NX) {
-  return 5 * pcg_vec_doubles(N, NX) + 32 + (size_t)2 * N * NX;
+  return PCG_NVEC * pcg_vec_doubles(N, NX) + 48 + (size_t)2 * N * NX;
 }
 
 __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
   const size_t v = pcg_vec_doubles(N, NX);
   PcgLds L;
   L.pbuf = lds + NX;
-  L.rbuf = L.pbuf + v;
-  L.wbuf = L.rbuf + v;
+  L.rbuf[0] = L.pbuf + v;
+  L.rbuf[1] = L.rbuf[0] + v;
+  L.abuf = L.rbuf[1] + v;
+  L.wbuf = L.abuf + v;
   L.tbuf = L.wbuf + v;
   L.xbuf = L.tbuf + v;
-  L.red = lds + 5 * v;     // 2 x 16
-  L.piv = L.red + 32;      // 2 x N x NX
+  L.red = lds + PCG_NVEC * v;   // 3 x 16 reduction slots
+  L.piv = L.red + 48;           // 2 x N x NX
   return L;
 }
 
@@ -417,12 +412,12 @@ __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
 __device__ __forceinline__ void pcg_lds_clear(double* lds, int N, int NX) {
   const size_t v = pcg_vec_doubles(N, NX);
   const int rows = N * NX;
-  for (int e = threadIdx.x; e < 5 * 2 * NX + 32; e += blockDim.x) {
-    if (e < 10 * NX) {
+  for (int e = threadIdx.x; e < PCG_NVEC * 2 * NX + 48; e += blockDim.x) {
+    if (e < PCG_NVEC * 2 * NX) {
       const int buf = e / (2 * NX), o = e - buf * 2 * NX;
       lds[buf * v + (o < NX ? o : rows + o)] = 0.0;
     } else {
-      lds[5 * v + (e - 10 * NX)] = 0.0;
+      lds[PCG_NVEC * v + (e - PCG_NVEC * 2 * NX)] = 0.0;
     }
   }
 }
@@ -436,6 +431,15 @@ __device__ __forceinline__ void pcg_lds_clear(double* lds, int N, int NX) {
 template <int NX, int RPL>
 __device__ __forceinline__ void pcg_precondition(PcgRow<NX> (&R)[RPL], int precond, const PcgLane<NX, RPL>& ln,
                                                  int N, double* piv, double* Pd_block) {
+  if (precond == PRECOND_NONE) {   // '0': P^-1 = I
+    if (Pd_block && ln.valid) {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m)
+#pragma unroll
+        for (int j = 0; j < NX; ++j) Pd_block[ln.r(m) * NX + j] = (j == ln.r(m)) ? 1.0 : 0.0;
+    }
+    return;
+  }
   if (precond == PRECOND_J) {
 #pragma unroll
     for (int m = 0; m < RPL; ++m) {
@@ -557,7 +561,59 @@ __device__ __forceinline__ void pcg_block_dot(const PcgRow<NX> (&R)[RPL], const 
   } while (0)
 #endif
 
-// The CG iteration (PCG.pcg, PCG.py:66-111).  x = the lane's entries of the solution.
+// Workgroup sums in two halves: red_put stores the wave's total in slot w of a
+// 16-slot area (slots of absent waves hold 0); after the next barrier
+// red_total reads all slots and reduces them by DPP.  A fixed tree: the result
+// is deterministic and independent of the problem's batch neighbours.  Split
+// this way, a reduction rides on a barrier the iteration needs anyway.
+__device__ __forceinline__ void red_put(double v, double* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+}
+__device__ __forceinline__ double red_total(const double* red) {
+  return readlane_f64(dpp_row_sum(red[threadIdx.x & 15]), 0);
+}
+
+// t = r - (S_{k,k-1} w_{k-1} + S_{k,k+1} w_{k+1}) for this lane's rows
+template <int NX, int RPL>
+__device__ __forceinline__ void pcg_off(const PcgRow<NX> (&R)[RPL], const double* __restrict__ w, int kb,
+                                        const double (&r)[RPL], double (&t)[RPL]) {
+  const double* wm = w + kb - NX;
+  constexpr int NC = RPL == 1 ? 2 : 1;
+  double a[NC][RPL];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) a[c][m] = 0.0;
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    const double wl = wm[j], wu = wm[2 * NX + j];
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) {
+      a[0][m] += R[m].sl[j] * wl;
+      a[NC - 1][m] += R[m].su[j] * wu;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < RPL; ++m) t[m] = r[m] - (NC == 2 ? a[0][m] + a[NC - 1][m] : a[0][m]);
+}
+
+// The CG iteration (PCG.pcg, PCG.py:66-111), arranged around as few workgroup
+// barriers as its data dependences allow -- SS 4 per iteration, BJ / J / 0 3:
+//   B1  p visible       Ap = S p (own rows) to LDS, partial p.Ap
+//   B2  p.Ap, Ap        alpha; every lane rebuilds r_k - Ap_k alpha for its whole
+//                       block k from the LDS copies of r and Ap (the owners' update,
+//                       operand for operand), x += p alpha, new r to the other r buffer;
+//                       SS: w = P_kk r_k to LDS; BJ: z = P_kk r_k; J / 0: z = r / S_ii, r;
+//                       BJ / J / 0: partial nu' = r.z
+//   B3  SS: w           t = r - S_{k,k-1} w_{k-1} - S_{k,k+1} w_{k+1} to LDS,
+//                       partial nu' = w.t  (= r^T P_kk t = r.z, P_kk symmetric)
+//   B4  SS: t, nu'      z = P_kk t_k   (the symmetric-stair P^-1 r, PCG.py:181-212)
+//   then                beta = nu'/nu, p = z + p beta to LDS -> B1
+// The element updates are the reference's, rounded as NumPy rounds them
+// (r - (Ap alpha), x + (p alpha), z + (p beta): no FMA contraction); only the
+// summation order of the dot and block products differs.  x = the lane's
+// entries of the solution.
 template <int NX, int RPL, int PRE>
 __device__ __forceinline__ void pcg_run(const PcgRow<NX> (&R)[RPL], const PcgLane<NX, RPL>& ln, int N,
                                         const PcgLds& L, const double (&bv)[RPL], const double* guess_v, double tol,
@@ -576,128 +632,165 @@ __device__ __forceinline__ void pcg_run(const PcgRow<NX> (&R)[RPL], const PcgLan
       for (int m = 0; m < RPL; ++m) buf[ln.row(m)] = v[m];
     }
   };
-  int rsel = 0;
-  auto reduce = [&](const double (&a)[RPL], const double (&b)[RPL]) -> double {
+  auto partial = [&](const double (&a)[RPL], const double (&b)[RPL]) -> double {
     double s = 0.0;
 #pragma unroll
     for (int m = 0; m < RPL; ++m) s += a[m] * b[m];
-    s = block_sum(ln.valid ? s : 0.0, L.red + 16 * rsel);
-    rsel ^= 1;
-    return s;
+    return ln.valid ? s : 0.0;
   };
-  // z = P^-1 r (PCG.py:88-90)
-  auto apply_P = [&](const double (&r)[RPL], double (&z)[RPL]) {
-    if (PRE == PRECOND_J) {
-#pragma unroll
-      for (int m = 0; m < RPL; ++m) z[m] = R[m].pr[0] * r[m];
-      return;
-    }
-    put(L.rbuf, r);
-    __syncthreads();
-    PCG_STAMP(5);
-    double w[RPL];
-    pcg_block_dot<NX, RPL>(R, L.rbuf + kb, w);
-    if (PRE == PRECOND_BJ) {
-#pragma unroll
-      for (int m = 0; m < RPL; ++m) z[m] = w[m];
-      return;
-    }
-    // SS: z = P_D (r - S_off P_D r)  ==  the symmetric-stair P^-1 r
-    put(L.wbuf, w);
-    __syncthreads();
-    PCG_STAMP(6);
-    const double* wm = L.wbuf + kb - NX;
-    constexpr int NC = RPL == 1 ? 2 : 1;
-    double a[NC][RPL];
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-      for (int m = 0; m < RPL; ++m) a[c][m] = 0.0;
-#pragma unroll
-    for (int j = 0; j < NX; ++j) {
-      const double wl = wm[j], wu = wm[2 * NX + j];
-#pragma unroll
-      for (int m = 0; m < RPL; ++m) {
-        a[0][m] += R[m].sl[j] * wl;
-        a[NC - 1][m] += R[m].su[j] * wu;
-      }
-    }
-    double tv[RPL];
-#pragma unroll
-    for (int m = 0; m < RPL; ++m) tv[m] = r[m] - (NC == 2 ? a[0][m] + a[NC - 1][m] : a[0][m]);
-    put(L.tbuf, tv);
-    __syncthreads();
-    PCG_STAMP(7);
-    pcg_block_dot<NX, RPL>(R, L.tbuf + kb, z);
-  };
-  // x0 = guess (default zeros, PCG.py:11-12); r = b - A x0 (:76).  The iterate x
-  // lives in L.xbuf (lane-private rows): it is only read at the end, so it
-  // costs no VGPRs inside the loop.
+  double* const redA = L.red;         // p.Ap
+  double* const redB = L.red + 16;    // nu'
+  double* const redC = L.red + 32;    // initial nu, true residual
+  // With two rows per lane the search direction p and the iterate x live only
+  // in LDS (own rows re-read where needed): the VGPR budget of 2 waves per SIMD
+  // holds the 96 matrix doubles per lane and little else.
+  constexpr bool IN_LDS = RPL > 1;
   double rv[RPL], zv[RPL], pv[RPL], av[RPL];
+  __syncthreads();   // the caller's pcg_lds_clear (pads, reduction slots) is complete
+  // x0 = guess (default zeros, PCG.py:11-12); r = b - A x0 (:76)
 #pragma unroll
   for (int m = 0; m < RPL; ++m) {
     xv[m] = (guess_v && ln.valid) ? guess_v[ln.row(m)] : 0.0;
     rv[m] = bv[m];
   }
-  put(L.xbuf, xv);
+  if (guess_v || IN_LDS) put(L.xbuf, xv);
   if (guess_v) {
     __syncthreads();
     pcg_spmv<NX, RPL>(R, L.xbuf, kb, av);
 #pragma unroll
     for (int m = 0; m < RPL; ++m) rv[m] = bv[m] - av[m];
-    __syncthreads();
   }
-  // With two rows per lane the search direction p also lives only in L.pbuf
-  // (own rows re-read where needed): the VGPR budget of 2 waves per SIMD holds
-  // the 96 matrix doubles per lane and little else.
-  constexpr bool P_IN_LDS = RPL > 1;
-  auto p_own = [&](double (&o)[RPL]) {
-#pragma unroll
-    for (int m = 0; m < RPL; ++m) o[m] = P_IN_LDS ? (ln.valid ? L.pbuf[ln.row(m)] : 0.0) : pv[m];
-  };
-  apply_P(rv, zv);
-#pragma unroll
-  for (int m = 0; m < RPL; ++m) pv[m] = zv[m];
-  double nu = reduce(rv, zv);
   auto true_residual = [&]() -> double {
-    // ||b - A x|| (PCG.py:83,95), trace only
+    // ||b - A x|| (PCG.py:83,95), trace only; the barrier also orders x's LDS copy
+    if (!IN_LDS) put(L.xbuf, xv);
     __syncthreads();
     double e[RPL];
     pcg_spmv<NX, RPL>(R, L.xbuf, kb, e);
 #pragma unroll
     for (int m = 0; m < RPL; ++m) e[m] = bv[m] - e[m];
-    return sqrt(reduce(e, e));
+    red_put(partial(e, e), redC);
+    __syncthreads();
+    const double s = red_total(redC);
+    __syncthreads();   // slot C is reused by the next call
+    return sqrt(s);
   };
+  // z = P^-1 r, nu = r^T z (:77-79)
+  put(L.rbuf[0], rv);
+  double nu;
+  if (PRE == PRECOND_BJ || PRE == PRECOND_SS) {
+    __syncthreads();
+    double w[RPL];
+    pcg_block_dot<NX, RPL>(R, L.rbuf[0] + kb, w);
+    if (PRE == PRECOND_BJ) {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) zv[m] = w[m];
+      red_put(partial(rv, zv), redC);
+      __syncthreads();
+    } else {
+      put(L.wbuf, w);
+      __syncthreads();
+      double tv[RPL];
+      pcg_off<NX, RPL>(R, L.wbuf, kb, rv, tv);
+      put(L.tbuf, tv);
+      red_put(partial(w, tv), redC);
+      __syncthreads();
+      pcg_block_dot<NX, RPL>(R, L.tbuf + kb, zv);
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) zv[m] = PRE == PRECOND_J ? R[m].pr[0] * rv[m] : rv[m];
+    red_put(partial(rv, zv), redC);
+    __syncthreads();
+  }
+  nu = red_total(redC);
+  __syncthreads();   // slot C free again
+#pragma unroll
+  for (int m = 0; m < RPL; ++m) pv[m] = zv[m];
+  put(L.pbuf, pv);
   if (tn && t == 0) tn[0] = fabs(nu);
   if (tr) {
     const double rn = true_residual();
     if (t == 0) tr[0] = rn;
   }
-  put(L.pbuf, pv);
   int it_done = max_iter;
+  int cur = 0;
   for (int it = 0; it < max_iter; ++it) {
     PCG_STAMP(0);
-    if (!P_IN_LDS) put(L.pbuf, pv);
-    __syncthreads();
+    __syncthreads();                                   // B1: p
     PCG_STAMP(1);
     pcg_spmv<NX, RPL>(R, L.pbuf, kb, av);
-    {
-      double po[RPL];
-      p_own(po);
-      const double pap = reduce(po, av);
-      PCG_STAMP(2);
-      const double alpha = nu / pap;
+    double po[RPL];
 #pragma unroll
-      for (int m = 0; m < RPL; ++m) {
-        rv[m] = rv[m] - av[m] * alpha;
-        if (ln.valid) L.xbuf[ln.row(m)] = L.xbuf[ln.row(m)] + po[m] * alpha;
-      }
-    }
+    for (int m = 0; m < RPL; ++m) po[m] = IN_LDS ? (ln.valid ? L.pbuf[ln.row(m)] : 0.0) : pv[m];
+    if (PRE == PRECOND_BJ || PRE == PRECOND_SS) put(L.abuf, av);   // J / 0 need only their own rows
+    red_put(partial(po, av), redA);
+    PCG_STAMP(2);
+    __syncthreads();                                   // B2: p.Ap, Ap
     PCG_STAMP(3);
-    apply_P(rv, zv);
+    const double alpha = nu / red_total(redA);
+    double w[RPL];
+    if (PRE == PRECOND_BJ || PRE == PRECOND_SS) {
+      // r_k - Ap_k alpha for the whole block; w = P_kk (new r_k); own rows kept
+      const double* ro = (cur ? L.rbuf[1] : L.rbuf[0]) + kb;   // no dynamic index: keeps L out of scratch
+      const double* ap = L.abuf + kb;
+      constexpr int NC = RPL == 1 ? 2 : 1;
+      double acc[NC][RPL];
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int m = 0; m < RPL; ++m) acc[c][m] = 0.0;
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        const double rj = __dsub_rn(ro[j], __dmul_rn(ap[j], alpha));
+#pragma unroll
+        for (int m = 0; m < RPL; ++m) {
+          acc[j % NC][m] += R[m].pr[j] * rj;
+          if (j == ln.r(m)) rv[m] = rj;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) w[m] = NC == 2 ? acc[0][m] + acc[NC - 1][m] : acc[0][m];
+    } else {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) rv[m] = __dsub_rn(rv[m], __dmul_rn(av[m], alpha));
+    }
+    if (IN_LDS) {
+      if (ln.valid) {
+#pragma unroll
+        for (int m = 0; m < RPL; ++m) L.xbuf[ln.row(m)] = __dadd_rn(L.xbuf[ln.row(m)], __dmul_rn(po[m], alpha));
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) xv[m] = __dadd_rn(xv[m], __dmul_rn(po[m], alpha));
+    }
+    if (PRE == PRECOND_BJ || PRE == PRECOND_SS) put(cur ? L.rbuf[0] : L.rbuf[1], rv);
+    cur ^= 1;
+    double nup;
+    if (PRE == PRECOND_SS) {
+      put(L.wbuf, w);
+      PCG_STAMP(4);
+      __syncthreads();                                 // B3: w
+      PCG_STAMP(5);
+      double tv[RPL];
+      pcg_off<NX, RPL>(R, L.wbuf, kb, rv, tv);
+      put(L.tbuf, tv);
+      red_put(partial(w, tv), redB);
+      PCG_STAMP(6);
+      __syncthreads();                                 // B4: t, nu'
+      PCG_STAMP(7);
+      nup = red_total(redB);
+      pcg_block_dot<NX, RPL>(R, L.tbuf + kb, zv);
+    } else {
+#pragma unroll
+      for (int m = 0; m < RPL; ++m)
+        zv[m] = PRE == PRECOND_BJ ? w[m] : (PRE == PRECOND_J ? R[m].pr[0] * rv[m] : rv[m]);
+      red_put(partial(rv, zv), redB);
+      PCG_STAMP(4);
+      __syncthreads();                                 // B3: nu'
+      PCG_STAMP(5);
+      nup = red_total(redB);
+    }
     PCG_STAMP(8);
-    const double nup = reduce(rv, zv);
-    PCG_STAMP(9);
     if (tn && t == 0) tn[it + 1] = fabs(nup);
     if (tr) {
       const double rn = true_residual();
@@ -708,20 +801,17 @@ __device__ __forceinline__ void pcg_run(const PcgRow<NX> (&R)[RPL], const PcgLan
       break;
     }
     const double beta = nup / nu;
-    if (P_IN_LDS) {
-      if (ln.valid) {
 #pragma unroll
-        for (int m = 0; m < RPL; ++m) L.pbuf[ln.row(m)] = zv[m] + L.pbuf[ln.row(m)] * beta;
-      }
-    } else {
-#pragma unroll
-      for (int m = 0; m < RPL; ++m) pv[m] = zv[m] + pv[m] * beta;
-    }
+    for (int m = 0; m < RPL; ++m) pv[m] = __dadd_rn(zv[m], __dmul_rn(po[m], beta));
+    put(L.pbuf, pv);
     nu = nup;
-    PCG_STAMP(10);
+    PCG_STAMP(9);
   }
+  if (IN_LDS) {
+    __syncthreads();
 #pragma unroll
-  for (int m = 0; m < RPL; ++m) xv[m] = ln.valid ? L.xbuf[ln.row(m)] : 0.0;
+    for (int m = 0; m < RPL; ++m) xv[m] = ln.valid ? L.xbuf[ln.row(m)] : 0.0;
+  }
 #ifdef TMPC_PCG_STAMPS
   if (tn_st && (t == 0 || t == ((int)blockDim.x - 1) / 64 * 64)) {
     double* o = tn_st + (t == 0 ? 0 : 16);
@@ -740,6 +830,8 @@ __device__ __forceinline__ void pcg_dispatch(int precond, const PcgRow<NX> (&R)[
     pcg_run<NX, RPL, PRECOND_J>(R, ln, N, L, bv, guess_v, tol, max_iter, tn, tr, iters_out, xv);
   else if (precond == PRECOND_BJ)
     pcg_run<NX, RPL, PRECOND_BJ>(R, ln, N, L, bv, guess_v, tol, max_iter, tn, tr, iters_out, xv);
+  else if (precond == PRECOND_NONE)
+    pcg_run<NX, RPL, PRECOND_NONE>(R, ln, N, L, bv, guess_v, tol, max_iter, tn, tr, iters_out, xv);
   else
     pcg_run<NX, RPL, PRECOND_SS>(R, ln, N, L, bv, guess_v, tol, max_iter, tn, tr, iters_out, xv);
 }
@@ -749,7 +841,10 @@ __device__ __forceinline__ void pcg_dispatch(int precond, const PcgRow<NX> (&R)[
 // per lane halve the LDS traffic but leave 2 waves per SIMD to hide the 9-cycle
 // fp64 FMA latency, and the VGPR budget of 256 then barely holds the matrix
 // rows).  Two rows per lane (<= 8 waves) for 769..1024 rows.
-__host__ __device__ inline int pcg_rpl(int N, int NX) { return (N * NX <= 768 || (NX & 1)) ? 1 : 2; }
+#ifndef TMPC_RPL1_MAX_ROWS
+#define TMPC_RPL1_MAX_ROWS 768
+#endif
+__host__ __device__ inline int pcg_rpl(int N, int NX) { return (N * NX <= TMPC_RPL1_MAX_ROWS || (NX & 1)) ? 1 : 2; }
 
 // ---- standalone PCG on given blocks (tmpc_pcg_batch: the PCG class)
 template <int NX, int RPL, int MAXT>
@@ -960,7 +1055,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
                                              double* __restrict__ du, double* __restrict__ lam_out,
                                              double* __restrict__ Sd_out, double* __restrict__ Sl_out,
                                              double* __restrict__ gam_out, double* __restrict__ Pd_out,
-                                             const double* __restrict__ jsoft) {
+                                             const double* __restrict__ jsoft, const double* __restrict__ guess) {
   constexpr int NX = 2 * NJ, NU = NJ;
   const int b = blockIdx.x;
   if (!active[b]) return;
@@ -1031,7 +1126,9 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   const PcgLds L = pcg_lds(lds, N, NX);
   pcg_precondition<NX, RPL>(R, precond, ln, N, L.piv, Pd_out ? Pd_out + ((size_t)b * N + k) * NX * NX : nullptr);
   int it_done = 0;
-  pcg_dispatch<NX, RPL>(precond, R, ln, N, L, bv, nullptr, tol, max_iter, nullptr, nullptr, &it_done, xv);
+  // PCG warm start (PCG.update_guess, TrajoptMPCReference.py:439-440): guess [B][N NX] or null
+  pcg_dispatch<NX, RPL>(precond, R, ln, N, L, bv, guess ? guess + (size_t)b * rows : nullptr, tol, max_iter, nullptr,
+                        nullptr, &it_done, xv);
   if (threadIdx.x == 0) iters[b] = it_done;
   }
 
@@ -1446,14 +1543,14 @@ struct LaunchNJ {
   static void qp(hipStream_t s, const CostDev* C, int B, int N, int precond, int mode, const double* x, const double* u,
                  const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
                  int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-                 double* Pd, const double* jsoft) {
+                 double* Pd, const double* jsoft, const double* guess) {
     constexpr int NX = 2 * NJ;
     const int rows = N * NX;
     const int rpl = pcg_rpl(N, NX);
     const int threads = ((rows / rpl + 63) / 64) * 64;
     const size_t lds = qp_lds_doubles(N, NX, NJ) * sizeof(double);
 #define TMPC_QP_ARGS s, C, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, \
-                     Sl, gam, Pd, jsoft
+                     Sl, gam, Pd, jsoft, guess
 #define TMPC_QP_LAUNCH(PKV, MODEV)                                                                        \
     if (rpl == 1)                                                                                          \
       hipLaunchKernelGGL((k_qp<NJ, 1, 768, PKV, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);        \
@@ -1743,11 +1840,11 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-              double* Pd, const double* jsoft) {
+              double* Pd, const double* jsoft, const double* guess) {
   if (N * 2 * nj > 1024) return -1;
   if (qp_lds_doubles(N, 2 * nj, nj) * sizeof(double) > 160 * 1024) return -3;
   TMPC_DISPATCH_NJ2(nj, qp(s, C, B, N, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd,
-                           Sl, gam, Pd, jsoft))
+                           Sl, gam, Pd, jsoft, guess))
 }
 int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
                      const int* active, const double* x, const double* u, const double* mu, const double* lam,

@@ -62,9 +62,6 @@ class PCG:
         if precon_type not in VALID_PRECONDITIONERS:
             raise ValueError("Invalid preconditioner options are [0: none, J : Jacobi, BJ: Block-Jacobi, "
                              "SS: Symmetric Stair]")
-        if precon_type == "0":
-            # the reference's identity branch returns the wrong type (PCG.py:114-118)
-            raise NotImplementedError("preconditioner '0' is not offered; use J, BJ or SS")
 
     def update_A(self, A):
         self.A = A
@@ -121,6 +118,8 @@ class PCG:
         P = np.zeros((N * b, N * b))
         if ptype == "J":
             return np.diag(1.0 / np.diag(np.asarray(self.A, dtype=np.float64)))
+        if ptype == "0":   # identity (PCG.py:114-118)
+            return np.identity(N * b)
         if self._Pd is None:
             self.solve()
         Pd = self._Pd

@@ -116,6 +116,14 @@ class TrajoptMPCReference:
         options.setdefault("max_iter_softConstraints", 10)
 
     # ------------------------------------------------------------------ lowering to libtmpc
+    def _check_xu(self, x, u, N):
+        """x [B][nx][N], u [B][nu][N-1] with the plant's nx = 2 n, nu = n (the reference's
+        column-per-knot arrays, TrajoptMPCReference.py:510, batched)."""
+        nx, nu = self.plant.get_num_pos() + self.plant.get_num_vel(), self.plant.get_num_cntrl()
+        if x.ndim != 3 or u.ndim != 3 or x.shape[0] != u.shape[0] or x.shape[1:] != (nx, N) \
+                or u.shape[1:] != (nu, N - 1):
+            raise ValueError(f"expected x [B][{nx}][{N}] and u [B][{nu}][{N - 1}], got {x.shape} and {u.shape}")
+
     def _context(self, options):
         if not isinstance(self.plant, URDFPlant):
             raise NotImplementedError("the GPU solver needs a URDFPlant (custom TrajoptPlant subclasses have no "
@@ -132,7 +140,10 @@ class TrajoptMPCReference:
             ctx.set_cost_ee(c.Q, c.QF, c.R, c.xg, c.QF_start, m.H0[:2], m.Ha[:2], m.Hb[:2])
         else:
             ctx.set_cost_quadratic(c.Q, c.QF, c.R, c.xg, c.QF_start)
-        ctx.set_options(**{v: options[k] for k, v in _OPTION_MAP.items()})
+        # pcg_warm_start (build option, default off = the reference): PCG of each QP starts from the
+        # previous QP's lambda, across MPC steps from the shifted last lambda (include/tmpc.h)
+        ctx.set_options(**{v: options[k] for k, v in _OPTION_MAP.items()},
+                        pcg_warm_start=int(bool(options.get("pcg_warm_start", False))))
         ctx.set_box_limits(spec)
         return ctx
 
@@ -151,8 +162,7 @@ class TrajoptMPCReference:
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
-        if x.ndim != 3 or u.ndim != 3 or x.shape[2] != N or u.shape[2] != N - 1 or x.shape[0] != u.shape[0]:
-            raise ValueError(f"expected x [B][nx][{N}] and u [B][nu][{N - 1}], got {x.shape} and {u.shape}")
+        self._check_xu(x, u, N)
         B = x.shape[0]
         soft = self.other_constraints.has_any()
         if soft:
@@ -217,8 +227,7 @@ class TrajoptMPCReference:
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
-        if x.ndim != 3 or u.ndim != 3 or x.shape[2] != N or u.shape[2] != N - 1 or x.shape[0] != u.shape[0]:
-            raise ValueError(f"expected x [B][nx][{N}] and u [B][nu][{N - 1}], got {x.shape} and {u.shape}")
+        self._check_xu(x, u, N)
         B = x.shape[0]
         soft = self.other_constraints.has_any()
         if soft:
@@ -279,8 +288,7 @@ class TrajoptMPCReference:
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
-        if x.ndim != 3 or u.ndim != 3 or x.shape[2] != N or u.shape[2] != N - 1 or x.shape[0] != u.shape[0]:
-            raise ValueError(f"expected x [B][nx][{N}] and u [B][nu][{N - 1}], got {x.shape} and {u.shape}")
+        self._check_xu(x, u, N)
         B = x.shape[0]
         soft = self.other_constraints.has_any()
         if soft:
@@ -313,6 +321,14 @@ class TrajoptMPCReference:
         x = np.asarray(x, dtype=np.float64)
         if not np.array_equal(np.asarray(xs), x[:, 0]):
             raise NotImplementedError("xs != x[:, 0] is not supported by the batched QP entry point")
-        r = ctx.qp_batch(x[None], np.asarray(u, dtype=np.float64)[None], N, dt, rho, method, want_blocks=False)
+        u = np.asarray(u, dtype=np.float64)
+        self._check_xu(x[None], u[None], N)
+        # options['guess'] -> PCG.update_guess (:439-440): the PCG's initial iterate
+        guess = options.get("guess")
+        if guess is not None:
+            guess = np.asarray(guess, dtype=np.float64).reshape(1, -1)
+            if guess.shape[1] != N * x.shape[0]:
+                raise ValueError(f"options['guess'] must have N * nx = {N * x.shape[0]} entries, got {guess.shape[1]}")
+        r = ctx.qp_batch(x[None], u[None], N, dt, rho, method, want_blocks=False, guess=guess if use_PCG else None)
         self.n_inner_iter = int(r["pcg_iters"][0])
         return r["dxul"][0].reshape(-1, 1)
