@@ -130,15 +130,29 @@ def test_no_cpu_fallback_without_gpu():
 
 
 def test_bench_cpu_baseline_runs_the_oracle_on_a_bounded_sample():
-    """bench.py's cpu_baseline leg: the oracle restatement of the same workload."""
+    """bench.py's cpu_baseline leg: the oracle restatement of the same workload; it also returns the
+    per-problem integers the bench's parity check compares with the GPU."""
     import bench
     v, wall, res = bench.cpu_baseline(2, 8, 2, 2, 0)
     assert v > 0 and wall > 0 and len(res) == 2
-    assert all(e in (1, 2, 3) for e, _ in res)
+    assert all(r["exit_sqp"] in (1, 2, 3) and len(r["pcg_iters"]) >= r["sqp_iter"] for r in res)
+    # parity_check against itself dressed as a GPU result: zero mismatches
+    B, W = len(res), 101
+    gpu = {"exit_sqp": np.array([r["exit_sqp"] for r in res]), "sqp_iter": np.array([r["sqp_iter"] for r in res]),
+           "x": np.array([r["x"] for r in res]), "u": np.array([r["u"] for r in res]),
+           "trace": {"pcg_iters": np.zeros((B, W), dtype=np.int32)}}
+    for i, r in enumerate(res):
+        gpu["trace"]["pcg_iters"][i, 1:1 + len(r["pcg_iters"])] = r["pcg_iters"]
+    p = bench.parity_check(gpu, res)
+    assert p["checked"] == 2 and p["mismatches"] == 0 and p["max_traj_rel_diff"] == 0.0
+    gpu["trace"]["pcg_iters"][1, 1] += 1
+    assert bench.parity_check(gpu, res)["mismatches"] == 1
 
 
 def test_bench_byte_and_flop_models():
-    """b_pcg = 8 (2 (2N-1) nx^2 + 10 N nx) = 354,048 B/iteration for arm6 N=64."""
+    """b_pcg = 8 (2 (2N-1) nx^2 + 10 N nx) = 354,048 B/iteration and
+    f_pcg = 2*3*nx^2*N*2 + 10*N*nx = 118,272 flop/iteration for arm6 N=64."""
     import bench
-    assert bench.pcg_bytes_per_iter(64, 12) == 354048
-    assert bench.pcg_flops_per_iter(64, 12, "PCG-SS") > bench.pcg_flops_per_iter(64, 12, "PCG-BJ")
+    assert bench.b_pcg_survey(64, 12) == 354048
+    assert bench.f_pcg_survey(64, 12) == 118272
+    assert bench.pcg_flops_impl(64, 12, "PCG-SS") > bench.pcg_flops_impl(64, 12, "PCG-BJ")
