@@ -246,23 +246,29 @@ def total_cost(cost, x, u, N, soft=None):
     return J
 
 
-def total_violation(model, x, u, xs, N, dt):
-    """totalHardConstraintViolation (:273-294), mode sum, no other constraints."""
+def total_violation(model, x, u, xs, N, dt, hard=None):
+    """totalHardConstraintViolation (:273-294), mode sum: initial state and dynamics defects, then
+    the hard box-constraint terms knot by knot (oracle/hard.py)."""
     cval = sum(map(abs, x[:, 0] - xs))
     xkp1 = rbd.euler(model, x[:, :N - 1].T, u.T, dt)
     for k in range(N - 1):
         cval = cval + sum(map(abs, x[:, k + 1] - xkp1[k]))
+    if hard is not None:
+        for t in hard.violation_terms(x, u, N):
+            cval = cval + t
     return cval
 
 
 # ------------------------------------------------------------------- SQP
-def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm=None):
+def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm=None, hard=None):
     """TrajoptMPCReference.SQP (:510-760).  Returns a dict.  `soft` (oracle.soft.SoftConstraints)
     enables the soft-constraint terms and the outer loop; its mu/lambda/phi are updated in place
     (the reference keeps them in the constraint object).
     `warm` (build option pcg_warm_start, include/tmpc.h): a dict whose "lam" (None = zeros) is each
     QP's PCG initial iterate and receives that QP's lambda -- the reference never forwards a guess
-    from SQP (:512-519), so warm=None is the reference behaviour."""
+    from SQP (:512-519), so warm=None is the reference behaviour.
+    `hard` (oracle.hard.HardConstraints): ACTIVE_SET / FULL_SET rows in the dense KKT system
+    (the reference's own dense formation, small sizes only)."""
     o = default_options(options)
     nx, nu = 2 * model.n, model.n
     n = nx + nu
@@ -275,19 +281,25 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
         rho = o["rho_init_SQP_DDP"]
         drho = 1
         J = total_cost(cost, x, u, N, soft)
-        c = total_violation(model, x, u, xs, N, dt)
+        c = total_violation(model, x, u, xs, N, dt, hard)
         mu = 10
         merit = J + mu * c
         trace = [dict(outer_iteration=outer, iteration=0, line_search_iteration=0, alpha=1, rho=rho, J=J, c=c,
                       merit=merit, D=None, reduction_ratio=None, succeeded_line_search=False)]
-        pcg_iters, dxuls = [], []
+        pcg_iters, dxuls, active_rows = [], [], []
         it = 0
         exit_sqp = 0
         while True:
-            guess = None if warm is None else warm.get("lam")
-            dxul, iters, ex = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o, soft, guess)
-            if warm is not None and iters is not None:
-                warm["lam"] = ex["lam"].copy()
+            if hard is not None:
+                from . import hard as ohard
+                G, g, C, cc = ohard.kkt_dense(model, cost, x, u, xs, N, dt, hard, soft)
+                dxul, iters, _ = ohard.solve_qp_dense(G, g, C, cc, rho, method, o, nx)
+                active_rows.append(C.shape[0] - nx * N)
+            else:
+                guess = None if warm is None else warm.get("lam")
+                dxul, iters, ex = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o, soft, guess)
+                if warm is not None and iters is not None:
+                    warm["lam"] = ex["lam"].copy()
             dxul = dxul.reshape(-1, 1)
             dxuls.append(dxul[:, 0].copy())
             if iters is not None:
@@ -303,7 +315,7 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
                     if k < N - 1:
                         u_new[:, k] = u_new[:, k] - alpha * dxul[n * k + nx:n * (k + 1), 0]
                 J_new = total_cost(cost, x_new, u_new, N, soft)
-                c_new = total_violation(model, x_new, u_new, xs, N, dt)
+                c_new = total_violation(model, x_new, u_new, xs, N, dt, hard)
                 D = 0
                 for k in range(N - 1):
                     D += float(cost.gradient(x_new[:, k], u_new[:, k], k) @ dxul[n * k:n * (k + 1), 0])
@@ -366,7 +378,7 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
         if done:
             break
     return dict(x=x, u=u, exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer, sqp_iter=it, trace=trace,
-                pcg_iters=pcg_iters, dxul=dxuls)
+                pcg_iters=pcg_iters, dxul=dxuls, active_rows=active_rows)
 
 
 def initial_problem(model, N, dt, seed):

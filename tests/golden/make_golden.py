@@ -402,6 +402,93 @@ def run_soft(args):
            f"outer={outer_iter} iters={sqp_iter} wall={wall:.1f}s"
 
 
+def run_hard(args):
+    """1-link arm, torque limits in a HARD mode (ACTIVE_SET / FULL_SET): the violated rows
+    [u - lb; ub - u] < 0 are appended to C after each knot's dynamics rows
+    (TrajoptMPCReference.py:238-248, TrajoptConstraint.py:53-130).  constraint_size 1 is the
+    only size the reference's BoxConstraint runs.  Records, per QP, the active rows
+    (knot, +1 lower / -1 upper) read back from the reference's own C, and the PCG counts."""
+    mode, method, N, q0, seed, dt, erm = args
+    _setup_reference()
+    sys.path.insert(0, os.path.dirname(OUT))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from trajoptmpcreference_amd.urdf import planar_arm_urdf
+    from TrajoptPlant import URDFPlant
+    from TrajoptConstraint import TrajoptConstraint
+    from TrajoptMPCReference import TrajoptMPCReference, SQPSolverMethods
+    from overloading import matrix_
+    matrix_.iteration = 0
+    matrix_.soft_constraint_iteration = 0
+    matrix_.line_search_iteration = 0
+    urdf = planar_arm_urdf(1)
+    d = tempfile.mkdtemp(prefix="tmpc_urdf_")
+    path = os.path.join(d, "arm1.urdf")
+    with open(path, "w") as f:
+        f.write(urdf)
+    plant = URDFPlant(options={"path_to_urdf": path, "overloading": False})
+    cost = make_cost(2, 1)
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((2, N))
+    x0[0, 0] = q0 + rng.uniform(-0.1, 0.1)
+    u0 = np.zeros((1, N - 1))
+    for k in range(N - 1):
+        x0[:, k + 1] = plant.integrator(x0[:, k], u0[:, k], dt)
+    lb, ub = -0.5, 0.5
+    con = TrajoptConstraint(1, 1, 1, N)
+    con.overloading = False   # attribute the reference reads but never sets (SURVEY F6)
+    con.set_torque_limits([ub], [lb], mode, {"overloading": False})
+    solver = TrajoptMPCReference(plant, cost, con)
+    m = {"S": SQPSolverMethods.S, "PCG-J": SQPSolverMethods.PCG_J, "PCG-BJ": SQPSolverMethods.PCG_BJ,
+         "PCG-SS": SQPSolverMethods.PCG_SS}[method]
+    opts = {"overloading": False}
+    if erm is not None:
+        opts["expected_reduction_min_SQP_DDP"] = erm
+    import io
+    import contextlib
+    t0 = time.time()
+    err = ""
+    try:
+        with contextlib.redirect_stdout(io.StringIO()):
+            x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(copy.deepcopy(x0), copy.deepcopy(u0), N,
+                                                                         dt, m, opts)
+    except Exception as e:   # the reference's own failure, recorded as data
+        err = repr(e)
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = x0, u0, -1, -1, -1, -1
+    wall = time.time() - t0
+    tr = solver.trace
+    keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
+            "succeeded_line_search"]
+    rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(np.asarray(t[k]).reshape(-1)[0]) for t in tr])
+           for k in keys}
+    # active rows per QP from the reference's C: rows past nx*N, in order; knot = column block, sign = entry
+    nx, n = 2, 3
+    act_knot, act_sign, act_qp = [], [], []
+    for q, dC in enumerate(solver.saved_C):
+        C = np.asarray(dC["value"])
+        for r in range(C.shape[0]):
+            row = C[r]
+            nzc = np.nonzero(row)[0]
+            if r >= nx and len(nzc) == 1 and (nzc[0] % n) == nx:   # a torque row: one entry in a u column
+                act_qp.append(q)
+                act_knot.append(int(nzc[0] // n))
+                act_sign.append(int(np.sign(row[nzc[0]])))
+    pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
+    dxul = [np.asarray(dd["value"])[:, 0] for dd in solver.saved_dxul]
+    rows = np.array([np.asarray(dC["value"]).shape[0] for dC in solver.saved_C], dtype=np.int32)
+    W = max([len(v) for v in dxul] + [1])
+    dx_pad = np.array([np.concatenate([v, np.full(W - len(v), np.nan)]) for v in dxul]) if dxul else np.zeros((0, 1))
+    tag = {"ACTIVE_SET": "AS", "FULL_SET": "FS"}[mode]
+    np.savez_compressed(os.path.join(OUT, f"hard_arm1_N{N}_{tag}_s{seed}_{method}.npz"),
+                        urdf=np.array(urdf), x0=x0, u0=u0, x=np.asarray(x), u=np.asarray(u), dt=dt, lb=lb, ub=ub,
+                        mode=np.array(mode), erm=np.nan if erm is None else erm, error=np.array(err),
+                        exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer_iter, sqp_iter=sqp_iter,
+                        pcg_iters=pcg_iters, C_rows=rows, act_qp=np.array(act_qp, dtype=np.int32),
+                        act_knot=np.array(act_knot, dtype=np.int32), act_sign=np.array(act_sign, dtype=np.int32),
+                        dxul=dx_pad, wall_s=wall, **rec)
+    return f"[golden] hard {tag} {method} N={N} seed={seed} erm={erm}: exit_sqp={exit_sqp} iters={sqp_iter} " \
+           f"rows={list(rows)} pcg={list(pcg_iters)} err={err[:80]} wall={wall:.1f}s"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="skip the slow arm6 N=64 solves")
@@ -434,6 +521,14 @@ def main():
                 ("d4", [-1.0, 1.5, 0.0, 0.0], "S")]
         with mp.get_context("fork").Pool(len(jobs)) as pool:
             for msg in pool.imap_unordered(run_ee_sqp, jobs):
+                print(msg, flush=True)
+    if a.only in (None, "hard"):
+        jobs = [("ACTIVE_SET", "PCG-SS", 8, 2.0, 0, 0.1, None), ("ACTIVE_SET", "S", 8, 2.0, 1, 0.1, None),
+                ("ACTIVE_SET", "PCG-BJ", 10, 1.5, 2, 0.1, None), ("ACTIVE_SET", "PCG-SS", 12, 2.5, 3, 0.1, -100.0),
+                ("ACTIVE_SET", "PCG-J", 8, 2.0, 4, 0.1, None), ("FULL_SET", "PCG-SS", 8, 2.0, 5, 0.1, None),
+                ("FULL_SET", "S", 8, 2.0, 6, 0.1, None)]
+        with mp.get_context("fork").Pool(min(8, len(jobs))) as pool:
+            for msg in pool.imap_unordered(run_hard, jobs):
                 print(msg, flush=True)
     if a.only in (None, "soft"):
         jobs = [("QUADRATIC_PENALTY", "PCG-SS", 8, 2.0, 0, 0.1), ("AUGMENTED_LAGRANGIAN", "PCG-SS", 8, 2.0, 0, 0.1),

@@ -81,3 +81,27 @@ def test_ilqr_long_horizon_n128():
     assert match, (got, [(o["exit_code"], o["iter"]) for o in runs])
     assert got[0] == 1
     assert np.allclose(r["x"][0], match[0]["x"], rtol=1e-6, atol=1e-7)
+
+
+def test_mpc_pcg_warm_start_matches_oracle():
+    """pcg_warm_start: every PCG starts from the problem's previous lambda, the first QP of an MPC
+    step from the previous step's last lambda shifted by one knot (oracle/mpc.py); the reference's
+    SQP never forwards options['guess'] (TrajoptMPCReference.py:512-519), so this is a build option."""
+    from oracle import mpc as ompc
+    from oracle import sqp as osqp
+    m = arm_model("arm3")
+    N, B, steps = 16, 3, 3
+    solver = _setup(3, N)
+    xs, us = zip(*[osqp.initial_problem(m, N, 0.1, 720 + i) for i in range(B)])
+    opts = {"max_iter_SQP_DDP": 8, "pcg_warm_start": True}
+    r = solver.MPC_batch(np.array(xs), np.array(us), N, 0.1, "QP-PCG-SS", dict(opts), mpc_steps=steps)
+    cold = solver.MPC_batch(np.array(xs), np.array(us), N, 0.1, "QP-PCG-SS", {"max_iter_SQP_DDP": 8},
+                            mpc_steps=steps)
+    for i in range(B):
+        o = ompc.mpc(m, osqp.QuadCost(*quad_cost_arrays(3)), xs[i], us[i], N, 0.1, "PCG-SS", steps,
+                     {"max_iter_SQP_DDP": 8}, pcg_warm_start=True)
+        assert list(r["exit_codes"][i]) == list(o["exit_codes"]), i
+        assert list(r["iters"][i]) == list(o["iters"]), i
+        assert np.allclose(r["x_exec"][i], o["x_exec"], rtol=1e-6, atol=1e-8)
+    # the warm start changes the PCG iterates (and typically the counts) relative to a cold start
+    assert not np.array_equal(r["x"], cold["x"])
