@@ -56,11 +56,17 @@ extern "C" {
 #define TMPC_JOINT_REVOLUTE 0  /* X(q) = X0 + cos(q) Xa + sin(q) Xb */
 #define TMPC_JOINT_PRISMATIC 1 /* X(q) = X0 + q Xa                  */
 
-/* soft box-limit modes (BoxConstraint modes, TrajoptConstraint.py:27-35; the hard modes
- * ACTIVE_SET / FULL_SET are not offered on the GPU) */
+/* box-limit modes (BoxConstraint modes, TrajoptConstraint.py:27-35).  Soft: penalty terms in the
+ * cost and the augmented-Lagrangian outer loop.  Hard: rows of C / c per knot
+ * (TrajoptMPCReference.py:238-248) -- ACTIVE_SET the violated entries, FULL_SET all of them (the
+ * inactive ones with zero jacobian rows: S is then singular, which the reference's PCG preconditioner
+ * rejects with LinAlgError and its method S answers with lstsq; here FULL_SET runs with method S and
+ * gives the inactive rows lambda = 0, the minimum-norm least-squares solution). */
 #define TMPC_LIMIT_NONE 0
 #define TMPC_LIMIT_QUADRATIC_PENALTY 1
 #define TMPC_LIMIT_AUGMENTED_LAGRANGIAN 2
+#define TMPC_LIMIT_ACTIVE_SET 3
+#define TMPC_LIMIT_FULL_SET 4
 
 typedef struct tmpc_ctx tmpc_ctx;
 
@@ -92,7 +98,7 @@ typedef struct tmpc_options {
 } tmpc_options;
 
 /* Box limits of TrajoptConstraint (set_joint_limits / set_velocity_limits / set_torque_limits,
- * TrajoptConstraint.py:190-206) in a soft mode, with the BoxConstraint options (:38-46).
+ * TrajoptConstraint.py:190-206) in a soft or hard mode, with the BoxConstraint options (:38-46).
  * Index 0 = joint (q), 1 = velocity (qd), 2 = torque (u); lb/ub have n entries.
  * Vector semantics for constraint_size > 1 and the other corrections of SURVEY F6 are
  * documented in oracle/soft.py. */

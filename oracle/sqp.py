@@ -286,7 +286,7 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
         merit = J + mu * c
         trace = [dict(outer_iteration=outer, iteration=0, line_search_iteration=0, alpha=1, rho=rho, J=J, c=c,
                       merit=merit, D=None, reduction_ratio=None, succeeded_line_search=False)]
-        pcg_iters, dxuls, active_rows = [], [], []
+        pcg_iters, dxuls, active_rows, active_sets = [], [], [], []
         it = 0
         exit_sqp = 0
         while True:
@@ -295,6 +295,8 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
                 G, g, C, cc = ohard.kkt_dense(model, cost, x, u, xs, N, dt, hard, soft)
                 dxul, iters, _ = ohard.solve_qp_dense(G, g, C, cc, rho, method, o, nx)
                 active_rows.append(C.shape[0] - nx * N)
+                active_sets.append([(k, int(sg)) for k in range(N)
+                                    for _, sg, _ in hard.rows(x[:, k], u[:, k] if k < N - 1 else None, k, N)])
             else:
                 guess = None if warm is None else warm.get("lam")
                 dxul, iters, ex = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o, soft, guess)
@@ -378,7 +380,7 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
         if done:
             break
     return dict(x=x, u=u, exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer, sqp_iter=it, trace=trace,
-                pcg_iters=pcg_iters, dxul=dxuls, active_rows=active_rows)
+                pcg_iters=pcg_iters, dxul=dxuls, active_rows=active_rows, active_sets=active_sets)
 
 
 def initial_problem(model, N, dt, seed):

@@ -526,7 +526,8 @@ def main():
         jobs = [("ACTIVE_SET", "PCG-SS", 8, 2.0, 0, 0.1, None), ("ACTIVE_SET", "S", 8, 2.0, 1, 0.1, None),
                 ("ACTIVE_SET", "PCG-BJ", 10, 1.5, 2, 0.1, None), ("ACTIVE_SET", "PCG-SS", 12, 2.5, 3, 0.1, -100.0),
                 ("ACTIVE_SET", "PCG-J", 8, 2.0, 4, 0.1, None), ("FULL_SET", "PCG-SS", 8, 2.0, 5, 0.1, None),
-                ("FULL_SET", "S", 8, 2.0, 6, 0.1, None)]
+                ("FULL_SET", "S", 8, 2.0, 6, 0.1, None), ("ACTIVE_SET", "PCG-BJ", 10, 2.5, 7, 0.1, None),
+                ("ACTIVE_SET", "PCG-SS", 16, 2.2, 8, 0.1, None), ("ACTIVE_SET", "S", 12, 3.0, 9, 0.1, -100.0)]
         with mp.get_context("fork").Pool(min(8, len(jobs))) as pool:
             for msg in pool.imap_unordered(run_hard, jobs):
                 print(msg, flush=True)

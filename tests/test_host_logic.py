@@ -156,3 +156,17 @@ def test_bench_byte_and_flop_models():
     assert bench.b_pcg_survey(64, 12) == 354048
     assert bench.f_pcg_survey(64, 12) == 118272
     assert bench.pcg_flops_impl(64, 12, "PCG-SS") > bench.pcg_flops_impl(64, 12, "PCG-BJ")
+
+
+def test_pendulum_model_closed_form():
+    """PendulumPlant's model (urdf.pendulum_urdf): the oracle's dynamics equal
+    qdd = (u - m g l sin q) / (m l^2 + I_bob) (the plant examples/pendulum.py needs)."""
+    from oracle import rbd
+    from trajoptmpcreference_amd.urdf import parse_urdf, pendulum_urdf
+    m = parse_urdf(pendulum_urdf(mass=2.0, length=0.5))
+    rng = np.random.default_rng(0)
+    x = np.column_stack([rng.uniform(-3, 3, 8), rng.uniform(-2, 2, 8)])
+    u = rng.uniform(-5, 5, (8, 1))
+    qdd = (rbd.euler(m, x, u, 1.0)[:, 1] - x[:, 1])
+    ref = (u[:, 0] - 2.0 * 9.81 * 0.5 * np.sin(x[:, 0])) / (2.0 * 0.25 + 1e-3)
+    assert np.allclose(qdd, ref, rtol=1e-12, atol=1e-12)

@@ -9,11 +9,12 @@ ctypes C ABI (include/tmpc.h).  No CPU fallback.
 from .constraint import BoxConstraint, TrajoptConstraint
 from .cost import QuadraticCost, TrajoptCost, UrdfCost
 from .pcg import PCG
-from .plant import TrajoptPlant, URDFPlant
+from .plant import PendulumPlant, TrajoptPlant, URDFPlant
 from .solver import MPCSolverMethods, SQPSolverMethods, TrajoptMPCReference
-from .urdf import RobotModel, parse_urdf, planar_arm_urdf
+from .urdf import RobotModel, parse_urdf, pendulum_urdf, planar_arm_urdf
 
 __all__ = [
     "BoxConstraint", "TrajoptConstraint", "QuadraticCost", "TrajoptCost", "UrdfCost", "PCG", "TrajoptPlant", "URDFPlant",
-    "MPCSolverMethods", "SQPSolverMethods", "TrajoptMPCReference", "RobotModel", "parse_urdf", "planar_arm_urdf",
+    "PendulumPlant", "MPCSolverMethods", "SQPSolverMethods", "TrajoptMPCReference", "RobotModel", "parse_urdf",
+    "pendulum_urdf", "planar_arm_urdf",
 ]

@@ -44,7 +44,7 @@ class tmpc_options(C.Structure):
     ]
 
 
-LIMIT_MODES = {"QUADRATIC_PENALTY": 1, "AUGMENTED_LAGRANGIAN": 2}
+LIMIT_MODES = {"QUADRATIC_PENALTY": 1, "AUGMENTED_LAGRANGIAN": 2, "ACTIVE_SET": 3, "FULL_SET": 4}
 
 
 class tmpc_box_limits(C.Structure):

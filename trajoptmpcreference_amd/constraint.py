@@ -13,9 +13,14 @@ with the corrections documented in oracle/soft.py: joint limits cover all N
 knots, terminal jacobians keep the state part, several soft types sum their
 jacobians (and their per-type outer products in the KKT Hessian).
 
-The hard modes (ACTIVE_SET / FULL_SET) change the row structure of the KKT
-system every iteration; they are not offered on the GPU and raise
-NotImplementedError (as ADMM_PROJECTION exits in the reference).
+The hard modes (ACTIVE_SET / FULL_SET) append rows to C / c per knot
+(TrajoptMPCReference.py:238-248); the GPU builds the resulting variable-size,
+banded Schur complement per problem and reproduces the reference's nx-aligned
+PCG preconditioner on it (csrc/tmpc_hard.hip).  Their semantics are the
+reference's for constraint_size 1 and the elementwise generalisation above
+(oracle/hard.py).  FULL_SET leaves zero rows in C for the inactive entries; the
+reference's PCG then raises LinAlgError and its method S falls back to lstsq, so
+FULL_SET runs with method S only.
 
 The host-side value / jacobian / update methods below are the plugin API for
 callers that evaluate constraints themselves; the solve never calls them.
@@ -177,11 +182,66 @@ class TrajoptConstraint:
                     total += c.constraint_size
         return total
 
+    def _hard_slices(self, xk, uk, timestep):
+        """(kind, constraint, z) of the hard limits at a knot, in value_hard_constraints' order
+        (:210-240); torque limits have no terminal-knot rows (:230)."""
+        T = self.num_timesteps
+        t = T - 1 if timestep is None else timestep
+        out = []
+        for kind, c in self.limits():
+            if not c.is_hard_constraint_mode():
+                continue
+            if kind == "torque_limits":
+                if t >= T - 1 or uk is None:
+                    continue
+                z = np.asarray(uk, dtype=np.float64).reshape(-1)
+            elif kind == "joint_limits":
+                z = np.asarray(xk, dtype=np.float64).reshape(-1)[:self.nq]
+            else:
+                z = np.asarray(xk, dtype=np.float64).reshape(-1)[self.nq:self.nq + self.nv]
+            out.append((kind, c, z))
+        return out
+
+    def value_hard_constraints(self, xk, uk=None, timestep=None):
+        """TrajoptConstraint.value_hard_constraints (:210-240), stacked 1-D."""
+        vals = [c.value(z) for _, c, z in self._hard_slices(xk, uk, timestep)]
+        return np.concatenate(vals) if vals else None
+
+    def jacobian_hard_constraints(self, xk, uk=None, timestep=None):
+        """TrajoptConstraint.jacobian_hard_constraints (:242-274): rows over [q; qd; u] (terminal: the
+        state columns)."""
+        n_xu = self.nq + self.nv + self.nu
+        rows = []
+        for kind, c, z in self._hard_slices(xk, uk, timestep):
+            v = c.full_value(z)
+            cs = c.constraint_size
+            col0 = {"joint_limits": 0, "velocity_limits": self.nq, "torque_limits": self.nq + self.nv}[kind]
+            for e in range(2 * cs):
+                active = v[e] < 0
+                if c.mode == "ACTIVE_SET" and not active:
+                    continue
+                r = np.zeros(n_xu)
+                if active:
+                    r[col0 + e % cs] = 1.0 if e < cs else -1.0
+                rows.append(r)
+        if not rows:
+            return None
+        J = np.array(rows)
+        T = self.num_timesteps
+        return J[:, :self.nq + self.nv] if (timestep is not None and timestep >= T - 1) else J
+
     def total_hard_constraints(self, x=None, u=None, timestep=None):
-        if any(c.is_hard_constraint_mode() for _, c in self.limits()):
-            raise NotImplementedError("hard box constraints (ACTIVE_SET / FULL_SET) are not offered on the GPU "
-                                      "path; use QUADRATIC_PENALTY or AUGMENTED_LAGRANGIAN")
-        return 0
+        """TrajoptConstraint.total_hard_constraints (:281-293)."""
+        if not any(c.is_hard_constraint_mode() for _, c in self.limits()):
+            return 0
+        T = self.num_timesteps
+        x = np.asarray(x)
+        ks = range(T) if timestep is None else [timestep]
+        tot = 0
+        for k in ks:
+            v = self.value_hard_constraints(x[:, k], None if (k >= T - 1 or u is None) else np.asarray(u)[:, k], k)
+            tot += 0 if v is None else len(v)
+        return tot
 
     def max_soft_constraint_value(self, x, u):
         m = 0
@@ -205,9 +265,7 @@ class TrajoptConstraint:
         """{joint|velocity|torque: {mode, lb, ub, options}} for Context.set_box_limits."""
         spec = {}
         for kind, c in self.limits():
-            if c.mode not in GPU_SOFT_MODES:
-                if c.is_hard_constraint_mode():
-                    self.total_hard_constraints()
+            if c.mode not in GPU_SOFT_MODES + HARD_MODES:
                 raise NotImplementedError(f"constraint mode {c.mode} is not implemented (the reference exits)")
             if c.constraint_size != self.nq:
                 raise ValueError(f"{kind}: constraint_size {c.constraint_size} != n = {self.nq}")

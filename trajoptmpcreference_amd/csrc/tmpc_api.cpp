@@ -230,6 +230,7 @@ struct Work {
   double *Gk, *jsoft, *smu, *slam;   // soft limits: per-knot Ghat, jacobian, AL constants
   const double* guess;               // PCG initial iterate [B][N nx] (nullable)
   double* lam_keep;                  // where the PCG path stores lambda (nullable; warm start)
+  HardArgs* hard;                    // hard box constraints: the variable-row QP (tmpc_hard.hip)
 };
 
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
@@ -259,6 +260,32 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   } else {
     Timed t(ctx, "ginv");
     LAUNCH_OK(launch_ginv(ctx->stream, nj, ctx->dcost, B, st.rho, st.active, w.G));
+  }
+  if (w.hard) {   // hard box constraints: rows of C per knot, banded S (tmpc_hard.hip)
+    HardArgs h = *w.hard;
+    h.precond = precond;
+    h.Ghat = G;
+    h.per_knot = soft || ctx->hcost.kind == COST_EE;
+    h.A = w.A;
+    h.Bm = w.Bm;
+    h.cvec = w.cvec;
+    h.jsoft = w.jsoft;
+    h.x = d_x;
+    h.u = d_u;
+    h.active = st.active;
+    h.iters = w.iters;
+    h.dx = w.dx;
+    h.du = w.du;
+    h.tol = ctx->opts.exit_tolerance_linSys;
+    h.max_iter = ctx->opts.max_iter_linSys;
+    HIP_OK(hipMemsetAsync(w.iters, 0, sizeof(int) * B, ctx->stream));
+    const char* names[3] = {"hard_schur", precond == 0 ? "hard_direct" : "hard_pcg", "dxu"};
+    for (int ph = 0; ph < 3; ++ph) {
+      Timed t(ctx, names[ph]);
+      h.phase = ph;
+      LAUNCH_OK(launch_hard(ctx->stream, nj, h));
+    }
+    return 0;
   }
   if (precond == 0) {   // method S: Schur blocks -> direct solve -> dxu
     {
@@ -303,7 +330,7 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   BUF(double, du, (size_t)B * K * nj);
   BUF(int, iters, (size_t)B);
   w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters,
-           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (with_blocks) {
     BUF(double, Sdiag, (size_t)B * N * nx * nx);
     BUF(double, Slo, (size_t)B * (K > 0 ? K : 1) * nx * nx);
@@ -365,6 +392,23 @@ static int alloc_soft(tmpc_ctx* ctx, int B, int N, double** mu, double** lam, do
   return 0;
 }
 
+// the hard box-constraint terms of the merit's violation at the line-search trial points
+static int hard_ls(tmpc_ctx* ctx, int nj, const HardArgs& base, int B, int N, int T, const double* alphas, const double* x,
+                   const double* u, double* dx, double* du, const int* active) {
+  HardArgs h = base;
+  h.phase = 3;
+  h.B = B;
+  h.N = N;
+  h.T = T;
+  h.alphas = alphas;
+  h.x = x;
+  h.u = u;
+  h.dx = dx;
+  h.du = du;
+  h.active = active;
+  return launch_hard(ctx->stream, nj, h);
+}
+
 // keep_warm: the PCG warm-start buffer already holds this batch's starting lambdas (MPC loop)
 static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
                       TraceDev* tr_out, bool keep_warm = false) {
@@ -413,7 +457,68 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     w.smu = smu;
     w.slam = slam;
   }
-  if (o.pcg_warm_start && precond != 0) {
+  // hard box constraints (ACTIVE_SET / FULL_SET): per-knot rows, a banded Schur complement per problem
+  HardArgs hard{};
+  double* hterms = nullptr;
+  if (ctx->hlim.any_hard) {
+    int ntypes = 0;
+    bool full = false;
+    for (int t = 0; t < 3; ++t) {
+      if (ctx->hlim.hard[t] != HARD_NONE) ++ntypes;
+      if (ctx->hlim.hard[t] == HARD_FULL) full = true;
+    }
+    if (full && precond != 0)
+      return fail(ctx, "FULL_SET box constraints with a PCG method: the inactive rows of C are zero, so S is "
+                  "singular and the reference's preconditioner raises LinAlgError (PCG.py:168-188); use method S");
+    hard.B = B;
+    hard.N = N;
+    hard.rmax = 2 * nj * ntypes;                 // both bounds of every limited entry, at most
+    hard.dmax = nx * N + N * hard.rmax;
+    const int gmax = nx + 2 * hard.rmax;         // the last group holds two knots' hard rows
+    hard.W = 2 * gmax - 1;
+    if (precond != 0 && (5 * (size_t)hard.dmax + 16) * sizeof(double) > 160 * 1024)
+      return fail(ctx, "hard constraints: Schur dimension up to %d exceeds the PCG's LDS vectors (max 4092)",
+                  hard.dmax);
+    if (hard.W > 1024) return fail(ctx, "hard constraints: band half-width %d > 1024", hard.W);
+    const size_t BW = 2 * (size_t)hard.W + 1, nbmax = hard.dmax / nx + 1;
+    hard.Cs = ctx->dlim;
+    hard.C = ctx->dcost;
+    BUF(int, hd_cnt, (size_t)B * N);
+    BUF(int, hd_col, (size_t)B * N * hard.rmax);
+    BUF(double, hd_sgn, (size_t)B * N * hard.rmax);
+    BUF(double, hd_val, (size_t)B * N * hard.rmax);
+    BUF(int, hd_roff, (size_t)B * N);
+    BUF(int, hd_hoff, (size_t)B * N);
+    BUF(int, hd_dim, (size_t)B);
+    BUF(int, hd_rkind, (size_t)B * hard.dmax);
+    BUF(int, hd_rknot, (size_t)B * hard.dmax);
+    BUF(int, hd_ridx, (size_t)B * hard.dmax);
+    BUF(int, hd_pk, (size_t)B * hard.dmax * 2);
+    BUF(double, hd_Y, (size_t)B * hard.dmax * 2 * (nx + nj));
+    BUF(double, hd_Sb, (size_t)B * hard.dmax * BW);
+    BUF(double, hd_gam, (size_t)B * hard.dmax);
+    BUF(double, hd_lam, (size_t)B * hard.dmax);
+    hard.cnt = hd_cnt; hard.hcol = hd_col; hard.hsgn = hd_sgn; hard.hval = hd_val;
+    hard.roff = hd_roff; hard.hoff = hd_hoff; hard.dim = hd_dim;
+    hard.rkind = hd_rkind; hard.rknot = hd_rknot; hard.ridx = hd_ridx; hard.PK = hd_pk;
+    hard.Y = hd_Y; hard.Sb = hd_Sb; hard.gam = hd_gam; hard.lam = hd_lam;
+    if (precond == 0) {
+      BUF(double, hd_M, (size_t)B * hard.dmax * BW);
+      BUF(double, hd_rhs, (size_t)B * hard.dmax);
+      hard.M = hd_M;
+      hard.rhs = hd_rhs;
+    } else {
+      BUF(double, hd_Pd, (size_t)B * nbmax * nx * nx);
+      BUF(double, hd_Pl, (size_t)B * nbmax * nx * nx);
+      BUF(double, hd_Pt, (size_t)B * nbmax * nx * nx);
+      hard.Pd = hd_Pd; hard.Pl = hd_Pl; hard.Ptmp = hd_Pt;
+    }
+    BUF(double, hd_terms, (size_t)B * T * N);
+    hterms = hd_terms;
+    hard.hterms = hd_terms;
+    w.hard = &hard;
+  }
+  if (o.pcg_warm_start && precond != 0 && !ctx->hlim.any_hard) {
     // PCG warm start: each QP starts from the problem's previous lambda (in place: a workgroup reads
     // its guess before it writes its lambda)
     BUF(double, lam_warm, (size_t)B * N * nx);
@@ -437,21 +542,23 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   // initial J, c, merit (:541-548)
   LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
                             alphas + T, d_x, d_u, w.xs, nullptr, nullptr, st.active, terms));
+  if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, st.active));
   HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
   launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
-                   st, nullptr, tr, active_count, nullptr);
+                   st, nullptr, tr, active_count, nullptr, hterms);
   for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
     if ((rc = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false))) return rc;
     {
       Timed t(ctx, "ls_terms");
       LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
                                 alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
+      if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, T, alphas, d_x, d_u, w.dx, w.du, st.active));
     }
     HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
     {
       Timed t(ctx, "ls_decide");
       launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
-                       st, w.iters, tr, active_count, prob_counters);
+                       st, w.iters, tr, active_count, prob_counters, hterms);
       HIP_OK(hipGetLastError());
     }
     HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -485,6 +592,8 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   int rc = check_ready(ctx, B, N, false);
   if (rc) return rc;
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "iLQR supports QuadraticCost only (UrdfCost: use SQP)");
+  if (ctx->hlim.any_hard)
+    return fail(ctx, "iLQR has no constraint rows: hard box constraints (ACTIVE_SET / FULL_SET) need SQP");
   const int nj = ctx->hmodel.n, nx = 2 * nj, K = N - 1;
   const bool chain = ctx->hmodel.chain != 0;
   const tmpc_options& o = ctx->opts;
@@ -621,6 +730,7 @@ int tmpc_create(int device, tmpc_ctx** out) {
     return -4;
   }
   pcg_set_max_lds();
+  hard_set_max_lds();
   tmpc_default_options(&ctx->opts);
   *out = ctx;
   return 0;
@@ -764,11 +874,16 @@ int tmpc_set_box_limits(tmpc_ctx* ctx, const tmpc_box_limits* L) {
   ConstrDev c{};
   if (L) {
     for (int t = 0; t < 3; ++t) {
-      if (L->mode[t] < TMPC_LIMIT_NONE || L->mode[t] > TMPC_LIMIT_AUGMENTED_LAGRANGIAN)
-        return fail(ctx, "limit %d: mode %d (valid: 0 none, 1 QUADRATIC_PENALTY, 2 AUGMENTED_LAGRANGIAN)", t,
-                    L->mode[t]);
-      c.mode[t] = L->mode[t];
-      if (c.mode[t] != SOFT_NONE) c.any = 1;
+      if (L->mode[t] < TMPC_LIMIT_NONE || L->mode[t] > TMPC_LIMIT_FULL_SET)
+        return fail(ctx, "limit %d: mode %d (valid: 0 none, 1 QUADRATIC_PENALTY, 2 AUGMENTED_LAGRANGIAN, "
+                    "3 ACTIVE_SET, 4 FULL_SET)", t, L->mode[t]);
+      if (L->mode[t] <= TMPC_LIMIT_AUGMENTED_LAGRANGIAN) {
+        c.mode[t] = L->mode[t];
+        if (c.mode[t] != SOFT_NONE) c.any = 1;
+      } else {
+        c.hard[t] = L->mode[t] == TMPC_LIMIT_ACTIVE_SET ? HARD_ACTIVE : HARD_FULL;
+        c.any_hard = 1;
+      }
       for (int i = 0; i < NJMAX; ++i) {
         c.lb[t][i] = L->lb[t][i];
         c.ub[t][i] = L->ub[t][i];
@@ -1086,6 +1201,7 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "tmpc_qp_batch supports QuadraticCost only");
+  if (ctx->hlim.any_hard) return fail(ctx, "tmpc_qp_batch: hard box constraints are solved inside tmpc_sqp_solve_batch");
   const int precond = precond_of(linsys);
   if (precond < 0) return fail(ctx, "linear system method %d is not available on the GPU", linsys);
   if (!rho || !x || !u) return fail(ctx, "null input");

@@ -154,10 +154,15 @@ __device__ __forceinline__ double ee_eval(const CostDev* __restrict__ C, const d
 // e < n the lower half (v = z - lb) and e >= n the upper half (v = ub - z).
 // Joint and velocity limits cover knots 0..N-1, torque limits 0..N-2.
 enum { SOFT_NONE = 0, SOFT_QP = 1, SOFT_AL = 2 };
+// hard modes (BoxConstraint ACTIVE_SET / FULL_SET, TrajoptConstraint.py:27-30,64-68,110-113):
+// rows of C / c per knot, tmpc_hard.hip
+enum { HARD_NONE = 0, HARD_ACTIVE = 1, HARD_FULL = 2 };
 
 struct ConstrDev {
   int mode[3];              // SOFT_* per type
   int any;                  // some type is soft
+  int hard[3];              // HARD_* per type (a type is soft or hard, not both)
+  int any_hard;             // some type is hard
   double lb[3][NJMAX], ub[3][NJMAX];
   double mu_init[3], mu_factor[3], mu_max[3], phi_init[3], phi_factor[3];   // BoxConstraint options (:38-46)
 };

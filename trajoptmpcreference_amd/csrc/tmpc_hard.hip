@@ -1,0 +1,687 @@
+// Hard box constraints (BoxConstraint ACTIVE_SET / FULL_SET) in the SQP QP, for gfx950.
+//
+// The reference appends each knot's constraint rows to C right after that knot's
+// dynamics rows (formKKTSystemBlocks, TrajoptMPCReference.py:238-248, 262-270), so
+// the Schur complement S = -C G^-1 C^T (:415-424) changes size every SQP iteration
+// and per problem.  In that row order
+//     R_0 | R_1 H_0 | R_2 H_1 | ... | R_{N-1} H_{N-2} H_{N-1}
+// (R_j the nx dynamics rows that define x_j, H_k knot k's hard rows) the groups
+// touch the knot variables {0}, {0,1}, {1,2}, ..., so S is block-tridiagonal with
+// VARIABLE block sizes: every row couples only with rows less than twice the
+// largest group away.  S is therefore stored as a band [dim][2W+1] per problem.
+// The reference's PCG preconditioner, however, cuts S into nx-aligned blocks from
+// row 0 (n_blocks = floor(dim / nx), PCG.py:182-212), which no longer line up with
+// the groups; it is reproduced exactly on the band (trailing dim mod nx rows have
+// zero preconditioner rows, as in the reference).
+//
+// Kernels (one problem per workgroup except the per-knot row selection):
+//   k_hard_rows     lane = (problem, knot): the knot's rows in the reference's order
+//                   (TrajoptConstraint.value_hard_constraints / jacobian_hard_constraints,
+//                   :53-128, 210-274): joint, velocity, torque; [z - lb; ub - z];
+//                   ACTIVE_SET keeps the entries < 0, FULL_SET all of them
+//   k_hard_layout   row offsets of the groups, dim, and a per-row table (kind, knot, index)
+//   k_hard_schur    per row its G^-1-weighted coefficient pieces, then the S band and gamma
+//   k_hard_pcg      preconditioner (0 / J / BJ / SS on nx-aligned blocks) + PCG (PCG.py:66-111)
+//   k_hard_direct   method S: banded elimination (S negative definite: no pivoting); FULL_SET's
+//                   zero rows get lambda = 0 (the reference's lstsq fallback, :431-436)
+//   k_hard_dxu      dxu_k = Ghat_k (g_k - (C^T lambda)_k)
+//   k_hard_ls       the hard terms of totalHardConstraintViolation (:286-293) per trial point
+// Parity of these semantics is pinned for the 1-link arm by tests/golden/hard_*.npz.
+#include "tmpc_internal.h"
+
+namespace tmpc {
+
+__device__ __forceinline__ bool h_use_QF(const CostDev* C, int k, int N) {
+  return (k == N - 1) || (C->QF_start >= 0 && k >= C->QF_start);
+}
+
+// the knot's rows in the reference order; returns the count (<= rmax)
+template <int NJ>
+__device__ __forceinline__ int hard_knot_rows(const ConstrDev* __restrict__ Cs, const double* z, bool terminal,
+                                              int rmax, int* col, double* sgn, double* val) {
+  int m = 0;
+  for (int t = 0; t < 3; ++t) {
+    const int hm = Cs->hard[t];
+    if (hm == HARD_NONE || (t == 2 && terminal)) continue;
+    for (int e = 0; e < 2 * NJ; ++e) {
+      const int i = e < NJ ? e : e - NJ;
+      const double zi = z[t * NJ + i];
+      const double v = e < NJ ? zi - Cs->lb[t][i] : Cs->ub[t][i] - zi;
+      const bool act = v < 0.0;
+      if (hm == HARD_ACTIVE && !act) continue;
+      if (m < rmax) {
+        col[m] = t * NJ + i;
+        sgn[m] = act ? (e < NJ ? 1.0 : -1.0) : 0.0;
+        val[m] = v;
+      }
+      ++m;
+    }
+  }
+  return m;
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(256) k_hard_rows(const ConstrDev* __restrict__ Cs, int B, int N, int rmax,
+                                                   const double* __restrict__ x, const double* __restrict__ u,
+                                                   const int* __restrict__ active, int* __restrict__ cnt,
+                                                   int* __restrict__ hcol, double* __restrict__ hsgn,
+                                                   double* __restrict__ hval) {
+  constexpr int NX = 2 * NJ;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * N) return;
+  const int b = gid / N, k = gid - b * N;
+  if (!active[b]) return;
+  const int K = N - 1;
+  double z[3 * NJ];
+  for (int m = 0; m < NX; ++m) z[m] = x[((size_t)b * NX + m) * N + k];
+  for (int m = 0; m < NJ; ++m) z[NX + m] = k < K ? u[((size_t)b * NJ + m) * K + k] : 0.0;
+  const size_t o = (size_t)gid * rmax;
+  cnt[gid] = hard_knot_rows<NJ>(Cs, z, k == K, rmax, hcol + o, hsgn + o, hval + o);
+}
+
+// Row layout of one problem: roff[j] = first row of R_j, hoff[k] = first row of H_k, dim;
+// per row: kind (0 dynamics / initial, 1 hard), knot (j for R_j, k for H_k), index.
+__global__ void __launch_bounds__(64) k_hard_layout(int B, int N, int NX, int rmax, const int* __restrict__ active,
+                                                    const int* __restrict__ cnt, int* __restrict__ roff,
+                                                    int* __restrict__ hoff, int* __restrict__ dim,
+                                                    int* __restrict__ rkind, int* __restrict__ rknot,
+                                                    int* __restrict__ ridx, int dmax) {
+  const int b = blockIdx.x;
+  if (!active[b]) return;
+  __shared__ int s_dim;
+  int* ro = roff + (size_t)b * N;
+  int* ho = hoff + (size_t)b * N;
+  const int* cb = cnt + (size_t)b * N;
+  if (threadIdx.x == 0) {
+    int row = 0;
+    ro[0] = 0;
+    row = NX;
+    for (int j = 1; j < N; ++j) {
+      ro[j] = row;
+      row += NX;
+      ho[j - 1] = row;
+      row += cb[j - 1];
+    }
+    ho[N - 1] = row;
+    row += cb[N - 1];
+    dim[b] = row;
+    s_dim = row;
+  }
+  __syncthreads();
+  int* rk = rkind + (size_t)b * dmax;
+  int* rn = rknot + (size_t)b * dmax;
+  int* ri = ridx + (size_t)b * dmax;
+  for (int j = 0; j < N; ++j) {
+    for (int i = threadIdx.x; i < NX; i += blockDim.x) {
+      rk[ro[j] + i] = 0;
+      rn[ro[j] + i] = j;
+      ri[ro[j] + i] = i;
+    }
+    for (int i = threadIdx.x; i < cb[j]; i += blockDim.x) {
+      rk[ho[j] + i] = 1;
+      rn[ho[j] + i] = j;
+      ri[ho[j] + i] = i;
+    }
+  }
+  (void)s_dim;
+}
+
+// Ghat blocks: the three distinct QuadraticCost blocks [B][3][NX*NX] (Q, QF, R), or per knot
+// [B][N][NX*NX + NU*NU] with soft limits (k_ginv / k_ginv_soft layouts)
+template <int NJ>
+struct HGhat {
+  static constexpr int NX = 2 * NJ, NU = NJ, GS = NX * NX + NU * NU;
+  const double* base;
+  bool pk;
+  __device__ __forceinline__ const double* x(const CostDev* C, int k, int N) const {
+    return pk ? base + (size_t)k * GS : base + (h_use_QF(C, k, N) ? NX * NX : 0);
+  }
+  __device__ __forceinline__ const double* u(int k) const {
+    return pk ? base + (size_t)k * GS + NX * NX : base + 2 * NX * NX;
+  }
+};
+
+// the cost gradient g_k = [(x_k - xg)^T Q_k, u_k^T R] (+ soft jacobian; UrdfCost's x part in jsoft)
+template <int NJ>
+__device__ __forceinline__ double hard_grad(const CostDev* __restrict__ C, const double* xb, const double* ub,
+                                            const double* js, int N, int k, int c) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int K = N - 1;
+  double g = 0.0;
+  if (c < NX) {
+    if (C->kind == COST_EE) return js ? js[k * (NX + NU) + c] : 0.0;
+    const double* Qk = h_use_QF(C, k, N) ? C->QF : C->Q;
+    for (int m = 0; m < NX; ++m) g += (xb[m * N + k] - C->xg[m]) * Qk[m * NX + c];
+  } else if (k < K) {
+    for (int m = 0; m < NU; ++m) g += ub[m * K + k] * C->R[m * NU + (c - NX)];
+  }
+  if (js) g = g + js[k * (NX + NU) + c];
+  return g;
+}
+
+// piece p of row a: the knot and the coefficient vector over [x_knot; u_knot]
+//   R_0 row i: (0, e_i);  R_j row i: (j-1, -[A_{j-1} B_{j-1}] row i), (j, e_i);  H_k row s: (k, sgn e_col)
+template <int NJ>
+__device__ __forceinline__ int row_piece(int kind, int knot, int idx, int p, const double* __restrict__ A,
+                                         const double* __restrict__ Bm, const int* hcol, const double* hsgn,
+                                         double (&cf)[3 * NJ]) {
+  constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
+  for (int m = 0; m < NXU; ++m) cf[m] = 0.0;
+  if (kind == 1) {
+    if (p) return -1;
+    cf[hcol[idx]] = hsgn[idx];
+    return knot;
+  }
+  if (knot == 0 || p == 1) {
+    if (knot == 0 && p == 1) return -1;
+    cf[idx] = 1.0;
+    return knot;
+  }
+  const double* Ak = A + (size_t)(knot - 1) * NX * NX;
+  const double* Bk = Bm + (size_t)(knot - 1) * NX * NU;
+  for (int m = 0; m < NX; ++m) cf[m] = -Ak[idx * NX + m];
+  for (int m = 0; m < NU; ++m) cf[NX + m] = -Bk[idx * NU + m];
+  return knot - 1;
+}
+
+// y = Ghat_k cf over [x; u] (terminal knot: x block only)
+template <int NJ>
+__device__ __forceinline__ void ghat_apply(const CostDev* C, const HGhat<NJ>& Gh, int k, int N,
+                                           const double (&cf)[3 * NJ], double (&y)[3 * NJ]) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const double* Gx = Gh.x(C, k, N);
+  for (int r = 0; r < NX; ++r) {
+    double acc = 0.0;
+    for (int c = 0; c < NX; ++c) acc += Gx[r * NX + c] * cf[c];
+    y[r] = acc;
+  }
+  if (k < N - 1) {
+    const double* Gu = Gh.u(k);
+    for (int r = 0; r < NU; ++r) {
+      double acc = 0.0;
+      for (int c = 0; c < NU; ++c) acc += Gu[r * NU + c] * cf[NX + c];
+      y[NX + r] = acc;
+    }
+  } else {
+    for (int r = 0; r < NU; ++r) y[NX + r] = 0.0;
+  }
+}
+
+// S band and gamma.  Phase 1: per row and piece, Y = Ghat cf (global scratch [dmax][2][NXU] per
+// problem); phase 2: S_ab = -sum over shared knots cf_a . Y_b, gamma_a = c_a - sum_p Y_a . g.
+template <int NJ>
+__global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ C, int B, int N, int W, int dmax,
+                                                    int rmax, const int* __restrict__ active,
+                                                    const double* __restrict__ Ghat, int per_knot,
+                                                    const double* __restrict__ Aall, const double* __restrict__ Ball,
+                                                    const double* __restrict__ cvec, const double* __restrict__ x,
+                                                    const double* __restrict__ u, const double* __restrict__ jsoft,
+                                                    const int* __restrict__ dim, const int* __restrict__ rkind,
+                                                    const int* __restrict__ rknot, const int* __restrict__ ridx,
+                                                    const int* __restrict__ hoff, const int* __restrict__ hcol,
+                                                    const double* __restrict__ hsgn, const double* __restrict__ hval,
+                                                    double* __restrict__ Y, int* __restrict__ PK,
+                                                    double* __restrict__ Sb, double* __restrict__ gam) {
+  constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
+  const int b = blockIdx.x;
+  if (!active[b]) return;
+  const int K = N - 1;
+  const int D = dim[b];
+  const double* A = Aall + (size_t)b * K * NX * NX;
+  const double* Bm = Ball + (size_t)b * K * NX * NU;
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NU * K;
+  const double* js = jsoft ? jsoft + (size_t)b * N * NXU : nullptr;
+  const HGhat<NJ> Gh{per_knot ? Ghat + (size_t)b * N * HGhat<NJ>::GS : Ghat + (size_t)b * 3 * NX * NX, per_knot != 0};
+  const int* rk = rkind + (size_t)b * dmax;
+  const int* rn = rknot + (size_t)b * dmax;
+  const int* ri = ridx + (size_t)b * dmax;
+  double* Yb = Y + (size_t)b * dmax * 2 * NXU;
+  int* PKb = PK + (size_t)b * dmax * 2;
+  const size_t hb = (size_t)b * N * rmax;
+  // phase 1
+  for (int a = threadIdx.x; a < D; a += blockDim.x) {
+    const int kind = rk[a], knot = rn[a], idx = ri[a];
+    const int* hc = hcol + hb + (size_t)knot * rmax;
+    const double* hs = hsgn + hb + (size_t)knot * rmax;
+    double g_dot = 0.0;
+    for (int p = 0; p < 2; ++p) {
+      double cf[3 * NJ], y[3 * NJ];
+      const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
+      PKb[a * 2 + p] = kp;
+      if (kp < 0) continue;
+      ghat_apply<NJ>(C, Gh, kp, N, cf, y);
+      for (int m = 0; m < NXU; ++m) Yb[((size_t)a * 2 + p) * NXU + m] = y[m];
+      double s = 0.0;
+      for (int m = 0; m < NXU; ++m) s += y[m] * (m < NX || kp < K ? hard_grad<NJ>(C, xb, ub, js, N, kp, m) : 0.0);
+      g_dot += s;
+    }
+    double ca;
+    if (kind == 0) ca = cvec[((size_t)b * N + knot) * NX + idx];
+    else ca = hval[hb + (size_t)knot * rmax + idx];
+    gam[(size_t)b * dmax + a] = ca - g_dot;
+  }
+  __syncthreads();
+  // phase 2: the band, row a, column c = a - W + o
+  const int BW = 2 * W + 1;
+  double* S = Sb + (size_t)b * dmax * BW;
+  for (int e = threadIdx.x; e < D * BW; e += blockDim.x) {
+    const int a = e / BW, o = e - a * BW;
+    const int c = a - W + o;
+    double s = 0.0;
+    if (c >= 0 && c < D) {
+      const int kind = rk[a], knot = rn[a], idx = ri[a];
+      const int* hc = hcol + hb + (size_t)knot * rmax;
+      const double* hs = hsgn + hb + (size_t)knot * rmax;
+      for (int p = 0; p < 2; ++p) {
+        double cf[3 * NJ];
+        const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
+        if (kp < 0) continue;
+        for (int q = 0; q < 2; ++q) {
+          if (PKb[c * 2 + q] != kp) continue;
+          const double* y = Yb + ((size_t)c * 2 + q) * NXU;
+          double d = 0.0;
+          for (int m = 0; m < NXU; ++m) d += cf[m] * y[m];
+          s += d;
+        }
+      }
+      s = -s;
+    }
+    S[(size_t)a * BW + o] = s;
+  }
+}
+
+// ---- workgroup sum (deterministic): wave DPP butterfly via shuffles + fixed-order fan-in
+__device__ __forceinline__ double h_block_sum(double v, double* red) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+__device__ __forceinline__ double band_at(const double* S, int BW, int W, int r, int c) {
+  const int o = c - r + W;
+  return (o >= 0 && o < BW) ? S[(size_t)r * BW + o] : 0.0;
+}
+
+// In-place Gauss-Jordan inverse of a small block (global memory, one thread), the operation order of
+// the augmented [M | I] elimination (no pivoting: principal blocks of the negative definite S).
+__device__ void h_gj_inverse(double* M, int n) {
+  for (int p = 0; p < n; ++p) {
+    const double d = M[p * n + p];
+    for (int j = 0; j < n; ++j) M[p * n + j] = (j == p) ? 1.0 / d : M[p * n + j] / d;
+    for (int r = 0; r < n; ++r) {
+      if (r == p) continue;
+      const double f = M[r * n + p];
+      M[r * n + p] = 0.0;
+      for (int j = 0; j < n; ++j) M[r * n + j] -= f * M[p * n + j];
+    }
+  }
+}
+
+// out = -(X (Y Z)) for n x n blocks (row-major), one thread
+__device__ void h_neg_triple(const double* X, const double* Yy, const double* Z, double* out, int n) {
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) {
+      double acc = 0.0;
+      for (int m = 0; m < n; ++m) {
+        double yz = 0.0;
+        for (int l = 0; l < n; ++l) yz += Yy[m * n + l] * Z[l * n + c];
+        acc += X[r * n + m] * yz;
+      }
+      out[r * n + c] = -acc;
+    }
+}
+
+// Preconditioner (compute_preconditioner on the dense S, PCG.py:113-212) + PCG (:66-111).
+// Pd [nb][NX][NX] diagonal inverses, Pl [nb-1][NX][NX] = P_{k+1,k} (P_{k,k+1} = Pl[k]^T: the
+// reference copies transposes), scratch [NX][NX] per problem for the off-diagonal products.
+template <int NX>
+__global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int precond, const int* __restrict__ active,
+                                                  const int* __restrict__ dim, const double* __restrict__ Sb,
+                                                  const double* __restrict__ gam, double tol, int max_iter,
+                                                  double* __restrict__ Pd, double* __restrict__ Pl,
+                                                  double* __restrict__ Ptmp, double* __restrict__ lam,
+                                                  int* __restrict__ iters) {
+  const int b = blockIdx.x;
+  if (!active[b]) return;
+  const int D = dim[b];
+  const int BW = 2 * W + 1;
+  const int nb = D / NX;
+  const double* S = Sb + (size_t)b * dmax * BW;
+  const size_t nbmax = dmax / NX + 1;
+  double* P = Pd + (size_t)b * nbmax * NX * NX;
+  double* PL = Pl + (size_t)b * nbmax * NX * NX;
+  double* T = Ptmp + (size_t)b * nbmax * NX * NX;
+  extern __shared__ __align__(16) double sh[];
+  double* xv = sh;
+  double* rv = xv + dmax;
+  double* pv = rv + dmax;
+  double* zv = pv + dmax;
+  double* av = zv + dmax;
+  double* red = av + dmax;
+  const bool blocks = precond == PRECOND_BJ || precond == PRECOND_SS;
+  if (blocks) {
+    for (int k = threadIdx.x; k < nb; k += blockDim.x) {
+      double* M = P + (size_t)k * NX * NX;
+      for (int i = 0; i < NX; ++i)
+        for (int j = 0; j < NX; ++j) M[i * NX + j] = band_at(S, BW, W, k * NX + i, k * NX + j);
+      h_gj_inverse(M, NX);
+    }
+    __syncthreads();
+    if (precond == PRECOND_SS) {
+      for (int k = 1 + threadIdx.x; k < nb; k += blockDim.x) {
+        double* Sk = T + (size_t)k * NX * NX;
+        if (k & 1) {   // P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1})
+          for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, BW, W, k * NX + i, (k - 1) * NX + j);
+          h_neg_triple(P + (size_t)k * NX * NX, Sk, P + (size_t)(k - 1) * NX * NX, PL + (size_t)(k - 1) * NX * NX, NX);
+        } else {       // P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk); stored as its transpose P_{k,k-1}
+          for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, BW, W, (k - 1) * NX + i, k * NX + j);
+          double prod[NX * NX];
+          h_neg_triple(P + (size_t)(k - 1) * NX * NX, Sk, P + (size_t)k * NX * NX, prod, NX);
+          for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NX; ++j) PL[(size_t)(k - 1) * NX * NX + j * NX + i] = prod[i * NX + j];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // PCG, x0 = 0
+  auto apply_P = [&](const double* r, double* z) {
+    for (int a = threadIdx.x; a < D; a += blockDim.x) {
+      double s;
+      if (precond == PRECOND_NONE) {
+        s = r[a];
+      } else if (precond == PRECOND_J) {
+        s = (1.0 / band_at(S, BW, W, a, a)) * r[a];
+      } else if (a >= nb * NX) {
+        s = 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
+      } else {
+        const int k = a / NX, i = a - k * NX;
+        const double* M = P + (size_t)k * NX * NX;
+        s = 0.0;
+        for (int j = 0; j < NX; ++j) s += M[i * NX + j] * r[k * NX + j];
+        if (precond == PRECOND_SS) {
+          if (k > 0) {
+            const double* L = PL + (size_t)(k - 1) * NX * NX;
+            for (int j = 0; j < NX; ++j) s += L[i * NX + j] * r[(k - 1) * NX + j];
+          }
+          if (k + 1 < nb) {
+            const double* U = PL + (size_t)k * NX * NX;   // P_{k,k+1} = P_{k+1,k}^T
+            for (int j = 0; j < NX; ++j) s += U[j * NX + i] * r[(k + 1) * NX + j];
+          }
+        }
+      }
+      z[a] = s;
+    }
+  };
+  auto spmv = [&](const double* v, double* out) {
+    for (int a = threadIdx.x; a < D; a += blockDim.x) {
+      double s = 0.0;
+      const int c0 = a - W > 0 ? a - W : 0, c1 = a + W < D - 1 ? a + W : D - 1;
+      for (int c = c0; c <= c1; ++c) s += S[(size_t)a * BW + (c - a + W)] * v[c];
+      out[a] = s;
+    }
+  };
+  const double* g = gam + (size_t)b * dmax;
+  for (int a = threadIdx.x; a < D; a += blockDim.x) {
+    xv[a] = 0.0;
+    rv[a] = g[a];
+  }
+  __syncthreads();
+  apply_P(rv, zv);
+  __syncthreads();
+  double part = 0.0;
+  for (int a = threadIdx.x; a < D; a += blockDim.x) {
+    pv[a] = zv[a];
+    part += rv[a] * zv[a];
+  }
+  double nu = h_block_sum(part, red);
+  int it_done = max_iter;
+  for (int it = 0; it < max_iter; ++it) {
+    __syncthreads();
+    spmv(pv, av);
+    part = 0.0;
+    for (int a = threadIdx.x; a < D; a += blockDim.x) part += pv[a] * av[a];
+    const double alpha = nu / h_block_sum(part, red);
+    for (int a = threadIdx.x; a < D; a += blockDim.x) {
+      rv[a] = rv[a] - av[a] * alpha;
+      xv[a] = xv[a] + pv[a] * alpha;
+    }
+    __syncthreads();
+    apply_P(rv, zv);
+    __syncthreads();
+    part = 0.0;
+    for (int a = threadIdx.x; a < D; a += blockDim.x) part += rv[a] * zv[a];
+    const double nup = h_block_sum(part, red);
+    if (fabs(nup) < tol) {
+      it_done = it + 1;
+      break;
+    }
+    const double beta = nup / nu;
+    for (int a = threadIdx.x; a < D; a += blockDim.x) pv[a] = zv[a] + pv[a] * beta;
+    nu = nup;
+  }
+  __syncthreads();
+  for (int a = threadIdx.x; a < D; a += blockDim.x) lam[(size_t)b * dmax + a] = xv[a];
+  if (threadIdx.x == 0) iters[b] = it_done;
+}
+
+// Method S: S lambda = gamma by banded elimination (S is negative definite: no pivoting).  Rows
+// that are identically zero (FULL_SET's inactive constraints) get lambda = 0: the minimum-norm
+// least-squares answer of the reference's lstsq fallback (:431-436).
+__global__ void __launch_bounds__(256) k_hard_direct(int B, int W, int dmax, const int* __restrict__ active,
+                                                     const int* __restrict__ dim, const double* __restrict__ Sb,
+                                                     const double* __restrict__ gam, double* __restrict__ M,
+                                                     double* __restrict__ rhs, double* __restrict__ lam) {
+  const int b = blockIdx.x;
+  if (!active[b]) return;
+  const int D = dim[b];
+  const int BW = 2 * W + 1;
+  const double* S = Sb + (size_t)b * dmax * BW;
+  double* Mb = M + (size_t)b * dmax * BW;
+  double* y = rhs + (size_t)b * dmax;
+  __shared__ double fcol[1024];
+  __shared__ double red[16];
+  for (int e = threadIdx.x; e < D * BW; e += blockDim.x) Mb[e] = S[e];
+  for (int a = threadIdx.x; a < D; a += blockDim.x) y[a] = gam[(size_t)b * dmax + a];
+  __syncthreads();
+  // zero rows -> identity rows with a zero right-hand side
+  for (int a = threadIdx.x; a < D; a += blockDim.x) {
+    bool zero = true;
+    for (int o = 0; o < BW; ++o) zero = zero && Mb[(size_t)a * BW + o] == 0.0;
+    if (zero) {
+      Mb[(size_t)a * BW + W] = 1.0;
+      y[a] = 0.0;
+    }
+  }
+  __syncthreads();
+  for (int p = 0; p < D; ++p) {
+    const int r1 = p + W < D - 1 ? p + W : D - 1;
+    const double piv = Mb[(size_t)p * BW + W];
+    for (int r = p + 1 + threadIdx.x; r <= r1; r += blockDim.x) fcol[r - p - 1] = Mb[(size_t)r * BW + (p - r + W)] / piv;
+    __syncthreads();
+    const int nr = r1 - p, nc = r1 - p + 1;
+    for (int e = threadIdx.x; e < nr * nc; e += blockDim.x) {
+      const int r = p + 1 + e / nc, c = p + e % nc;
+      const int oc = c - r + W;
+      if (oc < 0 || oc >= BW) continue;
+      const double f = fcol[r - p - 1];
+      Mb[(size_t)r * BW + oc] -= f * Mb[(size_t)p * BW + (c - p + W)];
+    }
+    for (int r = p + 1 + threadIdx.x; r <= r1; r += blockDim.x) y[r] -= fcol[r - p - 1] * y[p];
+    __syncthreads();
+  }
+  // back substitution
+  for (int p = D - 1; p >= 0; --p) {
+    const int c1 = p + W < D - 1 ? p + W : D - 1;
+    double part = 0.0;
+    for (int c = p + 1 + threadIdx.x; c <= c1; c += blockDim.x) part += Mb[(size_t)p * BW + (c - p + W)] * y[c];
+    const double s = h_block_sum(part, red);
+    if (threadIdx.x == 0) y[p] = (y[p] - s) / Mb[(size_t)p * BW + W];
+    __syncthreads();
+  }
+  for (int a = threadIdx.x; a < D; a += blockDim.x) lam[(size_t)b * dmax + a] = y[a];
+}
+
+// dxu_k = Ghat_k (g_k - (C^T lambda)_k) (:449-452), lane = (problem, knot)
+template <int NJ>
+__global__ void __launch_bounds__(64) k_hard_dxu(const CostDev* __restrict__ C, int B, int N, int dmax, int rmax,
+                                                 const int* __restrict__ active, const double* __restrict__ Ghat,
+                                                 int per_knot, const double* __restrict__ Aall,
+                                                 const double* __restrict__ Ball, const double* __restrict__ x,
+                                                 const double* __restrict__ u, const double* __restrict__ jsoft,
+                                                 const int* __restrict__ roff, const int* __restrict__ hoff,
+                                                 const int* __restrict__ cnt, const int* __restrict__ hcol,
+                                                 const double* __restrict__ hsgn, const double* __restrict__ lam,
+                                                 double* __restrict__ dx, double* __restrict__ du) {
+  constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * N) return;
+  const int b = gid / N, k = gid - b * N;
+  if (!active[b]) return;
+  const int K = N - 1;
+  const double* L = lam + (size_t)b * dmax;
+  const int* ro = roff + (size_t)b * N;
+  const int* ho = hoff + (size_t)b * N;
+  double ctl[3 * NJ];
+  for (int m = 0; m < NXU; ++m) ctl[m] = 0.0;
+  for (int i = 0; i < NX; ++i) ctl[i] = L[ro[k] + i];
+  if (k < K) {
+    const double* A = Aall + ((size_t)b * K + k) * NX * NX;
+    const double* Bk = Ball + ((size_t)b * K + k) * NX * NU;
+    const double* l1 = L + ro[k + 1];
+    for (int j = 0; j < NX; ++j) {
+      double atl = 0.0;
+      for (int m = 0; m < NX; ++m) atl += A[m * NX + j] * l1[m];
+      ctl[j] = ctl[j] - atl;
+    }
+    for (int j = 0; j < NU; ++j) {
+      double btl = 0.0;
+      for (int m = 0; m < NX; ++m) btl += Bk[m * NU + j] * l1[m];
+      ctl[NX + j] = -btl;
+    }
+  }
+  const size_t hb = ((size_t)b * N + k) * rmax;
+  for (int s = 0; s < cnt[(size_t)b * N + k]; ++s) ctl[hcol[hb + s]] += hsgn[hb + s] * L[ho[k] + s];
+  const HGhat<NJ> Gh{per_knot ? Ghat + (size_t)b * N * HGhat<NJ>::GS : Ghat + (size_t)b * 3 * NX * NX, per_knot != 0};
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NU * K;
+  const double* js = jsoft ? jsoft + (size_t)b * N * NXU : nullptr;
+  double rhs[3 * NJ];
+  for (int m = 0; m < NXU; ++m) rhs[m] = (m < NX || k < K) ? hard_grad<NJ>(C, xb, ub, js, N, k, m) - ctl[m] : 0.0;
+  const double* Gx = Gh.x(C, k, N);
+  for (int i = 0; i < NX; ++i) {
+    double acc = 0.0;
+    for (int j = 0; j < NX; ++j) acc += Gx[i * NX + j] * rhs[j];
+    dx[((size_t)b * N + k) * NX + i] = acc;
+  }
+  if (k < K) {
+    const double* Gu = Gh.u(k);
+    for (int i = 0; i < NU; ++i) {
+      double acc = 0.0;
+      for (int j = 0; j < NU; ++j) acc += Gu[i * NU + j] * rhs[NX + j];
+      du[((size_t)b * K + k) * NU + i] = acc;
+    }
+  }
+}
+
+// totalHardConstraintViolation's hard terms (:286-293): per trial point and knot,
+// sum(map(abs, value_hard_constraints)) in the reference's row order; hterms [B][T][N]
+template <int NJ>
+__global__ void __launch_bounds__(256) k_hard_ls(const ConstrDev* __restrict__ Cs, int B, int N, int T,
+                                                 const double* __restrict__ alphas, const double* __restrict__ x,
+                                                 const double* __restrict__ u, const double* __restrict__ dx,
+                                                 const double* __restrict__ du, const int* __restrict__ active,
+                                                 double* __restrict__ hterms) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * T * N) return;
+  const int k = gid % N, bt = gid / N, b = bt / T, t = bt - b * T;
+  if (!active[b]) return;
+  const int K = N - 1;
+  const double al = alphas[t];
+  double z[3 * NJ];
+  for (int m = 0; m < NX; ++m) {
+    const double xm = x[((size_t)b * NX + m) * N + k];
+    z[m] = dx ? xm - al * dx[((size_t)b * N + k) * NX + m] : xm;
+  }
+  for (int m = 0; m < NU; ++m) {
+    double um = k < K ? u[((size_t)b * NU + m) * K + k] : 0.0;
+    if (dx && k < K) um = um - al * du[((size_t)b * K + k) * NU + m];
+    z[NX + m] = um;
+  }
+  int col[6 * NJ];
+  double sg[6 * NJ], val[6 * NJ];
+  const int m = hard_knot_rows<NJ>(Cs, z, k == K, 6 * NJ, col, sg, val);
+  double s = 0.0;
+  for (int i = 0; i < m; ++i) s += fabs(val[i]);
+  hterms[gid] = s;
+}
+
+// ---------------------------------------------------------------- launchers
+#define HGRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
+
+template <int NJ>
+struct LaunchHard {
+  static void run(hipStream_t s, const HardArgs& h) {
+    constexpr int NX = 2 * NJ;
+    const int B = h.B, N = h.N;
+    if (h.phase == 0) {
+      hipLaunchKernelGGL((k_hard_rows<NJ>), HGRID(B * N, 256), 0, s, h.Cs, B, N, h.rmax, h.x, h.u, h.active, h.cnt,
+                         h.hcol, h.hsgn, h.hval);
+      hipLaunchKernelGGL(k_hard_layout, dim3(B), dim3(64), 0, s, B, N, NX, h.rmax, h.active, h.cnt, h.roff, h.hoff,
+                         h.dim, h.rkind, h.rknot, h.ridx, h.dmax);
+      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), 0, s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
+                         h.per_knot, h.A, h.Bm, h.cvec, h.x, h.u, h.jsoft, h.dim, h.rkind, h.rknot, h.ridx, h.hoff,
+                         h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam);
+    } else if (h.phase == 1) {
+      if (h.precond == 0) {
+        hipLaunchKernelGGL(k_hard_direct, dim3(B), dim3(256), 0, s, B, h.W, h.dmax, h.active, h.dim, h.Sb, h.gam, h.M,
+                           h.rhs, h.lam);
+      } else {
+        const size_t lds = ((size_t)5 * h.dmax + 16) * sizeof(double);
+        hipLaunchKernelGGL((k_hard_pcg<NX>), dim3(B), dim3(256), lds, s, B, h.W, h.dmax, h.precond, h.active, h.dim,
+                           h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, h.Ptmp, h.lam, h.iters);
+      }
+    } else if (h.phase == 2) {
+      hipLaunchKernelGGL((k_hard_dxu<NJ>), HGRID(B * N, 64), 0, s, h.C, B, N, h.dmax, h.rmax, h.active, h.Ghat,
+                         h.per_knot, h.A, h.Bm, h.x, h.u, h.jsoft, h.roff, h.hoff, h.cnt, h.hcol, h.hsgn, h.lam, h.dx,
+                         h.du);
+    } else {
+      hipLaunchKernelGGL((k_hard_ls<NJ>), HGRID(B * h.T * N, 256), 0, s, h.Cs, B, N, h.T, h.alphas, h.x, h.u, h.dx,
+                         h.du, h.active, h.hterms);
+    }
+  }
+};
+
+int launch_hard(hipStream_t s, int nj, const HardArgs& h) {
+  switch (nj) {
+    case 1: LaunchHard<1>::run(s, h); break;
+    case 2: LaunchHard<2>::run(s, h); break;
+    case 3: LaunchHard<3>::run(s, h); break;
+    case 4: LaunchHard<4>::run(s, h); break;
+    case 5: LaunchHard<5>::run(s, h); break;
+    case 6: LaunchHard<6>::run(s, h); break;
+    case 7: LaunchHard<7>::run(s, h); break;
+    default: return -2;
+  }
+  return 0;
+}
+
+int hard_set_max_lds() {
+  const int bytes = 160 * 1024;
+  int err = 0;
+#define SETH(V) err |= (int)hipFuncSetAttribute((const void*)k_hard_pcg<V>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  SETH(2) SETH(4) SETH(6) SETH(8) SETH(10) SETH(12) SETH(14)
+#undef SETH
+  return err;
+}
+
+}  // namespace tmpc

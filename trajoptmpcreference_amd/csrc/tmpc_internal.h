@@ -102,7 +102,7 @@ void launch_sum_counters(hipStream_t s, int B, const unsigned long long* pc, uns
 void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
-                      int* active_count, unsigned long long* counters);
+                      int* active_count, unsigned long long* counters, const double* hterms);
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active);
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
                        const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
@@ -125,5 +125,20 @@ void launch_soft_shift(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj,
 void launch_outer_init(hipStream_t s, int B, int* outer_active, int* outer_iter, int* exit_soft);
 void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, double* mu, double* lam,
                       double* phi);
+
+// Hard box constraints (tmpc_hard.hip): one argument block for its four launch phases
+// (0 rows + layout + Schur band, 1 PCG / direct solve, 2 dxu, 3 line-search terms).
+struct HardArgs {
+  int B, N, T, phase, precond, rmax, dmax, W, per_knot, max_iter;
+  double tol;
+  const ConstrDev* Cs;
+  const CostDev* C;
+  const double *x, *u, *Ghat, *A, *Bm, *cvec, *jsoft, *alphas;
+  const int* active;
+  int *cnt, *hcol, *roff, *hoff, *dim, *rkind, *rknot, *ridx, *PK, *iters;
+  double *hsgn, *hval, *Y, *Sb, *gam, *Pd, *Pl, *Ptmp, *M, *rhs, *lam, *dx, *du, *hterms;
+};
+int launch_hard(hipStream_t s, int nj, const HardArgs& h);
+int hard_set_max_lds();
 
 }  // namespace tmpc

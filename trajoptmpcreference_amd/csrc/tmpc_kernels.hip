@@ -1315,7 +1315,8 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
                                                   const double* __restrict__ du, ProbState st,
                                                   const int* __restrict__ pcg_iters, TraceDev tr,
                                                   int* __restrict__ active_count,
-                                                  unsigned long long* __restrict__ counters) {
+                                                  unsigned long long* __restrict__ counters,
+                                                  const double* __restrict__ hterms) {
   const int b = blockIdx.x;
   if (!st.active[b]) return;
   __shared__ double sJ[64], sC[64], sD[64];
@@ -1334,6 +1335,10 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
     for (int k = 0; k < N - 1; ++k) c = c + tm[k * 4 + 1];
     for (int k = 0; k < N - 1; ++k) D += tm[k * 4 + 2];
     D += tm[(N - 1) * 4 + 2];
+    if (hterms) {   // hard box-constraint terms after the dynamics ones, knot by knot (:286-293)
+      const double* th = hterms + ((size_t)b * T + t) * N;
+      for (int k = 0; k < N; ++k) c = c + th[k];
+    }
     sJ[t] = J;
     sC[t] = c;
     sD[t] = D;
@@ -1629,9 +1634,9 @@ int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* S
 void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
-                      int* active_count, unsigned long long* counters) {
+                      int* active_count, unsigned long long* counters, const double* hterms) {
   hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u, dx, du,
-                     st, pcg_iters, tr, active_count, counters);
+                     st, pcg_iters, tr, active_count, counters, hterms);
 }
 
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active) {

@@ -11,7 +11,7 @@ gradients are inconsistent in the reference, TrajoptPlant.py:189,193,235-243).
 import numpy as np
 
 from . import _native
-from .urdf import parse_urdf
+from .urdf import parse_urdf, pendulum_urdf
 
 
 class _RBDReferenceShim:
@@ -134,3 +134,18 @@ class URDFPlant(TrajoptPlant):
         if return_gradient:
             return r[0][0], r[1][0]
         return r[0]
+
+
+class PendulumPlant(URDFPlant):
+    """The pendulum the reference's package and examples/pendulum.py import but TrajoptPlant.py never
+    defines (__init__.py:1, examples/pendulum.py:7): one joint, nq = nv = nu = 1, a bob of
+    `mass` at `length` below the pivot, so qdd = (u - m g l sin q) / (m l^2 + I_bob) and q = pi is
+    upright (examples/pendulum.py's goal xg = [3.14159, 0]).  It is a URDF model (urdf.pendulum_urdf)
+    behind the URDFPlant surface, so it runs on the same GPU kernels as every other plant."""
+
+    def __init__(self, integrator_type: int = 0, options=None, device: int = 0, mass: float = 1.0,
+                 length: float = 1.0):
+        options = {} if options is None else options
+        options["path_to_urdf"] = pendulum_urdf(mass, length)
+        super().__init__(integrator_type, options, device)
+

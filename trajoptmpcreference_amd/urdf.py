@@ -360,3 +360,23 @@ def planar_arm_urdf(n_links: int, mass: float = 0.1, length: float = 1.0) -> str
                   '    </inertial>', '  </link>']
     parts.append('</robot>')
     return "\n".join(parts) + "\n"
+
+
+def pendulum_urdf(mass: float = 1.0, length: float = 1.0, bob_inertia: float = 1e-3) -> str:
+    """A pendulum: one revolute joint about x and a bob of `mass` hanging `length` below it along -z,
+    so gravity (options['gravity'], along z) gives the torque -mass g length sin(q) and q = pi is
+    upright.  The reference's examples/pendulum.py uses a PendulumPlant that TrajoptPlant.py never
+    defines; this URDF is the model behind plant.PendulumPlant.  Generated, not copied."""
+    i = bob_inertia
+    return "\n".join([
+        '<?xml version="1.0" ?>', '<robot name="pendulum">', '  <link name="base_link"/>',
+        '  <joint name="joint1" type="revolute">', '    <parent link="base_link"/>', '    <child link="bob"/>',
+        '    <origin rpy="0 0 0" xyz="0 0 0"/>', '    <axis xyz="1 0 0"/>', '  </joint>',
+        # the parser takes the COM offset from the link's own <origin>, as the reference's
+        # URDFParser does (Link.py:48-63); the inertial block repeats it (models/arm*.urdf style)
+        '  <link name="bob">', f'    <origin rpy="0 0 0" xyz="0 0 {-length!r}"/>', '    <inertial>',
+        f'      <origin rpy="0 0 0" xyz="0 0 {-length!r}"/>',
+        f'      <mass value="{mass!r}"/>',
+        f'      <inertia ixx="{i!r}" ixy="0.0" ixz="0.0" iyy="{i!r}" iyz="0.0" izz="{i!r}"/>',
+        '    </inertial>', '  </link>', '</robot>']) + "\n"
+
