@@ -234,7 +234,11 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
  * guess [B][N nx] (nullable) is the PCG initial iterate, options['guess'] of solveKKTSystem_Schur (:439-440).
  * dxul [B][n_xu(N-1)+nx + nx N] in the reference's interleaved order [x0,u0,x1,...,x_{N-1}; lambda].
  * S_diag [B][N][nx][nx], S_lo [B][N-1][nx][nx] (= S_{k+1,k}), gamma [B][N nx], P_diag [B][N][nx][nx]
- * are optional (nullable) copies of the intermediate blocks. */
+ * are optional (nullable) copies of the intermediate blocks.
+ * With hard box limits (ACTIVE_SET / FULL_SET) the knots' constraint rows join the QP
+ * (TrajoptMPCReference.py:238-248): the lambda part of dxul then holds the multipliers of the
+ * N nx dynamics / initial-state rows in knot order (the hard rows' multipliers are dropped), and
+ * guess, S_diag, S_lo, gamma, P_diag must be NULL (S is banded with variable blocks). */
 int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
                   const double* u, const double* guess, double* dxul, int32_t* pcg_iters, double* S_diag,
                   double* S_lo, double* gamma, double* P_diag);

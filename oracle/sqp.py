@@ -286,10 +286,11 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
         merit = J + mu * c
         trace = [dict(outer_iteration=outer, iteration=0, line_search_iteration=0, alpha=1, rho=rho, J=J, c=c,
                       merit=merit, D=None, reduction_ratio=None, succeeded_line_search=False)]
-        pcg_iters, dxuls, active_rows, active_sets = [], [], [], []
+        pcg_iters, dxuls, active_rows, active_sets, iterates = [], [], [], [], []
         it = 0
         exit_sqp = 0
         while True:
+            iterates.append((x.copy(), u.copy(), rho))
             if hard is not None:
                 from . import hard as ohard
                 G, g, C, cc = ohard.kkt_dense(model, cost, x, u, xs, N, dt, hard, soft)
@@ -380,7 +381,8 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
         if done:
             break
     return dict(x=x, u=u, exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer, sqp_iter=it, trace=trace,
-                pcg_iters=pcg_iters, dxul=dxuls, active_rows=active_rows, active_sets=active_sets)
+                pcg_iters=pcg_iters, dxul=dxuls, active_rows=active_rows, active_sets=active_sets,
+                iterates=iterates)
 
 
 def initial_problem(model, N, dt, seed):

@@ -489,6 +489,77 @@ def run_hard(args):
            f"rows={list(rows)} pcg={list(pcg_iters)} err={err[:80]} wall={wall:.1f}s"
 
 
+def run_pendulum(args):
+    """The pendulum of examples/pendulum.py on the reference's own URDFPlant / RBDReference: the
+    reference imports a PendulumPlant it never defines, so the build's PendulumPlant is a
+    URDF model (trajoptmpcreference_amd/urdf.py pendulum_urdf) and this runs that URDF through the
+    reference: the example's cost, N = 20, torque limits +-7 in a hard mode, the example's options."""
+    mode, method, N, lim = args
+    _setup_reference()
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from trajoptmpcreference_amd.urdf import pendulum_urdf
+    from TrajoptPlant import URDFPlant
+    from TrajoptCost import QuadraticCost
+    from TrajoptConstraint import TrajoptConstraint
+    from TrajoptMPCReference import TrajoptMPCReference, SQPSolverMethods
+    from overloading import matrix_
+    matrix_.iteration = 0
+    matrix_.soft_constraint_iteration = 0
+    matrix_.line_search_iteration = 0
+    urdf = pendulum_urdf()
+    d = tempfile.mkdtemp(prefix="tmpc_urdf_")
+    path = os.path.join(d, "pendulum.urdf")
+    with open(path, "w") as f:
+        f.write(urdf)
+    plant = URDFPlant(options={"path_to_urdf": path, "overloading": False})
+
+    class PassThroughQuadraticCost(QuadraticCost):
+        def value(self, x, u=None, timestep=None, *a, **k):
+            return QuadraticCost.value(self, x, u, timestep)
+
+        def gradient(self, x, u=None, timestep=None, *a, **k):
+            return QuadraticCost.gradient(self, x, u, timestep)
+
+        def hessian(self, x, u=None, timestep=None, *a, **k):
+            return QuadraticCost.hessian(self, x, u, timestep)
+
+    xg = np.array([3.14159, 0.0])
+    cost = PassThroughQuadraticCost(np.diag([1.0, 1.0]), np.diag([100.0, 100.0]), np.diag([0.1]), xg)
+    con = TrajoptConstraint(1, 1, 1, N)
+    con.overloading = False
+    con.set_torque_limits([lim], [-lim], mode, {"overloading": False})
+    solver = TrajoptMPCReference(plant, cost, con)
+    m = {"S": SQPSolverMethods.S, "PCG-SS": SQPSolverMethods.PCG_SS, "PCG-BJ": SQPSolverMethods.PCG_BJ}[method]
+    x0, u0 = np.zeros((2, N)), np.zeros((1, N - 1))
+    opts = {"expected_reduction_min_SQP_DDP": -100, "overloading": False}
+    import io
+    import contextlib
+    t0 = time.time()
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(copy.deepcopy(x0), copy.deepcopy(u0), N, 0.1, m,
+                                                                     opts)
+    wall = time.time() - t0
+    tr = solver.trace
+    keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
+            "succeeded_line_search"]
+    rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(np.asarray(t[k]).reshape(-1)[0]) for t in tr])
+           for k in keys}
+    pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
+    rows = np.array([np.asarray(dC["value"]).shape[0] for dC in solver.saved_C], dtype=np.int32)
+    # dynamics known answers on the same model
+    rng = np.random.default_rng(5)
+    X = np.column_stack([rng.uniform(-3, 3, 8), rng.uniform(-2, 2, 8)])
+    U = rng.uniform(-5, 5, (8, 1))
+    qdd = np.array([plant.forward_dynamics(X[i], U[i]) for i in range(8)]).reshape(8, -1)
+    tag = {"ACTIVE_SET": "AS", "AUGMENTED_LAGRANGIAN": "AL"}[mode]
+    np.savez_compressed(os.path.join(OUT, f"pendulum_N{N}_{tag}{int(lim)}_{method}.npz"),
+                        urdf=np.array(urdf), x0=x0, u0=u0, x=np.asarray(x), u=np.asarray(u), xg=xg, lim=lim,
+                        mode=np.array(mode), exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer_iter,
+                        sqp_iter=sqp_iter, pcg_iters=pcg_iters, C_rows=rows, X=X, U=U, qdd=qdd, wall_s=wall, **rec)
+    return f"[golden] pendulum {tag}{lim} {method} N={N}: exit={exit_sqp} iters={sqp_iter} rows={list(rows)} " \
+           f"pcg={list(pcg_iters)} wall={wall:.1f}s"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="skip the slow arm6 N=64 solves")
@@ -530,6 +601,12 @@ def main():
                 ("ACTIVE_SET", "PCG-SS", 16, 2.2, 8, 0.1, None), ("ACTIVE_SET", "S", 12, 3.0, 9, 0.1, -100.0)]
         with mp.get_context("fork").Pool(min(8, len(jobs))) as pool:
             for msg in pool.imap_unordered(run_hard, jobs):
+                print(msg, flush=True)
+    if a.only in (None, "pendulum"):
+        jobs = [("ACTIVE_SET", "S", 20, 7.0), ("ACTIVE_SET", "PCG-SS", 20, 7.0), ("ACTIVE_SET", "S", 20, 20.0),
+                ("AUGMENTED_LAGRANGIAN", "S", 20, 7.0)]
+        with mp.get_context("fork").Pool(len(jobs)) as pool:
+            for msg in pool.imap_unordered(run_pendulum, jobs):
                 print(msg, flush=True)
     if a.only in (None, "soft"):
         jobs = [("QUADRATIC_PENALTY", "PCG-SS", 8, 2.0, 0, 0.1), ("AUGMENTED_LAGRANGIAN", "PCG-SS", 8, 2.0, 0, 0.1),

@@ -10,6 +10,12 @@
 * Against the oracle's elementwise vector semantics (oracle/hard.py) for n > 1 and
   two limit types at once: integers exact except the PCG counts, which are held to
   the spread two summation orders of the oracle itself show there (see the test).
+* QP by QP (tmpc_qp_batch with the hard rows): at every iterate of the oracle's SQP
+  the GPU's QP step and dynamics-row multipliers against the oracle's dense solve.
+  This is the parity statement for runs whose SQP-level path is rounding-decided:
+  after a full step, entries land exactly on a bound and whether the next QP holds
+  them active is decided by the last bit (pendulum, iterate 3: u[8..10] = 7 - 8.9e-16,
+  7, 7 + 8.9e-16), so two correct solvers may take different active sets from there.
 """
 import glob
 import os
@@ -110,3 +116,109 @@ def test_hard_constraints_reject_ilqr():
     solver = TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(2)), con)
     with pytest.raises(_native.NativeError, match="iLQR"):
         solver.iLQR(np.zeros((4, 8)), np.zeros((2, 7)), 8, 0.1, {})
+
+
+def _dyn_rows(hard, x, u, N, nx):
+    """indices of the dynamics / initial-state rows in the oracle's row order (oracle/hard.py kkt_dense)"""
+    idx = list(range(nx))
+    r = nx
+    for k in range(N - 1):
+        idx += list(range(r, r + nx))
+        r += nx + len(hard.rows(x[:, k], u[:, k], k, N))
+    return idx
+
+
+QP_CASES = [
+    ("pendulum", 20, "S", {"torque": (-7.0, 7.0, "ACTIVE_SET")}),
+    ("pendulum", 20, "PCG-SS", {"torque": (-7.0, 7.0, "ACTIVE_SET")}),
+    ("arm3", 12, "PCG-SS", {"torque": (-0.3, 0.3, "ACTIVE_SET"), "velocity": (-0.6, 0.6, "ACTIVE_SET")}),
+    ("arm3", 12, "PCG-BJ", {"torque": (-0.3, 0.3, "ACTIVE_SET"), "velocity": (-0.6, 0.6, "ACTIVE_SET")}),
+    ("arm3", 12, "S", {"velocity": (-0.5, 0.5, "FULL_SET")}),
+    ("arm2", 16, "PCG-J", {"torque": (-0.4, 0.4, "ACTIVE_SET"), "joint": (-1.0, 1.0, "ACTIVE_SET")}),
+]
+
+
+@pytest.mark.parametrize("name,N,method,spec", QP_CASES,
+                         ids=[f"{c[0]}-N{c[1]}-{c[2]}-{'+'.join(c[3])}" for c in QP_CASES])
+def test_hard_qp_matches_oracle_at_every_iterate(name, N, method, spec):
+    """All QPs of one oracle SQP run, batched as B problems on the GPU: the step dxu and the
+    dynamics-row multipliers (1e-9 relative for the direct solve S; for PCG, as close to the exact
+    QP solution as the oracle's own PCG answer, up to 10x), PCG counts within the oracle's own
+    summation-order spread (+-5, see above; the pendulum's iterate 2, 7 active rows, is 41 vs 42)."""
+    from oracle import hard as ohard
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd import (PendulumPlant, QuadraticCost, TrajoptConstraint, TrajoptMPCReference,
+                                         URDFPlant, planar_arm_urdf)
+    if name == "pendulum":
+        plant = PendulumPlant()
+        n = 1
+        Q, QF, R, xg = np.diag([1.0, 1.0]), np.diag([100.0, 100.0]), np.diag([0.1]), np.array([3.14159, 0.0])
+        x0, u0 = np.zeros((2, N)), np.zeros((1, N - 1))
+        opts = {"expected_reduction_min_SQP_DDP": -100}
+    else:
+        m = arm_model(name)
+        n = m.n
+        plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(n)})
+        Q, QF, R, xg = quad_cost_arrays(n)
+        x0, u0 = osqp.initial_problem(m, N, 0.1, 430)
+        opts = {}
+    nx = 2 * n
+    con = TrajoptConstraint(n, n, n, N)
+    for kind, (lb, ub, mode) in spec.items():
+        getattr(con, f"set_{kind}_limits")([ub] * n, [lb] * n, mode)
+    solver = TrajoptMPCReference(plant, QuadraticCost(Q, QF, R, xg), con)
+    hard = ohard.HardConstraints([ohard.HardLimit(k, n, lb, ub, mode) for k, (lb, ub, mode) in spec.items()])
+    model = plant.model if name == "pendulum" else m
+    o = osqp.sqp(model, osqp.QuadCost(Q, QF, R, xg), x0, u0, N, 0.1, method, dict(opts), hard=hard)
+    its = o["iterates"]
+    assert len(its) == len(o["dxul"]) >= 2
+    full = dict(opts)
+    solver.set_default_options(full)
+    ctx = solver._context(full)
+    xs = np.array([x for x, _, _ in its])
+    us = np.array([u for _, u, _ in its])
+    rho = np.array([r for _, _, r in its])
+    xs[:, :, 0] = x0[:, 0]      # the SQP's xs: the QP's initial-state row is x_0 - xs
+    r = ctx.qp_batch(xs, us, N, 0.1, rho, method, want_blocks=False)
+    nz = (nx + n) * (N - 1) + nx
+    oc = osqp.QuadCost(Q, QF, R, xg)
+    o_opts = osqp.default_options(opts)
+    for i, (x, u, rho_i) in enumerate(its):
+        ref = o["dxul"][i]
+        rows = _dyn_rows(hard, x, u, N, nx)
+        lam_ref = ref[nz:][rows]
+        got = r["dxul"][i]
+        if method != "S":
+            assert abs(int(r["pcg_iters"][i]) - o["pcg_iters"][i]) <= 5, (i, int(r["pcg_iters"][i]),
+                                                                               o["pcg_iters"][i])
+        sc = max(1.0, float(np.max(np.abs(ref[:nz]))))
+        sl = max(1.0, float(np.max(np.abs(lam_ref))))
+        if method == "S":
+            assert float(np.max(np.abs(got[:nz] - ref[:nz]))) < 1e-9 * sc, i
+            assert float(np.max(np.abs(got[nz:] - lam_ref))) < 1e-9 * sl, i
+            continue
+        # PCG stops at |nu| < tol: its answer is as far from the exact QP solution as the tolerance
+        # leaves it.  The GPU's solution must be as close to the exact one (the direct dense solve)
+        # as the oracle's own PCG solution is, up to 10x.
+        G, g, Cm, cc = ohard.kkt_dense(model, oc, x, u, x0[:, 0], N, 0.1, hard)
+        ex, _, _ = ohard.solve_qp_dense(G, g, Cm, cc, rho_i, "S", o_opts, nx)
+        e_ref = float(np.max(np.abs(ref[:nz] - ex[:nz])))
+        e_got = float(np.max(np.abs(got[:nz] - ex[:nz])))
+        assert e_got <= 10 * e_ref + 1e-9 * sc, (i, e_got, e_ref)
+        el_ref = float(np.max(np.abs(lam_ref - ex[nz:][rows])))
+        el_got = float(np.max(np.abs(got[nz:] - ex[nz:][rows])))
+        assert el_got <= 10 * el_ref + 1e-9 * sl, (i, el_got, el_ref)
+
+
+def test_hard_qp_rejects_blocks():
+    from trajoptmpcreference_amd import (QuadraticCost, TrajoptConstraint, TrajoptMPCReference, URDFPlant, _native,
+                                         planar_arm_urdf)
+    plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(2)})
+    con = TrajoptConstraint(2, 2, 2, 8)
+    con.set_torque_limits([1.0] * 2, [-1.0] * 2, "ACTIVE_SET")
+    solver = TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(2)), con)
+    opts = {}
+    solver.set_default_options(opts)
+    ctx = solver._context(opts)
+    with pytest.raises(_native.NativeError, match="NULL"):
+        ctx.qp_batch(np.zeros((1, 4, 8)), np.zeros((1, 2, 7)), 8, 0.1, 0.001, "PCG-SS", want_blocks=True)

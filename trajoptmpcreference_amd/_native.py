@@ -380,7 +380,9 @@ class Context:
         return A, Bm, dq
 
     def qp_batch(self, x, u, N, dt, rho, method="PCG-SS", want_blocks=True, guess=None):
-        """guess [B][N nx]: the PCG initial iterate (solveKKTSystem_Schur's options['guess'])."""
+        """guess [B][N nx]: the PCG initial iterate (solveKKTSystem_Schur's options['guess']).
+        With hard box limits set, want_blocks must be False and the lambda part of dxul holds the
+        dynamics-row multipliers only (include/tmpc.h)."""
         x, u = _c64(x), _c64(u)
         self._check_traj(x, u, N)
         B, nx, _ = x.shape

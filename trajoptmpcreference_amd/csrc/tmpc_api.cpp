@@ -392,6 +392,66 @@ static int alloc_soft(tmpc_ctx* ctx, int B, int N, double** mu, double** lam, do
   return 0;
 }
 
+// Buffers of the hard-constraint QP (tmpc_hard.hip) for B problems of N knots; T line-search trials.
+static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs& hard) {
+  const int nj = ctx->hmodel.n, nx = 2 * nj;
+  int ntypes = 0;
+  bool full = false;
+  for (int t = 0; t < 3; ++t) {
+    if (ctx->hlim.hard[t] != HARD_NONE) ++ntypes;
+    if (ctx->hlim.hard[t] == HARD_FULL) full = true;
+  }
+  if (full && precond != 0)
+    return fail(ctx, "FULL_SET box constraints with a PCG method: the inactive rows of C are zero, so S is "
+                "singular and the reference's preconditioner raises LinAlgError (PCG.py:168-188); use method S");
+  hard = HardArgs{};
+  hard.B = B;
+  hard.N = N;
+  hard.rmax = 2 * nj * ntypes;                 // both bounds of every limited entry, at most
+  hard.dmax = nx * N + N * hard.rmax;
+  const int gmax = nx + 2 * hard.rmax;         // the last group holds two knots' hard rows
+  hard.W = 2 * gmax - 1;
+  if (precond != 0 && (5 * (size_t)hard.dmax + 16) * sizeof(double) > 160 * 1024)
+    return fail(ctx, "hard constraints: Schur dimension up to %d exceeds the PCG's LDS vectors (max 4092)", hard.dmax);
+  if (hard.W > 1024) return fail(ctx, "hard constraints: band half-width %d > 1024", hard.W);
+  const size_t BW = 2 * (size_t)hard.W + 1, nbmax = hard.dmax / nx + 1;
+  hard.Cs = ctx->dlim;
+  hard.C = ctx->dcost;
+  BUF(int, hd_cnt, (size_t)B * N);
+  BUF(int, hd_col, (size_t)B * N * hard.rmax);
+  BUF(double, hd_sgn, (size_t)B * N * hard.rmax);
+  BUF(double, hd_val, (size_t)B * N * hard.rmax);
+  BUF(int, hd_roff, (size_t)B * N);
+  BUF(int, hd_hoff, (size_t)B * N);
+  BUF(int, hd_dim, (size_t)B);
+  BUF(int, hd_rkind, (size_t)B * hard.dmax);
+  BUF(int, hd_rknot, (size_t)B * hard.dmax);
+  BUF(int, hd_ridx, (size_t)B * hard.dmax);
+  BUF(int, hd_pk, (size_t)B * hard.dmax * 2);
+  BUF(double, hd_Y, (size_t)B * hard.dmax * 2 * (nx + nj));
+  BUF(double, hd_Sb, (size_t)B * hard.dmax * BW);
+  BUF(double, hd_gam, (size_t)B * hard.dmax);
+  BUF(double, hd_lam, (size_t)B * hard.dmax);
+  hard.cnt = hd_cnt; hard.hcol = hd_col; hard.hsgn = hd_sgn; hard.hval = hd_val;
+  hard.roff = hd_roff; hard.hoff = hd_hoff; hard.dim = hd_dim;
+  hard.rkind = hd_rkind; hard.rknot = hd_rknot; hard.ridx = hd_ridx; hard.PK = hd_pk;
+  hard.Y = hd_Y; hard.Sb = hd_Sb; hard.gam = hd_gam; hard.lam = hd_lam;
+  if (precond == 0) {
+    BUF(double, hd_M, (size_t)B * hard.dmax * BW);
+    BUF(double, hd_rhs, (size_t)B * hard.dmax);
+    hard.M = hd_M;
+    hard.rhs = hd_rhs;
+  } else {
+    BUF(double, hd_Pd, (size_t)B * nbmax * nx * nx);
+    BUF(double, hd_Pl, (size_t)B * nbmax * nx * nx);
+    BUF(double, hd_Pt, (size_t)B * nbmax * nx * nx);
+    hard.Pd = hd_Pd; hard.Pl = hd_Pl; hard.Ptmp = hd_Pt;
+  }
+  BUF(double, hd_terms, (size_t)B * (T > 0 ? T : 1) * N);
+  hard.hterms = hd_terms;
+  return 0;
+}
+
 // the hard box-constraint terms of the merit's violation at the line-search trial points
 static int hard_ls(tmpc_ctx* ctx, int nj, const HardArgs& base, int B, int N, int T, const double* alphas, const double* x,
                    const double* u, double* dx, double* du, const int* active) {
@@ -461,61 +521,8 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   HardArgs hard{};
   double* hterms = nullptr;
   if (ctx->hlim.any_hard) {
-    int ntypes = 0;
-    bool full = false;
-    for (int t = 0; t < 3; ++t) {
-      if (ctx->hlim.hard[t] != HARD_NONE) ++ntypes;
-      if (ctx->hlim.hard[t] == HARD_FULL) full = true;
-    }
-    if (full && precond != 0)
-      return fail(ctx, "FULL_SET box constraints with a PCG method: the inactive rows of C are zero, so S is "
-                  "singular and the reference's preconditioner raises LinAlgError (PCG.py:168-188); use method S");
-    hard.B = B;
-    hard.N = N;
-    hard.rmax = 2 * nj * ntypes;                 // both bounds of every limited entry, at most
-    hard.dmax = nx * N + N * hard.rmax;
-    const int gmax = nx + 2 * hard.rmax;         // the last group holds two knots' hard rows
-    hard.W = 2 * gmax - 1;
-    if (precond != 0 && (5 * (size_t)hard.dmax + 16) * sizeof(double) > 160 * 1024)
-      return fail(ctx, "hard constraints: Schur dimension up to %d exceeds the PCG's LDS vectors (max 4092)",
-                  hard.dmax);
-    if (hard.W > 1024) return fail(ctx, "hard constraints: band half-width %d > 1024", hard.W);
-    const size_t BW = 2 * (size_t)hard.W + 1, nbmax = hard.dmax / nx + 1;
-    hard.Cs = ctx->dlim;
-    hard.C = ctx->dcost;
-    BUF(int, hd_cnt, (size_t)B * N);
-    BUF(int, hd_col, (size_t)B * N * hard.rmax);
-    BUF(double, hd_sgn, (size_t)B * N * hard.rmax);
-    BUF(double, hd_val, (size_t)B * N * hard.rmax);
-    BUF(int, hd_roff, (size_t)B * N);
-    BUF(int, hd_hoff, (size_t)B * N);
-    BUF(int, hd_dim, (size_t)B);
-    BUF(int, hd_rkind, (size_t)B * hard.dmax);
-    BUF(int, hd_rknot, (size_t)B * hard.dmax);
-    BUF(int, hd_ridx, (size_t)B * hard.dmax);
-    BUF(int, hd_pk, (size_t)B * hard.dmax * 2);
-    BUF(double, hd_Y, (size_t)B * hard.dmax * 2 * (nx + nj));
-    BUF(double, hd_Sb, (size_t)B * hard.dmax * BW);
-    BUF(double, hd_gam, (size_t)B * hard.dmax);
-    BUF(double, hd_lam, (size_t)B * hard.dmax);
-    hard.cnt = hd_cnt; hard.hcol = hd_col; hard.hsgn = hd_sgn; hard.hval = hd_val;
-    hard.roff = hd_roff; hard.hoff = hd_hoff; hard.dim = hd_dim;
-    hard.rkind = hd_rkind; hard.rknot = hd_rknot; hard.ridx = hd_ridx; hard.PK = hd_pk;
-    hard.Y = hd_Y; hard.Sb = hd_Sb; hard.gam = hd_gam; hard.lam = hd_lam;
-    if (precond == 0) {
-      BUF(double, hd_M, (size_t)B * hard.dmax * BW);
-      BUF(double, hd_rhs, (size_t)B * hard.dmax);
-      hard.M = hd_M;
-      hard.rhs = hd_rhs;
-    } else {
-      BUF(double, hd_Pd, (size_t)B * nbmax * nx * nx);
-      BUF(double, hd_Pl, (size_t)B * nbmax * nx * nx);
-      BUF(double, hd_Pt, (size_t)B * nbmax * nx * nx);
-      hard.Pd = hd_Pd; hard.Pl = hd_Pl; hard.Ptmp = hd_Pt;
-    }
-    BUF(double, hd_terms, (size_t)B * T * N);
-    hterms = hd_terms;
-    hard.hterms = hd_terms;
+    if ((rc = setup_hard(ctx, B, N, T, precond, hard))) return rc;
+    hterms = hard.hterms;
     w.hard = &hard;
   }
   if (o.pcg_warm_start && precond != 0 && !ctx->hlim.any_hard) {
@@ -1201,7 +1208,10 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "tmpc_qp_batch supports QuadraticCost only");
-  if (ctx->hlim.any_hard) return fail(ctx, "tmpc_qp_batch: hard box constraints are solved inside tmpc_sqp_solve_batch");
+  if (ctx->hlim.any_hard && guess) return fail(ctx, "tmpc_qp_batch: no PCG guess with hard box constraints");
+  if (ctx->hlim.any_hard && (S_diag || S_lo || gamma || P_diag))
+    return fail(ctx, "tmpc_qp_batch: with hard box constraints S is banded with variable blocks; "
+                     "S_diag / S_lo / gamma / P_diag must be NULL");
   const int precond = precond_of(linsys);
   if (precond < 0) return fail(ctx, "linear system method %d is not available on the GPU", linsys);
   if (!rho || !x || !u) return fail(ctx, "null input");
@@ -1225,8 +1235,26 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
     HIP_OK(hipMemcpyAsync(io_guess, guess, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
     w.guess = io_guess;
   }
-  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, true))) return rc;
+  // hard box constraints: the QP with the knots' constraint rows (tmpc_hard.hip); the lambda part of
+  // dxul then holds the multipliers of the N nx dynamics / initial-state rows, in knot order
+  HardArgs hard{};
+  if (ctx->hlim.any_hard) {
+    if ((rc = setup_hard(ctx, B, N, 0, precond, hard))) return rc;
+    w.hard = &hard;
+  }
+  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, !ctx->hlim.any_hard))) return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (ctx->hlim.any_hard) {
+    std::vector<int> roff((size_t)B * N);
+    std::vector<double> lh((size_t)B * hard.dmax);
+    HIP_OK(hipMemcpy(roff.data(), hard.roff, roff.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(lh.data(), hard.lam, lh.size() * sizeof(double), hipMemcpyDeviceToHost));
+    std::vector<double> lr((size_t)B * N * nx);
+    for (int b = 0; b < B; ++b)
+      for (int j = 0; j < N; ++j)
+        for (int i = 0; i < nx; ++i) lr[((size_t)b * N + j) * nx + i] = lh[(size_t)b * hard.dmax + roff[(size_t)b * N + j] + i];
+    HIP_OK(hipMemcpy(w.lam, lr.data(), lr.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
   resolve_timings(ctx);
   if (dxul) {
     std::vector<double> dx((size_t)B * N * nx), du((size_t)B * K * nj), lam((size_t)B * N * nx);
