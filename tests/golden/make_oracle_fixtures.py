@@ -12,7 +12,7 @@ stored for both of the oracle's [K | d] solves (Cholesky and LU): where
 rounding decides an integer outcome the GPU must match one of them
 (tests/test_gpu_ilqr.py).
 
-Usage:  python tests/golden/make_oracle_fixtures.py [--only config3|config4|config5]
+Usage:  python tests/golden/make_oracle_fixtures.py [--only config3|config4|config5|sqp128|mpc128sqp]
 """
 import argparse
 import multiprocessing as mp
@@ -32,6 +32,10 @@ C3 = dict(N=64, B=8, seed0=800, lb=-0.5, ub=0.5, opts={"max_iter_softConstraints
 C4 = dict(N=64, B=8, seed0=820, opts={})
 # BASELINE config 5: arm6 receding-horizon MPC loop, N = 128, iLQR horizon solves
 C5 = dict(N=128, B=2, seed0=900, steps=3, opts={})
+# config 5 on SQP: arm6 N = 128 (1536 Schur rows, past the register-resident PCG's 1024), single
+# PCG-SS solves and the MPC loop with the PCG warm start
+C5S = dict(N=128, B=4, seed0=940, opts={})
+C5M = dict(N=128, B=2, seed0=960, steps=3, opts={})
 
 
 def _model():
@@ -99,6 +103,28 @@ def job_config5(args):
                 u_exec=o["u_exec"])
 
 
+def job_sqp128(seed):
+    from oracle import sqp as osqp
+    m = _model()
+    N = C5S["N"]
+    x, u = osqp.initial_problem(m, N, 0.1, seed)
+    with np.errstate(all="ignore"):
+        o = osqp.sqp(m, _cost(), x, u, N, 0.1, "PCG-SS", dict(C5S["opts"]))
+    return dict(seed=seed, exit_sqp=o["exit_sqp"], sqp_iter=o["sqp_iter"], x=o["x"], u=o["u"],
+                pcg_iters=list(o["pcg_iters"]), alpha=[t["alpha"] for t in o["trace"][1:]])
+
+
+def job_mpc128sqp(seed):
+    from oracle import mpc as ompc
+    from oracle import sqp as osqp
+    m = _model()
+    N = C5M["N"]
+    x, u = osqp.initial_problem(m, N, 0.1, seed)
+    with np.errstate(all="ignore"):
+        o = ompc.mpc(m, _cost(), x, u, N, 0.1, "PCG-SS", C5M["steps"], dict(C5M["opts"]), pcg_warm_start=True)
+    return dict(seed=seed, exit_codes=o["exit_codes"], iters=o["iters"], x_exec=o["x_exec"], u_exec=o["u_exec"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
@@ -148,6 +174,27 @@ def main():
         np.savez_compressed(os.path.join(OUT, "oracle_config5_arm6_N128_mpc_ilqr.npz"), **rec)
         print(f"[oracle] config5: {time.time() - t:.0f} s; chol iters {rec['iters_0'].tolist()} "
               f"lu {rec['iters_1'].tolist()}", flush=True)
+    if a.only in (None, "sqp128"):
+        t = time.time()
+        res = pool.map(job_sqp128, [C5S["seed0"] + i for i in range(C5S["B"])], chunksize=1)
+        W = max(len(r["pcg_iters"]) for r in res)
+        Wa = max(len(r["alpha"]) for r in res)
+        rec = {"N": C5S["N"], "seeds": np.array([r["seed"] for r in res]),
+               "pcg_iters": np.array([r["pcg_iters"] + [-1] * (W - len(r["pcg_iters"])) for r in res]),
+               "alpha": np.array([r["alpha"] + [np.nan] * (Wa - len(r["alpha"])) for r in res])}
+        for k in ("exit_sqp", "sqp_iter", "x", "u"):
+            rec[k] = np.array([r[k] for r in res])
+        np.savez_compressed(os.path.join(OUT, "oracle_arm6_N128_sqp_pcgss.npz"), **rec)
+        print(f"[oracle] sqp128: {time.time() - t:.0f} s; (exit, iter) "
+              f"{list(zip(rec['exit_sqp'], rec['sqp_iter']))}", flush=True)
+    if a.only in (None, "mpc128sqp"):
+        t = time.time()
+        res = pool.map(job_mpc128sqp, [C5M["seed0"] + i for i in range(C5M["B"])], chunksize=1)
+        rec = {"N": C5M["N"], "steps": C5M["steps"], "seeds": np.array([r["seed"] for r in res])}
+        for k in ("exit_codes", "iters", "x_exec", "u_exec"):
+            rec[k] = np.array([r[k] for r in res])
+        np.savez_compressed(os.path.join(OUT, "oracle_config5_arm6_N128_mpc_sqp_pcgss.npz"), **rec)
+        print(f"[oracle] mpc128sqp: {time.time() - t:.0f} s; iters {rec['iters'].tolist()}", flush=True)
     pool.close()
 
 

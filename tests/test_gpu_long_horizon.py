@@ -1,0 +1,108 @@
+"""GPU parity past 1024 Schur rows: arm6 at N = 128 (1536 rows, BASELINE config 5)
+on the SQP path.
+
+Up to 1024 rows the fused QP kernel keeps every lane's rows of S and P^-1 in
+registers; past that they no longer fit a CU's register file and the GM
+instance keeps them in HBM (k_qp<..., GM>).  These tests check
+that instance against
+  * the oracle at N = 128 (tests/golden/oracle_arm6_N128_sqp_pcgss.npz and
+    oracle_config5_arm6_N128_mpc_sqp_pcgss.npz, made by
+    tests/golden/make_oracle_fixtures.py --only sqp128 / mpc128sqp), and
+  * the reference's own recorded solves, by forcing the GM instance at
+    N = 64 (TMPC_QP_GM_MIN_ROWS=1): exit codes, SQP / line-search iterations,
+    per-QP PCG counts and alpha paths identical.
+Integer outputs must be identical; trajectories within 1e-6 relative."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, arm_model, golden, quad_cost_arrays
+
+pytestmark = pytest.mark.gpu
+
+
+def _solver(n):
+    from trajoptmpcreference_amd import QuadraticCost, TrajoptMPCReference, URDFPlant, planar_arm_urdf
+    plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(n)})
+    return TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(n)))
+
+
+def _problems(N, seeds, dt=0.1):
+    from oracle import sqp as osqp
+    m = arm_model("arm6fix")
+    xs, us = zip(*[osqp.initial_problem(m, N, dt, int(s)) for s in seeds])
+    return np.array(xs), np.array(us)
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b))))
+
+
+def test_sqp_pcgss_arm6_n128_matches_oracle():
+    d = golden("oracle_arm6_N128_sqp_pcgss.npz")
+    N = int(d["N"])
+    x, u = _problems(N, d["seeds"])
+    r = _solver(6).SQP_batch(x, u, N, 0.1, "PCG-SS", {})
+    for i in range(len(d["seeds"])):
+        assert (int(r["exit_sqp"][i]), int(r["sqp_iter"][i])) == (int(d["exit_sqp"][i]), int(d["sqp_iter"][i])), i
+        ref = [int(v) for v in d["pcg_iters"][i] if v >= 0]
+        assert [int(v) for v in r["trace"]["pcg_iters"][i, 1:len(ref) + 1]] == ref, i
+        al = d["alpha"][i]
+        al = list(al[~np.isnan(al)])
+        assert list(r["trace"]["alpha"][i, 1:len(al) + 1]) == al, i
+        assert _rel(r["x"][i], d["x"][i]) < 1e-6, i
+        assert _rel(r["u"][i], d["u"][i]) < 1e-6, i
+
+
+def test_sqp_method_s_arm6_n128_matches_oracle():
+    """Method S past 1024 rows: the GM instance's Schur prologue / dxu epilogue around k_btsolve."""
+    from oracle import sqp as osqp
+    m = arm_model("arm6fix")
+    N = 128
+    x, u = _problems(N, [970, 971])
+    r = _solver(6).SQP_batch(x, u, N, 0.1, "S", {})
+    for i in range(2):
+        o = osqp.sqp(m, osqp.QuadCost(*quad_cost_arrays(6)), x[i], u[i], N, 0.1, "S")
+        assert (int(r["exit_sqp"][i]), int(r["sqp_iter"][i])) == (o["exit_sqp"], o["sqp_iter"]), i
+        assert _rel(r["x"][i], o["x"]) < 1e-6, i
+
+
+def test_config5_mpc_loop_sqp_pcgss_arm6_n128():
+    """BASELINE config 5 on SQP: the MPC loop with PCG-SS horizon solves and the PCG warm start."""
+    d = golden("oracle_config5_arm6_N128_mpc_sqp_pcgss.npz")
+    N, steps = int(d["N"]), int(d["steps"])
+    x, u = _problems(N, d["seeds"])
+    r = _solver(6).MPC_batch(x, u, N, 0.1, "QP-PCG-SS", {"pcg_warm_start": True}, mpc_steps=steps)
+    for i in range(len(d["seeds"])):
+        assert list(r["exit_codes"][i]) == list(d["exit_codes"][i]), i
+        assert list(r["iters"][i]) == list(d["iters"][i]), i
+        assert np.allclose(r["x_exec"][i], d["x_exec"][i], rtol=1e-6, atol=1e-8), i
+        assert np.allclose(r["u_exec"][i], d["u_exec"][i], rtol=1e-6, atol=1e-8), i
+
+
+@pytest.mark.parametrize("f", sorted(glob.glob(os.path.join(GOLDEN, "sqp_arm*_N*_s*_PCG-*.npz"))),
+                         ids=lambda f: os.path.basename(f))
+def test_gm_instance_matches_reference_fixtures(f, monkeypatch):
+    """The HBM-row instance forced at the reference's own sizes (N <= 64) reproduces its solves."""
+    monkeypatch.setenv("TMPC_QP_GM_MIN_ROWS", "1")
+    b = os.path.basename(f)[4:-4]
+    name, Ns, _, method = b.split("_")
+    N = int(Ns[1:])
+    from conftest import ARM_N
+    d = np.load(f)
+    solver = _solver(ARM_N[name])
+    x, u, exit_sqp, _, _, sqp_iter = solver.SQP(d["x0"], d["u0"], N, float(d["dt"]), method, {})
+    assert (exit_sqp, sqp_iter) == (int(d["exit_sqp"]), int(d["sqp_iter"]))
+    tr = solver.trace
+    assert [t["alpha"] for t in tr] == list(d["tr_alpha"])
+    ours = [t["inner_iters"] for t in tr[1:]]
+    if method == "PCG-J":   # test_gpu_sqp.py: Jacobi CG may stop one iteration apart after QP 0
+        assert ours[0] == int(d["pcg_iters"][0])
+        assert all(abs(a - int(v)) <= 1 for a, v in zip(ours, d["pcg_iters"]))
+    else:
+        assert ours == list(d["pcg_iters"])
+    rtol = 1e-4 if method == "PCG-J" else 1e-7
+    assert _rel(x, d["x"]) < rtol
+    assert _rel(u, d["u"]) < rtol

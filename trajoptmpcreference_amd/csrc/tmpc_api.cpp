@@ -216,9 +216,9 @@ static int check_ready(tmpc_ctx* ctx, int B, int N, bool qp = true) {
                 ctx->hmodel.n);
   if (B < 1) return fail(ctx, "batch size must be >= 1 (got %d)", B);
   if (N < 2) return fail(ctx, "N must be >= 2 (got %d)", N);
-  if (qp && N * ctx->hcost.nx > 1024)
-    return fail(ctx, "N * nx = %d exceeds 1024 rows (one PCG workgroup per problem); larger horizons are not "
-                "supported yet", N * ctx->hcost.nx);
+  if (qp && N * ctx->hcost.nx > QP_MAX_ROWS)
+    return fail(ctx, "N * nx = %d exceeds %d rows (one PCG workgroup per problem); larger horizons are not "
+                "supported", N * ctx->hcost.nx, QP_MAX_ROWS);
   return 0;
 }
 
@@ -231,6 +231,7 @@ struct Work {
   const double* guess;               // PCG initial iterate [B][N nx] (nullable)
   double* lam_keep;                  // where the PCG path stores lambda (nullable; warm start)
   HardArgs* hard;                    // hard box constraints: the variable-row QP (tmpc_hard.hip)
+  double* Sg;                        // S / P^-1 rows in HBM past 1024 rows (k_qp<..., GM>), else null
 };
 
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
@@ -292,7 +293,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
       Timed t(ctx, "schur");
       LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, G,
                           w.A, w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, nullptr, w.Sd, w.Sl, w.gam, nullptr,
-                          w.jsoft, nullptr));
+                          w.jsoft, nullptr, nullptr));
     }
     {
       Timed t(ctx, "btsolve");
@@ -302,7 +303,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
       Timed t(ctx, "dxu");
       LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, G, w.A,
                           w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, w.lam, nullptr, nullptr, nullptr, nullptr,
-                          w.jsoft, nullptr));
+                          w.jsoft, nullptr, nullptr));
     }
     return 0;
   }
@@ -312,7 +313,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
                         w.Bm, w.cvec, ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx,
                         w.du, keep_blocks ? w.lam : w.lam_keep, keep_blocks ? w.Sd : nullptr,
                         keep_blocks ? w.Sl : nullptr, keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr,
-                        w.jsoft, w.guess));
+                        w.jsoft, w.guess, w.Sg));
   }
   return 0;
 }
@@ -330,7 +331,11 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   BUF(double, du, (size_t)B * K * nj);
   BUF(int, iters, (size_t)B);
   w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters,
-           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (N * nx >= qp_gm_min_rows()) {   // the GM QP kernel's rows of S / P^-1
+    BUF(double, qp_gm, qp_gm_doubles(B, N, nx));
+    w.Sg = qp_gm;
+  }
   if (with_blocks) {
     BUF(double, Sdiag, (size_t)B * N * nx * nx);
     BUF(double, Slo, (size_t)B * (K > 0 ? K : 1) * nx * nx);

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "tmpc_device.h"
 #include "tmpc_models.h"
@@ -88,7 +89,19 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-              double* Pd, const double* jsoft, const double* guess);
+              double* Pd, const double* jsoft, const double* guess, double* Sg);
+// largest Schur dimension N nx of the fused QP: up to 1024 rows S / P^-1 stay in registers, up to
+// QP_MAX_ROWS (the GM kernels: two rows per lane, 12 waves = 3 per SIMD, i.e. 168 VGPRs) in HBM
+// scratch Sg of qp_gm_doubles(B, N, nx) doubles.  1536 = arm6 at N = 128 (BASELINE config 5).
+constexpr int QP_MAX_ROWS = 1536;
+inline size_t qp_gm_doubles(int B, int N, int nx) { return (size_t)B * 4 * nx * (size_t)N * nx; }
+// rows from which the QP takes the GM kernel: 1025, or TMPC_QP_GM_MIN_ROWS (parity tests run the GM
+// kernel on the reference's N = 64 fixtures this way)
+inline int qp_gm_min_rows() {
+  const char* e = getenv("TMPC_QP_GM_MIN_ROWS");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : 1025;
+}
 int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
                      const int* active, const double* x, const double* u, const double* mu, const double* lam,
                      double* Gk, double* jsoft);

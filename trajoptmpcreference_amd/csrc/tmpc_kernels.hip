@@ -376,6 +376,31 @@ struct PcgRow {
   double pr[NX];   // (S_kk)^-1 row  (J: pr[0] = 1 / S_ii)
 };
 
+// Past 1024 rows the four rows per lane no longer fit the register file (arm6
+// N = 128: 1536 rows x 48 doubles = 74k doubles > the CU's 64k-double VGPR
+// file), so the GM kernels keep S and P^-1 in HBM (L2 / MALL resident while a
+// problem is solved) and the lane reads its rows there every product.  Layout
+// per problem element-major [4][NX][rows] (sd, sl, su, pr): for a fixed entry
+// j the lanes of a wave read consecutive rows.  Same interface as PcgRow.
+struct GRowRef {
+  const double* __restrict__ p;
+  int stride;
+  __device__ __forceinline__ double operator[](int j) const { return p[(size_t)j * stride]; }
+};
+template <int NX>
+struct PcgRowG {
+  GRowRef sd, sl, su, pr;
+};
+// HBM rows: bound the loads in flight (the compiler would hoist all of a product's row loads, 2-4
+// dozen doubles per row, past the 168-VGPR budget of the GM kernel's 3 waves per SIMD)
+template <class RT> struct RowInHbm { static constexpr bool value = false; };
+template <int NX> struct RowInHbm<PcgRowG<NX>> { static constexpr bool value = true; };
+#define PCG_LOAD_FENCE(RT, j, acc)                                       \
+  if (RowInHbm<RT>::value && ((j) % 4) == 3) {                           \
+    _Pragma("unroll") for (int m_ = 0; m_ < RPL; ++m_)                   \
+      asm volatile("" : "+v"(acc[m_])::"memory");                        \
+  }
+
 // LDS vectors are [pad NX | N*NX rows | pad NX]: the pads stay zero so the
 // block-tridiagonal products need no edge branches.  r is double-buffered
 // (rbuf[it & 1]): in the same phase every lane reads the old r of its block
@@ -385,16 +410,17 @@ struct PcgLds {
   double *pbuf, *rbuf[2], *abuf, *wbuf, *tbuf, *xbuf, *red, *piv;
 };
 
-// Fixed stride (the 1024-row maximum plus the pads) so that every buffer is a
+// Fixed stride (the VR-row maximum plus the pads) so that every buffer is a
 // compile-time offset from one per-lane address: one address VGPR for all
-// vector traffic instead of one per buffer.
-__host__ __device__ constexpr size_t pcg_vec_doubles(int /*N*/, int NX) { return (size_t)1024 + 2 * NX; }
-__host__ __device__ inline size_t pcg_lds_doubles(int N, int NX) {
-  return PCG_NVEC * pcg_vec_doubles(N, NX) + 48 + (size_t)2 * N * NX;
+// vector traffic instead of one per buffer.  VR = 1024 for the register-row
+// kernels, QP_MAX_ROWS for the global-row ones (GM, more than 1024 rows).
+__host__ __device__ constexpr size_t pcg_vec_doubles(int NX, int VR) { return (size_t)VR + 2 * NX; }
+__host__ __device__ inline size_t pcg_lds_doubles(int N, int NX, int VR) {
+  return PCG_NVEC * pcg_vec_doubles(NX, VR) + 48 + (size_t)2 * N * NX;
 }
 
-__device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
-  const size_t v = pcg_vec_doubles(N, NX);
+__device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX, int VR) {
+  const size_t v = pcg_vec_doubles(NX, VR);
   PcgLds L;
   L.pbuf = lds + NX;
   L.rbuf[0] = L.pbuf + v;
@@ -409,8 +435,8 @@ __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX) {
 }
 
 // zero the pads and the reduction slots (callers barrier before first use)
-__device__ __forceinline__ void pcg_lds_clear(double* lds, int N, int NX) {
-  const size_t v = pcg_vec_doubles(N, NX);
+__device__ __forceinline__ void pcg_lds_clear(double* lds, int N, int NX, int VR) {
+  const size_t v = pcg_vec_doubles(NX, VR);
   const int rows = N * NX;
   for (int e = threadIdx.x; e < PCG_NVEC * 2 * NX + 48; e += blockDim.x) {
     if (e < PCG_NVEC * 2 * NX) {
@@ -494,8 +520,8 @@ __device__ __forceinline__ void pcg_precondition(PcgRow<NX> (&R)[RPL], int preco
 // all RPL rows.  With one row per lane: three independent chains (latency);
 // with two: one chain per row (the rows interleave, and the VGPR budget of a
 // 2-waves-per-SIMD launch has no room for more accumulators).
-template <int NX, int RPL>
-__device__ __forceinline__ void pcg_spmv(const PcgRow<NX> (&R)[RPL], const double* __restrict__ v, int kb,
+template <int NX, int RPL, class RT>
+__device__ __forceinline__ void pcg_spmv(const RT (&R)[RPL], const double* __restrict__ v, int kb,
                                          double (&out)[RPL]) {
   const double* vm = v + kb - NX;
   constexpr int NC = RPL == 1 ? 3 : 1;
@@ -526,8 +552,8 @@ __device__ __forceinline__ void pcg_spmv(const PcgRow<NX> (&R)[RPL], const doubl
 }
 
 // out[m] = P_kk row . v_k
-template <int NX, int RPL>
-__device__ __forceinline__ void pcg_block_dot(const PcgRow<NX> (&R)[RPL], const double* __restrict__ v,
+template <int NX, int RPL, class RT>
+__device__ __forceinline__ void pcg_block_dot(const RT (&R)[RPL], const double* __restrict__ v,
                                               double (&out)[RPL]) {
   constexpr int NC = RPL == 1 ? 2 : 1;
   double a[NC][RPL];
@@ -540,6 +566,7 @@ __device__ __forceinline__ void pcg_block_dot(const PcgRow<NX> (&R)[RPL], const 
     const double vj = v[j];
 #pragma unroll
     for (int m = 0; m < RPL; ++m) a[j % NC][m] += R[m].pr[j] * vj;
+    PCG_LOAD_FENCE(RT, j, a[0])
   }
 #pragma unroll
   for (int m = 0; m < RPL; ++m) out[m] = NC == 2 ? a[0][m] + a[NC - 1][m] : a[0][m];
@@ -575,8 +602,8 @@ __device__ __forceinline__ double red_total(const double* red) {
 }
 
 // t = r - (S_{k,k-1} w_{k-1} + S_{k,k+1} w_{k+1}) for this lane's rows
-template <int NX, int RPL>
-__device__ __forceinline__ void pcg_off(const PcgRow<NX> (&R)[RPL], const double* __restrict__ w, int kb,
+template <int NX, int RPL, class RT>
+__device__ __forceinline__ void pcg_off(const RT (&R)[RPL], const double* __restrict__ w, int kb,
                                         const double (&r)[RPL], double (&t)[RPL]) {
   const double* wm = w + kb - NX;
   constexpr int NC = RPL == 1 ? 2 : 1;
@@ -593,6 +620,7 @@ __device__ __forceinline__ void pcg_off(const PcgRow<NX> (&R)[RPL], const double
       a[0][m] += R[m].sl[j] * wl;
       a[NC - 1][m] += R[m].su[j] * wu;
     }
+    PCG_LOAD_FENCE(RT, j, a[0])
   }
 #pragma unroll
   for (int m = 0; m < RPL; ++m) t[m] = r[m] - (NC == 2 ? a[0][m] + a[NC - 1][m] : a[0][m]);
@@ -614,8 +642,8 @@ __device__ __forceinline__ void pcg_off(const PcgRow<NX> (&R)[RPL], const double
 // (r - (Ap alpha), x + (p alpha), z + (p beta): no FMA contraction); only the
 // summation order of the dot and block products differs.  x = the lane's
 // entries of the solution.
-template <int NX, int RPL, int PRE>
-__device__ __forceinline__ void pcg_run(const PcgRow<NX> (&R)[RPL], const PcgLane<NX, RPL>& ln, int N,
+template <int NX, int RPL, int PRE, class RT>
+__device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RPL>& ln, int N,
                                         const PcgLds& L, const double (&bv)[RPL], const double* guess_v, double tol,
                                         int max_iter, double* tn, double* tr, int* iters_out, double (&xv)[RPL]) {
   const int kb = ln.k * NX;
@@ -747,6 +775,7 @@ __device__ __forceinline__ void pcg_run(const PcgRow<NX> (&R)[RPL], const PcgLan
           acc[j % NC][m] += R[m].pr[j] * rj;
           if (j == ln.r(m)) rv[m] = rj;
         }
+        PCG_LOAD_FENCE(RT, j, acc[0])
       }
 #pragma unroll
       for (int m = 0; m < RPL; ++m) w[m] = NC == 2 ? acc[0][m] + acc[NC - 1][m] : acc[0][m];
@@ -821,8 +850,8 @@ __device__ __forceinline__ void pcg_run(const PcgRow<NX> (&R)[RPL], const PcgLan
   *iters_out = it_done;
 }
 
-template <int NX, int RPL>
-__device__ __forceinline__ void pcg_dispatch(int precond, const PcgRow<NX> (&R)[RPL], const PcgLane<NX, RPL>& ln,
+template <int NX, int RPL, class RT>
+__device__ __forceinline__ void pcg_dispatch(int precond, const RT (&R)[RPL], const PcgLane<NX, RPL>& ln,
                                              int N, const PcgLds& L, const double (&bv)[RPL], const double* guess_v,
                                              double tol, int max_iter, double* tn, double* tr, int* iters_out,
                                              double (&xv)[RPL]) {
@@ -857,8 +886,8 @@ __global__ void __launch_bounds__(MAXT) k_pcg(int B, int N, int precond, const d
   const int b = blockIdx.x;
   extern __shared__ __align__(16) double lds[];
   const int rows = N * NX;
-  pcg_lds_clear(lds, N, NX);
-  const PcgLds L = pcg_lds(lds, N, NX);
+  pcg_lds_clear(lds, N, NX, 1024);
+  const PcgLds L = pcg_lds(lds, N, NX, 1024);
   const PcgLane<NX, RPL> ln(threadIdx.x, N);
   const int k = ln.k, K = N - 1;
   PcgRow<NX> R[RPL];
@@ -926,14 +955,14 @@ __host__ __device__ inline size_t qp_stage_doubles(int N, int NX, int NU) {
 // (which start at 0); the cost gradients g_k = [dx_k^T Q_k, u_k^T R] live past
 // both because they must survive the PCG.  In the epilogue the x / u slots of
 // the staging area hold C^T lambda.
-__host__ __device__ inline size_t qp_g_offset(int N, int NX, int NU) {
+__host__ __device__ inline size_t qp_g_offset(int N, int NX, int NU, int VR) {
   const size_t a = qp_stage_doubles(N, NX, NU) + (size_t)N * NX;
-  const size_t p = pcg_lds_doubles(N, NX);
+  const size_t p = pcg_lds_doubles(N, NX, VR);
   return a > p ? a : p;
 }
 
-__host__ __device__ inline size_t qp_lds_doubles(int N, int NX, int NU) {
-  return qp_g_offset(N, NX, NU) + (size_t)N * (NX + NU);
+__host__ __device__ inline size_t qp_lds_doubles(int N, int NX, int NU, int VR) {
+  return qp_g_offset(N, NX, NU, VR) + (size_t)N * (NX + NU);
 }
 
 struct QpStage {
@@ -1045,7 +1074,9 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
 //       QP_MODE_SCHUR prologue only: S blocks and gamma to Sd_out / Sl_out / gam_out
 //                     (method S: the direct solve k_btsolve runs next);
 //       QP_MODE_DXU   epilogue only, lambda read from lam_out (method S, after k_btsolve).
-template <int NJ, int RPL, int MAXT, bool PK, int MODE>
+//       GM: more than 1024 rows -- S and P^-1 rows in HBM (Sg, [B][4][NX][rows], PcgRowG), two rows
+//           per lane, LDS vectors of QP_MAX_ROWS rows.
+template <int NJ, int RPL, int MAXT, bool PK, int MODE, bool GM = false>
 __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond,
                                              const double* __restrict__ x, const double* __restrict__ u,
                                              const int* __restrict__ active, const double* __restrict__ Ginv,
@@ -1055,8 +1086,10 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
                                              double* __restrict__ du, double* __restrict__ lam_out,
                                              double* __restrict__ Sd_out, double* __restrict__ Sl_out,
                                              double* __restrict__ gam_out, double* __restrict__ Pd_out,
-                                             const double* __restrict__ jsoft, const double* __restrict__ guess) {
+                                             const double* __restrict__ jsoft, const double* __restrict__ guess,
+                                             double* __restrict__ Sg) {
   constexpr int NX = 2 * NJ, NU = NJ;
+  constexpr int VR = GM ? QP_MAX_ROWS : 1024;
   const int b = blockIdx.x;
   if (!active[b]) return;
   extern __shared__ __align__(16) double lds[];
@@ -1073,7 +1106,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   __syncthreads();
 
   // cost gradients g_k = [(x_k - xg)^T Q_k, u_k^T R] (QuadraticCost.gradient, TrajoptCost.py:58-69)
-  double* g_lds = lds + qp_g_offset(N, NX, NU);    // [N][NX + NU]
+  double* g_lds = lds + qp_g_offset(N, NX, NU, VR);    // [N][NX + NU]
   for (int e = threadIdx.x; e < N * (NX + NU); e += blockDim.x) {
     const int kk = e / (NX + NU), c = e - kk * (NX + NU);
     double g = 0.0;
@@ -1099,6 +1132,9 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
   } else {
   PcgRow<NX> R[RPL];
   double bv[RPL];
+  // GM: this lane's rows of S / P^-1 in HBM (invalid lanes point at row m L and never use it)
+  double* const Sgb = GM ? Sg + (size_t)b * 4 * NX * rows : nullptr;
+  auto g_at = [&](int q, int m) { return Sgb + (size_t)q * NX * rows + ln.row(m); };
 #pragma unroll
   for (int m = 0; m < RPL; ++m) {
 #pragma unroll
@@ -1116,19 +1152,46 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
       }
       gam_out[(size_t)b * rows + ln.row(m)] = bv[m];
     }
+    if constexpr (GM && MODE == QP_MODE_PCG) {
+      // off-diagonal rows to HBM now; the diagonal row stays for the preconditioner
+#pragma unroll
+      for (int j = 0; j < NX; ++j) {
+        g_at(0, m)[(size_t)j * rows] = R[m].sd[j];
+        g_at(1, m)[(size_t)j * rows] = R[m].sl[j];
+        g_at(2, m)[(size_t)j * rows] = R[m].su[j];
+        R[m].sl[j] = R[m].su[j] = 0.0;
+      }
+    }
   }
   if constexpr (MODE == QP_MODE_SCHUR) {
     if (threadIdx.x == 0) iters[b] = 0;
     return;
   }
   __syncthreads();   // the PCG buffers alias the staging area
-  pcg_lds_clear(lds, N, NX);
-  const PcgLds L = pcg_lds(lds, N, NX);
+  pcg_lds_clear(lds, N, NX, VR);
+  const PcgLds L = pcg_lds(lds, N, NX, VR);
   pcg_precondition<NX, RPL>(R, precond, ln, N, L.piv, Pd_out ? Pd_out + ((size_t)b * N + k) * NX * NX : nullptr);
   int it_done = 0;
   // PCG warm start (PCG.update_guess, TrajoptMPCReference.py:439-440): guess [B][N NX] or null
-  pcg_dispatch<NX, RPL>(precond, R, ln, N, L, bv, guess ? guess + (size_t)b * rows : nullptr, tol, max_iter, nullptr,
-                        nullptr, &it_done, xv);
+  if constexpr (GM) {
+    PcgRowG<NX> RG[RPL];
+#pragma unroll
+    for (int m = 0; m < RPL; ++m) {
+      if (ln.valid) {
+#pragma unroll
+        for (int j = 0; j < NX; ++j) g_at(3, m)[(size_t)j * rows] = R[m].pr[j];
+      }
+      RG[m].sd = GRowRef{g_at(0, m), rows};
+      RG[m].sl = GRowRef{g_at(1, m), rows};
+      RG[m].su = GRowRef{g_at(2, m), rows};
+      RG[m].pr = GRowRef{g_at(3, m), rows};
+    }
+    pcg_dispatch<NX, RPL>(precond, RG, ln, N, L, bv, guess ? guess + (size_t)b * rows : nullptr, tol, max_iter,
+                          nullptr, nullptr, &it_done, xv);
+  } else {
+    pcg_dispatch<NX, RPL>(precond, R, ln, N, L, bv, guess ? guess + (size_t)b * rows : nullptr, tol, max_iter,
+                          nullptr, nullptr, &it_done, xv);
+  }
   if (threadIdx.x == 0) iters[b] = it_done;
   }
 
@@ -1548,16 +1611,21 @@ struct LaunchNJ {
   static void qp(hipStream_t s, const CostDev* C, int B, int N, int precond, int mode, const double* x, const double* u,
                  const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
                  int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-                 double* Pd, const double* jsoft, const double* guess) {
+                 double* Pd, const double* jsoft, const double* guess, double* Sg) {
     constexpr int NX = 2 * NJ;
     const int rows = N * NX;
-    const int rpl = pcg_rpl(N, NX);
+    // S / P^-1 rows in HBM (Sg), two rows per lane, up to 1024 lanes (method S past 1024 rows runs the
+    // same instance for its prologue / epilogue modes, which never touch Sg)
+    const bool gm = rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG);
+    const int rpl = gm ? 2 : pcg_rpl(N, NX);
     const int threads = ((rows / rpl + 63) / 64) * 64;
-    const size_t lds = qp_lds_doubles(N, NX, NJ) * sizeof(double);
+    const size_t lds = qp_lds_doubles(N, NX, NJ, gm ? QP_MAX_ROWS : 1024) * sizeof(double);
 #define TMPC_QP_ARGS s, C, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, \
-                     Sl, gam, Pd, jsoft, guess
+                     Sl, gam, Pd, jsoft, guess, Sg
 #define TMPC_QP_LAUNCH(PKV, MODEV)                                                                        \
-    if (rpl == 1)                                                                                          \
+    if (gm)                                                                                                \
+      hipLaunchKernelGGL((k_qp<NJ, 2, QP_MAX_ROWS / 2, PKV, MODEV, true>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS); \
+    else if (rpl == 1)                                                                                     \
       hipLaunchKernelGGL((k_qp<NJ, 1, 768, PKV, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);        \
     else                                                                                                   \
       hipLaunchKernelGGL((k_qp<NJ, 2, 512, PKV, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);
@@ -1592,7 +1660,9 @@ int pcg_set_max_lds() {
   err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1, 768, P, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                   bytes);                                                              \
   err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 2, 512, P, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                  bytes);
+                                  bytes);                                                              \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 2, QP_MAX_ROWS / 2, P, MD, true>,                          \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 #define SETQ1(V, P) SETQ2(V, P, QP_MODE_PCG) SETQ2(V, P, QP_MODE_SCHUR) SETQ2(V, P, QP_MODE_DXU)
 #define SETQ(V) SETQ1(V, false) SETQ1(V, true)
   SETQ(1) SETQ(2) SETQ(3) SETQ(4) SETQ(5) SETQ(6) SETQ(7)
@@ -1609,7 +1679,7 @@ static void launch_pcg_nx(hipStream_t s, int B, int N, int precond, const double
   const int rows = N * NX;
   const int rpl = pcg_rpl(N, NX);
   const int threads = ((rows / rpl + 63) / 64) * 64;
-  const size_t lds = pcg_lds_doubles(N, NX) * sizeof(double);
+  const size_t lds = pcg_lds_doubles(N, NX, 1024) * sizeof(double);
   if (rpl == 1)
     hipLaunchKernelGGL((k_pcg<NX, 1, 768>), dim3(B), dim3(threads), lds, s, B, N, precond, Sd, Sl, Su, gam, guess,
                        tol, max_iter, lam, iters, tnu, tres, Pd);
@@ -1845,11 +1915,14 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
-              double* Pd, const double* jsoft, const double* guess) {
-  if (N * 2 * nj > 1024) return -1;
-  if (qp_lds_doubles(N, 2 * nj, nj) * sizeof(double) > 160 * 1024) return -3;
+              double* Pd, const double* jsoft, const double* guess, double* Sg) {
+  const int rows = N * 2 * nj;
+  if (rows > QP_MAX_ROWS) return -1;
+  const bool gm = rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG);
+  if (gm && mode == QP_MODE_PCG && !Sg) return -4;
+  if (qp_lds_doubles(N, 2 * nj, nj, gm ? QP_MAX_ROWS : 1024) * sizeof(double) > 160 * 1024) return -3;
   TMPC_DISPATCH_NJ2(nj, qp(s, C, B, N, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd,
-                           Sl, gam, Pd, jsoft, guess))
+                           Sl, gam, Pd, jsoft, guess, Sg))
 }
 int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
                      const int* active, const double* x, const double* u, const double* mu, const double* lam,
