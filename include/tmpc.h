@@ -20,7 +20,8 @@
  *     tmpc_device_alloc on the same context;
  *   - one context per GPU, used by one host thread; calls are synchronous on
  *     the context's HIP stream;
- *   - all arithmetic is IEEE fp64, as in the reference.
+ *   - all arithmetic is IEEE fp64, as in the reference, unless tmpc_options.precision selects
+ *     fp32 dynamics (TMPC_PRECISION_F32 / _MIXED).
  *
  * Array layouts follow the reference's NumPy arrays in C order:
  *   x: [B][nx][N] (state column per knot), u: [B][nu][N-1],
@@ -36,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 4
+#define TMPC_ABI_VERSION 5
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). N (dense KKT) is not offered on the GPU. */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
@@ -94,8 +95,19 @@ typedef struct tmpc_options {
    * previous QP's lambda of the same problem, and in tmpc_mpc_batch the first QP of an MPC step starts
    * from the previous step's last lambda shifted by one knot (oracle/mpc.py). */
   int32_t pcg_warm_start;                /* 0      */
-  int32_t reserved0;
+  /* Arithmetic precision (BASELINE configs 3 and 5; the reference is fp64 throughout):
+   * TMPC_PRECISION_F64   everything fp64 (default, the reference's arithmetic);
+   * TMPC_PRECISION_F32   rigid-body dynamics (forward dynamics, M^-1, RNEA gradient: the QP build,
+   *                      line-search / rollout dynamics) and the iLQR Riccati sweep in fp32;
+   * TMPC_PRECISION_MIXED rigid-body dynamics in fp32, Schur complement / PCG and Riccati in fp64.
+   * In every mode the buffers, the merit / cost sums, the acceptance tests and the MPC loop's
+   * simulated plant step are fp64. */
+  int32_t precision;                     /* 0      */
 } tmpc_options;
+
+#define TMPC_PRECISION_F64 0
+#define TMPC_PRECISION_F32 1
+#define TMPC_PRECISION_MIXED 2
 
 /* Box limits of TrajoptConstraint (set_joint_limits / set_velocity_limits / set_torque_limits,
  * TrajoptConstraint.py:190-206) in a soft or hard mode, with the BoxConstraint options (:38-46).

@@ -1,0 +1,119 @@
+"""GPU checks of the precision modes (tmpc_options.precision; BASELINE configs 3
+and 5 name fp32 and mixed fp32-dynamics / fp64-PCG arithmetic, the reference
+is fp64 only, so these modes have no reference counterpart: "parity
+unpinned", checked against the fp64 oracle within stated tolerances).
+
+  F32    rigid-body dynamics (FD, M^-1, RNEA gradient) and the iLQR Riccati
+         sweep in fp32;
+  MIXED  dynamics in fp32, Schur / PCG / Riccati in fp64;
+buffers, merit sums, acceptance tests and the MPC plant step stay fp64.
+
+Tolerances (measured on MI355X, tools/debug/precision_probe.py, in brackets):
+  * fp32 dynamics vs the reference's fp64 outputs: 1e-5 of max|ref| [<= 9.8e-7];
+  * iLQR trajectories vs fp64, unconstrained arm3 / arm6: 2e-3 relative [4.9e-4].
+    Exit codes / iteration counts are NOT compared: the reference's exit test
+    dJ < 1e-6 is below fp32 rounding of the rollout costs, so fp32 solves end
+    on the rho schedule (exit 2) where fp64 ones converge (exit 1);
+  * config 5 (mixed, SQP PCG-SS MPC loop at N = 128): per-step exit codes and
+    SQP iterations identical to the fp64 oracle, executed states 1e-4 [6.7e-6].
+"""
+import numpy as np
+import pytest
+
+from conftest import arm_model, golden, quad_cost_arrays
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float(np.max(np.abs(np.asarray(a) - np.asarray(b)))) / max(1.0, float(np.max(np.abs(b))))
+
+
+def _solver(n, N, spec=None):
+    from trajoptmpcreference_amd import (QuadraticCost, TrajoptConstraint, TrajoptMPCReference, URDFPlant,
+                                         planar_arm_urdf)
+    plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(n)})
+    con = TrajoptConstraint(n, n, n, N)
+    for kind, (lb, ub, mode) in (spec or {}).items():
+        getattr(con, f"set_{kind}_limits")(ub, lb, mode)
+    return TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(n)), con)
+
+
+def _problems(name, N, seeds, dt=0.1):
+    from oracle import sqp as osqp
+    m = arm_model(name)
+    xs, us = zip(*[osqp.initial_problem(m, N, dt, int(s)) for s in seeds])
+    return np.array(xs), np.array(us)
+
+
+@pytest.mark.parametrize("name", ["arm2", "arm3", "arm6fix"])
+def test_fp32_dynamics_match_reference(ctx, name):
+    ctx.set_model(arm_model(name))
+    d = golden(f"dyn_{name}.npz")
+    ctx.set_options(precision=1)
+    try:
+        xn, qdd, Mi = ctx.fd_batch(d["x"], d["u"], float(d["dt"]))
+        A, B, dq = ctx.fd_grad_batch(d["x"], d["u"], float(d["dt"]))
+    finally:
+        ctx.set_options(precision=0)
+    for got, key in ((qdd, "qdd"), (Mi, "Minv"), (xn, "xnext"), (dq, "dqdd"), (A, "A"), (B, "B")):
+        err = _rel(got, d[key])
+        assert err < 1e-5, (key, err)
+        assert err > 0.0 or key in ("B",), key   # fp32 arithmetic really ran (B = dt Minv may round exactly)
+
+
+@pytest.mark.parametrize("name,n,N", [("arm3", 3, 32), ("arm6fix", 6, 64)])
+@pytest.mark.parametrize("prec", ["fp32", "mixed"])
+def test_reduced_precision_ilqr_tracks_fp64(name, n, N, prec):
+    x, u = _problems(name, N, range(300, 316))
+    s = _solver(n, N)
+    r64 = s.iLQR_batch(x.copy(), u.copy(), N, 0.1, {})
+    assert list(r64["exit_code"]) == [1] * len(x)
+    r = s.iLQR_batch(x.copy(), u.copy(), N, 0.1, {"precision": prec})
+    errs = [_rel(r["x"][i], r64["x"][i]) for i in range(len(x))]
+    assert max(errs) < 2e-3, errs
+    erru = [_rel(r["u"][i], r64["u"][i]) for i in range(len(x))]
+    assert max(erru) < 2e-2, erru
+    assert not np.array_equal(r["x"], r64["x"])
+
+
+def test_config3_fp32_ilqr_al_converged_problems():
+    """BASELINE config 3 in fp32 (arm6 N = 64 iLQR, augmented-Lagrangian torque limits): the problems
+    the fp64 oracle solves to convergence (exit 1) are solved by the fp32 path to the same optimum."""
+    d = golden("oracle_config3_arm6_N64_ilqr_al.npz")
+    N = int(d["N"])
+    lb, ub = float(d["lb"]), float(d["ub"])
+    s = _solver(6, N, {"torque": ([lb] * 6, [ub] * 6, "AUGMENTED_LAGRANGIAN")})
+    x, u = _problems("arm6fix", N, d["seeds"])
+    opts = {"max_iter_softConstraints": int(d["max_iter_softConstraints"]),
+            "max_iter_SQP_DDP": int(d["max_iter_SQP_DDP"]), "precision": "fp32"}
+    r = s.iLQR_batch(x, u, N, 0.1, opts)
+    conv = [i for i in range(len(x)) if int(d["exit_code_0"][i]) == 1]
+    assert conv
+    for i in conv:
+        assert int(r["exit_code"][i]) == 1, i
+        assert _rel(r["x"][i], d["x_0"][i]) < 2e-3, i
+    assert all(np.isfinite(r["x"]).ravel())
+
+
+def test_config5_mixed_mpc_sqp_n128():
+    """BASELINE config 5: receding-horizon MPC, arm6 N = 128, fp32 dynamics / fp64 PCG (SQP PCG-SS,
+    PCG warm start) against the fp64 oracle loop."""
+    d = golden("oracle_config5_arm6_N128_mpc_sqp_pcgss.npz")
+    N, steps = int(d["N"]), int(d["steps"])
+    x, u = _problems("arm6fix", N, d["seeds"])
+    r = _solver(6, N).MPC_batch(x, u, N, 0.1, "QP-PCG-SS", {"pcg_warm_start": True, "precision": "mixed"},
+                                mpc_steps=steps)
+    for i in range(len(d["seeds"])):
+        assert list(r["exit_codes"][i]) == list(d["exit_codes"][i]), i
+        assert list(r["iters"][i]) == list(d["iters"][i]), i
+        assert _rel(r["x_exec"][i], d["x_exec"][i]) < 1e-4, i
+
+
+def test_precision_option_is_validated(ctx):
+    from trajoptmpcreference_amd import _native
+    with pytest.raises(_native.NativeError):
+        ctx.set_options(precision=7)
+    ctx.set_options(precision=0)
+    with pytest.raises(ValueError):
+        _solver(3, 8).SQP_batch(*_problems("arm3", 8, [0]), 8, 0.1, "PCG-SS", {"precision": "bf16"})

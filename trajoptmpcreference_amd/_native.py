@@ -40,7 +40,7 @@ class tmpc_options(C.Structure):
         ("max_iter_softConstraints", C.c_int32),
         ("exit_tolerance_softConstraints", C.c_double),
         ("pcg_warm_start", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("precision", C.c_int32),
     ]
 
 

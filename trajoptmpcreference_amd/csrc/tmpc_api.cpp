@@ -167,6 +167,11 @@ static T* buf(tmpc_ctx* ctx, const char* name, size_t count) {
   if (!name) return fail(ctx, "device allocation of %s (%zu elements) failed", #name, \
                          (size_t)(count));
 
+// precision modes (tmpc_options.precision): rigid-body dynamics in fp32 for F32 and MIXED, the
+// Riccati sweep in fp32 for F32 only; Schur / PCG, merit sums and decisions stay fp64
+static bool dyn32(const tmpc_ctx* ctx) { return ctx->opts.precision != TMPC_PRECISION_F64; }
+static bool ric32(const tmpc_ctx* ctx) { return ctx->opts.precision == TMPC_PRECISION_F32; }
+
 static SolverOpts solver_opts(const tmpc_options& o) {
   SolverOpts s{};
   s.exit_tol_sqp = o.exit_tolerance_SQP_DDP;
@@ -242,16 +247,16 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   const double* G = soft ? w.Gk : w.G;
   {
     Timed t(ctx, "qp_fd");
-    LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
+    LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
                            w.cvec));
   }
   {
     Timed t(ctx, "qp_minv");
-    LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
+    LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
   }
   {
     Timed t(ctx, "qp_grad");
-    LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv, w.A,
+    LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv, w.A,
                              w.Bm));
   }
   if (soft) {
@@ -552,7 +557,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
   launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
   // initial J, c, merit (:541-548)
-  LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
+  LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
                             alphas + T, d_x, d_u, w.xs, nullptr, nullptr, st.active, terms));
   if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, st.active));
   HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
@@ -562,7 +567,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     if ((rc = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false))) return rc;
     {
       Timed t(ctx, "ls_terms");
-      LAUNCH_OK(launch_ls_terms(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
+      LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
                                 alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
       if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, T, alphas, d_x, d_u, w.dx, w.du, st.active));
     }
@@ -646,40 +651,40 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   }
   HIP_OK(hipMemcpyAsync(alphas, al.data(), al.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   // iLQR iterates are rollouts: start from the rollout of u from x[:, 0]
-  LAUNCH_OK(launch_rollout(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
+  LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
   for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
     launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
     HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-    LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
+    LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
                                   1, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
     launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st,
                        tr, active_count, nullptr);
     for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
       {
         Timed t(ctx, "qp_fd");
-        LAUNCH_OK(launch_qp_fd(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
+        LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
                                w.cvec));
       }
       {
         Timed t(ctx, "qp_minv");
-        LAUNCH_OK(launch_qp_minv(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
+        LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
       }
       {
         Timed t(ctx, "qp_grad");
-        LAUNCH_OK(launch_qp_grad(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv,
+        LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv,
                                  w.A, w.Bm));
       }
       {
         Timed t(ctx, "ilqr_backward");
-        LAUNCH_OK(launch_ilqr_backward(ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, d_x, d_u, st.rho, st.active,
+        LAUNCH_OK(launch_ilqr_backward(ric32(ctx), ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, d_x, d_u, st.rho, st.active,
                                        w.A, w.Bm, smu, slam, il_K, il_d, il_dV, il_ok));
       }
       {
         Timed t(ctx, "ilqr_forward");
-        LAUNCH_OK(launch_ilqr_forward(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T,
+        LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T,
                                       dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
       }
       HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
@@ -953,6 +958,8 @@ int tmpc_set_options(tmpc_ctx* ctx, const tmpc_options* o) {
     return fail(ctx, "max_iter options must be >= 1");
   if (!(o->alpha_factor_SQP_DDP > 0.0 && o->alpha_factor_SQP_DDP < 1.0))
     return fail(ctx, "alpha_factor_SQP_DDP must be in (0, 1)");
+  if (o->precision < TMPC_PRECISION_F64 || o->precision > TMPC_PRECISION_MIXED)
+    return fail(ctx, "precision %d (valid: 0 F64, 1 F32, 2 MIXED)", o->precision);
   ctx->opts = *o;
   return 0;
 }
@@ -1151,7 +1158,7 @@ int tmpc_rollout_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model");
   hipSetDevice(ctx->device);
-  LAUNCH_OK(launch_rollout(ctx->stream, ctx->hmodel.n, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
+  LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, ctx->hmodel.n, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1170,8 +1177,8 @@ int tmpc_fd_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const double
   BUF(double, u_minv, (size_t)K * nj * nj);
   HIP_OK(hipMemcpyAsync(u_x, x, sizeof(double) * K * nx, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(u_u, u, sizeof(double) * K * nj, hipMemcpyHostToDevice, ctx->stream));
-  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, K, dt, u_x, u_u, u_xn, u_qdd));
-  if (Minv) LAUNCH_OK(launch_unit_minv(ctx->stream, nj, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, K, u_x, u_minv));
+  LAUNCH_OK(launch_unit_fd(dyn32(ctx), ctx->stream, nj, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, K, dt, u_x, u_u, u_xn, u_qdd));
+  if (Minv) LAUNCH_OK(launch_unit_minv(dyn32(ctx), ctx->stream, nj, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, K, u_x, u_minv));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (xnext) HIP_OK(hipMemcpy(xnext, u_xn, sizeof(double) * K * nx, hipMemcpyDeviceToHost));
   if (qdd) HIP_OK(hipMemcpy(qdd, u_qdd, sizeof(double) * K * nj, hipMemcpyDeviceToHost));
@@ -1196,9 +1203,9 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
   BUF(double, u_dqdd, (size_t)K * nj * 3 * nj);
   HIP_OK(hipMemcpyAsync(u_x, x, sizeof(double) * K * nx, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(u_u, u, sizeof(double) * K * nj, hipMemcpyHostToDevice, ctx->stream));
-  LAUNCH_OK(launch_unit_fd(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, 0.0, u_x, u_u, nullptr, u_qdd));
-  LAUNCH_OK(launch_unit_minv(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, u_x, u_minv));
-  LAUNCH_OK(launch_unit_grad(ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, dt, u_x, u_qdd, u_minv, u_A, u_B, u_dqdd));
+  LAUNCH_OK(launch_unit_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, 0.0, u_x, u_u, nullptr, u_qdd));
+  LAUNCH_OK(launch_unit_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, u_x, u_minv));
+  LAUNCH_OK(launch_unit_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, K, dt, u_x, u_qdd, u_minv, u_A, u_B, u_dqdd));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (A) HIP_OK(hipMemcpy(A, u_A, sizeof(double) * K * nx * nx, hipMemcpyDeviceToHost));
   if (Bo) HIP_OK(hipMemcpy(Bo, u_B, sizeof(double) * K * nx * nj, hipMemcpyDeviceToHost));

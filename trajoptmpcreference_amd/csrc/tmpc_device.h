@@ -223,6 +223,16 @@ __device__ __forceinline__ const ModelDev* stage_model(const ModelDev* __restric
   return sM;
 }
 
+// ----------------------------------------------------------------- scalar type
+// The dynamics routines below are templated on the arithmetic type R: double
+// (the reference's fp64, bit-for-bit the untemplated code) or float (the
+// fp32 / mixed precision modes of tmpc_options.precision).  Model
+// coefficients are stored in double and rounded to R where they are used.
+__device__ __forceinline__ void sincos_r(double q, double& s, double& c) { sincos(q, &s, &c); }
+__device__ __forceinline__ void sincos_r(float q, float& s, float& c) { sincosf(q, &s, &c); }
+__device__ __forceinline__ double fma_r(double a, double b, double c) { return __fma_rn(a, b, c); }
+__device__ __forceinline__ float fma_r(float a, float b, float c) { return __fmaf_rn(a, b, c); }
+
 // ----------------------------------------------------------------- model access
 // The dynamics routines take the model as `const MT& M` and read it as
 // `M->field`:
@@ -258,10 +268,10 @@ __device__ __forceinline__ bool in_subtree(const MT& M, int j, int s) {
   return CHAIN ? (s >= j) : ((M->subtree[j] >> s) & 1u);
 }
 
-template <class MT>
-__device__ __forceinline__ void joint_cs(const MT& M, int j, double q, double& c, double& s) {
+template <class MT, class R>
+__device__ __forceinline__ void joint_cs(const MT& M, int j, R q, R& c, R& s) {
   if (M->jtype[j] == 0) {
-    sincos(q, &s, &c);
+    sincos_r(q, s, c);
   } else {
     c = q;
     s = 0.0;
@@ -270,34 +280,35 @@ __device__ __forceinline__ void joint_cs(const MT& M, int j, double q, double& c
 
 // Opaque copy: stops the compiler from CSE-ing X entries across passes
 // (which would keep 36 doubles per joint live for the whole kernel).
-__device__ __forceinline__ void opaque(double& c, double& s) { asm volatile("" : "+v"(c), "+v"(s)); }
+template <class R>
+__device__ __forceinline__ void opaque(R& c, R& s) { asm volatile("" : "+v"(c), "+v"(s)); }
 
 // entry e of X_j(q) = X0 + cos(q) Xa + sin(q) Xb; false for a structural zero
-template <class MT>
-__device__ __forceinline__ bool xent(const MT& M, int j, int e, double c, double s, double& x) {
+template <class MT, class R>
+__device__ __forceinline__ bool xent(const MT& M, int j, int e, R c, R s, R& x) {
   const double a0 = M->X0[j][e], a1 = M->Xa[j][e], a2 = M->Xb[j][e];
   if (!MT::STATIC) {
-    x = a0 + c * a1 + s * a2;
+    x = R(a0) + c * R(a1) + s * R(a2);
     return true;
   }
   if (a0 == 0.0 && a1 == 0.0 && a2 == 0.0) return false;
-  double t = a0;
-  if (a1 != 0.0) t = a0 != 0.0 ? __fma_rn(c, a1, a0) : c * a1;
-  if (a2 != 0.0) t = (a0 != 0.0 || a1 != 0.0) ? __fma_rn(s, a2, t) : s * a2;
+  R t = a0;
+  if (a1 != 0.0) t = a0 != 0.0 ? fma_r(c, R(a1), R(a0)) : c * R(a1);
+  if (a2 != 0.0) t = (a0 != 0.0 || a1 != 0.0) ? fma_r(s, R(a2), t) : s * R(a2);
   x = t;
   return true;
 }
 
 // y = X v, rows formed on the fly
-template <class MT>
-__device__ __forceinline__ void mvX(const MT& M, int j, double c, double s, const double v[6], double y[6]) {
+template <class MT, class R>
+__device__ __forceinline__ void mvX(const MT& M, int j, R c, R s, const R v[6], R y[6]) {
   opaque(c, s);
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    double acc = 0.0;
+    R acc = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      double x;
+      R x;
       if (xent(M, j, r * 6 + k, c, s, x)) acc += x * v[k];
     }
     y[r] = acc;
@@ -305,16 +316,16 @@ __device__ __forceinline__ void mvX(const MT& M, int j, double c, double s, cons
 }
 
 // y += X^T f, columns formed on the fly
-template <class MT>
-__device__ __forceinline__ void add_mtvX(const MT& M, int j, double c, double s, const double f[6], double y[6]) {
+template <class MT, class R>
+__device__ __forceinline__ void add_mtvX(const MT& M, int j, R c, R s, const R f[6], R y[6]) {
   opaque(c, s);
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
-    double acc = 0.0;
+    R acc = 0.0;
     bool any = false;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      double x;
+      R x;
       if (xent(M, j, r * 6 + k, c, s, x)) {
         acc += x * f[r];
         any = true;
@@ -325,22 +336,22 @@ __device__ __forceinline__ void add_mtvX(const MT& M, int j, double c, double s,
 }
 
 // o = I_j v
-template <class MT>
-__device__ __forceinline__ void mvI(const MT& M, int j, const double v[6], double o[6]) {
+template <class MT, class R>
+__device__ __forceinline__ void mvI(const MT& M, int j, const R v[6], R o[6]) {
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    double acc = 0.0;
+    R acc = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k)
-      if (nz<MT>(M->I[j][r * 6 + k])) acc += M->I[j][r * 6 + k] * v[k];
+      if (nz<MT>(M->I[j][r * 6 + k])) acc += R(M->I[j][r * 6 + k]) * v[k];
     o[r] = acc;
   }
 }
 
 // crm(w) S_j for a 0/1 subspace vector S (mxS, RBDReference.py:57-62)
-template <class MT>
-__device__ __forceinline__ void crmS(const double w[6], const MT& M, int j, double o[6]) {
-#define S_(i) M->S[j][i]
+template <class MT, class R>
+__device__ __forceinline__ void crmS(const R w[6], const MT& M, int j, R o[6]) {
+#define S_(i) R(M->S[j][i])
   if (!MT::STATIC) {
     o[0] = -w[2] * S_(1) + w[1] * S_(2);
     o[1] = w[2] * S_(0) - w[0] * S_(2);
@@ -352,8 +363,8 @@ __device__ __forceinline__ void crmS(const double w[6], const MT& M, int j, doub
   }
   // S is a unit vector: each output has at most one term, and the products are exact
 #define T_(acc, sign, wi, si) \
-  if (S_(si) != 0.0) acc += (sign) * w[wi] * S_(si);
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0;
+  if (S_(si) != 0.0) acc += R(sign) * w[wi] * S_(si);
+  R a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0;
   T_(a0, -1.0, 2, 1) T_(a0, 1.0, 1, 2)
   T_(a1, 1.0, 2, 0) T_(a1, -1.0, 0, 2)
   T_(a2, -1.0, 1, 0) T_(a2, 1.0, 0, 1)
@@ -366,24 +377,26 @@ __device__ __forceinline__ void crmS(const double w[6], const MT& M, int j, doub
 }
 
 // S_j . v
-template <class MT>
-__device__ __forceinline__ double dotS(const MT& M, int j, const double v[6]) {
-  double acc = 0.0;
+template <class MT, class R>
+__device__ __forceinline__ R dotS(const MT& M, int j, const R v[6]) {
+  R acc = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k)
-    if (nz<MT>(M->S[j][k])) acc += M->S[j][k] * v[k];
+    if (nz<MT>(M->S[j][k])) acc += R(M->S[j][k]) * v[k];
   return acc;
 }
 
-__device__ __forceinline__ double dot6(const double a[6], const double b[6]) {
-  double acc = 0.0;
+template <class R>
+__device__ __forceinline__ R dot6(const R a[6], const R b[6]) {
+  R acc = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) acc += a[k] * b[k];
   return acc;
 }
 
 // o += fxv(f, t) = crf(f) t (RBDReference.py:71-91); vxIv(v, I) = fxv(v, I v) (:98-116)
-__device__ __forceinline__ void add_fxv(const double f[6], const double t[6], double o[6]) {
+template <class R>
+__device__ __forceinline__ void add_fxv(const R f[6], const R t[6], R o[6]) {
   o[0] += -f[2] * t[1] + f[1] * t[2] - f[5] * t[4] + f[4] * t[5];
   o[1] += f[2] * t[0] - f[0] * t[2] + f[5] * t[3] - f[3] * t[5];
   o[2] += -f[1] * t[0] + f[0] * t[1] - f[4] * t[3] + f[3] * t[4];
@@ -398,8 +411,8 @@ __device__ __forceinline__ constexpr int sidx(int r, int c) {
 }
 
 // column k of X_j (structural-zero mask in nzm)
-template <class MT>
-__device__ __forceinline__ void Xcol(const MT& M, int j, double c, double s, int k, double x[6], bool nzm[6]) {
+template <class MT, class R>
+__device__ __forceinline__ void Xcol(const MT& M, int j, R c, R s, int k, R x[6], bool nzm[6]) {
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     nzm[r] = xent(M, j, r * 6 + k, c, s, x[r]);
@@ -409,17 +422,17 @@ __device__ __forceinline__ void Xcol(const MT& M, int j, double c, double s, int
 
 // out = X^T A X for symmetric A (21 entries).  Column-at-a-time so that only
 // two 6-vectors of X and one of A X are live (X columns are recomputed).
-template <class MT>
-__device__ __forceinline__ void XtAX(const MT& M, int j, double c, double s, const double A[21], double out[21]) {
+template <class MT, class R>
+__device__ __forceinline__ void XtAX(const MT& M, int j, R c, R s, const R A[21], R out[21]) {
   opaque(c, s);
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
-    double xk[6], z[6];
+    R xk[6], z[6];
     bool nk[6];
     Xcol(M, j, c, s, k, xk, nk);
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      double acc = 0.0;
+      R acc = 0.0;
 #pragma unroll
       for (int m = 0; m < 6; ++m)
         if (nk[m]) acc += A[sidx(r, m)] * xk[m];
@@ -427,7 +440,7 @@ __device__ __forceinline__ void XtAX(const MT& M, int j, double c, double s, con
     }
 #pragma unroll
     for (int r = 0; r <= k; ++r) {
-      double xr[6];
+      R xr[6];
       bool nr[6];
       if (r == k) {
 #pragma unroll
@@ -438,7 +451,7 @@ __device__ __forceinline__ void XtAX(const MT& M, int j, double c, double s, con
       } else {
         Xcol(M, j, c, s, r, xr, nr);
       }
-      double acc = 0.0;
+      R acc = 0.0;
 #pragma unroll
       for (int m = 0; m < 6; ++m)
         if (nr[m]) acc += xr[m] * z[m];
@@ -448,16 +461,16 @@ __device__ __forceinline__ void XtAX(const MT& M, int j, double c, double s, con
 }
 
 // y1 = X v1, y2 = X v2 sharing the formation of each X row
-template <class MT>
-__device__ __forceinline__ void mvX2(const MT& M, int j, double c, double s, const double v1[6], const double v2[6],
-                                     double y1[6], double y2[6]) {
+template <class MT, class R>
+__device__ __forceinline__ void mvX2(const MT& M, int j, R c, R s, const R v1[6], const R v2[6],
+                                     R y1[6], R y2[6]) {
   opaque(c, s);
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    double a1 = 0.0, a2 = 0.0;
+    R a1 = 0.0, a2 = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      double x;
+      R x;
       if (xent(M, j, r * 6 + k, c, s, x)) {
         a1 += x * v1[k];
         a2 += x * v2[k];
@@ -474,10 +487,10 @@ __device__ __forceinline__ void mvX2(const MT& M, int j, double c, double s, con
 // M^-1 tau (qd = 0, no gravity).  Velocities are recomputed in pass 3
 // instead of being kept from pass 1, so at most ~8 doubles per joint are
 // stored across passes.
-template <int NJ, bool CHAIN, bool UNIT = false, class MT>
-__device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const double sq[NJ], const double qd[NJ],
-                                       const double tau[NJ], double qdd[NJ]) {
-  double v[NJ][6];
+template <int NJ, bool CHAIN, bool UNIT = false, class MT, class R>
+__device__ __forceinline__ void fd_aba(const MT& M, const R cq[NJ], const R sq[NJ], const R qd[NJ],
+                                       const R tau[NJ], R qdd[NJ]) {
+  R v[NJ][6];
   // pass 1: velocities
   if (!UNIT) {
 #pragma unroll
@@ -491,11 +504,11 @@ __device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const d
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i)
-        if (nz<MT>(M->S[j][i])) v[j][i] += M->S[j][i] * qd[j];
+        if (nz<MT>(M->S[j][i])) v[j][i] += R(M->S[j][i]) * qd[j];
     }
   }
   // pass 2: articulated inertias / bias forces, leaf to root
-  double chIA[NJ][21], chpA[NJ][6];
+  R chIA[NJ][21], chpA[NJ][6];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
 #pragma unroll
@@ -503,23 +516,23 @@ __device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const d
 #pragma unroll
     for (int e = 0; e < 6; ++e) chpA[j][e] = 0.0;
   }
-  double U[NJ][6], Dd[NJ], uu[NJ];
+  R U[NJ][6], Dd[NJ], uu[NJ];
 #pragma unroll
   for (int j = NJ - 1; j >= 0; --j) {
-    double IA[21];
+    R IA[21];
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
       for (int k = r; k < 6; ++k)
-        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? M->I[j][r * 6 + k] + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
-    double pA[6], cj[6];
+        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? R(M->I[j][r * 6 + k]) + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
+    R pA[6], cj[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) pA[i] = chpA[j][i];
     if (!UNIT) {
-      double Iv[6];
+      R Iv[6];
       mvI(M, j, v[j], Iv);
       add_fxv(v[j], Iv, pA);
-      double cc[6];
+      R cc[6];
       crmS(v[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) cj[i] = qd[j] * cc[i];
@@ -529,33 +542,33 @@ __device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const d
     }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      double acc = 0.0;
+      R acc = 0.0;
 #pragma unroll
       for (int k = 0; k < 6; ++k)
-        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * M->S[j][k];
+        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * R(M->S[j][k]);
       U[j][r] = acc;
     }
     Dd[j] = dotS(M, j, U[j]);
     uu[j] = tau[j] - dotS(M, j, pA);
     const int p = parent_of<CHAIN>(M, j);
     if (p >= 0) {
-      const double dinv = 1.0 / Dd[j];
+      const R dinv = R(1) / Dd[j];
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int k = r; k < 6; ++k) IA[sidx(r, k)] -= U[j][r] * (dinv * U[j][k]);   // Ia
-      double pa[6];
-      const double ud = uu[j] * dinv;
+      R pa[6];
+      const R ud = uu[j] * dinv;
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        double acc = pA[r] + U[j][r] * ud;
+        R acc = pA[r] + U[j][r] * ud;
         if (!UNIT) {
 #pragma unroll
           for (int k = 0; k < 6; ++k) acc += IA[sidx(r, k)] * cj[k];
         }
         pa[r] = acc;
       }
-      double t[21];
+      R t[21];
       XtAX(M, j, cq[j], sq[j], IA, t);
 #pragma unroll
       for (int e = 0; e < 21; ++e) chIA[p][e] += t[e];
@@ -563,8 +576,8 @@ __device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const d
     }
   }
   // pass 3: accelerations, root to leaf (velocities recomputed)
-  double v3[NJ][6], a[NJ][6];
-  const double g[6] = {0.0, 0.0, 0.0, 0.0, 0.0, UNIT ? 0.0 : -M->gravity};
+  R v3[NJ][6], a[NJ][6];
+  const R g[6] = {0.0, 0.0, 0.0, 0.0, 0.0, UNIT ? R(0) : -R(M->gravity)};
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int p = parent_of<CHAIN>(M, j);
@@ -583,8 +596,8 @@ __device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const d
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i)
-        if (nz<MT>(M->S[j][i])) v3[j][i] += M->S[j][i] * qd[j];
-      double cc[6];
+        if (nz<MT>(M->S[j][i])) v3[j][i] += R(M->S[j][i]) * qd[j];
+      R cc[6];
       crmS(v3[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) a[j][i] += qd[j] * cc[i];
@@ -592,7 +605,7 @@ __device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const d
     qdd[j] = (uu[j] - dot6(U[j], a[j])) / Dd[j];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
-      if (nz<MT>(M->S[j][i])) a[j][i] += M->S[j][i] * qdd[j];
+      if (nz<MT>(M->S[j][i])) a[j][i] += R(M->S[j][i]) * qdd[j];
   }
 }
 
@@ -601,12 +614,12 @@ __device__ __forceinline__ void fd_aba(const MT& M, const double cq[NJ], const d
 // before symmetrising, :908-930) following minv_bpass / minv_fpass
 // restricted to column `col` (F[:, :, col] is per column; IA, U, Dinv are
 // recomputed per lane).
-template <int NJ, bool CHAIN, class MT>
-__device__ __forceinline__ void minv_column(const MT& M, const double cq[NJ], const double sq[NJ], int col,
-                                            double mcol[NJ]) {
-  double chIA[NJ][21];
-  double Fc[NJ][6];      // F[j][:, col]
-  double U[NJ][6], Dinv[NJ];
+template <int NJ, bool CHAIN, class MT, class R>
+__device__ __forceinline__ void minv_column(const MT& M, const R cq[NJ], const R sq[NJ], int col,
+                                            R mcol[NJ]) {
+  R chIA[NJ][21];
+  R Fc[NJ][6];      // F[j][:, col]
+  R U[NJ][6], Dinv[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     mcol[j] = 0.0;
@@ -618,21 +631,21 @@ __device__ __forceinline__ void minv_column(const MT& M, const double cq[NJ], co
   // backward pass (:805-866)
 #pragma unroll
   for (int j = NJ - 1; j >= 0; --j) {
-    double IA[21];
+    R IA[21];
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
       for (int k = r; k < 6; ++k)
-        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? M->I[j][r * 6 + k] + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
+        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? R(M->I[j][r * 6 + k]) + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      double acc = 0.0;
+      R acc = 0.0;
 #pragma unroll
       for (int k = 0; k < 6; ++k)
-        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * M->S[j][k];
+        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * R(M->S[j][k]);
       U[j][r] = acc;
     }
-    Dinv[j] = 1.0 / dotS(M, j, U[j]);
+    Dinv[j] = R(1) / dotS(M, j, U[j]);
     const bool mine = in_subtree<CHAIN>(M, j, col);
     if (j == col) mcol[j] = Dinv[j];
     if (mine) mcol[j] -= Dinv[j] * dotS(M, j, Fc[j]);
@@ -643,33 +656,33 @@ __device__ __forceinline__ void minv_column(const MT& M, const double cq[NJ], co
         for (int r = 0; r < 6; ++r) Fc[j][r] += U[j][r] * mcol[j];
         add_mtvX(M, j, cq[j], sq[j], Fc[j], Fc[p]);
       }
-      double Ia[21];
+      R Ia[21];
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int k = r; k < 6; ++k) Ia[sidx(r, k)] = IA[sidx(r, k)] - U[j][r] * (Dinv[j] * U[j][k]);
-      double t[21];
+      R t[21];
       XtAX(M, j, cq[j], sq[j], Ia, t);
 #pragma unroll
       for (int e = 0; e < 21; ++e) chIA[p][e] += t[e];
     }
   }
   // forward pass (:868-906), rows j <= col
-  double Ff[NJ][6];
+  R Ff[NJ][6];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     if (j > col) break;
     const int p = parent_of<CHAIN>(M, j);
     if (p >= 0) {
-      double XF[6];
+      R XF[6];
       mvX(M, j, cq[j], sq[j], Ff[p], XF);   // X F[p][:, col]
       // (U^T X) F[p][:, col] == U^T (X F[p][:, col])
       mcol[j] -= Dinv[j] * dot6(U[j], XF);
 #pragma unroll
-      for (int r = 0; r < 6; ++r) Ff[j][r] = nz<MT>(M->S[j][r]) ? M->S[j][r] * mcol[j] + XF[r] : XF[r];
+      for (int r = 0; r < 6; ++r) Ff[j][r] = nz<MT>(M->S[j][r]) ? R(M->S[j][r]) * mcol[j] + XF[r] : XF[r];
     } else {
 #pragma unroll
-      for (int r = 0; r < 6; ++r) Ff[j][r] = nz<MT>(M->S[j][r]) ? M->S[j][r] * mcol[j] : 0.0;
+      for (int r = 0; r < 6; ++r) Ff[j][r] = nz<MT>(M->S[j][r]) ? R(M->S[j][r]) * mcol[j] : 0.0;
     }
   }
 }
@@ -678,18 +691,18 @@ __device__ __forceinline__ void minv_column(const MT& M, const double cq[NJ], co
 // d c / d q_col (colqd = false) or d c / d qd_col (colqd = true) at (q, qd, qdd):
 // rnea_grad forward passes (:561-690) and backward passes (:692-771) for ONE
 // column, fused with the RNEA passes that produce v, a and the accumulated f.
-template <int NJ, bool CHAIN, class MT>
-__device__ __forceinline__ void rnea_grad_column(const MT& M, const double cq[NJ], const double sq[NJ],
-                                                 const double qd[NJ], const double qdd[NJ], int col, bool colqd,
-                                                 double dc[NJ]) {
-  double v[NJ][6], a[NJ][6], f[NJ][6];
-  double dv[NJ][6], da[NJ][6], df[NJ][6];
-  const double g[6] = {0.0, 0.0, 0.0, 0.0, 0.0, -M->gravity};
+template <int NJ, bool CHAIN, class MT, class R>
+__device__ __forceinline__ void rnea_grad_column(const MT& M, const R cq[NJ], const R sq[NJ],
+                                                 const R qd[NJ], const R qdd[NJ], int col, bool colqd,
+                                                 R dc[NJ]) {
+  R v[NJ][6], a[NJ][6], f[NJ][6];
+  R dv[NJ][6], da[NJ][6], df[NJ][6];
+  const R g[6] = {0.0, 0.0, 0.0, 0.0, 0.0, -R(M->gravity)};
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int p = parent_of<CHAIN>(M, j);
     // ---- RNEA forward (with qdd)
-    double Xvp[6], Xap[6];
+    R Xvp[6], Xap[6];
     if (p < 0) {
 #pragma unroll
       for (int i = 0; i < 6; ++i) Xvp[i] = 0.0;
@@ -699,18 +712,18 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const double cq[NJ
       mvX(M, j, cq[j], sq[j], a[p], Xap);
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) v[j][i] = nz<MT>(M->S[j][i]) ? Xvp[i] + M->S[j][i] * qd[j] : Xvp[i];
+    for (int i = 0; i < 6; ++i) v[j][i] = nz<MT>(M->S[j][i]) ? Xvp[i] + R(M->S[j][i]) * qd[j] : Xvp[i];
     {
-      double cc[6];
+      R cc[6];
       crmS(v[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
-        double t = Xap[i] + qd[j] * cc[i];
-        if (nz<MT>(M->S[j][i])) t += M->S[j][i] * qdd[j];
+        R t = Xap[i] + qd[j] * cc[i];
+        if (nz<MT>(M->S[j][i])) t += R(M->S[j][i]) * qdd[j];
         a[j][i] = t;
       }
     }
-    double Iv[6];
+    R Iv[6];
     mvI(M, j, a[j], f[j]);
     mvI(M, j, v[j], Iv);
     add_fxv(v[j], Iv, f[j]);
@@ -725,7 +738,7 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const double cq[NJ
     if (j == col) {
       if (!colqd) {
         if (p >= 0) {
-          double cc[6];
+          R cc[6];
           crmS(Xvp, M, j, cc);
 #pragma unroll
           for (int i = 0; i < 6; ++i) dv[j][i] += cc[i];
@@ -733,24 +746,24 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const double cq[NJ
       } else {
 #pragma unroll
         for (int i = 0; i < 6; ++i)
-          if (nz<MT>(M->S[j][i])) dv[j][i] += M->S[j][i];
+          if (nz<MT>(M->S[j][i])) dv[j][i] += R(M->S[j][i]);
       }
     }
     {
-      double cc[6];
+      R cc[6];
       crmS(dv[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) da[j][i] += qd[j] * cc[i];
     }
     if (j == col) {
-      double cc[6];
+      R cc[6];
       crmS(colqd ? v[j] : Xap, M, j, cc);  // mxS(S, v) or mxS(S, X a_parent) / mxS(S, X g)
 #pragma unroll
       for (int i = 0; i < 6; ++i) da[j][i] += cc[i];
     }
     mvI(M, j, da[j], df[j]);
     add_fxv(dv[j], Iv, df[j]);
-    double Idv[6];
+    R Idv[6];
     mvI(M, j, dv[j], Idv);
     add_fxv(v[j], Idv, df[j]);
   }
@@ -763,7 +776,7 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const double cq[NJ
       add_mtvX(M, j, cq[j], sq[j], df[j], df[p]);
       if (!colqd && j == col) {
         // delta = X^T fxS(S, f) = -X^T (crm(f) S)
-        double cc[6];
+        R cc[6];
         crmS(f[j], M, j, cc);
 #pragma unroll
         for (int i = 0; i < 6; ++i) cc[i] = -cc[i];

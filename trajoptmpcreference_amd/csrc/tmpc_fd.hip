@@ -16,7 +16,7 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
 // evaluated at, TrajoptPlant.py:313) and the dynamics defect
 // c_{k+1} = x_{k+1} - f(x_k, u_k) (formKKTSystemBlocks :227-231); lane k = 0
 // also writes c_0 = x_0 - xs (:213-214).
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class MT, class R>
 __global__ void __launch_bounds__(256) k_qp_fd(MT M, int B, int N, double dt,
                                                const double* __restrict__ x, const double* __restrict__ u,
                                                const double* __restrict__ xs, const int* __restrict__ need,
@@ -29,15 +29,19 @@ __global__ void __launch_bounds__(256) k_qp_fd(MT M, int B, int N, double dt,
   if (!need[b]) return;
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NJ * K;
-  double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
+  double q[NJ], qd[NJ], qdd[NJ];
+  R qdr[NJ], ur[NJ], qddr[NJ], cq[NJ], sq[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     q[j] = xb[j * N + k];
     qd[j] = xb[(NJ + j) * N + k];
-    uu[j] = ub[j * K + k];
-    joint_cs(M, j, q[j], cq[j], sq[j]);
+    qdr[j] = R(qd[j]);
+    ur[j] = R(ub[j * K + k]);
+    joint_cs(M, j, R(q[j]), cq[j], sq[j]);
   }
-  fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
+  fd_aba<NJ, CHAIN>(M, cq, sq, qdr, ur, qddr);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) qdd[j] = double(qddr[j]);
   const size_t kk = (size_t)b * K + k;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) qdd_out[kk * NJ + j] = qdd[j];
@@ -64,7 +68,7 @@ __global__ void __launch_bounds__(256) k_qp_fd(MT M, int B, int N, double dt,
 // |x_0 - xs| violation term.  SOFT: soft-limit value (slot 3, summed after
 // the cost terms as totalCost does, :303-307) and jacobian . dxu added to D
 // (:633-646).  terms: [B][T][N][4] = cost, violation, D, soft value.
-template <int NJ, bool CHAIN, bool SOFT, class MT>
+template <int NJ, bool CHAIN, bool SOFT, class MT, class R>
 __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restrict__ C,
                                                   const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                   const double* __restrict__ lam,
@@ -145,13 +149,18 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
     }
     cost += 0.5 * vr;
     // dynamics defect at the trial point
-    double cq[NJ], sq[NJ], qd[NJ], qdd[NJ];
+    double qd[NJ], qdd[NJ];
+    R cq[NJ], sq[NJ], qdr[NJ], ur[NJ], qddr[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       qd[j] = xk[NJ + j];
-      joint_cs(M, j, xk[j], cq[j], sq[j]);
+      qdr[j] = R(qd[j]);
+      ur[j] = R(uk[j]);
+      joint_cs(M, j, R(xk[j]), cq[j], sq[j]);
     }
-    fd_aba<NJ, CHAIN>(M, cq, sq, qd, uk, qdd);
+    fd_aba<NJ, CHAIN>(M, cq, sq, qdr, ur, qddr);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) qdd[j] = double(qddr[j]);
 #pragma unroll
     for (int m = 0; m < NX; ++m) {
       const double dxn = dxb ? dxb[(k + 1) * NX + m] : 0.0;
@@ -191,22 +200,26 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
 }
 
 // ======================================================================= kernel-level entry points
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class MT, class R>
 __global__ void __launch_bounds__(256) k_unit_fd(MT M, int K, double dt,
                                                  const double* __restrict__ x, const double* __restrict__ u,
                                                  double* __restrict__ xnext, double* __restrict__ qdd_out) {
   constexpr int NX = 2 * NJ;
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
-  double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
+  double q[NJ], qd[NJ], qdd[NJ];
+  R qdr[NJ], ur[NJ], qddr[NJ], cq[NJ], sq[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     q[j] = x[(size_t)k * NX + j];
     qd[j] = x[(size_t)k * NX + NJ + j];
-    uu[j] = u[(size_t)k * NJ + j];
-    joint_cs(M, j, q[j], cq[j], sq[j]);
+    qdr[j] = R(qd[j]);
+    ur[j] = R(u[(size_t)k * NJ + j]);
+    joint_cs(M, j, R(q[j]), cq[j], sq[j]);
   }
-  fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
+  fd_aba<NJ, CHAIN>(M, cq, sq, qdr, ur, qddr);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) qdd[j] = double(qddr[j]);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     qdd_out[(size_t)k * NJ + j] = qdd[j];
@@ -218,7 +231,7 @@ __global__ void __launch_bounds__(256) k_unit_fd(MT M, int K, double dt,
 }
 
 // sequential Euler rollout, one lane per problem (workload setup: §8d)
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class MT, class R>
 __global__ void __launch_bounds__(64) k_rollout(MT M, int B, int N, double dt,
                                                 double* __restrict__ x, const double* __restrict__ u) {
   constexpr int NX = 2 * NJ;
@@ -231,13 +244,17 @@ __global__ void __launch_bounds__(64) k_rollout(MT M, int B, int N, double dt,
 #pragma unroll
   for (int j = 0; j < NJ; ++j) { q[j] = xb[j * N]; qd[j] = xb[(NJ + j) * N]; }
   for (int k = 0; k < K; ++k) {
-    double uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
+    double qdd[NJ];
+    R ur[NJ], qdr[NJ], qddr[NJ], cq[NJ], sq[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      uu[j] = ub[j * K + k];
-      joint_cs(M, j, q[j], cq[j], sq[j]);
+      ur[j] = R(ub[j * K + k]);
+      qdr[j] = R(qd[j]);
+      joint_cs(M, j, R(q[j]), cq[j], sq[j]);
     }
-    fd_aba<NJ, CHAIN>(M, cq, sq, qd, uu, qdd);
+    fd_aba<NJ, CHAIN>(M, cq, sq, qdr, ur, qddr);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) qdd[j] = double(qddr[j]);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const double nq = __dadd_rn(q[j], __dmul_rn(dt, qd[j]));
@@ -266,6 +283,7 @@ __global__ void __launch_bounds__(64) k_mpc_shift(MT M, int B, int N, double dt,
   double* ub = u + (size_t)b * NU * K;
   __shared__ double xn[NX];
   if (t == 0) {
+    // the simulated plant is fp64 in every precision mode
     double q[NJ], qd[NJ], uu[NJ], qdd[NJ], cq[NJ], sq[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -302,33 +320,43 @@ __global__ void __launch_bounds__(64) k_mpc_shift(MT M, int B, int N, double dt,
 
 template <int NJ, bool CHAIN, class MT>
 struct LaunchFD {
-  static void qp_fd(hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const double* u,
+  static void qp_fd(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const double* u,
                     const double* xs, const int* need, double* qdd, double* cvec) {
-    hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), B, N, dt, x, u, xs, need, qdd,
-                       cvec);
+    if (f32)
+      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), B, N, dt, x, u, xs,
+                         need, qdd, cvec);
+    else
+      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), B, N, dt, x, u, xs,
+                         need, qdd, cvec);
   }
-  static void ls_terms(hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
+  static void ls_terms(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
                        const double* lam, int B, int N, int T, double dt, const double* alphas, const double* x,
                        const double* u, const double* xs, const double* dx, const double* du, const int* active,
                        double* terms) {
-    if (mu)
-      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, true, MT>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, lam, B, N, T,
-                         dt, alphas, x, u, xs, dx, du, active, terms);
-    else
-      hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, false, MT>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, lam, B, N,
-                         T, dt, alphas, x, u, xs, dx, du, active, terms);
+#define TMPC_LS(SOFTV, RV)                                                                                        \
+    hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, SOFTV, MT, RV>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, \
+                       lam, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms);
+    if (mu) { if (f32) { TMPC_LS(true, float) } else { TMPC_LS(true, double) } }
+    else { if (f32) { TMPC_LS(false, float) } else { TMPC_LS(false, double) } }
+#undef TMPC_LS
   }
-  static void unit_fd(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
+  static void unit_fd(bool f32, hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
                       double* xnext, double* qdd) {
-    hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
+    if (f32)
+      hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT, float>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
+    else
+      hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT, double>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
   }
   static void mpc_shift(hipStream_t s, const ModelDev* M, int B, int N, double dt, int step, int steps, double* x,
                         double* u, double* xe, double* ue) {
     hipLaunchKernelGGL((k_mpc_shift<NJ, CHAIN, MT>), dim3(B), dim3(64), 0, s, MT::make(M), B, N, dt, step, steps, x,
                        u, xe, ue);
   }
-  static void rollout(hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u) {
-    hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT>), TMPC_GRID(B, 64), 0, s, MT::make(M), B, N, dt, x, u);
+  static void rollout(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u) {
+    if (f32)
+      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, float>), TMPC_GRID(B, 64), 0, s, MT::make(M), B, N, dt, x, u);
+    else
+      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, double>), TMPC_GRID(B, 64), 0, s, MT::make(M), B, N, dt, x, u);
   }
 };
 
@@ -350,23 +378,23 @@ struct LaunchFD {
   }                                                                                                    \
   return 0;
 
-int launch_qp_fd(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
-                 const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
-  TMPC_DISPATCH_NJ(nj, chain, qp_fd(s, M, B, N, dt, x, u, xs, need, qdd, cvec))
+int launch_qp_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt,
+                 const double* x, const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
+  TMPC_DISPATCH_NJ(nj, chain, qp_fd(f32, s, M, B, N, dt, x, u, xs, need, qdd, cvec))
 }
-int launch_ls_terms(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
-                    const double* mu, const double* lam, int B, int N, int T, double dt, const double* alphas,
-                    const double* x, const double* u, const double* xs, const double* dx, const double* du,
-                    const int* active, double* terms) {
-  TMPC_DISPATCH_NJ(nj, chain, ls_terms(s, M, C, Cs, mu, lam, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
+int launch_ls_terms(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C,
+                    const ConstrDev* Cs, const double* mu, const double* lam, int B, int N, int T, double dt,
+                    const double* alphas, const double* x, const double* u, const double* xs, const double* dx,
+                    const double* du, const int* active, double* terms) {
+  TMPC_DISPATCH_NJ(nj, chain, ls_terms(f32, s, M, C, Cs, mu, lam, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
 }
-int launch_unit_fd(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
-                   const double* u, double* xnext, double* qdd) {
-  TMPC_DISPATCH_NJ(nj, chain, unit_fd(s, M, K, dt, x, u, xnext, qdd))
+int launch_unit_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt,
+                   const double* x, const double* u, double* xnext, double* qdd) {
+  TMPC_DISPATCH_NJ(nj, chain, unit_fd(f32, s, M, K, dt, x, u, xnext, qdd))
 }
-int launch_rollout(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
-                   const double* u) {
-  TMPC_DISPATCH_NJ(nj, chain, rollout(s, M, B, N, dt, x, u))
+int launch_rollout(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt,
+                   double* x, const double* u) {
+  TMPC_DISPATCH_NJ(nj, chain, rollout(f32, s, M, B, N, dt, x, u))
 }
 
 int launch_mpc_shift(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, int step,

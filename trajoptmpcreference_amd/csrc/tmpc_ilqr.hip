@@ -26,20 +26,20 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
 }
 
 // ======================================================================= backward (Riccati) sweep
-template <int NJ>
+template <int NJ, class R>
 struct IlqrLds {
   static constexpr int NX = 2 * NJ, NU = NJ;
-  double Vxx[NX * NX], Vx[NX];
-  double A[NX * NX], Bm[NX * NU];
-  double P[NX * NX], R[NX * NU];         // V_xx A, V_xx B (then the unsymmetrised V_xx)
-  double Qxx[NX * NX], Qux[NU * NX], Quu[NU * NU], Qx[NX], Qu[NU];
-  double KD[NU * (NX + 1)];              // [Q_uu^-1 Q_ux | Q_uu^-1 Q_u], row-major
-  double lx[NX], lu[NU], jac[3 * NJ];
-  double dv[2];
+  R Vxx[NX * NX], Vx[NX];
+  R A[NX * NX], Bm[NX * NU];
+  R P[NX * NX], VB[NX * NU];        // V_xx A, V_xx B (P then holds the unsymmetrised V_xx)
+  R Qxx[NX * NX], Qux[NU * NX], Quu[NU * NU], Qx[NX], Qu[NU];
+  R KD[NU * (NX + 1)];              // [Q_uu^-1 Q_ux | Q_uu^-1 Q_u], row-major
+  R lx[NX], lu[NU], jac[3 * NJ];
+  R dv[2];
   int fail;
 };
 
-template <int NJ>
+template <int NJ, class R>
 __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
                                                       int B, int N, const double* __restrict__ x,
                                                       const double* __restrict__ u, const double* __restrict__ rho_in,
@@ -51,10 +51,10 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   constexpr int NX = 2 * NJ, NU = NJ, NC = NX + 1, MC = 6 * NJ;
   const int b = blockIdx.x;
   if (!active[b]) return;
-  __shared__ IlqrLds<NJ> L;
+  __shared__ IlqrLds<NJ, R> L;
   const int t = threadIdx.x;
   const int K = N - 1;
-  const double rho = rho_in[b];
+  const R rho = R(rho_in[b]);
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NU * K;
   const bool soft = Cs->any != 0;
@@ -78,21 +78,21 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     __syncthreads();
     const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
     if (t < NX) {
-      double g = 0.0;
-      for (int m = 0; m < NX; ++m) g += (xb[m * N + k] - C->xg[m]) * Qk[m * NX + t];
+      R g = 0.0;
+      for (int m = 0; m < NX; ++m) g += R(xb[m * N + k] - C->xg[m]) * R(Qk[m * NX + t]);
       L.lx[t] = g + L.jac[t];
     } else if (t < NX + NU && !term) {
       const int c = t - NX;
-      double g = 0.0;
-      for (int m = 0; m < NU; ++m) g += ub[m * K + k] * C->R[m * NU + c];
+      R g = 0.0;
+      for (int m = 0; m < NU; ++m) g += R(ub[m * K + k]) * R(C->R[m * NU + c]);
       L.lu[c] = g + L.jac[NX + c];
     }
   };
   // l_xx (+ per-type outer products on the q / qd diagonal blocks)
-  auto lxx = [&](int k, int r, int c) -> double {
+  auto lxx = [&](int k, int r, int c) -> R {
     const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
-    const double o = (r / NJ == c / NJ) ? L.jac[r] * L.jac[c] : 0.0;
-    return Qk[r * NX + c] + o;
+    const R o = (r / NJ == c / NJ) ? L.jac[r] * L.jac[c] : 0.0;
+    return R(Qk[r * NX + c]) + o;
   };
 
   // terminal value function: V_x = l_x(N-1), V_xx = l_xx(N-1)
@@ -115,25 +115,25 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     for (int e = t; e < NX * NX + NX * NU + NX + NU; e += 64) {
       if (e < NX * NX) {
         const int r = e / NX, c = e % NX;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NX; ++m) s += L.Vxx[r * NX + m] * L.A[m * NX + c];
         L.P[e] = s;
       } else if (e < NX * NX + NX * NU) {
         const int f = e - NX * NX, r = f / NU, c = f % NU;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NX; ++m) s += L.Vxx[r * NX + m] * L.Bm[m * NU + c];
-        L.R[f] = s;
+        L.VB[f] = s;
       } else if (e < NX * NX + NX * NU + NX) {
         const int r = e - NX * NX - NX * NU;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NX; ++m) s += L.A[m * NX + r] * L.Vx[m];
         L.Qx[r] = L.lx[r] + s;
       } else {
         const int r = e - NX * NX - NX * NU - NX;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NX; ++m) s += L.Bm[m * NU + r] * L.Vx[m];
         L.Qu[r] = L.lu[r] + s;
@@ -144,19 +144,19 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     for (int e = t; e < NX * NX + NU * NU + NU * NX; e += 64) {
       if (e < NX * NX) {
         const int r = e / NX, c = e % NX;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NX; ++m) s += L.A[m * NX + r] * L.P[m * NX + c];
         L.Qxx[e] = lxx(k, r, c) + s;
       } else if (e < NX * NX + NU * NU) {
         const int f = e - NX * NX, r = f / NU, c = f % NU;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.Bm[m * NU + r] * L.R[m * NU + c];
-        L.Quu[f] = (C->R[f] + L.jac[NX + r] * L.jac[NX + c]) + s + (r == c ? rho : 0.0);
+        for (int m = 0; m < NX; ++m) s += L.Bm[m * NU + r] * L.VB[m * NU + c];
+        L.Quu[f] = (R(C->R[f]) + L.jac[NX + r] * L.jac[NX + c]) + s + (r == c ? rho : R(0));
       } else {
         const int f = e - NX * NX - NU * NU, r = f / NX, c = f % NX;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NX; ++m) s += L.Bm[m * NU + r] * L.P[m * NX + c];
         L.Qux[f] = s;
@@ -166,35 +166,35 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     // [K | d] = -Q_uu^-1 [Q_ux | Q_u]: Cholesky Q_uu = L L^T (every lane, from LDS), then lane c
     // solves its right-hand-side column c; Q_uu not positive definite -> backward failure
     if (t < NC) {
-      double Lc[NU][NU];
+      R Lc[NU][NU];
       bool pd = true;
 #pragma unroll
       for (int j = 0; j < NU; ++j) {
-        double s = L.Quu[j * NU + j];
+        R s = L.Quu[j * NU + j];
 #pragma unroll
         for (int m = 0; m < j; ++m) s -= Lc[j][m] * Lc[j][m];
-        pd = pd && (s > 0.0);
-        const double dj = sqrt(s);
+        pd = pd && (s > R(0));
+        const R dj = sqrt(s);
         Lc[j][j] = dj;
 #pragma unroll
         for (int i = j + 1; i < NU; ++i) {
-          double v = L.Quu[i * NU + j];
+          R v = L.Quu[i * NU + j];
 #pragma unroll
           for (int m = 0; m < j; ++m) v -= Lc[i][m] * Lc[j][m];
           Lc[i][j] = v / dj;
         }
       }
-      double y[NU];
+      R y[NU];
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
-        double v = t < NX ? L.Qux[i * NX + t] : L.Qu[i];
+        R v = t < NX ? L.Qux[i * NX + t] : L.Qu[i];
 #pragma unroll
         for (int m = 0; m < i; ++m) v -= Lc[i][m] * y[m];
         y[i] = v / Lc[i][i];
       }
 #pragma unroll
       for (int i = NU - 1; i >= 0; --i) {
-        double v = y[i];
+        R v = y[i];
 #pragma unroll
         for (int m = i + 1; m < NU; ++m) v -= Lc[m][i] * y[m];
         y[i] = v / Lc[i][i];
@@ -209,51 +209,51 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     for (int e = t; e < NX * NX + NX; e += 64) {
       if (e < NX * NX) {
         const int r = e / NX, c = e % NX;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NU; ++m) s += L.Qux[m * NX + r] * L.KD[m * NC + c];
         L.P[e] = L.Qxx[e] + s;
       } else {
         const int r = e - NX * NX;
-        double s = 0.0;
+        R s = 0.0;
 #pragma unroll
         for (int m = 0; m < NU; ++m) s += L.Qux[m * NX + r] * L.KD[m * NC + NX];
         L.Vx[r] = L.Qx[r] + s;
       }
     }
     if (t == 63) {
-      double s1 = 0.0, s2 = 0.0;
+      R s1 = 0.0, s2 = 0.0;
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
-        const double di = L.KD[i * NC + NX];
+        const R di = L.KD[i * NC + NX];
         s1 += di * L.Qu[i];
-        double qd = 0.0;
+        R qd = 0.0;
 #pragma unroll
         for (int m = 0; m < NU; ++m) qd += L.Quu[i * NU + m] * L.KD[m * NC + NX];
         s2 += di * qd;
       }
       L.dv[0] += s1;
-      L.dv[1] += 0.5 * s2;
+      L.dv[1] += R(0.5) * s2;
     }
     // K_k, d_k to HBM ([B][K][NU][NX], [B][K][NU])
     for (int e = t; e < NU * NC; e += 64) {
       const int i = e / NC, c = e % NC;
       if (c < NX)
-        Kout[(((size_t)b * K + k) * NU + i) * NX + c] = L.KD[e];
+        Kout[(((size_t)b * K + k) * NU + i) * NX + c] = double(L.KD[e]);
       else
-        dout[((size_t)b * K + k) * NU + i] = L.KD[e];
+        dout[((size_t)b * K + k) * NU + i] = double(L.KD[e]);
     }
     __syncthreads();
     for (int e = t; e < NX * NX; e += 64) {
       const int r = e / NX, c = e % NX;
-      L.Vxx[e] = 0.5 * (L.P[r * NX + c] + L.P[c * NX + r]);
+      L.Vxx[e] = R(0.5) * (L.P[r * NX + c] + L.P[c * NX + r]);
     }
     __syncthreads();
   }
   if (t == 0) {
     ok[b] = L.fail ? 0 : 1;
-    dV[2 * b] = L.dv[0];
-    dV[2 * b + 1] = L.dv[1];
+    dV[2 * b] = double(L.dv[0]);
+    dV[2 * b + 1] = double(L.dv[1]);
   }
 }
 
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
 // trajectories are kept ([B][T][nx][N], [B][T][nu][N-1]) so the decision kernel
 // copies the accepted one.  Cost sums in totalCost's order (:296-310): the
 // QuadraticCost terms, then the soft values.
-template <int NJ, bool CHAIN, bool SOFT, class MT>
+template <int NJ, bool CHAIN, bool SOFT, class MT, class R>
 __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __restrict__ C,
                                                      const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                      const double* __restrict__ lam, int B, int N, int T, double dt,
@@ -342,13 +342,18 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
     }
     J = J + cost;
     if (!term && !init) {
-      double cq[NJ], sq[NJ], qd[NJ], qdd[NJ];
+      double qd[NJ], qdd[NJ];
+      R cq[NJ], sq[NJ], qdr[NJ], ur[NJ], qddr[NJ];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         qd[j] = xh[NJ + j];
-        joint_cs(M, j, xh[j], cq[j], sq[j]);
+        qdr[j] = R(qd[j]);
+        ur[j] = R(uh[j]);
+        joint_cs(M, j, R(xh[j]), cq[j], sq[j]);
       }
-      fd_aba<NJ, CHAIN>(M, cq, sq, qd, uh, qdd);
+      fd_aba<NJ, CHAIN>(M, cq, sq, qdr, ur, qddr);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) qdd[j] = double(qddr[j]);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const double nq = __dadd_rn(xh[j], __dmul_rn(dt, qd[j]));
@@ -481,22 +486,26 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
 
 template <int NJ, bool CHAIN, class MT>
 struct LaunchIlqr {
-  static void backward(hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
+  static void backward(bool f32, hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                        const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                        const double* mu, const double* lam, double* K, double* d, double* dV, int* ok) {
-    hipLaunchKernelGGL((k_ilqr_backward<NJ>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu, lam,
-                       K, d, dV, ok);
+    if (f32)
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, float>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu,
+                         lam, K, d, dV, ok);
+    else
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, double>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu,
+                         lam, K, d, dV, ok);
   }
-  static void forward(hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
+  static void forward(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
                       const double* lam, int B, int N, int T, double dt, int init, const double* alphas,
                       const double* x, const double* u, const double* K, const double* d, const int* active,
                       const int* ok, double* xt, double* ut, double* Jt) {
-    if (mu)
-      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, true, MT>), TMPC_GRID(B * T, 64), 0, s, MT::make(M), C, Cs, mu, lam, B, N, T,
-                         dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
-    else
-      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, false, MT>), TMPC_GRID(B * T, 64), 0, s, MT::make(M), C, Cs, mu, lam, B, N, T,
-                         dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
+#define TMPC_FWD(SOFTV, RV)                                                                                          \
+    hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV>), TMPC_GRID(B * T, 64), 0, s, MT::make(M), C, Cs, mu, \
+                       lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
+    if (mu) { if (f32) { TMPC_FWD(true, float) } else { TMPC_FWD(true, double) } }
+    else { if (f32) { TMPC_FWD(false, float) } else { TMPC_FWD(false, double) } }
+#undef TMPC_FWD
   }
 };
 
@@ -517,19 +526,20 @@ struct LaunchIlqr {
   }                                                                                                    \
   return 0;
 
-int launch_ilqr_backward(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
-                         const double* u, const double* rho, const int* active, const double* A, const double* Bm,
-                         const double* mu, const double* lam, double* K, double* d, double* dV, int* ok) {
+int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N,
+                         const double* x, const double* u, const double* rho, const int* active, const double* A,
+                         const double* Bm, const double* mu, const double* lam, double* K, double* d, double* dV,
+                         int* ok) {
   const int mid = 0;
-  TMPC_DISPATCH_ILQR(nj, true, backward(s, C, Cs, B, N, x, u, rho, active, A, Bm, mu, lam, K, d, dV, ok))
+  TMPC_DISPATCH_ILQR(nj, true, backward(f32, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu, lam, K, d, dV, ok))
 }
 
-int launch_ilqr_forward(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
-                        const double* mu, const double* lam, int B, int N, int T, double dt, int init,
-                        const double* alphas, const double* x, const double* u, const double* K, const double* d,
-                        const int* active, const int* ok, double* xt, double* ut, double* Jt) {
-  TMPC_DISPATCH_ILQR(nj, chain, forward(s, M, C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt,
-                                        ut, Jt))
+int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C,
+                        const ConstrDev* Cs, const double* mu, const double* lam, int B, int N, int T, double dt,
+                        int init, const double* alphas, const double* x, const double* u, const double* K,
+                        const double* d, const int* active, const int* ok, double* xt, double* ut, double* Jt) {
+  TMPC_DISPATCH_ILQR(nj, chain, forward(f32, s, M, C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok,
+                                        xt, ut, Jt))
 }
 
 void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,

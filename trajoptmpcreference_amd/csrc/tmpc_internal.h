@@ -67,22 +67,24 @@ struct TraceDev {
   int* pcg_iters;
 };
 
-int launch_qp_fd(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
+// f32: rigid-body dynamics (and, for launch_ilqr_backward, the Riccati sweep) in fp32 --
+// tmpc_options.precision F32 / MIXED; every buffer stays fp64
+int launch_qp_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
                  const double* u, const double* xs, const int* need, double* qdd, double* cvec);
-int launch_qp_minv(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, const double* x,
+int launch_qp_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, const double* x,
                    const int* need, double* minv);
-int launch_qp_grad(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
+int launch_qp_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
                    const int* need, const double* qdd, const double* minv, double* A, double* Bm);
-int launch_ls_terms(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
+int launch_ls_terms(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
                     const double* mu, const double* lam, int B, int N, int T, double dt, const double* alphas,
                     const double* x, const double* u, const double* xs, const double* dx, const double* du,
                     const int* active, double* terms);
-int launch_unit_fd(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
+int launch_unit_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
                    const double* u, double* xnext, double* qdd);
-int launch_unit_minv(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, const double* x, double* minv);
-int launch_unit_grad(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
+int launch_unit_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, const double* x, double* minv);
+int launch_unit_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
                      const double* qdd, const double* minv, double* A, double* Bm, double* dqdd);
-int launch_rollout(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
+int launch_rollout(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
                    const double* u);
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G);
 int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, int mode, const double* x,
@@ -120,10 +122,10 @@ void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& s
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
                        const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
                        int* outer_iter, int* exit_soft, int* outer_count);
-int launch_ilqr_backward(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
+int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                          const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                          const double* mu, const double* lam, double* K, double* d, double* dV, int* ok);
-int launch_ilqr_forward(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
+int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
                         const double* mu, const double* lam, int B, int N, int T, double dt, int init,
                         const double* alphas, const double* x, const double* u, const double* K, const double* d,
                         const int* active, const int* ok, double* xt, double* ut, double* Jt);

@@ -25,23 +25,23 @@ namespace tmpc {
 // lane = (knot, col), col < NJ; writes the full symmetric matrix (column col
 // above the diagonal and row col left of it, :908-930).  x is [K][NX] rows
 // with row stride `xstride` per knot and element stride `estride`.
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class R, class MT>
 __device__ __forceinline__ void minv_lane_store(const MT& M, const double q[NJ], int col,
                                                 double* __restrict__ Mo) {
-  double cq[NJ], sq[NJ], mc[NJ];
+  R cq[NJ], sq[NJ], mc[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) joint_cs(M, j, q[j], cq[j], sq[j]);
+  for (int j = 0; j < NJ; ++j) joint_cs(M, j, R(q[j]), cq[j], sq[j]);
   minv_column<NJ, CHAIN>(M, cq, sq, col, mc);
 #pragma unroll
   for (int r = 0; r < NJ; ++r) {
     if (r <= col) {
-      Mo[r * NJ + col] = mc[r];
-      Mo[col * NJ + r] = mc[r];
+      Mo[r * NJ + col] = double(mc[r]);
+      Mo[col * NJ + r] = double(mc[r]);
     }
   }
 }
 
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class MT, class R>
 __global__ void __launch_bounds__(256) k_qp_minv(MT M, int B, int N,
                                                  const double* __restrict__ x, const int* __restrict__ need,
                                                  double* __restrict__ minv_out) {
@@ -57,29 +57,34 @@ __global__ void __launch_bounds__(256) k_qp_minv(MT M, int B, int N,
   double q[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) q[j] = xb[j * N + k];
-  minv_lane_store<NJ, CHAIN>(M, q, col, minv_out + (size_t)bk * NJ * NJ);
+  minv_lane_store<NJ, CHAIN, R>(M, q, col, minv_out + (size_t)bk * NJ * NJ);
 }
 
 // ======================================================================= gradient columns -> A, B
 // lane = (b, k, col), col < 2 NJ.  dqdd[:, col] = -Minv dc[:, col]
 // (TrajoptPlant.py:313-316); A = I + dt [[0, I], [dqdd_q, dqdd_qd]],
 // B = dt [[0], [Minv]] (TrajoptPlant.py:100-108).
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class R, class MT>
 __device__ __forceinline__ void grad_lane_store(const MT& M, double dt, const double q[NJ],
                                                 const double qd[NJ], const double qdd[NJ],
                                                 const double* __restrict__ Mi, int col, double* __restrict__ A,
                                                 double* __restrict__ Bm, double* __restrict__ dqdd) {
   constexpr int NX = 2 * NJ;
-  double cq[NJ], sq[NJ], dc[NJ];
+  R cq[NJ], sq[NJ], dc[NJ], qdr[NJ], qddr[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) joint_cs(M, j, q[j], cq[j], sq[j]);
+  for (int j = 0; j < NJ; ++j) {
+    joint_cs(M, j, R(q[j]), cq[j], sq[j]);
+    qdr[j] = R(qd[j]);
+    qddr[j] = R(qdd[j]);
+  }
   const bool colqd = col >= NJ;
-  rnea_grad_column<NJ, CHAIN>(M, cq, sq, qd, qdd, colqd ? col - NJ : col, colqd, dc);
+  rnea_grad_column<NJ, CHAIN>(M, cq, sq, qdr, qddr, colqd ? col - NJ : col, colqd, dc);
 #pragma unroll
   for (int r = 0; r < NJ; ++r) {
-    double acc = 0.0;
+    R accr = 0.0;
 #pragma unroll
-    for (int m = 0; m < NJ; ++m) acc += (-Mi[r * NJ + m]) * dc[m];
+    for (int m = 0; m < NJ; ++m) accr += (-R(Mi[r * NJ + m])) * dc[m];
+    const double acc = double(accr);
     if (dqdd) {
       dqdd[r * 3 * NJ + col] = acc;
       if (col < NJ) dqdd[r * 3 * NJ + NX + col] = Mi[r * NJ + col];
@@ -95,7 +100,7 @@ __device__ __forceinline__ void grad_lane_store(const MT& M, double dt, const do
   }
 }
 
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class MT, class R>
 __global__ void __launch_bounds__(256) k_qp_grad(MT M, int B, int N, double dt,
                                                  const double* __restrict__ x, const int* __restrict__ need,
                                                  const double* __restrict__ qdd_in, const double* __restrict__ minv_in,
@@ -116,7 +121,7 @@ __global__ void __launch_bounds__(256) k_qp_grad(MT M, int B, int N, double dt,
     qd[j] = xb[(NJ + j) * N + k];
     qdd[j] = qdd_in[(size_t)bk * NJ + j];
   }
-  grad_lane_store<NJ, CHAIN>(M, dt, q, qd, qdd, minv_in + (size_t)bk * NJ * NJ, col,
+  grad_lane_store<NJ, CHAIN, R>(M, dt, q, qd, qdd, minv_in + (size_t)bk * NJ * NJ, col,
                              Aout + (size_t)bk * NX * NX, Bout + (size_t)bk * NX * NJ, nullptr);
 }
 
@@ -1546,7 +1551,7 @@ __global__ void k_init_state(int B, double rho_init, ProbState st, const int* __
 
 // ======================================================================= kernel-level entry points
 // [K][nx] / [K][nu] row layout, one lane per knot (or per knot and column)
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class MT, class R>
 __global__ void __launch_bounds__(256) k_unit_minv(MT M, int K, const double* __restrict__ x,
                                                    double* __restrict__ minv_out) {
   constexpr int NX = 2 * NJ;
@@ -1556,10 +1561,10 @@ __global__ void __launch_bounds__(256) k_unit_minv(MT M, int K, const double* __
   double q[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) q[j] = x[(size_t)k * NX + j];
-  minv_lane_store<NJ, CHAIN>(M, q, col, minv_out + (size_t)k * NJ * NJ);
+  minv_lane_store<NJ, CHAIN, R>(M, q, col, minv_out + (size_t)k * NJ * NJ);
 }
 
-template <int NJ, bool CHAIN, class MT>
+template <int NJ, bool CHAIN, class MT, class R>
 __global__ void __launch_bounds__(256) k_unit_grad(MT M, int K, double dt,
                                                    const double* __restrict__ x, const double* __restrict__ qdd_in,
                                                    const double* __restrict__ minv_in, double* __restrict__ Aout,
@@ -1575,7 +1580,7 @@ __global__ void __launch_bounds__(256) k_unit_grad(MT M, int K, double dt,
     qd[j] = x[(size_t)k * NX + NJ + j];
     qdd[j] = qdd_in[(size_t)k * NJ + j];
   }
-  grad_lane_store<NJ, CHAIN>(M, dt, q, qd, qdd, minv_in + (size_t)k * NJ * NJ, col,
+  grad_lane_store<NJ, CHAIN, R>(M, dt, q, qd, qdd, minv_in + (size_t)k * NJ * NJ, col,
                              Aout ? Aout + (size_t)k * NX * NX : nullptr, Bout ? Bout + (size_t)k * NX * NJ : nullptr,
                              dqdd ? dqdd + (size_t)k * NJ * 3 * NJ : nullptr);
 }
@@ -1583,23 +1588,41 @@ __global__ void __launch_bounds__(256) k_unit_grad(MT M, int K, double dt,
 // ======================================================================= launchers
 #define TMPC_GRID(n, bs) dim3(((n) + (bs) - 1) / (bs)), dim3(bs)
 
+// f32: the dynamics in fp32 (tmpc_options.precision F32 / MIXED), fp64 in and out
 template <int NJ, bool CHAIN, class MT>
 struct Launch {
-  static void qp_minv(hipStream_t s, const ModelDev* M, int B, int N, const double* x, const int* need, double* minv) {
-    hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), B, N, x, need, minv);
+  static void qp_minv(bool f32, hipStream_t s, const ModelDev* M, int B, int N, const double* x, const int* need,
+                      double* minv) {
+    if (f32)
+      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), B, N, x,
+                         need, minv);
+    else
+      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), B, N, x,
+                         need, minv);
   }
-  static void qp_grad(hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const int* need,
-                      const double* qdd, const double* minv, double* A, double* Bm) {
-    hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), B, N, dt, x, need,
-                       qdd, minv, A, Bm);
+  static void qp_grad(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x,
+                      const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
+    if (f32)
+      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), B, N,
+                         dt, x, need, qdd, minv, A, Bm);
+    else
+      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), B, N,
+                         dt, x, need, qdd, minv, A, Bm);
   }
-  static void unit_minv(hipStream_t s, const ModelDev* M, int K, const double* x, double* minv) {
-    hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
+  static void unit_minv(bool f32, hipStream_t s, const ModelDev* M, int K, const double* x, double* minv) {
+    if (f32)
+      hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT, float>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
+    else
+      hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT, double>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
   }
-  static void unit_grad(hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* qdd,
+  static void unit_grad(bool f32, hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* qdd,
                         const double* minv, double* A, double* Bm, double* dqdd) {
-    hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN, MT>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd, minv, A, Bm,
-                       dqdd);
+    if (f32)
+      hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN, MT, float>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
+                         minv, A, Bm, dqdd);
+    else
+      hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN, MT, double>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
+                         minv, A, Bm, dqdd);
   }
 };
 
@@ -1893,20 +1916,21 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
   }                                                                                \
   return 0;
 
-int launch_qp_minv(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, const double* x,
-                   const int* need, double* minv) {
-  TMPC_DISPATCH_NJ(nj, chain, qp_minv(s, M, B, N, x, need, minv))
+int launch_qp_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N,
+                   const double* x, const int* need, double* minv) {
+  TMPC_DISPATCH_NJ(nj, chain, qp_minv(f32, s, M, B, N, x, need, minv))
 }
-int launch_qp_grad(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
-                   const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
-  TMPC_DISPATCH_NJ(nj, chain, qp_grad(s, M, B, N, dt, x, need, qdd, minv, A, Bm))
+int launch_qp_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt,
+                   const double* x, const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
+  TMPC_DISPATCH_NJ(nj, chain, qp_grad(f32, s, M, B, N, dt, x, need, qdd, minv, A, Bm))
 }
-int launch_unit_minv(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, const double* x, double* minv) {
-  TMPC_DISPATCH_NJ(nj, chain, unit_minv(s, M, K, x, minv))
+int launch_unit_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, const double* x,
+                     double* minv) {
+  TMPC_DISPATCH_NJ(nj, chain, unit_minv(f32, s, M, K, x, minv))
 }
-int launch_unit_grad(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
-                     const double* qdd, const double* minv, double* A, double* Bm, double* dqdd) {
-  TMPC_DISPATCH_NJ(nj, chain, unit_grad(s, M, K, dt, x, qdd, minv, A, Bm, dqdd))
+int launch_unit_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt,
+                     const double* x, const double* qdd, const double* minv, double* A, double* Bm, double* dqdd) {
+  TMPC_DISPATCH_NJ(nj, chain, unit_grad(f32, s, M, K, dt, x, qdd, minv, A, Bm, dqdd))
 }
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G) {
   TMPC_DISPATCH_NJ2(nj, ginv(s, C, B, rho, active, G))

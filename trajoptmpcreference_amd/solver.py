@@ -35,6 +35,9 @@ class MPCSolverMethods(enum.Enum):
     QP_PCG_SS = "QP-PCG-SS"
 
 
+# options['precision'] (a build option; the reference is fp64): include/tmpc.h TMPC_PRECISION_*
+_PRECISION = {"fp64": 0, "fp32": 1, "mixed": 2}
+
 _OPTION_MAP = {
     "exit_tolerance_linSys": "exit_tolerance_linSys",
     "max_iter_linSys": "max_iter_linSys",
@@ -142,8 +145,13 @@ class TrajoptMPCReference:
             ctx.set_cost_quadratic(c.Q, c.QF, c.R, c.xg, c.QF_start)
         # pcg_warm_start (build option, default off = the reference): PCG of each QP starts from the
         # previous QP's lambda, across MPC steps from the shifted last lambda (include/tmpc.h)
+        prec = options.get("precision", "fp64")
+        if prec not in _PRECISION:
+            raise ValueError(f"options['precision'] must be one of {sorted(_PRECISION)}, got {prec!r}")
+        if prec != "fp64" and isinstance(c, UrdfCost):
+            raise NotImplementedError("the fp32 / mixed precision modes support QuadraticCost only")
         ctx.set_options(**{v: options[k] for k, v in _OPTION_MAP.items()},
-                        pcg_warm_start=int(bool(options.get("pcg_warm_start", False))))
+                        pcg_warm_start=int(bool(options.get("pcg_warm_start", False))), precision=_PRECISION[prec])
         ctx.set_box_limits(spec)
         return ctx
 
