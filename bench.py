@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E (MI355X_MICROARCH.md: 8.0 TB/s)
 FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector (= fp64 matrix) peak
+FP32_PEAK_TFLOPS = 157.3    # MI355X fp32 vector peak (non-packed FMA)
 LDS_PEAK_GBS = 256 * 2.4 * 256   # 256 B/clk/CU (ds_read_b64/b128) x 2.4 GHz x 256 CUs
 
 
@@ -71,6 +72,11 @@ def parse(argv=None):
     ap.add_argument("--cost", default="quadratic", choices=["quadratic", "ee"],
                     help="ee: UrdfCost (SURVEY 8f row 4; 2-link only) with examples/twolinks.py's Q, QF, R, "
                          "xg = [-1, 1.5, 0, 0]; use with --links 2")
+    ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "mixed"],
+                    help="tmpc_options.precision: fp32 = BASELINE config 3 (fp32 dynamics + Riccati), "
+                         "mixed = config 5 (fp32 dynamics, fp64 PCG); the workload rollout stays fp64")
+    ap.add_argument("--pcg-warm-start", action="store_true",
+                    help="tmpc_options.pcg_warm_start: each PCG starts from the previous lambda (MPC loop)")
     ap.add_argument("--seed0", type=int, default=0)
     ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
     ap.add_argument("--cpu-procs", type=int, default=16)
@@ -283,6 +289,8 @@ def main():
     ctx.h2d(d_x0, x0)
     ctx.h2d(d_u0, u0)
     ctx.rollout_device(B, N, dt, d_x0, d_u0)
+    prec_id = {"fp64": 0, "fp32": 1, "mixed": 2}[a.precision]
+    ctx.set_options(precision=prec_id, pcg_warm_start=int(a.pcg_warm_start))   # after the fp64 workload rollout
 
     if a.mpc_steps > 0:
         K1 = a.mpc_steps
@@ -370,23 +378,28 @@ def main():
 
     name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
     headline = a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and not limits and \
-        a.cost == "quadratic"
+        a.cost == "quadratic" and N == 64 and a.precision == "fp64"
     if a.limits != "none":
         name += f", soft box constraints {a.limits}"
     if a.cost == "ee":
         name += ", UrdfCost end-effector cost (twolinks.py goal)"
     if a.mpc_steps > 0:
         name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
+    if a.precision != "fp64":
+        name += ", fp32 dynamics + Riccati" if a.precision == "fp32" else ", mixed fp32 dynamics / fp64 PCG"
     out = {
         "metric": ("MPC solves/sec (arm6.urdf, N=64, SQP-PCG) at 1/2/4/8 GPUs; KKT residual vs ref" if headline
                    else f"MPC solves/sec (arm{n}.urdf, N={N}, {name})"),
         "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
+        "dtype": {"fp64": "f64", "fp32": "f32", "mixed": "f32 dynamics / f64 Schur-PCG"}[a.precision], "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
         "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} {a.solver.upper()} "
                                f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU"
                                + ("" if a.limits == "none" else f", limits {a.limits}")
-                               + (", UrdfCost" if a.cost == "ee" else ""),
+                               + (", UrdfCost" if a.cost == "ee" else "")
+                               + ("" if a.precision == "fp64" else f", precision {a.precision}")
+                               + (f", MPC loop of {a.mpc_steps} steps" if a.mpc_steps > 0 else "")
+                               + (", PCG warm start" if a.pcg_warm_start else ""),
                    "global_batch": B * world, "N": N, "method": a.method if a.solver == "sqp" else "iLQR",
                    "parallelism": f"shard{world} (RCCL broadcast of start states, gather of results)"},
     }
@@ -398,8 +411,10 @@ def main():
         per_launch = int(counters[0]) / max(1, bw["launches"])
         flops = per_launch * (N - 1) * ilqr_backward_flops_per_knot(nx, nu)
         ach = flops / (bw["avg_ms"] / 1e3) / 1e12
-        roofline = {"kernel": "k_ilqr_backward", "bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
+        f32 = a.precision == "fp32"
+        peak = FP32_PEAK_TFLOPS if f32 else FP64_PEAK_TFLOPS
+        roofline = {"kernel": "k_ilqr_backward", "bound": "fp32-valu" if f32 else "fp64-valu", "achieved": ach,
+                    "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": None,
                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
                     "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
     out["roofline"] = roofline
@@ -426,6 +441,11 @@ def main():
                        "ls_trials_per_qp": int(counters[3]) // max(1, a.steps)}
     out["kernels"] = kernels
     out["dominant_kernel"] = dominant
+    # lock-step cost: every iteration launches the whole batch until its slowest problem exits
+    it_name = "ilqr_decide" if a.solver == "ilqr" else "ls_decide"
+    if it_name in kernels:
+        out["lockstep"] = {"batch_iterations_per_solve": kernels[it_name]["launches"] / a.steps / max(1, a.mpc_steps),
+                           "problem_iterations_mean": int(counters[0]) / (B * a.steps * max(1, a.mpc_steps))}
     out["exit_codes"] = {str(k): int(v) for k, v in zip(*np.unique(exit_all, return_counts=True))}
     out["iters_mean"] = float(np.mean(iters_all))
     out["iters_max"] = int(np.max(iters_all))

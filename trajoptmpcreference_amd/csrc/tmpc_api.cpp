@@ -502,7 +502,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   if ((rc = alloc_trace(ctx, B, W, tr))) return rc;
   BUF(double, alphas, T + 1);
   BUF(double, terms, (size_t)B * T * N * 4);   // [B][T][N][cost, violation, D, soft value]
-  BUF(int, active_count, 1);
+  BUF(int, active_count, 2);   // [0] some problem in its inner loop, [1] some problem restarted a pass
   BUF(unsigned long long, counters, 4);
   BUF(unsigned long long, prob_counters, (size_t)B * 3);   // per-problem tallies of k_ls_decide
   BUF(int, outer_active, B);
@@ -552,44 +552,75 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
-  // soft-constraint outer loop (:531-757): one inner SQP loop per pass for every problem still
-  // in the outer loop, then check_and_update_soft_constraints on the device
-  for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
   launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
-  // initial J, c, merit (:541-548)
-  LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
-                            alphas + T, d_x, d_u, w.xs, nullptr, nullptr, st.active, terms));
-  if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, st.active));
-  HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-  launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
-                   st, nullptr, tr, active_count, nullptr, hterms);
-  for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
-    if ((rc = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false))) return rc;
+  // initial J, c, merit (:541-548) of the problems in `mask` (st.active: all, act_init: restarted passes)
+  auto init_merit = [&](int* mask) -> int {
+    ProbState sti = st;
+    sti.active = mask;
+    LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1,
+                              dt, alphas + T, d_x, d_u, w.xs, nullptr, nullptr, mask, terms));
+    if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, mask));
+    launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
+                     sti, nullptr, tr, active_count, nullptr, hterms);
+    HIP_OK(hipGetLastError());
+    return 0;
+  };
+  // one SQP iteration (:550-757) of every problem in its inner loop; flags[0] = some problem continues
+  auto sqp_iteration = [&]() -> int {
+    int rc2 = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false);
+    if (rc2) return rc2;
     {
       Timed t(ctx, "ls_terms");
       LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
                                 alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
       if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, T, alphas, d_x, d_u, w.dx, w.du, st.active));
     }
-    HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-    {
-      Timed t(ctx, "ls_decide");
-      launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
-                       st, w.iters, tr, active_count, prob_counters, hterms);
-      HIP_OK(hipGetLastError());
+    Timed t(ctx, "ls_decide");
+    launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
+                     st, w.iters, tr, active_count, prob_counters, hterms);
+    HIP_OK(hipGetLastError());
+    return 0;
+  };
+  HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
+  if ((rc = init_merit(st.active))) return rc;
+  if (!soft) {
+    // unconstrained: one inner loop; check_and_update_soft_constraints then exits 1 (:531-757)
+    for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
+      HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
+      if ((rc = sqp_iteration())) return rc;
+      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+      HIP_OK(hipStreamSynchronize(ctx->stream));
+      if (ctx->h_count[0] == 0) break;
     }
-    HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
-    if (*ctx->h_count == 0) break;
-  }
-  HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-  launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints, o.max_iter_softConstraints,
-                    d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft, active_count);
-  HIP_OK(hipGetLastError());
-  if (!soft) break;   // unconstrained: exit_soft 1 after one pass, as the reference
-  HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_OK(hipStreamSynchronize(ctx->stream));
-  if (*ctx->h_count == 0) break;
+    launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints, o.max_iter_softConstraints,
+                      d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft, active_count);
+    HIP_OK(hipGetLastError());
+  } else {
+    // soft-constraint outer loop (:531-757), per problem: a problem whose inner loop exits runs
+    // check_and_update_soft_constraints at once (k_soft_outer, per-problem mode) and starts its
+    // next pass the following iteration, while the rest of the batch carries on.  Launches per
+    // solve: the largest per-problem total of SQP iterations, not the sum over passes of each
+    // pass's slowest problem (BASELINE config 4: 657 -> see DESIGN.md).  Each problem's own
+    // sequence of operations is the lock-step one, so its results are identical.
+    BUF(int, act_init, B);
+    HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
+    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 2;
+    for (long it = 0; it < cap; ++it) {
+      HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
+      if ((rc = sqp_iteration())) return rc;
+      launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
+                        o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
+                        active_count + 1, &st, act_init, o.rho_init_SQP_DDP);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+      HIP_OK(hipStreamSynchronize(ctx->stream));
+      if (ctx->h_count[0] == 0 && ctx->h_count[1] == 0) break;
+      if (ctx->h_count[1]) {   // restarted passes: initial merit, then into the inner loop
+        if ((rc = init_merit(act_init))) return rc;
+        launch_activate(ctx->stream, B, act_init, st.active);
+        HIP_OK(hipGetLastError());
+      }
+    }
   }
   launch_sum_counters(ctx->stream, B, prob_counters, counters);
   unsigned long long hc[4] = {0, 0, 0, 0};
@@ -632,7 +663,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   BUF(double, il_xt, (size_t)B * T * nx * N);
   BUF(double, il_ut, (size_t)B * T * nj * K);
   BUF(double, il_J, (size_t)B * T);
-  BUF(int, active_count, 1);
+  BUF(int, active_count, 2);
   BUF(int, outer_active, B);
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
@@ -655,58 +686,88 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
-  for (int pass = 0; pass <= o.max_iter_softConstraints; ++pass) {
-    launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
-    HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-    LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1, dt,
-                                  1, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
-    launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st,
+  launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
+  // J at the current trajectory of the problems in `mask` (st.active: all, act_init: restarted passes)
+  auto init_cost = [&](int* mask) -> int {
+    ProbState sti = st;
+    sti.active = mask;
+    LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
+                                  B, N, 1, dt, 1, alphas, d_x, d_u, il_K, il_d, mask, il_ok, il_xt, il_ut, il_J));
+    launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, sti,
                        tr, active_count, nullptr);
+    HIP_OK(hipGetLastError());
+    return 0;
+  };
+  // one iLQR iteration of every problem in its inner loop; flags[0] = some problem continues
+  auto ilqr_iteration = [&]() -> int {
+    {
+      Timed t(ctx, "qp_fd");
+      LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs,
+                             st.need_grad, w.qdd, w.cvec));
+    }
+    {
+      Timed t(ctx, "qp_minv");
+      LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad,
+                               w.minv));
+    }
+    {
+      Timed t(ctx, "qp_grad");
+      LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad,
+                               w.qdd, w.minv, w.A, w.Bm));
+    }
+    {
+      Timed t(ctx, "ilqr_backward");
+      LAUNCH_OK(launch_ilqr_backward(ric32(ctx), ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, d_x, d_u, st.rho, st.active,
+                                     w.A, w.Bm, smu, slam, il_K, il_d, il_dV, il_ok));
+    }
+    {
+      Timed t(ctx, "ilqr_forward");
+      LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu,
+                                    slam, B, N, T, dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut,
+                                    il_J));
+    }
+    Timed t(ctx, "ilqr_decide");
+    launch_ilqr_decide(ctx->stream, B, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st, tr,
+                       active_count, counters);
+    HIP_OK(hipGetLastError());
+    return 0;
+  };
+  HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
+  if ((rc = init_cost(st.active))) return rc;
+  if (!soft) {
     for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
-      {
-        Timed t(ctx, "qp_fd");
-        LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
-                               w.cvec));
-      }
-      {
-        Timed t(ctx, "qp_minv");
-        LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
-      }
-      {
-        Timed t(ctx, "qp_grad");
-        LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv,
-                                 w.A, w.Bm));
-      }
-      {
-        Timed t(ctx, "ilqr_backward");
-        LAUNCH_OK(launch_ilqr_backward(ric32(ctx), ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, d_x, d_u, st.rho, st.active,
-                                       w.A, w.Bm, smu, slam, il_K, il_d, il_dV, il_ok));
-      }
-      {
-        Timed t(ctx, "ilqr_forward");
-        LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T,
-                                      dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut, il_J));
-      }
       HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-      {
-        Timed t(ctx, "ilqr_decide");
-        launch_ilqr_decide(ctx->stream, B, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u,
-                           st, tr, active_count, counters);
-        HIP_OK(hipGetLastError());
-      }
+      if ((rc = ilqr_iteration())) return rc;
       HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
       HIP_OK(hipStreamSynchronize(ctx->stream));
-      if (*ctx->h_count == 0) break;
+      if (ctx->h_count[0] == 0) break;
     }
-    HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
     launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
                       o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
                       active_count);
     HIP_OK(hipGetLastError());
-    if (!soft) break;
-    HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
-    if (*ctx->h_count == 0) break;
+  } else {
+    // soft-constraint outer loop per problem (as sqp_device): a problem starts its next pass as soon
+    // as its own inner loop exits
+    BUF(int, act_init, B);
+    HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
+    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 2;
+    for (long it = 0; it < cap; ++it) {
+      HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
+      if ((rc = ilqr_iteration())) return rc;
+      launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
+                        o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
+                        active_count + 1, &st, act_init, o.rho_init_SQP_DDP);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+      HIP_OK(hipStreamSynchronize(ctx->stream));
+      if (ctx->h_count[0] == 0 && ctx->h_count[1] == 0) break;
+      if (ctx->h_count[1]) {
+        if ((rc = init_cost(act_init))) return rc;
+        launch_activate(ctx->stream, B, act_init, st.active);
+        HIP_OK(hipGetLastError());
+      }
+    }
   }
   unsigned long long hc[4] = {0, 0, 0, 0};
   HIP_OK(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
@@ -742,7 +803,7 @@ int tmpc_create(int device, tmpc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&ctx->dmodel, sizeof(ModelDev)) != hipSuccess || hipMalloc(&ctx->dcost, sizeof(CostDev)) != hipSuccess ||
       hipMalloc(&ctx->dlim, sizeof(ConstrDev)) != hipSuccess || hipMemset(ctx->dlim, 0, sizeof(ConstrDev)) != hipSuccess ||
-      hipHostMalloc(&ctx->h_count, sizeof(int)) != hipSuccess) {
+      hipHostMalloc(&ctx->h_count, 4 * sizeof(int)) != hipSuccess) {
     delete ctx;
     return -4;
   }

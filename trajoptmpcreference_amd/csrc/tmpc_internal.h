@@ -119,9 +119,12 @@ void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mo
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
                       int* active_count, unsigned long long* counters, const double* hterms);
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active);
+// st / act_init / rho_init: the per-problem outer loop (null act_init: lock-step, tmpc_kernels.hip)
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
                        const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
-                       int* outer_iter, int* exit_soft, int* outer_count);
+                       int* outer_iter, int* exit_soft, int* outer_count, const ProbState* st = nullptr,
+                       int* act_init = nullptr, double rho_init = 0.0);
+void launch_activate(hipStream_t s, int B, int* act_init, int* active);
 int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                          const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                          const double* mu, const double* lam, double* K, double* d, double* dV, int* ok);

@@ -1744,6 +1744,13 @@ void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& s
 //   otherwise update_soft_constraint_constants (:137-166) elementwise and exit 3
 //   when no constant changed (all mu at their limit).
 // Unconstrained problems (no soft type) take the reference's path: max_c = 0 -> exit 1.
+// Two drivers:
+//   lock-step (inner == null): every problem still in the outer loop, after the whole batch's
+//     inner loops have exited; *outer_count = 1 when some problem continues;
+//   per-problem (inner = the inner loop's active flags): only problems whose inner loop has just
+//     exited (outer_active && !inner && !init); one that continues is reset for its next pass
+//     (k_init_state's reset) and flagged in act_init for its initial merit evaluation, so each
+//     problem runs its passes back to back instead of waiting for the batch's slowest pass.
 __device__ __forceinline__ double soft_v(const ConstrDev* Cs, int t, int e, int n, double z) {
   const int i = e < n ? e : e - n;
   return e < n ? z - Cs->lb[t][i] : Cs->ub[t][i] - z;
@@ -1754,9 +1761,12 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
                                                    const double* __restrict__ u, double* __restrict__ mu,
                                                    double* __restrict__ lam, double* __restrict__ phi,
                                                    int* __restrict__ outer_active, int* __restrict__ outer_iter,
-                                                   int* __restrict__ exit_soft, int* __restrict__ outer_count) {
+                                                   int* __restrict__ exit_soft, int* __restrict__ outer_count,
+                                                   ProbState st, int* __restrict__ act_init, double rho_init) {
   const int b = blockIdx.x;
   if (!outer_active[b]) return;
+  const bool per_problem = act_init != nullptr;
+  if (per_problem && (st.active[b] || act_init[b])) return;
   const int t0 = threadIdx.x;
   const int NX = 2 * NJ, K = N - 1, MC = 6 * NJ;
   const double* xb = x + (size_t)b * NX * N;
@@ -1819,16 +1829,38 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
       exit_soft[b] = ex;
       outer_active[b] = 0;
     } else {
-      atomicAdd(outer_count, 1);
+      *outer_count = 1;   // the host only tests for zero
+      if (per_problem) {  // next pass: the reset of k_init_state, then the initial merit (act_init)
+        st.rho[b] = rho_init;
+        st.drho[b] = 1.0;
+        st.iter[b] = 0;
+        st.need_grad[b] = 1;
+        st.exit_sqp[b] = 0;
+        act_init[b] = 1;
+      }
     }
   }
 }
 
+// act_init -> active once the initial merit of a restarted pass is set
+__global__ void k_activate(int B, int* __restrict__ act_init, int* __restrict__ active) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B || !act_init[b]) return;
+  act_init[b] = 0;
+  active[b] = 1;
+}
+
+void launch_activate(hipStream_t s, int B, int* act_init, int* active) {
+  hipLaunchKernelGGL(k_activate, TMPC_GRID(B, 256), 0, s, B, act_init, active);
+}
+
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
                        const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
-                       int* outer_iter, int* exit_soft, int* outer_count) {
+                       int* outer_iter, int* exit_soft, int* outer_count, const ProbState* st, int* act_init,
+                       double rho_init) {
+  ProbState none{};
   hipLaunchKernelGGL(k_soft_outer, dim3(B), dim3(64), 0, s, Cs, B, N, nj, tol, max_iter, x, u, mu, lam, phi,
-                     outer_active, outer_iter, exit_soft, outer_count);
+                     outer_active, outer_iter, exit_soft, outer_count, st ? *st : none, act_init, rho_init);
 }
 
 // BoxConstraint.__init__ (:21-24): mu = mu_init, lambda = 0, phi = phi_init
