@@ -30,16 +30,47 @@ template <int NJ, class R>
 struct IlqrLds {
   static constexpr int NX = 2 * NJ, NU = NJ;
   R Vxx[NX * NX], Vx[NX];
-  R A[NX * NX], Bm[NX * NU];
-  R P[NX * NX], VB[NX * NU];        // V_xx A, V_xx B (P then holds the unsymmetrised V_xx)
+  R A[2][NX * NX], Bm[2][NX * NU];      // knot k's A_k, B_k and the prefetched A_{k-1}, B_{k-1}
+  R P[NX * NX], VB[NX * NU];            // V_xx A, V_xx B (P then holds the unsymmetrised V_xx)
   R Qxx[NX * NX], Qux[NU * NX], Quu[NU * NU], Qx[NX], Qu[NU];
-  R KD[NU * (NX + 1)];              // [Q_uu^-1 Q_ux | Q_uu^-1 Q_u], row-major
+  R KD[NU * (NX + 1)];                  // [Q_uu^-1 Q_ux | Q_uu^-1 Q_u], row-major
   R lx[NX], lu[NU], jac[3 * NJ];
+  R Q[NX * NX], QF[NX * NX], Rc[NU * NU];   // the cost's Hessian blocks, staged once
+  double xg[NX];
+  double z[2][NX + NU];                 // knot k's [x_k; u_k] and the prefetched knot's (fp64: the soft terms)
   R dv[2];
   int fail;
 };
 
-template <int NJ, class R>
+// One 64-lane workgroup = one wave: LDS written by one lane is visible to the others once the
+// wave's LDS operations have completed, so the phases below are ordered by `s_waitcnt lgkmcnt(0)`
+// alone.  __syncthreads() would also drain the wave's outstanding global memory operations
+// (vmcnt(0)): the K_k / d_k stores of the previous knot and the next knot's prefetch loads.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Diagnostic build only (-DTMPC_ILQR_STAMPS): per-phase s_memtime cycle totals of block 0's
+// backward sweep, printed at its end (tools/debug/ilqr_stamps.py).
+#ifdef TMPC_ILQR_STAMPS
+#define IL_STAMP(i)                                             \
+  do {                                                          \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+    st_[i] += n_ - st_prev_;                                    \
+    st_prev_ = n_;                                              \
+  } while (0)
+#else
+#define IL_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
+// MF (fp64 only): the Q-function products on the fp64 matrix cores (v_mfma_f64_16x16x4f64, one
+// wave): P|VB = V_xx [A B] with [Q_x; Q_u] - l as an extra row, then [A B]^T [P VB] taking the
+// first product's accumulators as its B operand in place (the f64 C/D layout puts row 4s + lane/16
+// of reg s on the lane the next MFMA's k-step s reads), then M | V_x = Q_ux^T [K d].  Every output
+// is the same products summed in the same order as the VALU loops.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <int NJ, class R, bool MF>
 __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
                                                       int B, int N, const double* __restrict__ x,
                                                       const double* __restrict__ u, const double* __restrict__ rho_in,
@@ -49,6 +80,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
                                                       double* __restrict__ dout, double* __restrict__ dV,
                                                       int* __restrict__ ok) {
   constexpr int NX = 2 * NJ, NU = NJ, NC = NX + 1, MC = 6 * NJ;
+  constexpr int NA = (NX * NX + 63) / 64, NB = (NX * NU + 63) / 64;   // prefetch slots per lane
   const int b = blockIdx.x;
   if (!active[b]) return;
   __shared__ IlqrLds<NJ, R> L;
@@ -58,111 +90,235 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NU * K;
   const bool soft = Cs->any != 0;
+  const int qf_start = C->QF_start;
+
+  // the cost blocks once (QuadraticCost, TrajoptCost.py:71-83)
+  for (int e = t; e < NX * NX; e += 64) {
+    L.Q[e] = R(C->Q[e]);
+    L.QF[e] = R(C->QF[e]);
+  }
+  for (int e = t; e < NU * NU; e += 64) L.Rc[e] = R(C->R[e]);
+  if (t < NX) L.xg[t] = C->xg[t];
+  auto use_qf = [&](int k) { return (k == N - 1) || (qf_start >= 0 && k >= qf_start); };
+  // [x_k; u_k] of a knot, one entry per lane (u_{N-1} := 0)
+  auto load_z = [&](int k) -> double {
+    if (t < NX) return xb[t * N + k];
+    if (t < NX + NU) return k < K ? ub[(t - NX) * K + k] : 0.0;
+    return 0.0;
+  };
+  // prefetched A_k / B_k entries of this lane
+  double pa[NA], pb[NB];
+  auto load_ab = [&](int k) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int e = t + 64 * i;
+      pa[i] = e < NX * NX ? Aall[((size_t)b * K + k) * NX * NX + e] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int e = t + 64 * i;
+      pb[i] = e < NX * NU ? Ball[((size_t)b * K + k) * NX * NU + e] : 0.0;
+    }
+  };
+  auto store_ab = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      if (t + 64 * i < NX * NX) L.A[slot][t + 64 * i] = R(pa[i]);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (t + 64 * i < NX * NU) L.Bm[slot][t + 64 * i] = R(pb[i]);
+  };
 
   // stage the cost derivatives of knot k (QuadraticCost.gradient / hessian, TrajoptCost.py:58-83,
-  // plus the soft-limit jacobian, :220-225) into L.lx / L.lu / L.jac
-  auto stage_l = [&](int k) {
+  // plus the soft-limit jacobian, :220-225) into L.lx / L.lu / L.jac; z = L.z[zs]
+  auto stage_l = [&](int k, int zs) {
     const bool term = k == K;
+    const double* zk = L.z[zs];
     if (soft && t == 0) {
       double z[3 * NJ], jac[3 * NJ];
 #pragma unroll
-      for (int m = 0; m < NX; ++m) z[m] = xb[m * N + k];
+      for (int m = 0; m < NX; ++m) z[m] = zk[m];
 #pragma unroll
-      for (int m = 0; m < NU; ++m) z[NX + m] = term ? 0.0 : ub[m * K + k];
+      for (int m = 0; m < NU; ++m) z[NX + m] = term ? 0.0 : zk[NX + m];
       const size_t ko = ((size_t)b * N + k) * MC;
       soft_knot<NJ>(Cs, mu + ko, lam + ko, term, z, jac);
 #pragma unroll
       for (int m = 0; m < 3 * NJ; ++m) L.jac[m] = jac[m];
     }
     if (!soft && t < 3 * NJ) L.jac[t] = 0.0;
-    __syncthreads();
-    const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
+    wave_lds_sync();
+    const R* Qk = use_qf(k) ? L.QF : L.Q;
     if (t < NX) {
       R g = 0.0;
-      for (int m = 0; m < NX; ++m) g += R(xb[m * N + k] - C->xg[m]) * R(Qk[m * NX + t]);
+      for (int m = 0; m < NX; ++m) g += R(zk[m] - L.xg[m]) * Qk[m * NX + t];
       L.lx[t] = g + L.jac[t];
     } else if (t < NX + NU && !term) {
       const int c = t - NX;
       R g = 0.0;
-      for (int m = 0; m < NU; ++m) g += R(ub[m * K + k]) * R(C->R[m * NU + c]);
+      for (int m = 0; m < NU; ++m) g += R(zk[NX + m]) * L.Rc[m * NU + c];
       L.lu[c] = g + L.jac[NX + c];
     }
   };
   // l_xx (+ per-type outer products on the q / qd diagonal blocks)
   auto lxx = [&](int k, int r, int c) -> R {
-    const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
+    const R* Qk = use_qf(k) ? L.QF : L.Q;
     const R o = (r / NJ == c / NJ) ? L.jac[r] * L.jac[c] : 0.0;
-    return R(Qk[r * NX + c]) + o;
+    return Qk[r * NX + c] + o;
   };
 
-  // terminal value function: V_x = l_x(N-1), V_xx = l_xx(N-1)
-  stage_l(K);
-  __syncthreads();
-  for (int e = t; e < NX * NX; e += 64) L.Vxx[e] = lxx(K, e / NX, e % NX);
-  if (t < NX) L.Vx[t] = L.lx[t];
-  if (t == 0) {
-    L.dv[0] = L.dv[1] = 0.0;
-    L.fail = 0;
+  // terminal value function: V_x = l_x(N-1), V_xx = l_xx(N-1); A_{K-1}, B_{K-1} and z_{K-1} in flight
+  {
+    const double zt = load_z(K);
+    load_ab(K - 1);
+    const double zn = load_z(K - 1);
+    if (t < NX + NU) L.z[0][t] = zt;
+    wave_lds_sync();
+    stage_l(K, 0);
+    wave_lds_sync();
+    for (int e = t; e < NX * NX; e += 64) L.Vxx[e] = lxx(K, e / NX, e % NX);
+    if (t < NX) L.Vx[t] = L.lx[t];
+    if (t == 0) {
+      L.dv[0] = L.dv[1] = 0.0;
+      L.fail = 0;
+    }
+    store_ab(0);
+    if (t < NX + NU) L.z[1][t] = zn;
+    wave_lds_sync();
   }
-  __syncthreads();
 
+#ifdef TMPC_ILQR_STAMPS
+  unsigned long long st_[8] = {}, st_prev_ = __builtin_amdgcn_s_memtime();
+#endif
   for (int k = K - 1; k >= 0; --k) {
-    for (int e = t; e < NX * NX; e += 64) L.A[e] = Aall[((size_t)b * K + k) * NX * NX + e];
-    for (int e = t; e < NX * NU; e += 64) L.Bm[e] = Ball[((size_t)b * K + k) * NX * NU + e];
-    stage_l(k);
-    __syncthreads();
+    IL_STAMP(7);
+    const int cur = (K - 1 - k) & 1;
+    const R* A = L.A[cur];
+    const R* Bm = L.Bm[cur];
+    // next knot's A, B, z: loads issued now, written to the other slot at the end of this knot
+    double zn = 0.0;
+    if (k > 0) {
+      load_ab(k - 1);
+      zn = load_z(k - 1);
+    }
+    stage_l(k, 1 - cur);
+    wave_lds_sync();
+    IL_STAMP(0);
+    if constexpr (MF) {
+      // fragments: lane l = (row / col l & 15, k-offset l >> 4) of each 16x16x4 k-step
+      constexpr int KS = (NX + 3) / 4;
+      const int lo = t & 15, hi = t >> 4;
+      double vf[KS], abf[2][KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int kk = 4 * s + hi;
+        vf[s] = kk < NX ? (lo < NX ? double(L.Vxx[lo * NX + kk]) : (lo == NX ? double(L.Vx[kk]) : 0.0)) : 0.0;
+#pragma unroll
+        for (int tl = 0; tl < 2; ++tl) {
+          const int c = 16 * tl + lo;
+          abf[tl][s] = kk < NX ? (c < NX ? double(A[kk * NX + c]) : (c < NX + NU ? double(Bm[kk * NU + c - NX]) : 0.0))
+                               : 0.0;
+        }
+      }
+      // P | VB (rows < NX) and [A B]^T V_x (row NX) = V_xx' [A B]
+      dbl4 pv[2];
+#pragma unroll
+      for (int tl = 0; tl < 2; ++tl) {
+        pv[tl] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) pv[tl] = __builtin_amdgcn_mfma_f64_16x16x4f64(vf[s], abf[tl][s], pv[tl], 0, 0, 0);
+      }
+#pragma unroll
+      for (int tl = 0; tl < 2; ++tl)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (hi + 4 * i == NX) {
+            const int c = 16 * tl + lo;
+            if (c < NX) L.Qx[c] = L.lx[c] + R(pv[tl][i]);
+            else if (c < NX + NU) L.Qu[c - NX] = L.lu[c - NX] + R(pv[tl][i]);
+          }
+      // [A B]^T [P VB]: tile (tr, tc); B operand of k-step s = reg s of pv[tc] (rows >= NX zeroed)
+#pragma unroll
+      for (int tr = 0; tr < 2; ++tr)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc) {
+          dbl4 q{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const double bop = 4 * s + hi < NX ? pv[tc][s] : 0.0;
+            q = __builtin_amdgcn_mfma_f64_16x16x4f64(abf[tr][s], bop, q, 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 16 * tr + hi + 4 * i, c = 16 * tc + lo;
+            const R v = R(q[i]);
+            if (r < NX && c < NX) {
+              L.Qxx[r * NX + c] = lxx(k, r, c) + v;
+            } else if (r >= NX && r < NX + NU && c < NX) {
+              L.Qux[(r - NX) * NX + c] = v;
+            } else if (r >= NX && r < NX + NU && c >= NX && c < NX + NU) {
+              const int rr = r - NX, cc = c - NX;
+              L.Quu[rr * NU + cc] = (L.Rc[rr * NU + cc] + L.jac[NX + rr] * L.jac[NX + cc]) + v + (rr == cc ? rho : R(0));
+            }
+          }
+        }
+      wave_lds_sync();
+      IL_STAMP(1);
+    } else {
     // P = V_xx A, R = V_xx B; Q_x = l_x + A^T V_x, Q_u = l_u + B^T V_x
     for (int e = t; e < NX * NX + NX * NU + NX + NU; e += 64) {
       if (e < NX * NX) {
         const int r = e / NX, c = e % NX;
         R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.Vxx[r * NX + m] * L.A[m * NX + c];
+        for (int m = 0; m < NX; ++m) s += L.Vxx[r * NX + m] * A[m * NX + c];
         L.P[e] = s;
       } else if (e < NX * NX + NX * NU) {
         const int f = e - NX * NX, r = f / NU, c = f % NU;
         R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.Vxx[r * NX + m] * L.Bm[m * NU + c];
+        for (int m = 0; m < NX; ++m) s += L.Vxx[r * NX + m] * Bm[m * NU + c];
         L.VB[f] = s;
       } else if (e < NX * NX + NX * NU + NX) {
         const int r = e - NX * NX - NX * NU;
         R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.A[m * NX + r] * L.Vx[m];
+        for (int m = 0; m < NX; ++m) s += A[m * NX + r] * L.Vx[m];
         L.Qx[r] = L.lx[r] + s;
       } else {
         const int r = e - NX * NX - NX * NU - NX;
         R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.Bm[m * NU + r] * L.Vx[m];
+        for (int m = 0; m < NX; ++m) s += Bm[m * NU + r] * L.Vx[m];
         L.Qu[r] = L.lu[r] + s;
       }
     }
-    __syncthreads();
+    wave_lds_sync();
+    IL_STAMP(1);
     // Q_xx = l_xx + A^T P, Q_uu = l_uu + B^T R + rho I, Q_ux = B^T P
     for (int e = t; e < NX * NX + NU * NU + NU * NX; e += 64) {
       if (e < NX * NX) {
         const int r = e / NX, c = e % NX;
         R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.A[m * NX + r] * L.P[m * NX + c];
+        for (int m = 0; m < NX; ++m) s += A[m * NX + r] * L.P[m * NX + c];
         L.Qxx[e] = lxx(k, r, c) + s;
       } else if (e < NX * NX + NU * NU) {
         const int f = e - NX * NX, r = f / NU, c = f % NU;
         R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.Bm[m * NU + r] * L.VB[m * NU + c];
-        L.Quu[f] = (R(C->R[f]) + L.jac[NX + r] * L.jac[NX + c]) + s + (r == c ? rho : R(0));
+        for (int m = 0; m < NX; ++m) s += Bm[m * NU + r] * L.VB[m * NU + c];
+        L.Quu[f] = (L.Rc[f] + L.jac[NX + r] * L.jac[NX + c]) + s + (r == c ? rho : R(0));
       } else {
         const int f = e - NX * NX - NU * NU, r = f / NX, c = f % NX;
         R s = 0.0;
 #pragma unroll
-        for (int m = 0; m < NX; ++m) s += L.Bm[m * NU + r] * L.P[m * NX + c];
+        for (int m = 0; m < NX; ++m) s += Bm[m * NU + r] * L.P[m * NX + c];
         L.Qux[f] = s;
       }
     }
-    __syncthreads();
+    wave_lds_sync();
+    }   // MF
+    IL_STAMP(2);
     // [K | d] = -Q_uu^-1 [Q_ux | Q_u]: Cholesky Q_uu = L L^T (every lane, from LDS), then lane c
     // solves its right-hand-side column c; Q_uu not positive definite -> backward failure
     if (t < NC) {
@@ -203,9 +359,29 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       for (int i = 0; i < NU; ++i) L.KD[i * NC + t] = -y[i];
       if (t == 0 && !pd) L.fail = 1;
     }
-    __syncthreads();
+    wave_lds_sync();
+    IL_STAMP(3);
     if (L.fail) break;
     // V_x = Q_x + Q_ux^T d, M = Q_xx + Q_ux^T K; dV1 += d^T Q_u, dV2 += d^T Q_uu d / 2
+    if constexpr (MF) {
+      // [M | V_x] - [Q_xx | Q_x] = Q_ux^T [K | d]: one 16-column tile, k over the NU controls
+      constexpr int KU = (NU + 3) / 4;
+      const int lo = t & 15, hi = t >> 4;
+      dbl4 mv{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < KU; ++s) {
+        const int kk = 4 * s + hi;
+        const double aop = (kk < NU && lo < NX) ? double(L.Qux[kk * NX + lo]) : 0.0;
+        const double bop = (kk < NU && lo < NC) ? double(L.KD[kk * NC + lo]) : 0.0;
+        mv = __builtin_amdgcn_mfma_f64_16x16x4f64(aop, bop, mv, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = hi + 4 * i, c = lo;
+        if (r < NX && c < NX) L.P[r * NX + c] = L.Qxx[r * NX + c] + R(mv[i]);
+        else if (r < NX && c == NX) L.Vx[r] = L.Qx[r] + R(mv[i]);
+      }
+    } else
     for (int e = t; e < NX * NX + NX; e += 64) {
       if (e < NX * NX) {
         const int r = e / NX, c = e % NX;
@@ -222,20 +398,30 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       }
     }
     if (t == 63) {
+      // operands to registers first (one wave alone: each LDS read in the chain would expose its latency)
+      R dd[NU], qu[NU], quu[NU * NU];
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        dd[i] = L.KD[i * NC + NX];
+        qu[i] = L.Qu[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NU * NU; ++i) quu[i] = L.Quu[i];
       R s1 = 0.0, s2 = 0.0;
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
-        const R di = L.KD[i * NC + NX];
-        s1 += di * L.Qu[i];
+        const R di = dd[i];
+        s1 += di * qu[i];
         R qd = 0.0;
 #pragma unroll
-        for (int m = 0; m < NU; ++m) qd += L.Quu[i * NU + m] * L.KD[m * NC + NX];
+        for (int m = 0; m < NU; ++m) qd += quu[i * NU + m] * dd[m];
         s2 += di * qd;
       }
       L.dv[0] += s1;
       L.dv[1] += R(0.5) * s2;
     }
-    // K_k, d_k to HBM ([B][K][NU][NX], [B][K][NU])
+    IL_STAMP(4);
+    // K_k, d_k to HBM ([B][K][NU][NX], [B][K][NU]); not waited for (wave_lds_sync)
     for (int e = t; e < NU * NC; e += 64) {
       const int i = e / NC, c = e % NC;
       if (c < NX)
@@ -243,13 +429,25 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       else
         dout[((size_t)b * K + k) * NU + i] = double(L.KD[e]);
     }
-    __syncthreads();
+    wave_lds_sync();
     for (int e = t; e < NX * NX; e += 64) {
       const int r = e / NX, c = e % NX;
       L.Vxx[e] = R(0.5) * (L.P[r * NX + c] + L.P[c * NX + r]);
     }
-    __syncthreads();
+    IL_STAMP(5);
+    if (k > 0) {
+      store_ab(1 - cur);
+      if (t < NX + NU) L.z[cur][t] = zn;
+    }
+    wave_lds_sync();
+    IL_STAMP(6);
   }
+#ifdef TMPC_ILQR_STAMPS
+  if (b == 0 && t == 0)
+    printf("ilqr_stamps K=%d prefetch+stage_l %llu P/VB/Qx/Qu %llu Qxx/Quu/Qux %llu chol %llu Vx/M/dv %llu "
+           "Kstore/Vxx %llu store_ab %llu loop %llu\n", K, st_[0], st_[1], st_[2], st_[3], st_[4], st_[5], st_[6],
+           st_[7]);
+#endif
   if (t == 0) {
     ok[b] = L.fail ? 0 : 1;
     dV[2 * b] = double(L.dv[0]);
@@ -489,12 +687,18 @@ struct LaunchIlqr {
   static void backward(bool f32, hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                        const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                        const double* mu, const double* lam, double* K, double* d, double* dV, int* ok) {
+    // fp64: the matrix-core products (MF) unless TMPC_ILQR_VALU=1 (the VALU loops, for comparison)
+    const char* v = getenv("TMPC_ILQR_VALU");
+    const bool mf = !(v && v[0] == '1');
     if (f32)
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, float>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu,
-                         lam, K, d, dV, ok);
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, float, false>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
+                         Bm, mu, lam, K, d, dV, ok);
+    else if (mf)
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, true>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
+                         Bm, mu, lam, K, d, dV, ok);
     else
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, double>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu,
-                         lam, K, d, dV, ok);
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, false>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
+                         Bm, mu, lam, K, d, dV, ok);
   }
   static void forward(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
                       const double* lam, int B, int N, int T, double dt, int init, const double* alphas,
