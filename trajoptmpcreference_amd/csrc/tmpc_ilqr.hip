@@ -460,7 +460,27 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
 // trajectories are kept ([B][T][nx][N], [B][T][nu][N-1]) so the decision kernel
 // copies the accepted one.  Cost sums in totalCost's order (:296-310): the
 // QuadraticCost terms, then the soft values.
-template <int NJ, bool CHAIN, bool SOFT, class MT, class R>
+// Prefetch (PF) of the feedback law's operands: the knot loop is one serial chain per lane
+// (~25k cycles per knot at one wave per SIMD, profiles/r02: ~40 % of it the loads of K_k, d_k,
+// x_k, u_k), so the next knot's operands of every problem of the workgroup go global -> LDS by
+// LDS-DMA (global_load_lds: no VGPRs, the kernel is at the register cap) while this knot's
+// dynamics run.  Per problem and knot: K_k in 16-byte pieces, then d_k, x_k, u_k in dwords
+// (x / u are strided by knot in the reference layout).  Buffer [2][nprob][SK + SS] doubles.
+template <int NJ>
+struct FwdPf {
+  static constexpr int NX = 2 * NJ, NU = NJ;
+  static constexpr int SK = NU * NX;            // K_k
+  static constexpr int SS = NU + NX + NU;       // d_k, x_k, u_k
+  static constexpr int CK = SK / 2;             // 16-byte pieces of K_k (SK is even)
+  static __host__ __device__ int nprob(int T) { return 63 / T + 2; }   // problems a 64-lane group can touch
+  // regions rounded up to whole wave-instructions (64 x 16 B, 64 x 4 B): the last instruction's
+  // spare lanes land inside the region, not in the next one
+  static __host__ __device__ size_t rk(int T) { return (size_t)((nprob(T) * CK + 63) / 64) * 128; }
+  static __host__ __device__ size_t rs(int T) { return (size_t)((nprob(T) * 2 * SS + 63) / 64) * 32; }
+  static __host__ __device__ size_t lds_doubles(int T) { return 2 * (rk(T) + rs(T)); }
+};
+
+template <int NJ, bool CHAIN, bool SOFT, class MT, class R, bool PF>
 __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __restrict__ C,
                                                      const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                      const double* __restrict__ lam, int B, int N, int T, double dt,
@@ -475,23 +495,69 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
   MT M = Mg;
   if constexpr (!MT::STATIC) M = ModelRef{stage_model(Mg.p, &sM)};
   constexpr int NX = 2 * NJ, NU = NJ;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * T) return;
-  const int b = gid / T, tr = gid - b * T;
-  if (!active[b] || (!init && !ok[b])) return;
+  using P = FwdPf<NJ>;
+  extern __shared__ __align__(16) double pfb[];
+  const int lane = threadIdx.x;
+  const int gid = blockIdx.x * blockDim.x + lane;
+  const int bl = min(gid, B * T - 1) / T;   // (dead lanes of the last group: the last problem, unused)
+  const int b = bl, tr = min(gid, B * T - 1) - b * T;
+  const bool live = gid < B * T && active[b] && (init || ok[b]);
+  const bool pf = PF && !init;
+  if (pf) {
+    if (__ballot(live) == 0) return;   // the whole wave: no work, no prefetch to share
+  } else if (!live) {
+    return;
+  }
   const int K = N - 1;
   const double al = init ? 0.0 : alphas[tr];
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NU * K;
   double* xo = xt + (size_t)gid * NX * N;
   double* uo = ut + (size_t)gid * NU * K;
+  // prefetch bookkeeping: problems [p0, p0 + nprob) of this group, this lane's problem slot pl
+  const int p0 = (int)(blockIdx.x * blockDim.x) / T;
+  const int npf = P::nprob(T);
+  const int pl = b - p0;
+  auto prefetch = [&](int kn, int slot) {
+    double* buf = pfb + (size_t)slot * (P::rk(T) + P::rs(T));
+    // K_kn: 16-byte pieces, lane-linear destinations
+    for (int j = 0; j * 64 < npf * P::CK; ++j) {
+      const int c = j * 64 + lane;
+      const int p = c / P::CK, w = c - p * P::CK;
+      const int bb = min(p0 + p, B - 1);
+      const double* src = Kg + ((size_t)bb * K + kn) * P::SK + 2 * w;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + (size_t)j * 128), 16, 0, 0);
+    }
+    // d_kn, x_kn, u_kn: dwords
+    double* sb = buf + P::rk(T);
+    for (int j = 0; j * 64 < npf * 2 * P::SS; ++j) {
+      const int q = j * 64 + lane;
+      const int p = q / (2 * P::SS), r = q - p * (2 * P::SS), item = r >> 1, half = r & 1;
+      const int bb = min(p0 + p, B - 1);
+      const double* src = item < NU ? dg + ((size_t)bb * K + kn) * NU + item
+                        : item < NU + NX ? x + ((size_t)bb * NX + (item - NU)) * N + kn
+                                         : u + ((size_t)bb * NU + (item - NU - NX)) * K + kn;
+      __builtin_amdgcn_global_load_lds((const char*)src + 4 * half,
+                                       (__attribute__((address_space(3))) void*)(sb + (size_t)j * 32), 4, 0, 0);
+    }
+  };
+  if (pf) prefetch(0, 0);
   double xh[NX];
 #pragma unroll
   for (int m = 0; m < NX; ++m) xh[m] = xb[m * N];
   double J = 0.0;
+#ifdef TMPC_ILQR_STAMPS
+  unsigned long long st_[8] = {}, st_prev_ = __builtin_amdgcn_s_memtime();
+#endif
   for (int k = 0; k <= K; ++k) {
+    IL_STAMP(7);
     const bool term = k == K;
     double uh[NU];
+    if (pf && !term) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // knot k's operands have landed in LDS
+      if (k + 1 < K) prefetch(k + 1, (k + 1) & 1);
+    }
+    if (live) {
     if (!init) {
 #pragma unroll
       for (int m = 0; m < NX; ++m) xo[m * N + k] = xh[m];
@@ -503,6 +569,21 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
       if (init) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) uh[i] = ub[i * K + k];
+      } else if (pf) {
+        const double* buf = pfb + (size_t)(k & 1) * (P::rk(T) + P::rs(T));
+        const double* Kk = buf + (size_t)pl * P::SK;
+        const double* sk = buf + P::rk(T) + (size_t)pl * P::SS;   // d_k | x_k | u_k
+        double dx[NX];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) dx[m] = xh[m] - sk[NU + m];
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+          double fb = 0.0;
+#pragma unroll
+          for (int m = 0; m < NX; ++m) fb += Kk[i * NX + m] * dx[m];
+          uh[i] = (sk[NU + NX + i] + al * sk[i]) + fb;
+          uo[i * K + k] = uh[i];
+        }
       } else {
         const double* Kk = Kg + ((size_t)b * K + k) * NU * NX;
         const double* dk = dg + ((size_t)b * K + k) * NU;
@@ -516,6 +597,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
         }
       }
     }
+    IL_STAMP(0);
     // QuadraticCost.value (TrajoptCost.py:49-56): 0.5 dx^T (Q dx) [+ 0.5 u^T (R u)]
     const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
     double vq = 0.0;
@@ -539,6 +621,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
       cost += 0.5 * vr;
     }
     J = J + cost;
+    IL_STAMP(1);
     if (!term && !init) {
       double qd[NJ], qdd[NJ];
       R cq[NJ], sq[NJ], qdr[NJ], ur[NJ], qddr[NJ];
@@ -550,6 +633,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
         joint_cs(M, j, R(xh[j]), cq[j], sq[j]);
       }
       fd_aba<NJ, CHAIN>(M, cq, sq, qdr, ur, qddr);
+      IL_STAMP(2);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) qdd[j] = double(qddr[j]);
 #pragma unroll
@@ -559,8 +643,11 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
         xh[j] = nq;
         xh[NJ + j] = nv;
       }
+      IL_STAMP(3);
     }
+    }   // live
   }
+  if (!live) return;
   if (SOFT) {
     // value_soft_constraints per knot, summed after the cost terms
     const double* xs_ = init ? xb : xo;
@@ -575,6 +662,11 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
       J = J + soft_knot<NJ>(Cs, mu + ko, lam + ko, k == K, z, jac);
     }
   }
+#ifdef TMPC_ILQR_STAMPS
+  if (gid == 0 && !init)
+    printf("ilqr_fwd_stamps K=%d loads+feedback %llu cost %llu aba %llu euler %llu soft %llu\n", K, st_[0], st_[1],
+           st_[2], st_[3] + st_[7], 0ull);
+#endif
   Jt[gid] = J;
 }
 
@@ -704,9 +796,18 @@ struct LaunchIlqr {
                       const double* lam, int B, int N, int T, double dt, int init, const double* alphas,
                       const double* x, const double* u, const double* K, const double* d, const int* active,
                       const int* ok, double* xt, double* ut, double* Jt) {
+    // the prefetching instance when its LDS buffers fit (T >= 2: <= 33 problems per group); init
+    // evaluations (no feedback law) take the plain one.  TMPC_ILQR_NOPF=1: plain only (comparison)
+    const char* npf = getenv("TMPC_ILQR_NOPF");
+    const size_t pf_lds = FwdPf<NJ>::lds_doubles(T) * sizeof(double);
+    const bool pf = !init && pf_lds <= 48 * 1024 && !(npf && npf[0] == '1');
 #define TMPC_FWD(SOFTV, RV)                                                                                          \
-    hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV>), TMPC_GRID(B * T, 64), 0, s, MT::make(M), C, Cs, mu, \
-                       lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
+    if (pf)                                                                                                          \
+      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV, true>), TMPC_GRID(B * T, 64), pf_lds, s,           \
+                         MT::make(M), C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt); \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV, false>), TMPC_GRID(B * T, 64), 0, s, MT::make(M),  \
+                         C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
     if (mu) { if (f32) { TMPC_FWD(true, float) } else { TMPC_FWD(true, double) } }
     else { if (f32) { TMPC_FWD(false, float) } else { TMPC_FWD(false, double) } }
 #undef TMPC_FWD
