@@ -393,7 +393,7 @@ def main():
         "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": {"fp64": "f64", "fp32": "f32", "mixed": "f32 dynamics / f64 Schur-PCG"}[a.precision], "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
-        "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} {a.solver.upper()} "
+        "config": {"workload": f"arm{n}.urdf{' (joint6 fixed)' if n == 6 else ''} N={N} {a.solver.upper()} "
                                f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU"
                                + ("" if a.limits == "none" else f", limits {a.limits}")
                                + (", UrdfCost" if a.cost == "ee" else "")
