@@ -79,6 +79,45 @@ def test_ilqr_batch_matches_oracle(name, N, B):
         _check(r, i, _oracle(m, cost, xs[i], us[i], N))
 
 
+def test_ilqr_nonfinite_trials_rejected(monkeypatch):
+    """Line-search trials whose rollout diverges (inf / NaN states or cost) must be
+    rejected exactly as the oracle rejects them: the acceptance test
+    `ratio >= min and ratio <= max` is false for a NaN ratio and for +-inf outside
+    [min, max], so the search halves alpha and goes on.  The oracle is instrumented
+    to record which problems met such a trial; the test requires that some did (the
+    semantics are exercised, not incidental) and that the GPU's alpha path, exit
+    code, iteration count and final trajectory match on every one of them."""
+    from oracle import ilqr as oilqr
+    from oracle import sqp as osqp
+    m = arm_model("arm3")
+    N, B = 32, 16
+    flagged = set()
+    cur = {"i": -1}
+    fwd = oilqr.forward
+
+    def forward(*a, **k):
+        xn, un = fwd(*a, **k)
+        if not (np.all(np.isfinite(xn)) and np.all(np.isfinite(un))):
+            flagged.add(cur["i"])
+        return xn, un
+
+    monkeypatch.setattr(oilqr, "forward", forward)
+    solver = _solver(m.n, N)
+    xs, us = zip(*[osqp.initial_problem(m, N, 0.1, 500 + i) for i in range(B)])
+    r = solver.iLQR_batch(np.array(xs), np.array(us), N, 0.1, {})
+    cost = osqp.QuadCost(*quad_cost_arrays(m.n))
+    runs = []
+    with np.errstate(over="ignore", invalid="ignore"):
+        for i in range(B):
+            cur["i"] = i
+            runs.append(_oracle(m, cost, xs[i], us[i], N))
+    assert flagged, "no diverging trial in this workload: the test no longer exercises non-finite rejection"
+    for i in sorted(flagged):
+        _check(r, i, runs[i])
+        assert np.all(np.isfinite(r["x"][i])) and np.all(np.isfinite(r["u"][i]))
+        assert np.isfinite(r["trace"]["J"][i, len(runs[i][0][0]["trace"]) - 1])
+
+
 def test_ilqr_soft_limits_match_oracle():
     """iLQR with soft torque limits (augmented Lagrangian outer loop)."""
     from oracle import ilqr as oilqr
