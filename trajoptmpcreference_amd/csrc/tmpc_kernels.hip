@@ -325,9 +325,9 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
 // ======================================================================= block-tridiagonal PCG
 // One workgroup per problem, one lane per row of S (PCG.pcg, PCG.py:66-111).
 //
-// Reductions are DPP butterflies inside the wave (VALU only; ds_bpermute
-// shuffles cost an LDS round trip per step) and one LDS fan-in of the
-// per-wave totals, reduced again by DPP: a fixed tree, so the result is
+// Reductions are DPP / permlane butterflies inside the wave (VALU only;
+// ds_bpermute shuffles cost an LDS round trip per step) and one LDS fan-in of
+// the per-wave totals, reduced again by DPP: a fixed tree, so the result is
 // deterministic and identical for a problem whatever its batch neighbours.
 // dpp_get: see the G-block inverses above
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
@@ -345,12 +345,27 @@ __device__ __forceinline__ double dpp_row_sum(double v) {
   return v;
 }
 
-// wave64 sum, returned uniform (SGPR broadcast)
+// v_permlane16_swap / v_permlane32_swap of a double with itself (gfx950): lane l gets
+// its own value and that of lane l ^ 16 (resp. l ^ 32), in a fixed (lower, upper) order
+__device__ __forceinline__ double perm_pair_sum16(double v) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double perm_pair_sum32(double v) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+
+// wave64 sum in every lane: row sums R_q by DPP, then (R0 + R1) + (R2 + R3) by the
+// two permlane swaps -- the tree of the row_bcast:15 / row_bcast:31 reduction, so
+// bitwise the same total, without the readlane round trip through SGPRs.  (Both
+// reductions on the fp64 matrix core -- two v_mfma_f64_16x16x4f64 with B = 1 per
+// sum, 3 VALU adds instead of 18 -- measured 12 % slower per PCG-SS iteration:
+// the MFMA latency sits on the barrier-to-barrier critical path.)
 __device__ __forceinline__ double wave_sum(double v) {
-  v = dpp_row_sum(v);
-  v += dpp_get<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
-  v += dpp_get<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
-  return readlane_f64(v, 63);
+  return perm_pair_sum32(perm_pair_sum16(dpp_row_sum(v)));
 }
 
 // Lane geometry of the one-workgroup-per-problem kernels: RPL rows of S per
@@ -597,7 +612,9 @@ __device__ __forceinline__ void pcg_block_dot(const RT (&R)[RPL], const double* 
 // 16-slot area (slots of absent waves hold 0); after the next barrier
 // red_total reads all slots and reduces them by DPP.  A fixed tree: the result
 // is deterministic and independent of the problem's batch neighbours.  Split
-// this way, a reduction rides on a barrier the iteration needs anyway.
+// this way, a reduction rides on a barrier the iteration needs anyway.  (Reading
+// the slots as broadcast ds_read_b128 and adding them in the same tree measured
+// slower: the compiler splits the reads into two dependent LDS round trips.)
 __device__ __forceinline__ void red_put(double v, double* red) {
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -643,9 +660,10 @@ __device__ __forceinline__ void pcg_off(const RT (&R)[RPL], const double* __rest
 //                       partial nu' = w.t  (= r^T P_kk t = r.z, P_kk symmetric)
 //   B4  SS: t, nu'      z = P_kk t_k   (the symmetric-stair P^-1 r, PCG.py:181-212)
 //   then                beta = nu'/nu, p = z + p beta to LDS -> B1
-// The element updates are the reference's, rounded as NumPy rounds them
-// (r - (Ap alpha), x + (p alpha), z + (p beta): no FMA contraction); only the
-// summation order of the dot and block products differs.  x = the lane's
+// The element updates are the reference's (r - Ap alpha, x + p alpha, z + p beta);
+// hipcc contracts each into one fused multiply-add (__dmul_rn is a plain product
+// here), one rounding where NumPy has two, and the summation order of the dot and
+// block products differs -- iteration counts stay exact on every fixture.  x = the lane's
 // entries of the solution.
 template <int NX, int RPL, int PRE, class RT>
 __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RPL>& ln, int N,
@@ -776,12 +794,13 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
       for (int j = 0; j < NX; ++j) {
         const double rj = __dsub_rn(ro[j], __dmul_rn(ap[j], alpha));
 #pragma unroll
-        for (int m = 0; m < RPL; ++m) {
-          acc[j % NC][m] += R[m].pr[j] * rj;
-          if (j == ln.r(m)) rv[m] = rj;
-        }
+        for (int m = 0; m < RPL; ++m) acc[j % NC][m] += R[m].pr[j] * rj;
         PCG_LOAD_FENCE(RT, j, acc[0])
       }
+      // own rows from the registers: the same operands as the LDS copies
+      // (ro[r(m)] = rv[m], ap[r(m)] = av[m]), the same expression, the same value
+#pragma unroll
+      for (int m = 0; m < RPL; ++m) rv[m] = __dsub_rn(rv[m], __dmul_rn(av[m], alpha));
 #pragma unroll
       for (int m = 0; m < RPL; ++m) w[m] = NC == 2 ? acc[0][m] + acc[NC - 1][m] : acc[0][m];
     } else {
@@ -1677,7 +1696,11 @@ int pcg_set_max_lds() {
 #define SETA(V)                                                                                                    \
   err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 1, 768>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes); \
   err |= (int)hipFuncSetAttribute((const void*)k_pcg<V, 2, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#ifdef TMPC_DEV_NJ
+  SETA(2 * TMPC_DEV_NJ)
+#else
   SETA(2) SETA(4) SETA(6) SETA(8) SETA(10) SETA(12) SETA(14) SETA(16)
+#endif
 #undef SETA
 #define SETQ2(V, P, MD)                                                                                  \
   err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1, 768, P, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
@@ -1688,7 +1711,11 @@ int pcg_set_max_lds() {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 #define SETQ1(V, P) SETQ2(V, P, QP_MODE_PCG) SETQ2(V, P, QP_MODE_SCHUR) SETQ2(V, P, QP_MODE_DXU)
 #define SETQ(V) SETQ1(V, false) SETQ1(V, true)
+#ifdef TMPC_DEV_NJ
+  SETQ(TMPC_DEV_NJ)
+#else
   SETQ(1) SETQ(2) SETQ(3) SETQ(4) SETQ(5) SETQ(6) SETQ(7)
+#endif
 #undef SETQ
 #undef SETQ1
 #undef SETQ2
@@ -1718,7 +1745,11 @@ int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* S
   switch (nx) {
 #define CASE_NX(V) \
   case V: launch_pcg_nx<V>(s, B, N, precond, Sd, Sl, Su, gam, guess, tol, max_iter, lam, iters, tnu, tres, Pd); return 0;
+#ifdef TMPC_DEV_NJ
+    CASE_NX(2 * TMPC_DEV_NJ)
+#else
     CASE_NX(2) CASE_NX(4) CASE_NX(6) CASE_NX(8) CASE_NX(10) CASE_NX(12) CASE_NX(14) CASE_NX(16)
+#endif
 #undef CASE_NX
     default: return -2;
   }
@@ -1918,6 +1949,13 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
 }
 
 // dispatch tables over the joint count and the chain specialisation
+#ifdef TMPC_DEV_NJ
+#define TMPC_DISPATCH_NJ(nj, chain, CALL)                                          \
+  if (nj != TMPC_DEV_NJ) return -2;                                                 \
+  if (chain) Launch<TMPC_DEV_NJ, true, ModelRef>::CALL;                             \
+  else Launch<TMPC_DEV_NJ, false, ModelRef>::CALL;                                  \
+  return 0;
+#else
 #define TMPC_DISPATCH_NJ(nj, chain, CALL)                                                              \
   switch (mid) {                                                                                       \
     TMPC_STATIC_MODEL_CASES(Launch, CALL)                                                            \
@@ -1934,7 +1972,15 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
     default: return -2;                                                                                \
   }                                                                                                    \
   return 0;
+#endif
 
+#ifdef TMPC_DEV_NJ
+// experiment builds (make dev): one joint count only, a fraction of the compile time
+#define TMPC_DISPATCH_NJ2(nj, CALL)                      \
+  if (nj != TMPC_DEV_NJ) return -2;                      \
+  LaunchNJ<TMPC_DEV_NJ>::CALL;                           \
+  return 0;
+#else
 #define TMPC_DISPATCH_NJ2(nj, CALL)          \
   switch (nj) {                              \
     case 1: LaunchNJ<1>::CALL; break;        \
@@ -1947,6 +1993,7 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
     default: return -2;                      \
   }                                                                                \
   return 0;
+#endif
 
 int launch_qp_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N,
                    const double* x, const int* need, double* minv) {
