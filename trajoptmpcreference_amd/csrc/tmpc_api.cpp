@@ -480,6 +480,35 @@ static int hard_ls(tmpc_ctx* ctx, int nj, const HardArgs& base, int B, int N, in
 }
 
 // keep_warm: the PCG warm-start buffer already holds this batch's starting lambdas (MPC loop)
+// Lock-step batch loop with a lag-1 termination test.  Each batch iteration writes its two flags
+// (some problem continues its inner loop / some problem restarted an outer pass) into its own half
+// of active_count[2][2]; the host copies them to pinned memory and tests iteration `it` only after
+// iteration `it + 1` has been enqueued, so the GPU never idles while the host decides.  Every kernel
+// masks itself with the per-problem state, so the one iteration enqueued after the batch finished
+// is a no-op for every problem (need_grad / active / outer_active are all 0).
+template <class Body>
+static int lockstep_loop(tmpc_ctx* ctx, long cap, int* active_count, Body body) {
+  hipEvent_t ev[2] = {get_event(ctx), get_event(ctx)};
+  if (!ev[0] || !ev[1]) return fail(ctx, "hipEventCreate failed");
+  int rc = 0;
+  for (long it = 0; it < cap; ++it) {
+    const int p = (int)(it & 1);
+    int* ac = active_count + 2 * p;
+    HIP_OK(hipMemsetAsync(ac, 0, 2 * sizeof(int), ctx->stream));
+    if ((rc = body(ac))) break;
+    HIP_OK(hipMemcpyAsync(ctx->h_count + 2 * p, ac, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipEventRecord(ev[p], ctx->stream));
+    if (it > 0) {
+      HIP_OK(hipEventSynchronize(ev[p ^ 1]));
+      const int* h = ctx->h_count + 2 * (p ^ 1);
+      if (h[0] == 0 && h[1] == 0) break;
+    }
+  }
+  ctx->event_pool.push_back(ev[0]);
+  ctx->event_pool.push_back(ev[1]);
+  return rc;
+}
+
 static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
                       TraceDev* tr_out, bool keep_warm = false) {
   int rc = check_ready(ctx, B, N);
@@ -502,7 +531,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   if ((rc = alloc_trace(ctx, B, W, tr))) return rc;
   BUF(double, alphas, T + 1);
   BUF(double, terms, (size_t)B * T * N * 4);   // [B][T][N][cost, violation, D, soft value]
-  BUF(int, active_count, 2);   // [0] some problem in its inner loop, [1] some problem restarted a pass
+  BUF(int, active_count, 4);   // [2][2] (lag-1 double buffer): [0] some problem in its inner loop, [1] some problem restarted a pass
   BUF(unsigned long long, counters, 4);
   BUF(unsigned long long, prob_counters, (size_t)B * 3);   // per-problem tallies of k_ls_decide
   BUF(int, outer_active, B);
@@ -554,19 +583,19 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
   launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
   // initial J, c, merit (:541-548) of the problems in `mask` (st.active: all, act_init: restarted passes)
-  auto init_merit = [&](int* mask) -> int {
+  auto init_merit = [&](int* mask, int* ac) -> int {
     ProbState sti = st;
     sti.active = mask;
     LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1,
                               dt, alphas + T, d_x, d_u, w.xs, nullptr, nullptr, mask, terms));
     if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, mask));
     launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
-                     sti, nullptr, tr, active_count, nullptr, hterms);
+                     sti, nullptr, tr, ac, nullptr, hterms);
     HIP_OK(hipGetLastError());
     return 0;
   };
   // one SQP iteration (:550-757) of every problem in its inner loop; flags[0] = some problem continues
-  auto sqp_iteration = [&]() -> int {
+  auto sqp_iteration = [&](int* ac) -> int {
     int rc2 = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false);
     if (rc2) return rc2;
     {
@@ -577,21 +606,17 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     }
     Timed t(ctx, "ls_decide");
     launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
-                     st, w.iters, tr, active_count, prob_counters, hterms);
+                     st, w.iters, tr, ac, prob_counters, hterms);
     HIP_OK(hipGetLastError());
     return 0;
   };
-  HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
-  if ((rc = init_merit(st.active))) return rc;
+  HIP_OK(hipMemsetAsync(active_count, 0, 4 * sizeof(int), ctx->stream));
+  if ((rc = init_merit(st.active, active_count))) return rc;
   if (!soft) {
-    // unconstrained: one inner loop; check_and_update_soft_constraints then exits 1 (:531-757)
-    for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
-      HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-      if ((rc = sqp_iteration())) return rc;
-      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-      HIP_OK(hipStreamSynchronize(ctx->stream));
-      if (ctx->h_count[0] == 0) break;
-    }
+    // unconstrained: one inner loop (at most max_iter iterations, + 1 for the lag of the exit test);
+    // check_and_update_soft_constraints then exits 1 (:531-757)
+    rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, [&](int* ac) { return sqp_iteration(ac); });
+    if (rc) return rc;
     launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints, o.max_iter_softConstraints,
                       d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft, active_count);
     HIP_OK(hipGetLastError());
@@ -604,23 +629,22 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     // sequence of operations is the lock-step one, so its results are identical.
     BUF(int, act_init, B);
     HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
-    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 2;
-    for (long it = 0; it < cap; ++it) {
-      HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
-      if ((rc = sqp_iteration())) return rc;
+    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
+    rc = lockstep_loop(ctx, cap, active_count, [&](int* ac) -> int {
+      int r = sqp_iteration(ac);
+      if (r) return r;
       launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
                         o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
-                        active_count + 1, &st, act_init, o.rho_init_SQP_DDP);
+                        ac + 1, &st, act_init, o.rho_init_SQP_DDP);
       HIP_OK(hipGetLastError());
-      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-      HIP_OK(hipStreamSynchronize(ctx->stream));
-      if (ctx->h_count[0] == 0 && ctx->h_count[1] == 0) break;
-      if (ctx->h_count[1]) {   // restarted passes: initial merit, then into the inner loop
-        if ((rc = init_merit(act_init))) return rc;
-        launch_activate(ctx->stream, B, act_init, st.active);
-        HIP_OK(hipGetLastError());
-      }
-    }
+      // restarted passes (act_init, set by k_soft_outer): initial merit, then into the inner loop;
+      // masked by act_init, so a no-op when no pass restarted
+      if ((r = init_merit(act_init, ac))) return r;
+      launch_activate(ctx->stream, B, act_init, st.active);
+      HIP_OK(hipGetLastError());
+      return 0;
+    });
+    if (rc) return rc;
   }
   launch_sum_counters(ctx->stream, B, prob_counters, counters);
   unsigned long long hc[4] = {0, 0, 0, 0};
@@ -663,7 +687,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   BUF(double, il_xt, (size_t)B * T * nx * N);
   BUF(double, il_ut, (size_t)B * T * nj * K);
   BUF(double, il_J, (size_t)B * T);
-  BUF(int, active_count, 2);
+  BUF(int, active_count, 4);   // [2][2], as sqp_device
   BUF(int, outer_active, B);
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
@@ -688,18 +712,18 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
   launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
   // J at the current trajectory of the problems in `mask` (st.active: all, act_init: restarted passes)
-  auto init_cost = [&](int* mask) -> int {
+  auto init_cost = [&](int* mask, int* ac) -> int {
     ProbState sti = st;
     sti.active = mask;
     LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
                                   B, N, 1, dt, 1, alphas, d_x, d_u, il_K, il_d, mask, il_ok, il_xt, il_ut, il_J));
     launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, sti,
-                       tr, active_count, nullptr);
+                       tr, ac, nullptr);
     HIP_OK(hipGetLastError());
     return 0;
   };
   // one iLQR iteration of every problem in its inner loop; flags[0] = some problem continues
-  auto ilqr_iteration = [&]() -> int {
+  auto ilqr_iteration = [&](int* ac) -> int {
     {
       Timed t(ctx, "qp_fd");
       LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs,
@@ -728,20 +752,15 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     }
     Timed t(ctx, "ilqr_decide");
     launch_ilqr_decide(ctx->stream, B, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st, tr,
-                       active_count, counters);
+                       ac, counters);
     HIP_OK(hipGetLastError());
     return 0;
   };
-  HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
-  if ((rc = init_cost(st.active))) return rc;
+  HIP_OK(hipMemsetAsync(active_count, 0, 4 * sizeof(int), ctx->stream));
+  if ((rc = init_cost(st.active, active_count))) return rc;
   if (!soft) {
-    for (int it = 0; it < o.max_iter_SQP_DDP; ++it) {
-      HIP_OK(hipMemsetAsync(active_count, 0, sizeof(int), ctx->stream));
-      if ((rc = ilqr_iteration())) return rc;
-      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-      HIP_OK(hipStreamSynchronize(ctx->stream));
-      if (ctx->h_count[0] == 0) break;
-    }
+    rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, [&](int* ac) { return ilqr_iteration(ac); });
+    if (rc) return rc;
     launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
                       o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
                       active_count);
@@ -751,23 +770,20 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     // as its own inner loop exits
     BUF(int, act_init, B);
     HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
-    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 2;
-    for (long it = 0; it < cap; ++it) {
-      HIP_OK(hipMemsetAsync(active_count, 0, 2 * sizeof(int), ctx->stream));
-      if ((rc = ilqr_iteration())) return rc;
+    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
+    rc = lockstep_loop(ctx, cap, active_count, [&](int* ac) -> int {
+      int r = ilqr_iteration(ac);
+      if (r) return r;
       launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
                         o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
-                        active_count + 1, &st, act_init, o.rho_init_SQP_DDP);
+                        ac + 1, &st, act_init, o.rho_init_SQP_DDP);
       HIP_OK(hipGetLastError());
-      HIP_OK(hipMemcpyAsync(ctx->h_count, active_count, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-      HIP_OK(hipStreamSynchronize(ctx->stream));
-      if (ctx->h_count[0] == 0 && ctx->h_count[1] == 0) break;
-      if (ctx->h_count[1]) {
-        if ((rc = init_cost(act_init))) return rc;
-        launch_activate(ctx->stream, B, act_init, st.active);
-        HIP_OK(hipGetLastError());
-      }
-    }
+      if ((r = init_cost(act_init, ac))) return r;   // masked by act_init: a no-op when no pass restarted
+      launch_activate(ctx->stream, B, act_init, st.active);
+      HIP_OK(hipGetLastError());
+      return 0;
+    });
+    if (rc) return rc;
   }
   unsigned long long hc[4] = {0, 0, 0, 0};
   HIP_OK(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
@@ -803,7 +819,7 @@ int tmpc_create(int device, tmpc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&ctx->dmodel, sizeof(ModelDev)) != hipSuccess || hipMalloc(&ctx->dcost, sizeof(CostDev)) != hipSuccess ||
       hipMalloc(&ctx->dlim, sizeof(ConstrDev)) != hipSuccess || hipMemset(ctx->dlim, 0, sizeof(ConstrDev)) != hipSuccess ||
-      hipHostMalloc(&ctx->h_count, 4 * sizeof(int)) != hipSuccess) {
+      hipHostMalloc(&ctx->h_count, 8 * sizeof(int)) != hipSuccess) {
     delete ctx;
     return -4;
   }
