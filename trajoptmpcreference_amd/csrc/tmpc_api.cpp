@@ -715,8 +715,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   auto init_cost = [&](int* mask, int* ac) -> int {
     ProbState sti = st;
     sti.active = mask;
-    LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
-                                  B, N, 1, dt, 1, alphas, d_x, d_u, il_K, il_d, mask, il_ok, il_xt, il_ut, il_J));
+    LAUNCH_OK(launch_ilqr_init_cost(ctx->stream, nj, ctx->dcost, ctx->dlim, smu, slam, B, N, d_x, d_u, mask, il_J));
     launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, sti,
                        tr, ac, nullptr);
     HIP_OK(hipGetLastError());

@@ -455,6 +455,83 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   }
 }
 
+// QuadraticCost.value of one knot (TrajoptCost.py:49-56): 0.5 dx^T (Q dx) [+ 0.5 u^T (R u)], one
+// expression shared by the rollouts and the INIT evaluation so both round alike
+template <int NJ>
+__device__ __forceinline__ double knot_quad_cost(const CostDev* __restrict__ C, int k, int N, const double* xh,
+                                                 const double* uh, bool term) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
+  double vq = 0.0;
+#pragma unroll
+  for (int r = 0; r < NX; ++r) {
+    double qd = 0.0;
+#pragma unroll
+    for (int c = 0; c < NX; ++c) qd += Qk[r * NX + c] * (xh[c] - C->xg[c]);
+    vq += (xh[r] - C->xg[r]) * qd;
+  }
+  double cost = 0.5 * vq;
+  if (!term) {
+    double vr = 0.0;
+#pragma unroll
+    for (int r = 0; r < NU; ++r) {
+      double ru = 0.0;
+#pragma unroll
+      for (int c = 0; c < NU; ++c) ru += C->R[r * NU + c] * uh[c];
+      vr += uh[r] * ru;
+    }
+    cost += 0.5 * vr;
+  }
+  return cost;
+}
+
+// J at the current trajectory (the iLQR drivers' INIT evaluation, oracle/ilqr.py:130) of the
+// problems in `mask`: one 64-lane workgroup per problem, lanes over knots for the per-knot cost
+// and soft value (sc[k], sc[N + k]), then lane 0 sums them in knot order, the cost terms first --
+// totalCost's order (:296-310) and the serial sums of k_ilqr_forward operand for operand.  Run
+// under the act_init mask every outer-loop iteration, so it must be cheap when few problems
+// restart (the serial INIT rollout lane took 0.19 ms per launch on average).
+template <int NJ, bool SOFT>
+__global__ void __launch_bounds__(64) k_ilqr_init_cost(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
+                                                       const double* __restrict__ mu, const double* __restrict__ lam,
+                                                       int N, const double* __restrict__ x,
+                                                       const double* __restrict__ u, const int* __restrict__ mask,
+                                                       double* __restrict__ Jt) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int b = blockIdx.x;
+  if (!mask[b]) return;
+  extern __shared__ double sc[];   // [2][N]
+  const int K = N - 1;
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NU * K;
+  for (int k = threadIdx.x; k < N; k += 64) {
+    const bool term = k == K;
+    double xh[NX], uh[NU];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) xh[m] = xb[m * N + k];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) uh[i] = term ? 0.0 : ub[i * K + k];
+    sc[k] = knot_quad_cost<NJ>(C, k, N, xh, uh, term);
+    if (SOFT) {
+      double z[3 * NJ], jac[3 * NJ];
+#pragma unroll
+      for (int m = 0; m < NX; ++m) z[m] = xh[m];
+#pragma unroll
+      for (int m = 0; m < NU; ++m) z[NX + m] = uh[m];
+      const size_t ko = ((size_t)b * N + k) * 6 * NJ;
+      sc[N + k] = soft_knot<NJ>(Cs, mu + ko, lam + ko, term, z, jac);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double J = 0.0;
+    for (int k = 0; k < N; ++k) J = J + sc[k];
+    if (SOFT)
+      for (int k = 0; k < N; ++k) J = J + sc[N + k];
+    Jt[b] = J;
+  }
+}
+
 // ======================================================================= forward sweep (closed-loop rollouts)
 // lane = (b, trial t).  INIT: J at the current trajectory (no rollout).  Trial
 // trajectories are kept ([B][T][nx][N], [B][T][nu][N-1]) so the decision kernel
@@ -598,29 +675,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
       }
     }
     IL_STAMP(0);
-    // QuadraticCost.value (TrajoptCost.py:49-56): 0.5 dx^T (Q dx) [+ 0.5 u^T (R u)]
-    const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
-    double vq = 0.0;
-#pragma unroll
-    for (int r = 0; r < NX; ++r) {
-      double qd = 0.0;
-#pragma unroll
-      for (int c = 0; c < NX; ++c) qd += Qk[r * NX + c] * (xh[c] - C->xg[c]);
-      vq += (xh[r] - C->xg[r]) * qd;
-    }
-    double cost = 0.5 * vq;
-    if (!term) {
-      double vr = 0.0;
-#pragma unroll
-      for (int r = 0; r < NU; ++r) {
-        double ru = 0.0;
-#pragma unroll
-        for (int c = 0; c < NU; ++c) ru += C->R[r * NU + c] * uh[c];
-        vr += uh[r] * ru;
-      }
-      cost += 0.5 * vr;
-    }
-    J = J + cost;
+    J = J + knot_quad_cost<NJ>(C, k, N, xh, uh, term);
     IL_STAMP(1);
     if (!term && !init) {
       double qd[NJ], qdd[NJ];
@@ -845,6 +900,26 @@ int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, co
                         const double* d, const int* active, const int* ok, double* xt, double* ut, double* Jt) {
   TMPC_DISPATCH_ILQR(nj, chain, forward(f32, s, M, C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok,
                                         xt, ut, Jt))
+}
+
+int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, const double* mu,
+                          const double* lam, int B, int N, const double* x, const double* u, const int* mask,
+                          double* Jt) {
+  const size_t lds = (size_t)2 * N * sizeof(double);
+  if (lds > 64 * 1024) return -1;
+#define TMPC_INIT_COST(V)                                                                                      \
+  case V:                                                                                                      \
+    if (mu)                                                                                                    \
+      hipLaunchKernelGGL((k_ilqr_init_cost<V, true>), dim3(B), dim3(64), lds, s, C, Cs, mu, lam, N, x, u, mask, Jt); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_ilqr_init_cost<V, false>), dim3(B), dim3(64), lds, s, C, Cs, mu, lam, N, x, u, mask, Jt); \
+    return 0;
+  switch (nj) {
+    TMPC_INIT_COST(1) TMPC_INIT_COST(2) TMPC_INIT_COST(3) TMPC_INIT_COST(4) TMPC_INIT_COST(5) TMPC_INIT_COST(6)
+    TMPC_INIT_COST(7)
+    default: return -2;
+  }
+#undef TMPC_INIT_COST
 }
 
 void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,

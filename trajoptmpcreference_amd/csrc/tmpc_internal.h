@@ -132,6 +132,9 @@ int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, co
                         const double* mu, const double* lam, int B, int N, int T, double dt, int init,
                         const double* alphas, const double* x, const double* u, const double* K, const double* d,
                         const int* active, const int* ok, double* xt, double* ut, double* Jt);
+int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, const double* mu,
+                          const double* lam, int B, int N, const double* x, const double* u, const int* mask,
+                          double* Jt);
 void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
