@@ -694,7 +694,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   BUF(unsigned long long, counters, 4);
   HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
   const bool soft = ctx->hlim.any != 0;
-  double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
+  double *smu = nullptr, *slam = nullptr, *sphi = nullptr, *il_jac = nullptr;
   if (soft) {
     if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
     if (ctx->soft_B != B || ctx->soft_N != N) {
@@ -703,6 +703,8 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
       ctx->soft_B = B;
       ctx->soft_N = N;
     }
+    BUF(double, il_jac_buf, (size_t)B * N * 3 * nj);   // soft-limit jacobians of every knot (Riccati sweep)
+    il_jac = il_jac_buf;
   }
   HIP_OK(hipMemcpyAsync(alphas, al.data(), al.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   // iLQR iterates are rollouts: start from the rollout of u from x[:, 0]
@@ -741,7 +743,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     {
       Timed t(ctx, "ilqr_backward");
       LAUNCH_OK(launch_ilqr_backward(ric32(ctx), ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, d_x, d_u, st.rho, st.active,
-                                     w.A, w.Bm, smu, slam, il_K, il_d, il_dV, il_ok));
+                                     w.A, w.Bm, smu, slam, il_jac, il_K, il_d, il_dV, il_ok));
     }
     {
       Timed t(ctx, "ilqr_forward");

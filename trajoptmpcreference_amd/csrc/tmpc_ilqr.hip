@@ -76,10 +76,11 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
                                                       const double* __restrict__ u, const double* __restrict__ rho_in,
                                                       const int* __restrict__ active, const double* __restrict__ Aall,
                                                       const double* __restrict__ Ball, const double* __restrict__ mu,
-                                                      const double* __restrict__ lam, double* __restrict__ Kout,
+                                                      const double* __restrict__ lam,
+                                                      const double* __restrict__ jsoft, double* __restrict__ Kout,
                                                       double* __restrict__ dout, double* __restrict__ dV,
                                                       int* __restrict__ ok) {
-  constexpr int NX = 2 * NJ, NU = NJ, NC = NX + 1, MC = 6 * NJ;
+  constexpr int NX = 2 * NJ, NU = NJ, NC = NX + 1;
   constexpr int NA = (NX * NX + 63) / 64, NB = (NX * NU + 63) / 64;   // prefetch slots per lane
   const int b = blockIdx.x;
   if (!active[b]) return;
@@ -89,7 +90,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   const R rho = R(rho_in[b]);
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NU * K;
-  const bool soft = Cs->any != 0;
+  const bool soft = jsoft != nullptr;   // soft limits: their jacobians precomputed (k_ilqr_soft_jac)
   const int qf_start = C->QF_start;
 
   // the cost blocks once (QuadraticCost, TrajoptCost.py:71-83)
@@ -106,8 +107,12 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     if (t < NX + NU) return k < K ? ub[(t - NX) * K + k] : 0.0;
     return 0.0;
   };
-  // prefetched A_k / B_k entries of this lane
-  double pa[NA], pb[NB];
+  // prefetched A_k / B_k entries of this lane, and (soft limits) entry t of the knot's soft-limit
+  // jacobian, precomputed for every knot by k_ilqr_soft_jac ([B][N][3 NJ])
+  double pa[NA], pb[NB], pj = 0.0, pjn = 0.0;
+  auto load_jac = [&](int k) -> double {
+    return (soft && t < 3 * NJ) ? jsoft[((size_t)b * N + k) * 3 * NJ + t] : 0.0;
+  };
   auto load_ab = [&](int k) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -134,18 +139,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   auto stage_l = [&](int k, int zs) {
     const bool term = k == K;
     const double* zk = L.z[zs];
-    if (soft && t == 0) {
-      double z[3 * NJ], jac[3 * NJ];
-#pragma unroll
-      for (int m = 0; m < NX; ++m) z[m] = zk[m];
-#pragma unroll
-      for (int m = 0; m < NU; ++m) z[NX + m] = term ? 0.0 : zk[NX + m];
-      const size_t ko = ((size_t)b * N + k) * MC;
-      soft_knot<NJ>(Cs, mu + ko, lam + ko, term, z, jac);
-#pragma unroll
-      for (int m = 0; m < 3 * NJ; ++m) L.jac[m] = jac[m];
-    }
-    if (!soft && t < 3 * NJ) L.jac[t] = 0.0;
+    if (t < 3 * NJ) L.jac[t] = R(pj);   // 0 without soft limits
     wave_lds_sync();
     const R* Qk = use_qf(k) ? L.QF : L.Q;
     if (t < NX) {
@@ -169,7 +163,9 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   // terminal value function: V_x = l_x(N-1), V_xx = l_xx(N-1); A_{K-1}, B_{K-1} and z_{K-1} in flight
   {
     const double zt = load_z(K);
+    pj = load_jac(K);
     load_ab(K - 1);
+    pjn = load_jac(K - 1);
     const double zn = load_z(K - 1);
     if (t < NX + NU) L.z[0][t] = zt;
     wave_lds_sync();
@@ -183,6 +179,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     }
     store_ab(0);
     if (t < NX + NU) L.z[1][t] = zn;
+    pj = pjn;
     wave_lds_sync();
   }
 
@@ -198,6 +195,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     double zn = 0.0;
     if (k > 0) {
       load_ab(k - 1);
+      pjn = load_jac(k - 1);
       zn = load_z(k - 1);
     }
     stage_l(k, 1 - cur);
@@ -438,6 +436,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     if (k > 0) {
       store_ab(1 - cur);
       if (t < NX + NU) L.z[cur][t] = zn;
+      pj = pjn;
     }
     wave_lds_sync();
     IL_STAMP(6);
@@ -725,6 +724,70 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
   Jt[gid] = J;
 }
 
+// The soft-limit values of the trial trajectories (value_soft_constraints, summed after the cost
+// terms as totalCost does, :296-310): one 64-lane workgroup per (problem, trial), lanes over knots
+// for soft_knot (z from the trial trajectory, mu / lambda of the knot), then lane 0 adds them to
+// the rollout's cost sum in knot order -- the serial tail of k_ilqr_forward operand for operand,
+// which paid one dependent round trip to HBM per knot inside a single lane (0.4 ms of config 3's
+// 1.0 ms forward launches).
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ilqr_soft_add(const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
+                                                      const double* __restrict__ lam, int B, int N, int T,
+                                                      const double* __restrict__ xt, const double* __restrict__ ut,
+                                                      const int* __restrict__ active, const int* __restrict__ ok,
+                                                      double* __restrict__ Jt) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int gid = blockIdx.x, b = gid / T;
+  if (!active[b] || !ok[b]) return;
+  extern __shared__ double sv[];   // [N]
+  const int K = N - 1;
+  const double* xo = xt + (size_t)gid * NX * N;
+  const double* uo = ut + (size_t)gid * NU * K;
+  for (int k = threadIdx.x; k < N; k += 64) {
+    double z[3 * NJ], jac[3 * NJ];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) z[m] = xo[m * N + k];
+#pragma unroll
+    for (int m = 0; m < NU; ++m) z[NX + m] = k < K ? uo[m * K + k] : 0.0;
+    const size_t ko = ((size_t)b * N + k) * 6 * NJ;
+    sv[k] = soft_knot<NJ>(Cs, mu + ko, lam + ko, k == K, z, jac);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double J = Jt[gid];
+    for (int k = 0; k < N; ++k) J = J + sv[k];
+    Jt[gid] = J;
+  }
+}
+
+// The soft-limit jacobians of every knot of the current trajectory (BoxConstraint.jacobian,
+// TrajoptConstraint.py:53-128, through soft_knot) for the Riccati sweep: lane = (problem, knot),
+// [B][N][3 NJ].  The sweep used to evaluate them in lane 0 at each knot, one dependent round trip
+// to mu / lambda in HBM per knot on its critical path; it now prefetches row k - 1 with A_{k-1}.
+template <int NJ>
+__global__ void __launch_bounds__(256) k_ilqr_soft_jac(const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
+                                                       const double* __restrict__ lam, int B, int N,
+                                                       const double* __restrict__ x, const double* __restrict__ u,
+                                                       const int* __restrict__ active, double* __restrict__ jout) {
+  constexpr int NX = 2 * NJ, NU = NJ;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= B * N) return;
+  const int b = gid / N, k = gid - b * N;
+  if (!active[b]) return;
+  const int K = N - 1;
+  const double* xb = x + (size_t)b * NX * N;
+  const double* ub = u + (size_t)b * NU * K;
+  double z[3 * NJ], jac[3 * NJ];
+#pragma unroll
+  for (int m = 0; m < NX; ++m) z[m] = xb[m * N + k];
+#pragma unroll
+  for (int m = 0; m < NU; ++m) z[NX + m] = k < K ? ub[m * K + k] : 0.0;
+  const size_t ko = ((size_t)b * N + k) * 6 * NJ;
+  soft_knot<NJ>(Cs, mu + ko, lam + ko, k == K, z, jac);
+#pragma unroll
+  for (int m = 0; m < 3 * NJ; ++m) jout[(size_t)gid * 3 * NJ + m] = jac[m];
+}
+
 // ======================================================================= decision + state machine
 // One 64-lane workgroup per problem.  Acceptance ratio (J - J^) / (-alpha (dV1 + alpha dV2)) in
 // [exp_red_min, exp_red_max] in the reference's alpha order (oracle/ilqr.py), rho schedule and exit
@@ -833,19 +896,26 @@ template <int NJ, bool CHAIN, class MT>
 struct LaunchIlqr {
   static void backward(bool f32, hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                        const double* u, const double* rho, const int* active, const double* A, const double* Bm,
-                       const double* mu, const double* lam, double* K, double* d, double* dV, int* ok) {
+                       const double* mu, const double* lam, double* jscratch, double* K, double* d, double* dV,
+                       int* ok) {
     // fp64: the matrix-core products (MF) unless TMPC_ILQR_VALU=1 (the VALU loops, for comparison)
     const char* v = getenv("TMPC_ILQR_VALU");
     const bool mf = !(v && v[0] == '1');
+    // soft limits: every knot's jacobian first, in parallel ([B][N][3 NJ] in jscratch)
+    const double* js = nullptr;
+    if (mu) {
+      hipLaunchKernelGGL((k_ilqr_soft_jac<NJ>), TMPC_GRID(B * N, 256), 0, s, Cs, mu, lam, B, N, x, u, active, jscratch);
+      js = jscratch;
+    }
     if (f32)
       hipLaunchKernelGGL((k_ilqr_backward<NJ, float, false>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
-                         Bm, mu, lam, K, d, dV, ok);
+                         Bm, mu, lam, js, K, d, dV, ok);
     else if (mf)
       hipLaunchKernelGGL((k_ilqr_backward<NJ, double, true>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
-                         Bm, mu, lam, K, d, dV, ok);
+                         Bm, mu, lam, js, K, d, dV, ok);
     else
       hipLaunchKernelGGL((k_ilqr_backward<NJ, double, false>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
-                         Bm, mu, lam, K, d, dV, ok);
+                         Bm, mu, lam, js, K, d, dV, ok);
   }
   static void forward(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
                       const double* lam, int B, int N, int T, double dt, int init, const double* alphas,
@@ -863,9 +933,13 @@ struct LaunchIlqr {
     else                                                                                                             \
       hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV, false>), TMPC_GRID(B * T, 64), 0, s, MT::make(M),  \
                          C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
-    if (mu) { if (f32) { TMPC_FWD(true, float) } else { TMPC_FWD(true, double) } }
+    // soft limits: the rollouts sum the cost terms, k_ilqr_soft_add the soft values (INIT: in the kernel)
+    if (mu && init) { if (f32) { TMPC_FWD(true, float) } else { TMPC_FWD(true, double) } }
     else { if (f32) { TMPC_FWD(false, float) } else { TMPC_FWD(false, double) } }
 #undef TMPC_FWD
+    if (mu && !init)
+      hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B * T), dim3(64), N * sizeof(double), s, Cs, mu, lam, B, N, T, xt,
+                         ut, active, ok, Jt);
   }
 };
 
@@ -888,10 +962,10 @@ struct LaunchIlqr {
 
 int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N,
                          const double* x, const double* u, const double* rho, const int* active, const double* A,
-                         const double* Bm, const double* mu, const double* lam, double* K, double* d, double* dV,
-                         int* ok) {
+                         const double* Bm, const double* mu, const double* lam, double* jscratch, double* K,
+                         double* d, double* dV, int* ok) {
   const int mid = 0;
-  TMPC_DISPATCH_ILQR(nj, true, backward(f32, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu, lam, K, d, dV, ok))
+  TMPC_DISPATCH_ILQR(nj, true, backward(f32, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu, lam, jscratch, K, d, dV, ok))
 }
 
 int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C,

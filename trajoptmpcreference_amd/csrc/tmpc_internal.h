@@ -127,7 +127,8 @@ void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj,
 void launch_activate(hipStream_t s, int B, int* act_init, int* active);
 int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
                          const double* u, const double* rho, const int* active, const double* A, const double* Bm,
-                         const double* mu, const double* lam, double* K, double* d, double* dV, int* ok);
+                         const double* mu, const double* lam, double* jscratch, double* K, double* d, double* dV,
+                         int* ok);
 int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
                         const double* mu, const double* lam, int B, int N, int T, double dt, int init,
                         const double* alphas, const double* x, const double* u, const double* K, const double* d,
