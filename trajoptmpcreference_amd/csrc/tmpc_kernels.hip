@@ -221,6 +221,7 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
 // knot, x|u block), one row per lane, Gauss-Jordan as k_ginv.  Also writes the
 // summed jacobian (the g_k increment) to jsoft [B][N][NX + NU].
 // Layout of Gk: [B][N][NX*NX + NU*NU] (x block, then the packed u block).
+constexpr int GINV_SOFT_GROUPS = 8;
 template <int NJ>
 __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
                                                   int B, int N, const double* __restrict__ rho,
@@ -229,16 +230,22 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
                                                   const double* __restrict__ lam, double* __restrict__ Gk,
                                                   double* __restrict__ jsoft) {
   constexpr int NX = 2 * NJ, NU = NJ, MC = 6 * NJ;
+  // one workgroup per (problem, GINV_SOFT_GROUPS x 4 of its 2N matrices): an inactive problem costs a
+  // handful of workgroups, not 2N / 4 (config 4 runs most of its 528 batch iterations with a few
+  // percent of the problems active, and dispatching 131k early-exit workgroups took 0.1 ms)
   const int lane = threadIdx.x & 63;
-  const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
   const int r = lane & 15;
-  const bool in_range = slot < B * N * 2;
-  const int b = in_range ? slot / (2 * N) : 0;
-  const int rem = in_range ? slot - b * 2 * N : 0;
-  const int k = rem >> 1, which = rem & 1;
+  const int wpp = (2 * N + 4 * GINV_SOFT_GROUPS - 1) / (4 * GINV_SOFT_GROUPS);
+  const int b = blockIdx.x / wpp;
+  if (b >= B || !active[b]) return;   // workgroup-uniform exit
+  const int c0 = (blockIdx.x - b * wpp) * 4 * GINV_SOFT_GROUPS;
+  for (int grp = 0; grp < GINV_SOFT_GROUPS; ++grp) {
+  const int rem = c0 + 4 * grp + (lane >> 4);
+  const bool in_range = rem < 2 * N;
+  if (!__any(in_range)) break;   // wave-uniform: past the problem's last matrix
+  const int k = in_range ? rem >> 1 : 0, which = in_range ? rem & 1 : 0;
   const bool terminal = k == N - 1;
-  const bool act = in_range && active[b] && !(which == 1 && terminal);
-  if (!__any(in_range && active[b])) return;   // wave-uniform exit
+  const bool act = in_range && !(which == 1 && terminal);
   const int n = which ? NJ : NX;
   double z[3 * NJ], jac[3 * NJ];
   const double* xb = x + (size_t)b * NX * N;
@@ -298,7 +305,7 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
     a[c] = (act && r < n && c < n) ? (h + outer) + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
   }
   GjSweep<0, NX>::run(a, r);
-  if (!in_range || !active[b] || r >= n) return;
+  if (!in_range || r >= n) continue;
   if (act) {
     double* out = Gk + ((size_t)b * N + k) * (NX * NX + NU * NU) + (which ? NX * NX : 0);
 #pragma unroll
@@ -320,6 +327,7 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
       if (m == r) jr = terminal ? 0.0 : jac[NX + m];
   }
   jsoft[((size_t)b * N + k) * (NX + NU) + (which ? NX : 0) + r] = jr;
+  }   // grp
 }
 
 // ======================================================================= block-tridiagonal PCG
@@ -1685,8 +1693,9 @@ struct LaunchNJ {
   static void ginv_soft(hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
                         const int* active, const double* x, const double* u, const double* mu, const double* lam,
                         double* Gk, double* jsoft) {
-    hipLaunchKernelGGL((k_ginv_soft<NJ>), TMPC_GRID(B * N * 2 * 16, 64), 0, s, C, Cs, B, N, rho, active, x, u, mu,
-                       lam, Gk, jsoft);
+    const int wpp = (2 * N + 4 * GINV_SOFT_GROUPS - 1) / (4 * GINV_SOFT_GROUPS);
+    hipLaunchKernelGGL((k_ginv_soft<NJ>), dim3(B * wpp), dim3(64), 0, s, C, Cs, B, N, rho, active, x, u, mu, lam, Gk,
+                       jsoft);
   }
 };
 
