@@ -279,8 +279,9 @@ int tmpc_synchronize(tmpc_ctx* ctx);
 int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
 int tmpc_reset_stats(tmpc_ctx* ctx);
 
-/* Work counters of the last SQP solve on this context: [0] problem-QPs solved, [1] total PCG
- * iterations, [2] QPs that recomputed the dynamics gradient, [3] line-search trials per QP. */
+/* Work counters of the last solve call on this context: [0] problem-QPs solved (iLQR: problem-
+ * iterations), [1] total PCG iterations, [2] QPs that recomputed the dynamics gradient, [3] line-search
+ * trials per QP.  After tmpc_mpc_batch[_device], [0..2] are summed over all its horizon solves. */
 int tmpc_solve_counters(tmpc_ctx* ctx, int64_t* counters);
 
 /* ---- multi-GPU: one process per GPU, RCCL over xGMI ----

@@ -64,6 +64,23 @@ class HardConstraints:
                 out.append((lim.col0() + (e % n), sign, full[e]))
         return out
 
+    def active_masks(self, x, u, N):
+        """Per knot, the active-set bitmask of the QP's hard rows: bit t * 2n + e for limit kind t
+        (0 joint, 1 velocity, 2 torque) and entry e of [z - lb; ub - z] (e < n lower bound, e >= n
+        upper), set when that entry is violated (< 0) -- ACTIVE_SET's rows, FULL_SET's nonzero rows.
+        The GPU reports the same masks (tmpc_trace.hard_active, tmpc_qp_hard_info)."""
+        out = []
+        for k in range(N):
+            m = 0
+            for col, sign, _ in self.rows(x[:, k], u[:, k] if k < N - 1 else None, k, N):
+                if sign == 0:
+                    continue
+                n = self.limits[0].n if self.limits else 1
+                t, i = divmod(col, n)
+                m |= 1 << (t * 2 * n + (i if sign > 0 else n + i))
+            out.append(m)
+        return out
+
     def violation_terms(self, x, u, N):
         """the per-knot sum(map(abs, c_err)) terms of :286-293, in order"""
         terms = []
@@ -160,8 +177,150 @@ def preconditioner_dense(S, nx, ptype):
     return P
 
 
+# ------------------------------------------------------------------ canonical summation order
+# PCG on these active-set Schur complements (the trailing dim mod nx rows have no preconditioner
+# rows, PCG.py:182) is summation-order sensitive: on the SAME S, the reference's NumPy / OpenBLAS
+# order (pcg_dense with preconditioner_dense, CPU-dependent) and a plain sequential order
+# stop up to 5 iterations apart on the arm3 cases of tests/test_gpu_hard.py.  So the oracle fixes
+# ONE order -- every sum sequential from 0.0 in index order, every product and sum rounded on its
+# own (no fused multiply-add), dot products as per-thread partials over 256 threads (row a on thread
+# a mod 256) reduced by a 64-lane xor butterfly and a fan-in over the 4 waves -- and the GPU's
+# k_hard_pcg follows it operation for operation (tmpc_hard.hip, fp contraction off), so the two are
+# bitwise equal on identical S and gamma.  The reference's own fixtures pin both orders on their
+# integers except where a count is decided by the order itself: the pendulum ACTIVE_SET PCG-SS run's
+# QPs 2 and 6 stop one iteration apart (42 vs 41 at QP 2, 7 active rows)
+# (tests/test_oracle_golden.py::test_canonical_order_on_reference_fixtures).
+
+def _gj_inverse(M):
+    """Gauss-Jordan inverse of the augmented [M | I] without pivoting (principal blocks of the
+    negative definite S), in place of np.linalg.inv's LU: row p /= pivot, then every other row r
+    -= M[r, p] * row p."""
+    M = np.array(M, dtype=float)
+    n = M.shape[0]
+    for p in range(n):
+        d = M[p, p]
+        row = M[p] / d
+        row[p] = 1.0 / d
+        M[p] = row
+        for r in range(n):
+            if r == p:
+                continue
+            f = M[r, p]
+            M[r, p] = 0.0
+            M[r] = M[r] - f * M[p]
+    return M
+
+
+def _neg_triple(X, Y, Z):
+    """-(X (Y Z)), both products summed sequentially (PCG.py:196-206's -P (S P))."""
+    n = X.shape[0]
+    yz = np.zeros((n, n))
+    for l in range(n):
+        yz = yz + Y[:, l:l + 1] * Z[l:l + 1, :]
+    acc = np.zeros((n, n))
+    for m in range(n):
+        acc = acc + X[:, m:m + 1] * yz[m:m + 1, :]
+    return -acc
+
+
+def _dot(a, b):
+    """sum(a * b): per-thread partials (thread t sums rows t, t + 256, ... in order), a 64-lane xor
+    butterfly per wave, then the 4 wave totals in order."""
+    prod = a * b
+    D = len(prod)
+    J = (D + 255) // 256
+    pad = np.zeros(J * 256)
+    pad[:D] = prod
+    part = np.zeros(256)
+    for j in range(J):
+        part = part + pad[j * 256:(j + 1) * 256]
+    idx = np.arange(256)
+    for off in (32, 16, 8, 4, 2, 1):
+        part = part + part[idx ^ off]
+    s = 0.0
+    for w in range(4):
+        s = s + part[w * 64]
+    return s
+
+
+def preconditioner_canonical(S, nx, ptype):
+    """compute_preconditioner (PCG.py:113-212) in the canonical order: the diagonal blocks of the
+    first floor(dim / nx) nx-aligned blocks by _gj_inverse, SS's stair blocks P_{k,k-1} = -P_kk
+    (S_{k,k-1} P_{k-1,k-1}) for odd k and P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk) for even k, each
+    mirrored by its transpose.  Returns (Pd [nb][nx][nx], Pl [nb-1][nx][nx] = P_{k+1,k})."""
+    nb = S.shape[0] // nx
+    Pd = np.zeros((nb, nx, nx))
+    Pl = np.zeros((max(nb - 1, 0), nx, nx))
+    if ptype in ("BJ", "SS"):
+        for k in range(nb):
+            Pd[k] = _gj_inverse(S[k * nx:(k + 1) * nx, k * nx:(k + 1) * nx])
+    if ptype == "SS":
+        for k in range(1, nb):
+            if k % 2:
+                Pl[k - 1] = _neg_triple(Pd[k], S[k * nx:(k + 1) * nx, (k - 1) * nx:k * nx], Pd[k - 1])
+            else:
+                Pl[k - 1] = _neg_triple(Pd[k - 1], S[(k - 1) * nx:k * nx, k * nx:(k + 1) * nx], Pd[k]).T
+    return Pd, Pl
+
+
+def pcg_canonical(S, b, nx, ptype, tol, max_iter):
+    """PCG.pcg (PCG.py:66-111, x0 = 0) with the preconditioner ptype in {0, J, BJ, SS} on the dense S,
+    every operation in the canonical order above.  Returns (x, iterations)."""
+    S = np.asarray(S, dtype=float)
+    D = S.shape[0]
+    nb = D // nx
+    Pd, Pl = preconditioner_canonical(S, nx, ptype)
+    diag = np.diag(S).copy()
+
+    def apply_P(r):
+        if ptype == "0":
+            return r.copy()
+        if ptype == "J":
+            return (1.0 / diag) * r
+        z = np.zeros(D)
+        R = r[:nb * nx].reshape(nb, nx)
+        s = np.zeros((nb, nx))
+        for j in range(nx):
+            s = s + Pd[:, :, j] * R[:, j:j + 1]
+        if ptype == "SS" and nb > 1:
+            for j in range(nx):       # P_{k,k-1} r_{k-1}
+                s[1:] = s[1:] + Pl[:, :, j] * R[:-1, j:j + 1]
+            for j in range(nx):       # P_{k,k+1} r_{k+1} = P_{k+1,k}^T r_{k+1}
+                s[:-1] = s[:-1] + Pl[:, j, :] * R[1:, j:j + 1]
+        z[:nb * nx] = s.reshape(-1)   # rows past the last full block: 0 (PCG.py:182)
+        return z
+
+    def spmv(v):
+        s = np.zeros(D)
+        for c in range(D):
+            s = s + S[:, c] * v[c]
+        return s
+
+    x = np.zeros(D)
+    r = np.array(b, dtype=float)
+    z = apply_P(r)
+    p = z.copy()
+    nu = _dot(r, z)
+    it_done = max_iter
+    for it in range(max_iter):
+        Ap = spmv(p)
+        alpha = nu / _dot(p, Ap)
+        r = r - Ap * alpha
+        x = x + p * alpha
+        z = apply_P(r)
+        nup = _dot(r, z)
+        if abs(nup) < tol:
+            it_done = it + 1
+            break
+        beta = nup / nu
+        p = z + p * beta
+        nu = nup
+    return x, it_done
+
+
 def pcg_dense(S, b, P, tol, max_iter):
-    """PCG.pcg (PCG.py:66-111) with x0 = 0."""
+    """PCG.pcg (PCG.py:66-111) with x0 = 0, NumPy's summation order (the reference's own arithmetic,
+    CPU-dependent; kept to document the order sensitivity, see above)."""
     x = np.zeros_like(b)
     r = b - S @ x
     rt = P @ r
@@ -183,7 +342,24 @@ def pcg_dense(S, b, P, tol, max_iter):
     return x, it
 
 
-def solve_qp_dense(G, g, C, c, rho, method, options, nx):
+def solve_kkt_dense(G, g, C, c, rho):
+    """solveKKTSystem, numpy branch (TrajoptMPCReference.py:313-359): G + rho I (when rho != 0) and
+    [G C^T; C 0] [dxu; lambda] = [g; c] by np.linalg.solve, falling back to lstsq with the
+    `singular` flag when LAPACK reports a singular matrix (:353-357).  Returns (dxul, singular)."""
+    Gr = G + rho * np.eye(G.shape[0]) if rho != 0 else G
+    m = C.shape[0]
+    KKT = np.hstack((np.vstack((Gr, C)), np.vstack((C.T, np.zeros((m, m))))))
+    rhs = np.concatenate([g, c])
+    try:
+        return np.linalg.solve(KKT, rhs), False
+    except np.linalg.LinAlgError:
+        return np.linalg.lstsq(KKT, rhs, rcond=None)[0], True
+
+
+def solve_qp_dense(G, g, C, c, rho, method, options, nx, flags=None, order="numpy"):
+    """`flags` (a dict, optional) receives "singular": the least-squares fallback ran.  order:
+    "numpy" -- the reference's own arithmetic (preconditioner_dense + pcg_dense), which reproduces
+    its fixtures; "canonical" -- pcg_canonical, the order the GPU's k_hard_pcg follows bit for bit."""
     """solveKKTSystem_Schur, numpy branch (:415-455).  Method S uses np.linalg.solve; when S is
     singular (FULL_SET: the inactive rows of C are zero) the reference falls back to lstsq (:431-436)."""
     Gr = G + rho * np.eye(G.shape[0])
@@ -196,8 +372,17 @@ def solve_qp_dense(G, g, C, c, rho, method, options, nx):
             lam = np.linalg.solve(S, gamma)
         except np.linalg.LinAlgError:
             lam = np.linalg.lstsq(S, gamma, rcond=None)[0]
+            if flags is not None:
+                flags["singular"] = True
     else:
-        P = preconditioner_dense(S, nx, method[4:])
-        lam, iters = pcg_dense(S, gamma, P, options["exit_tolerance_linSys"], options["max_iter_linSys"])
+        ptype = method[4:]
+        tol, mi = options["exit_tolerance_linSys"], options["max_iter_linSys"]
+        if order == "canonical":
+            if ptype in ("BJ", "SS"):   # the reference's np.linalg.inv raises on a singular block (FULL_SET)
+                for k in range(S.shape[0] // nx):
+                    np.linalg.inv(S[k * nx:(k + 1) * nx, k * nx:(k + 1) * nx])
+            lam, iters = pcg_canonical(S, gamma, nx, ptype, tol, mi)
+        else:
+            lam, iters = pcg_dense(S, gamma, preconditioner_dense(S, nx, ptype), tol, mi)
     dxu = invG @ (g - C.T @ lam)
     return np.concatenate([dxu, lam]), iters, S

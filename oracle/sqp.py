@@ -260,7 +260,8 @@ def total_violation(model, x, u, xs, N, dt, hard=None):
 
 
 # ------------------------------------------------------------------- SQP
-def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm=None, hard=None):
+def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm=None, hard=None,
+        order="numpy"):
     """TrajoptMPCReference.SQP (:510-760).  Returns a dict.  `soft` (oracle.soft.SoftConstraints)
     enables the soft-constraint terms and the outer loop; its mu/lambda/phi are updated in place
     (the reference keeps them in the constraint object).
@@ -268,7 +269,8 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
     QP's PCG initial iterate and receives that QP's lambda -- the reference never forwards a guess
     from SQP (:512-519), so warm=None is the reference behaviour.
     `hard` (oracle.hard.HardConstraints): ACTIVE_SET / FULL_SET rows in the dense KKT system
-    (the reference's own dense formation, small sizes only)."""
+    (the reference's own dense formation, small sizes only); `order` selects its PCG's summation
+    order (oracle/hard.py solve_qp_dense: "numpy" the reference's, "canonical" the GPU's)."""
     o = default_options(options)
     nx, nu = 2 * model.n, model.n
     n = nx + nu
@@ -286,19 +288,29 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
         merit = J + mu * c
         trace = [dict(outer_iteration=outer, iteration=0, line_search_iteration=0, alpha=1, rho=rho, J=J, c=c,
                       merit=merit, D=None, reduction_ratio=None, succeeded_line_search=False)]
-        pcg_iters, dxuls, active_rows, active_sets, iterates = [], [], [], [], []
+        pcg_iters, dxuls, active_rows, active_sets, active_masks, singular, iterates = [], [], [], [], [], [], []
         it = 0
         exit_sqp = 0
         while True:
             iterates.append((x.copy(), u.copy(), rho))
-            if hard is not None:
+            if hard is not None or method == "N":
                 from . import hard as ohard
-                G, g, C, cc = ohard.kkt_dense(model, cost, x, u, xs, N, dt, hard, soft)
-                dxul, iters, _ = ohard.solve_qp_dense(G, g, C, cc, rho, method, o, nx)
+                hc = hard if hard is not None else ohard.HardConstraints([])
+                G, g, C, cc = ohard.kkt_dense(model, cost, x, u, xs, N, dt, hc, soft)
+                if method == "N":   # solveKKTSystem (:313-359), the reference's default method
+                    dxul, sing = ohard.solve_kkt_dense(G, g, C, cc, rho)
+                    iters = None
+                else:
+                    fl = {}
+                    dxul, iters, _ = ohard.solve_qp_dense(G, g, C, cc, rho, method, o, nx, fl, order)
+                    sing = fl.get("singular", False)
+                singular.append(bool(sing))
                 active_rows.append(C.shape[0] - nx * N)
                 active_sets.append([(k, int(sg)) for k in range(N)
-                                    for _, sg, _ in hard.rows(x[:, k], u[:, k] if k < N - 1 else None, k, N)])
+                                    for _, sg, _ in hc.rows(x[:, k], u[:, k] if k < N - 1 else None, k, N)])
+                active_masks.append(hc.active_masks(x, u, N))
             else:
+                singular.append(False)
                 guess = None if warm is None else warm.get("lam")
                 dxul, iters, ex = solve_qp(model, cost, x, u, xs, N, dt, rho, method, o, soft, guess)
                 if warm is not None and iters is not None:
@@ -382,7 +394,7 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
             break
     return dict(x=x, u=u, exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer, sqp_iter=it, trace=trace,
                 pcg_iters=pcg_iters, dxul=dxuls, active_rows=active_rows, active_sets=active_sets,
-                iterates=iterates)
+                active_masks=active_masks, singular=singular, iterates=iterates)
 
 
 def initial_problem(model, N, dt, seed):

@@ -330,7 +330,7 @@ def run_sqp(args):
     wall = time.time() - t0
     tr = solver.trace
     keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
-            "succeeded_line_search", "inner_iters"]
+            "succeeded_line_search", "inner_iters", "singular"]
     rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(t[k]) for t in tr]) for k in keys}
     pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
     dxul = np.array([d["value"][:, 0] for d in solver.saved_dxul])
@@ -439,7 +439,7 @@ def run_hard(args):
     con.set_torque_limits([ub], [lb], mode, {"overloading": False})
     solver = TrajoptMPCReference(plant, cost, con)
     m = {"S": SQPSolverMethods.S, "PCG-J": SQPSolverMethods.PCG_J, "PCG-BJ": SQPSolverMethods.PCG_BJ,
-         "PCG-SS": SQPSolverMethods.PCG_SS}[method]
+         "PCG-SS": SQPSolverMethods.PCG_SS, "N": SQPSolverMethods.N}[method]
     opts = {"overloading": False}
     if erm is not None:
         opts["expected_reduction_min_SQP_DDP"] = erm
@@ -457,7 +457,7 @@ def run_hard(args):
     wall = time.time() - t0
     tr = solver.trace
     keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
-            "succeeded_line_search"]
+            "succeeded_line_search", "singular"]
     rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(np.asarray(t[k]).reshape(-1)[0]) for t in tr])
            for k in keys}
     # active rows per QP from the reference's C: rows past nx*N, in order; knot = column block, sign = entry
@@ -487,6 +487,60 @@ def run_hard(args):
                         dxul=dx_pad, wall_s=wall, **rec)
     return f"[golden] hard {tag} {method} N={N} seed={seed} erm={erm}: exit_sqp={exit_sqp} iters={sqp_iter} " \
            f"rows={list(rows)} pcg={list(pcg_iters)} err={err[:80]} wall={wall:.1f}s"
+
+
+def gen_soft_hooks(N=8, seed=2024):
+    """The reference's soft-constraint plugin hooks on their own (TrajoptConstraint.py:53-166,
+    295-378), 1-link arm (constraint_size 1, the size the reference's BoxConstraint runs):
+    value_soft_constraints / jacobian_soft_constraints at random (x_k, u_k, k) with random mu /
+    lambda / phi, and update_soft_constraint_constants on random trajectories (flag + constants after).
+    Torque limits (N-1 knots) and joint limits (the reference sizes them N-1 knots, so the
+    trajectories keep knot N-1 inside the bounds) in QUADRATIC_PENALTY and AUGMENTED_LAGRANGIAN."""
+    _setup_reference()
+    from TrajoptConstraint import TrajoptConstraint
+    rng = np.random.default_rng(seed)
+    out = {"N": N}
+    for kind in ("torque", "joint"):
+        for mode, tag in (("QUADRATIC_PENALTY", "QP"), ("AUGMENTED_LAGRANGIAN", "AL")):
+            con = TrajoptConstraint(1, 1, 1, N)
+            con.overloading = False   # attribute the reference reads but never sets (SURVEY F6)
+            getattr(con, f"set_{kind}_limits")([0.5], [-0.5], mode, {"overloading": False})
+            box = getattr(con, f"{kind}_limits")
+            T = box.num_timesteps
+            box.quadratic_penalty_mu[:] = 10.0 ** rng.uniform(-2, 2, (2, T))
+            box.augmented_lagrangian_lambda[:] = rng.uniform(-1, 1, (2, T))
+            box.augmented_lagrangian_phi[:] = 10.0 ** rng.uniform(-3, 0, (2, T))
+            pre = f"{kind}_{tag}_"
+            out[pre + "mu0"] = box.quadratic_penalty_mu.copy()
+            out[pre + "lam0"] = box.augmented_lagrangian_lambda.copy()
+            out[pre + "phi0"] = box.augmented_lagrangian_phi.copy()
+            P = 24
+            xs = rng.uniform(-1.2, 1.2, (P, 2))
+            us = rng.uniform(-1.2, 1.2, (P, 1))
+            ks = rng.integers(0, N - 1, P)
+            vals, jacs = [], []
+            for i in range(P):
+                vals.append(float(np.asarray(con.value_soft_constraints(xs[i], us[i], int(ks[i]))).reshape(-1)[0]))
+                jacs.append(np.asarray(con.jacobian_soft_constraints(xs[i], us[i], int(ks[i])), dtype=float).reshape(-1))
+            out[pre + "xk"], out[pre + "uk"], out[pre + "k"] = xs, us, ks.astype(np.int32)
+            out[pre + "value"], out[pre + "jac"] = np.array(vals), np.array(jacs)
+            # AL updates on two random trajectories (|z| up to 0.8: some violations near phi, some far)
+            flags, mus, lams, phis, Xs, Us = [], [], [], [], [], []
+            for r in range(2):
+                X = rng.uniform(-0.8, 0.8, (2, N))
+                X[:, N - 1] = rng.uniform(-0.4, 0.4, 2)
+                U = rng.uniform(-0.8, 0.8, (1, N - 1))
+                flags.append(bool(con.update_soft_constraint_constants(X, U)))
+                mus.append(box.quadratic_penalty_mu.copy())
+                lams.append(box.augmented_lagrangian_lambda.copy())
+                phis.append(box.augmented_lagrangian_phi.copy())
+                Xs.append(X)
+                Us.append(U)
+            out[pre + "upd_x"], out[pre + "upd_u"] = np.array(Xs), np.array(Us)
+            out[pre + "upd_flag"] = np.array(flags)
+            out[pre + "upd_mu"], out[pre + "upd_lam"], out[pre + "upd_phi"] = np.array(mus), np.array(lams), np.array(phis)
+    np.savez_compressed(os.path.join(OUT, "hooks_soft_arm1.npz"), **out)
+    print(f"[golden] soft hooks: {len(out)} arrays")
 
 
 def run_pendulum(args):
@@ -598,7 +652,9 @@ def main():
                 ("ACTIVE_SET", "PCG-BJ", 10, 1.5, 2, 0.1, None), ("ACTIVE_SET", "PCG-SS", 12, 2.5, 3, 0.1, -100.0),
                 ("ACTIVE_SET", "PCG-J", 8, 2.0, 4, 0.1, None), ("FULL_SET", "PCG-SS", 8, 2.0, 5, 0.1, None),
                 ("FULL_SET", "S", 8, 2.0, 6, 0.1, None), ("ACTIVE_SET", "PCG-BJ", 10, 2.5, 7, 0.1, None),
-                ("ACTIVE_SET", "PCG-SS", 16, 2.2, 8, 0.1, None), ("ACTIVE_SET", "S", 12, 3.0, 9, 0.1, -100.0)]
+                ("ACTIVE_SET", "PCG-SS", 16, 2.2, 8, 0.1, None), ("ACTIVE_SET", "S", 12, 3.0, 9, 0.1, -100.0),
+                # method N (the dense KKT solve): the active set's rows, and FULL_SET's singular KKT -> lstsq
+                ("ACTIVE_SET", "N", 8, 2.0, 10, 0.1, None), ("FULL_SET", "N", 8, 2.0, 11, 0.1, None)]
         with mp.get_context("fork").Pool(min(8, len(jobs))) as pool:
             for msg in pool.imap_unordered(run_hard, jobs):
                 print(msg, flush=True)
@@ -607,6 +663,14 @@ def main():
                 ("AUGMENTED_LAGRANGIAN", "S", 20, 7.0)]
         with mp.get_context("fork").Pool(len(jobs)) as pool:
             for msg in pool.imap_unordered(run_pendulum, jobs):
+                print(msg, flush=True)
+    if a.only in (None, "hooks"):
+        gen_soft_hooks()
+    if a.only in (None, "sqpN"):
+        # method N (dense KKT, solveKKTSystem :313-359), the reference's default SQP method
+        jobs = [("arm2", 8, 0, "N", 0.1), ("arm3", 8, 1, "N", 0.1), ("arm3", 32, 0, "N", 0.1)]
+        with mp.get_context("fork").Pool(len(jobs)) as pool:
+            for msg in pool.imap_unordered(run_sqp, jobs):
                 print(msg, flush=True)
     if a.only in (None, "soft"):
         jobs = [("QUADRATIC_PENALTY", "PCG-SS", 8, 2.0, 0, 0.1), ("AUGMENTED_LAGRANGIAN", "PCG-SS", 8, 2.0, 0, 0.1),

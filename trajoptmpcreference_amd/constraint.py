@@ -22,8 +22,11 @@ reference's for constraint_size 1 and the elementwise generalisation above
 reference's PCG then raises LinAlgError and its method S falls back to lstsq, so
 FULL_SET runs with method S only.
 
-The host-side value / jacobian / update methods below are the plugin API for
-callers that evaluate constraints themselves; the solve never calls them.
+The host-side value / jacobian / update methods below are the reference's plugin
+hooks (value/jacobian_hard_constraints, value/jacobian_soft_constraints,
+update/shift_soft_constraint_constants, ...) for callers that evaluate constraints
+themselves; the GPU solve computes the same quantities on the device and never
+calls them.
 """
 from typing import List
 
@@ -128,6 +131,32 @@ class BoxConstraint:
         for t in range(self.num_timesteps):
             m = max(m, abs(min(self.full_value(z_of_t[:, t]))))
         return m
+
+    def update_soft_constraint_constants(self, z_of_t):
+        """BoxConstraint.update_soft_constraint_constants (:138-166) on the limited slice z_of_t
+        (constraint_size x num_timesteps, one column per knot): per entry of [z - lb; ub - z] < 0,
+        mu *= mu_factor (capped at mu_max) when |value| >= phi, else lambda += mu value and
+        phi /= phi_factor.  Returns True when no constant changed (every violated mu at its cap)."""
+        z_of_t = np.asarray(z_of_t, dtype=np.float64)
+        o = self.options
+        flag = True
+        for t in range(self.num_timesteps):
+            v = self.full_value(z_of_t[:, t])
+            lflag = np.abs(v) < self.augmented_lagrangian_phi[:, t]
+            for i in range(len(v)):
+                if not v[i] < 0:
+                    continue
+                if not lflag[i]:
+                    cur = self.quadratic_penalty_mu[i, t]
+                    if cur < o["quadratic_penalty_mu_max"]:
+                        flag = False
+                        self.quadratic_penalty_mu[i, t] = min(o["quadratic_penalty_mu_max"],
+                                                              cur * o["quadratic_penalty_mu_factor"])
+                else:
+                    flag = False
+                    self.augmented_lagrangian_lambda[i, t] += self.quadratic_penalty_mu[i, t] * v[i]
+                    self.augmented_lagrangian_phi[i, t] /= o["augmentated_lagrangian_phi_factor"]
+        return flag
 
     def shift_soft_constraint_constants(self, shift_steps: int):
         """Receding-horizon shift (:168-176)."""
@@ -242,6 +271,66 @@ class TrajoptConstraint:
             v = self.value_hard_constraints(x[:, k], None if (k >= T - 1 or u is None) else np.asarray(u)[:, k], k)
             tot += 0 if v is None else len(v)
         return tot
+
+    def _soft_slices(self, xk, uk, timestep):
+        """(kind, constraint, z) of the soft limits at a knot in the reference's order (joint, velocity,
+        torque; torque limits have no terminal-knot term, :305,327)."""
+        T = self.num_timesteps
+        t = T - 1 if timestep is None else timestep
+        out = []
+        for kind, c in self.limits():
+            if not c.is_soft_constraint_mode():
+                continue
+            if kind == "torque_limits":
+                if t >= T - 1 or uk is None:
+                    continue
+                z = np.asarray(uk, dtype=np.float64).reshape(-1)
+            elif kind == "joint_limits":
+                z = np.asarray(xk, dtype=np.float64).reshape(-1)[:self.nq]
+            else:
+                z = np.asarray(xk, dtype=np.float64).reshape(-1)[self.nq:self.nq + self.nv]
+            out.append((kind, c, z, t))
+        return out
+
+    def value_soft_constraints(self, xk, uk=None, timestep=None):
+        """TrajoptConstraint.value_soft_constraints (:295-307): the sum over the soft limits of
+        sum_i mu_i v_i^2 (+ sum_i lambda_i v_i for AUGMENTED_LAGRANGIAN) at `timestep`
+        (default: the terminal knot).  0 when no limit is soft.  Velocity limits act on the qd slice
+        of xk (the reference's BoxConstraint reads xk[:constraint_size], i.e. q, for every kind:
+        oracle/soft.py)."""
+        val = 0
+        for _, c, z, t in self._soft_slices(xk, uk, timestep):
+            val = val + c.value(z, t)
+        return val
+
+    def jacobian_soft_constraints(self, xk, uk=None, timestep=None):
+        """TrajoptConstraint.jacobian_soft_constraints (:309-337): the (nq + nv + nu) x 1 column
+        d value_soft_constraints / d[x; u] at `timestep`, None when no limit is soft.  With several
+        soft limit kinds the reference vstacks their columns (which its SQP cannot consume, SURVEY F6);
+        here they are summed, the gradient of the summed value (oracle/soft.py)."""
+        jac = None
+        for _, c, z, t in self._soft_slices(xk, uk, timestep):
+            j = c.jacobian(z, t)
+            jac = j if jac is None else jac + j
+        return jac
+
+    def update_soft_constraint_constants(self, x, u):
+        """TrajoptConstraint.update_soft_constraint_constants (:369-378) for trajectories x
+        (nq + nv) x N and u nu x (N - 1): the AL update of every limit; True when no constant changed.
+        Every limit is updated (the reference's `flag and update(...)` skips the later kinds once a
+        flag is False, which would leave their constants stale: oracle/soft.py)."""
+        x = np.asarray(x, dtype=np.float64)
+        flag = True
+        for kind, c in self.limits():
+            if kind == "joint_limits":
+                z = x[:self.nq]
+            elif kind == "velocity_limits":
+                z = x[self.nq:self.nq + self.nv]
+            else:
+                z = np.asarray(u, dtype=np.float64)
+            f = c.update_soft_constraint_constants(z)
+            flag = flag and f
+        return flag
 
     def max_soft_constraint_value(self, x, u):
         m = 0

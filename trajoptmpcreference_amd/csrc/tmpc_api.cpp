@@ -564,7 +564,10 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     hterms = hard.hterms;
     w.hard = &hard;
   }
-  if (o.pcg_warm_start && precond != 0 && !ctx->hlim.any_hard) {
+  if (o.pcg_warm_start && precond != 0 && ctx->hlim.any_hard)
+    return fail(ctx, "pcg_warm_start with hard box constraints: the Schur dimension changes with the active set "
+                "from QP to QP, so a previous lambda is no PCG guess; unset pcg_warm_start");
+  if (o.pcg_warm_start && precond != 0) {
     // PCG warm start: each QP starts from the problem's previous lambda (in place: a workgroup reads
     // its guess before it writes its lambda)
     BUF(double, lam_warm, (size_t)B * N * nx);
@@ -1156,8 +1159,13 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "the MPC loop supports QuadraticCost only");
   if (steps < 1) return fail(ctx, "steps must be >= 1");
   if (!ilqr && precond_of(solver) < 0) return fail(ctx, "solver %d: use TMPC_LINSYS_* or TMPC_SOLVER_ILQR", solver);
+  if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0 && ctx->hlim.any_hard)
+    return fail(ctx, "pcg_warm_start with hard box constraints: the Schur dimension changes with the active set "
+                "from QP to QP, so a previous lambda is no PCG guess; unset pcg_warm_start");
   const int nj = ctx->hmodel.n, nx = 2 * nj;
   const bool chain = ctx->hmodel.chain != 0;
+  // work counters of the whole loop: the sum over its horizon solves (tmpc_solve_counters)
+  int64_t sum_counters[3] = {0, 0, 0};
   // executed state 0 = x[:, 0]
   HIP_OK(hipMemcpy2DAsync(d_xe, (size_t)(steps + 1) * sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double),
                           (size_t)B * nx, hipMemcpyDeviceToDevice, ctx->stream));
@@ -1165,7 +1173,8 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
     rc = ilqr ? ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr)
               : sqp_device(ctx, B, N, dt, solver, d_x, d_u, nullptr, /*keep_warm=*/s > 0);
     if (rc) return rc;
-    if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0) {
+    for (int i = 0; i < 3; ++i) sum_counters[i] += ctx->last_counters[i];
+    if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0 && !ctx->hlim.any_hard) {
       // the next step's first PCG starts from this step's last lambda shifted by one knot
       // (lambda_k <- lambda_{k+1}, last block kept), as x and u are shifted (oracle/mpc.py)
       double* lw = (double*)ctx->bufs["lam_warm"].ptr;
@@ -1195,6 +1204,7 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
     }
   }
   HIP_OK(hipStreamSynchronize(ctx->stream));
+  for (int i = 0; i < 3; ++i) ctx->last_counters[i] = sum_counters[i];
   return 0;
 }
 

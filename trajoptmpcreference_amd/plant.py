@@ -145,7 +145,8 @@ class PendulumPlant(URDFPlant):
 
     def __init__(self, integrator_type: int = 0, options=None, device: int = 0, mass: float = 1.0,
                  length: float = 1.0):
-        options = {} if options is None else options
+        # a copy: the caller's dict must not come back pointing at the pendulum model
+        options = dict(options or {})
         options["path_to_urdf"] = pendulum_urdf(mass, length)
         super().__init__(integrator_type, options, device)
 
