@@ -49,6 +49,9 @@ LIMIT_PRESETS = {
     "torque-qp": {"torque": dict(mode="QUADRATIC_PENALTY", lb=-0.5, ub=0.5)},
     "torque-joint-al": {"torque": dict(mode="AUGMENTED_LAGRANGIAN", lb=-0.5, ub=0.5),
                         "joint": dict(mode="AUGMENTED_LAGRANGIAN", lb=-1.0, ub=1.0)},
+    # hard limits (ACTIVE_SET rows in C, TrajoptMPCReference.py:238-248): the banded Schur path
+    "torque-velocity-as": {"torque": dict(mode="ACTIVE_SET", lb=-0.5, ub=0.5),
+                           "velocity": dict(mode="ACTIVE_SET", lb=-1.0, ub=1.0)},
 }
 
 
@@ -78,17 +81,41 @@ def parse(argv=None):
     ap.add_argument("--pcg-warm-start", action="store_true",
                     help="tmpc_options.pcg_warm_start: each PCG starts from the previous lambda (MPC loop)")
     ap.add_argument("--seed0", type=int, default=0)
+    ap.add_argument("--q0-scale", type=float, default=1.0, help="start states q0 ~ U(-s, s)^n (SURVEY 8d: s = 1)")
+    ap.add_argument("--erm", type=float, default=None,
+                    help="options['expected_reduction_min_SQP_DDP'] (default 0.05; examples/twolinks.py uses -100)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="problems for the CPU baseline (-1: 40 per process, ~10-20 s)")
-    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="CPU-baseline processes (0: the cores this job may use -- the cgroup CPU quota when one "
+                         "is set, else os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args(argv)
 
 
-def initial_states(n, B, seed0):
+def initial_states(n, B, seed0, scale=1.0):
     q0 = np.zeros((B, n))
     for i in range(B):
-        q0[i] = np.random.default_rng(seed0 + i).uniform(-1.0, 1.0, n)
+        q0[i] = np.random.default_rng(seed0 + i).uniform(-scale, scale, n)
     return q0
+
+
+def host_cores():
+    """(cores this job may use, os.cpu_count(), basis): BASELINE.md section 3 asks for the host's cores;
+    on a shared GPU box the job's share is its cgroup CPU quota (cpu.max), which os.cpu_count() -- the
+    whole machine -- does not show."""
+    total = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            share = max(1, int(int(quota) // int(period)))
+            return min(share, total), total, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+        return aff, total, "sched_getaffinity"
+    except AttributeError:
+        return total, total, "os.cpu_count()"
 
 
 # ------------------------------------------------------------------ flop / byte models
@@ -127,15 +154,32 @@ def qp_schur_flops(N, nx, nu):
     return N * per_knot
 
 
-def measured_traffic(kernel_prefix):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_summary.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+def workload_key(a):
+    """file name of this workload's committed PMC summary, profiles/pmc/<key>.json"""
+    key = f"{a.solver}_{a.method if a.solver == 'sqp' else 'ilqr'}_arm{a.links}_N{a.N}_B{a.batch}"
+    if a.limits != "none":
+        key += "_" + a.limits
+    if a.mpc_steps > 0:
+        key += f"_mpc{a.mpc_steps}"
+    if a.precision != "fp64":
+        key += "_" + a.precision
+    if a.pcg_warm_start:
+        key += "_warm"
+    if a.cost != "quadratic":
+        key += "_" + a.cost
+    return key.replace("/", "-")
+
+
+def measured_traffic(kernel_prefix, key):
+    """HBM bytes per launch of a kernel from THIS workload's rocprofv3 PMC summary (tools/pmc_summary.py
+    writes profiles/pmc/<workload key>.json from separate FETCH_SIZE and WRITE_SIZE passes), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc", key + ".json")
     if not os.path.exists(path):
         return None, None
     d = json.load(open(path))
     for k, v in d["kernels"].items():
         if k.startswith(kernel_prefix):
-            return v["hbm_bytes_per_launch"], d.get("source")
+            return v["hbm_bytes_per_launch"], d.get("source", os.path.relpath(path, ROOT))
     return None, None
 
 
@@ -232,7 +276,9 @@ def sqp_roofline(a, N, nx, nu, kernels, counters):
     ach = flops / avg_s / 1e12
     impl = per_launch_iters * pcg_flops_impl(N, nx, a.method) + per_launch_qps * qp_schur_flops(N, nx, nu)
     lds_bytes = per_launch_iters * pcg_lds_bytes_per_iter(N, nx, a.method)
-    traffic, src = measured_traffic(f"void tmpc::k_qp<{nx // 2}, ")
+    traffic, src = measured_traffic(f"void tmpc::k_qp<{nx // 2}, ", workload_key(a))
+    if N * nx > 1024:
+        return gm_roofline(a, N, nx, qp, per_launch_iters, per_launch_qps, traffic, src)
     out = {"kernel": "k_qp (Schur + PCG + dxu, fused)", "bound": "fp64-valu", "achieved": ach,
            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": traffic,
            "avg_launch_ms": qp["avg_ms"], "pcg_iters_per_launch": per_launch_iters,
@@ -257,6 +303,27 @@ def sqp_roofline(a, N, nx, nu, kernels, counters):
     return out
 
 
+def gm_roofline(a, N, nx, qp, per_launch_iters, per_launch_qps, traffic, src):
+    """k_qp<..., GM> (N nx > 1024 rows, BASELINE config 5): the rows of S and P^-1 no longer fit a CU's
+    registers and are re-read from HBM scratch (through L2 / MALL) every PCG iteration -- the design
+    SURVEY 8(d)'s byte model prices, so the HBM roofline applies: achieved = b_pcg x PCG iterations per
+    launch / launch time, against 8 TB/s; traffic = the PMC bytes of this workload."""
+    avg_s = qp["avg_ms"] / 1000.0
+    alg = per_launch_iters * b_pcg_survey(N, nx)
+    ach = alg / avg_s / 1e9
+    out = {"kernel": "k_qp<GM> (Schur + PCG + dxu, S / P^-1 rows in HBM)", "bound": "hbm", "achieved": ach,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+           "avg_launch_ms": qp["avg_ms"], "pcg_iters_per_launch": per_launch_iters,
+           "problem_qps_per_launch": per_launch_qps,
+           "bytes_basis": f"SURVEY 8(d) b_pcg = 8 (2 (2N-1) nx^2 + 10 N nx) = {b_pcg_survey(N, nx)} B per PCG "
+                          f"iteration at N={N}, nx={nx}, x PCG iterations per launch",
+           "algorithmic_bytes_per_launch": alg}
+    if traffic:
+        out.update(hbm_GBps=traffic / avg_s / 1e9, hbm_frac=traffic / avg_s / 1e9 / HBM_PEAK_GBS,
+                   traffic_source=src)
+    return out
+
+
 def main():
     a = parse()
     from trajoptmpcreference_amd import _native, dist
@@ -267,7 +334,10 @@ def main():
     nx, nu = 2 * n, n
     model = parse_urdf(planar_arm_urdf(n))
     ctx = _native.Context(local_rank)
-    comm = dist.make_comm(ctx, rank, world)
+    # every rank must run the same configuration: its hash rides on the RCCL id exchange (dist.py)
+    cfg = dist.config_hash({k: v for k, v in sorted(vars(a).items()) if k != "cpu_procs"}, model.X0, model.Xa,
+                           model.Xb, model.I, np.asarray(model.parent), bytes(ctx.options))
+    comm = dist.make_comm(ctx, rank, world, cfg)
     ctx.set_model(model)
     if a.cost == "ee":
         if n != 2:
@@ -280,7 +350,7 @@ def main():
     ctx.set_box_limits(limits)
 
     # ---- workload: rank 0 draws every rank's start states, RCCL broadcast, own slice resident in HBM
-    q0 = dist.scatter_from_root(comm, rank, B, lambda count: initial_states(n, count, a.seed0), (n,))
+    q0 = dist.scatter_from_root(comm, rank, B, lambda count: initial_states(n, count, a.seed0, a.q0_scale), (n,))
     x0 = np.zeros((B, nx, N))
     x0[:, :n, 0] = q0
     u0 = np.zeros((B, nu, N - 1))
@@ -291,6 +361,8 @@ def main():
     ctx.rollout_device(B, N, dt, d_x0, d_u0)
     prec_id = {"fp64": 0, "fp32": 1, "mixed": 2}[a.precision]
     ctx.set_options(precision=prec_id, pcg_warm_start=int(a.pcg_warm_start))   # after the fp64 workload rollout
+    if a.erm is not None:
+        ctx.set_options(expected_reduction_min_SQP_DDP=float(a.erm))
 
     if a.mpc_steps > 0:
         K1 = a.mpc_steps
@@ -339,7 +411,8 @@ def main():
 
     kernels = {}
     for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "schur", "btsolve", "dxu", "ls_terms", "ls_decide",
-                 "ilqr_backward", "ilqr_forward", "ilqr_decide"]:
+                 "hard_schur", "hard_pcg", "hard_direct", "ilqr_backward", "ilqr_forward", "ilqr_decide",
+                 "mpc_shift"]:
         cnt, ms = ctx.kernel_stats(name)
         if cnt:
             kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
@@ -406,27 +479,40 @@ def main():
     roofline = None
     if a.solver == "sqp" and a.method.startswith("PCG") and a.mpc_steps == 0 and "qp" in kernels:
         roofline = sqp_roofline(a, N, nx, nu, kernels, counters)
-    elif a.solver == "ilqr" and a.mpc_steps == 0 and "ilqr_backward" in kernels:
+    elif a.solver == "sqp" and a.method.startswith("PCG") and a.mpc_steps > 0 and "qp" in kernels and N * nx > 1024:
+        # config 5 with SQP horizon solves: the GM QP kernel streams S / P^-1 rows (HBM roofline)
+        roofline = sqp_roofline(a, N, nx, nu, kernels, counters)
+    elif a.solver == "ilqr" and "ilqr_backward" in kernels:
         bw = kernels["ilqr_backward"]
         per_launch = int(counters[0]) / max(1, bw["launches"])
         flops = per_launch * (N - 1) * ilqr_backward_flops_per_knot(nx, nu)
         ach = flops / (bw["avg_ms"] / 1e3) / 1e12
         f32 = a.precision == "fp32"
         peak = FP32_PEAK_TFLOPS if f32 else FP64_PEAK_TFLOPS
+        traffic, src = measured_traffic("void tmpc::k_ilqr_backward<", workload_key(a))
         roofline = {"kernel": "k_ilqr_backward", "bound": "fp32-valu" if f32 else "fp64-valu", "achieved": ach,
-                    "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": None,
+                    "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": traffic,
                     "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
                     "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
+        if traffic:
+            roofline.update(hbm_GBps=traffic / (bw["avg_ms"] / 1e3) / 1e9, traffic_source=src)
+        fw = kernels.get("ilqr_forward")
+        if fw:
+            ft, fsrc = measured_traffic("void tmpc::k_ilqr_forward<", workload_key(a))
+            roofline["forward"] = {"kernel": "k_ilqr_forward", "avg_launch_ms": fw["avg_ms"], "traffic": ft,
+                                   "hbm_GBps": ft / (fw["avg_ms"] / 1e3) / 1e9 if ft else None}
     out["roofline"] = roofline
 
     cpu, par = None, None
     if headline and not a.no_cpu_baseline and world == 1:
-        procs = max(1, min(a.cpu_procs, os.cpu_count() or 1))
+        share, total, basis = host_cores()
+        procs = a.cpu_procs if a.cpu_procs > 0 else share
         sample = min(B, a.cpu_sample if a.cpu_sample > 0 else 40 * procs)
         v, wall, res = cpu_baseline(n, N, sample, procs, a.seed0)
         cpu = {"value": v, "unit": "solves/s", "cores": procs, "kind": "port",
                "sample": f"{sample} problems of the same workload (seeds {a.seed0}..{a.seed0 + sample - 1}), "
-                         f"oracle NumPy restatement (no SymPy), {procs} processes x 1 BLAS thread, {wall:.1f} s"}
+                         f"oracle NumPy restatement (no SymPy), {procs} processes x 1 BLAS thread, {wall:.1f} s",
+               "cores_basis": f"{basis}: this job may use {share} cores of the {total} os.cpu_count() reports"}
         # the GPU's own results for those problems (rank 0's first `sample` problems), with trace
         gr = ctx.sqp_solve_batch(x0_host(ctx, d_x0, B, nx, N)[:sample], u0[:sample], N, dt, a.method)
         par = parity_check(gr, res)
@@ -435,6 +521,9 @@ def main():
         out["parity"] = par
         out["kkt_residual"] = kkt_residual_check(ctx, n)
         out["pcie_inclusive"] = pcie
+        out["value_basis"] = ("HBM-resident: inputs resident on the GPU before the timed region, each step a D2D "
+                              "restore + one batched solve (the bench contract's definition); SURVEY 8(d) / "
+                              "BASELINE.md section 3 count H2D/D2H in wall time -- that rate is pcie_inclusive")
         out["work"] = {"problem_qps_per_step": int(counters[0]) / a.steps,
                        "pcg_iters_per_step": int(counters[1]) / a.steps,
                        "grad_evals_per_step": int(counters[2]) / a.steps,

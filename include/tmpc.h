@@ -37,15 +37,22 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 5
+#define TMPC_ABI_VERSION 6
 
-/* SQPSolverMethods (TrajoptMPCReference.py:13-18). N (dense KKT) is not offered on the GPU. */
+/* SQPSolverMethods (TrajoptMPCReference.py:13-18). */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
 #define TMPC_LINSYS_PCG_J 2  /* PCG, Jacobi preconditioner            PCG.py:168-169 */
 #define TMPC_LINSYS_PCG_BJ 3 /* PCG, block-Jacobi preconditioner      PCG.py:171-179 */
 #define TMPC_LINSYS_PCG_SS 4 /* PCG, symmetric-stair preconditioner   PCG.py:181-212 */
 #define TMPC_LINSYS_PCG_0 5  /* PCG, no preconditioner ('0', identity) PCG.py:114-118 (no SQPSolverMethods member;
                                 reachable through solveKKTSystem_Schur's options['preconditioner_type']) */
+#define TMPC_LINSYS_N 6      /* N, the reference's default: the dense KKT solve [G + rho I, C^T; C, 0] [dxu; lambda] =
+                                [g; c] (solveKKTSystem :313-359).  Its solution is the Schur complement's
+                                (lambda = S^-1 gamma, dxu = G^-1 (g - C^T lambda)), so it runs the direct Schur
+                                path of method S; where the KKT matrix is singular the reference takes lstsq
+                                (:353-357) and so does this path (trace.singular; the zero-row and duplicate-row
+                                cases of hard limits, see tmpc_hard.hip) -- the KKT least-squares answer equals the
+                                Schur one for consistent constraint sets and for FULL_SET's zero rows. */
 
 /* preconditioner ids for tmpc_pcg_batch (PCG options['preconditioner_type']) */
 #define TMPC_PRECOND_J 1
@@ -141,6 +148,14 @@ typedef struct tmpc_trace {
   double* reduction_ratio; /* NaN in row 0 */
   int32_t* succeeded_line_search;
   int32_t* pcg_iters;      /* PCG iterations of the QP solved in that SQP iteration (0 in row 0) */
+  int32_t* singular;       /* 1: that QP's direct solve took the least-squares answer (S / KKT singular: the
+                              reference's lstsq fallback, :353-357, 431-436; its self.singular is this flag
+                              made sticky) */
+  uint64_t* hard_active;   /* [B][max_iter_SQP_DDP + 1][N] (hard box limits only, else zeros): the active set of
+                              that QP per knot, bit t * 2n + e for limit kind t (0 joint, 1 velocity, 2 torque)
+                              and entry e of [z - lb; ub - z] (e < n lower, e >= n upper) when that entry is
+                              violated -- ACTIVE_SET's rows, FULL_SET's nonzero rows (TrajoptConstraint.py:64-68,
+                              110-111; TrajoptMPCReference.py:238-248) */
 } tmpc_trace;
 
 int tmpc_abi_version(void);
@@ -242,7 +257,8 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
                        double* dqdd);
 
 /* One QP of the SQP loop for B problems: formKKTSystemBlocks + solveKKTSystem_Schur with PCG
- * (TrajoptMPCReference.py:200-271,415-455) at the given trajectories and regularisation rho[B].
+ * (TrajoptMPCReference.py:200-271,415-455) at the given trajectories and regularisation rho[B];
+ * xs [B][nx] (nullable: x[:, :, 0]) is the SQP's initial state, the initial-state row's c_0 = x_0 - xs.
  * guess [B][N nx] (nullable) is the PCG initial iterate, options['guess'] of solveKKTSystem_Schur (:439-440).
  * dxul [B][n_xu(N-1)+nx + nx N] in the reference's interleaved order [x0,u0,x1,...,x_{N-1}; lambda].
  * S_diag [B][N][nx][nx], S_lo [B][N-1][nx][nx] (= S_{k+1,k}), gamma [B][N nx], P_diag [B][N][nx][nx]
@@ -252,8 +268,26 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
  * N nx dynamics / initial-state rows in knot order (the hard rows' multipliers are dropped), and
  * guess, S_diag, S_lo, gamma, P_diag must be NULL (S is banded with variable blocks). */
 int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
-                  const double* u, const double* guess, double* dxul, int32_t* pcg_iters, double* S_diag,
-                  double* S_lo, double* gamma, double* P_diag);
+                  const double* u, const double* xs, const double* guess, double* dxul, int32_t* pcg_iters,
+                  double* S_diag, double* S_lo, double* gamma, double* P_diag);
+
+/* Hard-limit detail of the last tmpc_qp_batch call with hard box limits (same B, N): sizes[2] = {dmax, W} of
+ * the banded Schur complement (rows padded to dmax, half band W), dim [B] its dimension per problem
+ * (N nx + hard rows), active [B][N] the per-knot active-set bitmasks (as tmpc_trace.hard_active),
+ * lambda_hard [B][N][6 n] the hard rows' multipliers by slot t * 2n + e (0 where no row), S_band
+ * [B][dmax][2W+1] (row a, column a - W + o at offset o) and gamma [B][dmax] in the reference's row order
+ * R_0 | R_1 H_0 | ... | R_{N-1} H_{N-2} H_{N-1}, singular [B] (the direct solve's least-squares flag).
+ * Every output is nullable. */
+int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim, uint64_t* active,
+                      double* lambda_hard, double* S_band, double* gamma, int32_t* singular);
+
+/* The hard-limit QP's PCG (GBD-PCG-Python/PCG.py:66-212 on the banded S of dimension dim[b], nx-aligned
+ * preconditioner blocks from row 0, n_blocks = floor(dim / nx), PCG.py:182) on given systems: S_band
+ * [B][dmax][2W+1], gamma [B][dmax] -> lambda [B][dmax], iters [B].  precond: TMPC_PRECOND_*.  Summation
+ * order: the canonical one of oracle/hard.py pcg_canonical (bitwise reproducible on the CPU). */
+int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int32_t* dim, int precond,
+                        const double* S_band, const double* gamma, double tol, int max_iter, double* lambda,
+                        int32_t* iters);
 
 /* PCG(S, gamma, nx, N, options={'preconditioner_type': J|BJ|SS, exit_tolerance, max_iter}).solve()
  * (GBD-PCG-Python/PCG.py:66-111) on B block-tridiagonal systems given by their blocks:

@@ -342,6 +342,25 @@ def pcg_dense(S, b, P, tol, max_iter):
     return x, it
 
 
+def structurally_singular(C):
+    """C has a zero row (FULL_SET's inactive entries) or two rows equal up to sign (a knot-0 hard row on
+    a state entry duplicates the initial-state row: xs violates a joint / velocity limit), so S = -C G^-1
+    C^T is singular in exact arithmetic.  The reference's np.linalg.solve raises for the first and, for
+    the second, raises or returns a rounding-sized pivot's answer depending on the elimination's
+    rounding; the build defines both as singular and takes lstsq's minimum-norm answer (the
+    reference's fallback, TrajoptMPCReference.py:431-436), as tmpc_hard.hip's k_hard_direct does."""
+    if np.any(np.all(C == 0, axis=1)):
+        return True
+    seen = set()
+    for row in C:
+        lead = row[np.flatnonzero(row)[0]]
+        key = ((row if lead > 0 else -row) + 0.0).tobytes()   # rows equal up to sign share a key (+0.0: no -0)
+        if key in seen:
+            return True
+        seen.add(key)
+    return False
+
+
 def solve_kkt_dense(G, g, C, c, rho):
     """solveKKTSystem, numpy branch (TrajoptMPCReference.py:313-359): G + rho I (when rho != 0) and
     [G C^T; C 0] [dxu; lambda] = [g; c] by np.linalg.solve, falling back to lstsq with the
@@ -351,6 +370,8 @@ def solve_kkt_dense(G, g, C, c, rho):
     KKT = np.hstack((np.vstack((Gr, C)), np.vstack((C.T, np.zeros((m, m))))))
     rhs = np.concatenate([g, c])
     try:
+        if structurally_singular(C):   # singular KKT matrix: defined as the lstsq answer (see above)
+            raise np.linalg.LinAlgError("structurally singular KKT matrix")
         return np.linalg.solve(KKT, rhs), False
     except np.linalg.LinAlgError:
         return np.linalg.lstsq(KKT, rhs, rcond=None)[0], True
@@ -369,6 +390,8 @@ def solve_qp_dense(G, g, C, c, rho, method, options, nx, flags=None, order="nump
     iters = None
     if method == "S":
         try:
+            if structurally_singular(C):
+                raise np.linalg.LinAlgError("structurally singular S")
             lam = np.linalg.solve(S, gamma)
         except np.linalg.LinAlgError:
             lam = np.linalg.lstsq(S, gamma, rcond=None)[0]

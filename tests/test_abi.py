@@ -37,7 +37,7 @@ def test_binding_matches_header():
     from trajoptmpcreference_amd import _native
     assert sorted(_native.SIGNATURES) == header_functions()
     lib = _native.load_library()
-    assert lib.tmpc_abi_version() == 5
+    assert lib.tmpc_abi_version() == 6
 
 
 def test_options_struct_layout_and_defaults():
@@ -70,3 +70,12 @@ def test_null_context_is_an_error_not_a_crash():
     lib = _native.load_library()
     assert lib.tmpc_set_options(None, None) < 0
     assert lib.tmpc_last_error(None) == b"null context"
+
+
+def test_trace_struct_layout():
+    """tmpc_trace: 13 pointers in the header's order (ABI 6 added singular and hard_active)."""
+    from trajoptmpcreference_amd import _native
+    names = [f[0] for f in _native.tmpc_trace._fields_]
+    assert names == ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
+                     "succeeded_line_search", "pcg_iters", "singular", "hard_active"]
+    assert ctypes.sizeof(_native.tmpc_trace) == 13 * 8

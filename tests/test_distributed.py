@@ -138,11 +138,61 @@ def test_single_rank_comm_is_a_no_op():
 
 
 def test_unique_id_file_exchange(tmp_path, monkeypatch):
-    """Rank 0 publishes the RCCL id atomically; another rank reads exactly those bytes (the
-    id itself comes from libtmpc on the GPU box: faked here)."""
+    """TMPC_COMM_ID_FILE set by the launcher: rank 0 publishes the RCCL id atomically; another rank reads
+    exactly those bytes (the id itself comes from libtmpc on the GPU box: faked here)."""
     path = tmp_path / "uid"
     monkeypatch.setenv("TMPC_COMM_ID_FILE", str(path))
     fake = bytes(range(128))
-    monkeypatch.setattr(dist._native, "comm_unique_id", lambda: fake)
-    assert dist.exchange_unique_id(0) == fake
-    assert dist.exchange_unique_id(1, timeout_s=5) == fake
+    assert dist.exchange_unique_id(0, 2, make_id=lambda: fake) == fake
+    assert dist.exchange_unique_id(1, 2, timeout_s=5, make_id=lambda: fake) == fake
+
+
+_RANK_SCRIPT = """
+import os, sys
+sys.path.insert(0, {root!r})
+from trajoptmpcreference_amd import dist
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+cfg = dist.config_hash({{"B": 4096, "N": int(os.environ["TEST_N"])}})
+try:
+    uid = dist.exchange_unique_id(rank, world, cfg, timeout_s=60, make_id=lambda: bytes(range(7, 135)))
+    print("OK", os.getppid(), uid.hex())
+except RuntimeError as e:
+    print("REFUSED", os.getppid(), e)
+"""
+
+
+def _launch_ranks(world, port, Ns):
+    """world processes with DIFFERENT parents: rank 0 a child of this test process, the others children of
+    their own `bash -c` (so nothing keyed on the parent pid could pair them)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    script = _RANK_SCRIPT.format(root=ROOT)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(world),
+                   TEST_N=str(Ns[r]))
+        env.pop("TMPC_COMM_ID_FILE", None)
+        cmd = [sys.executable, "-c", script]
+        if r:
+            cmd = ["bash", "-c", 'exec_py="$0"; "$exec_py" -c "$1"; true', sys.executable, script]
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    return [p.communicate(timeout=120)[0].strip().splitlines()[-1] for p in procs]
+
+
+def test_unique_id_tcp_exchange_across_process_trees():
+    """The RCCL id over TCP at MASTER_ADDR : MASTER_PORT + 1 (dist.exchange_unique_id): every rank gets
+    rank 0's id, whatever the process tree (the ranks here have different parents)."""
+    port = _free_port()
+    out = _launch_ranks(3, port - 1, [64, 64, 64])
+    assert all(line.startswith("OK") for line in out), out
+    assert len({line.split()[2] for line in out}) == 1
+    assert len({line.split()[1] for line in out}) == 3      # three different parent pids
+
+
+def test_mismatched_configuration_fails_fast():
+    """A rank whose configuration hash differs from rank 0's is refused, and rank 0 raises too."""
+    port = _free_port()
+    out = _launch_ranks(2, port - 1, [64, 32])
+    assert out[0].startswith("REFUSED") and "ranks [1]" in out[0], out
+    assert out[1].startswith("REFUSED"), out

@@ -4,7 +4,9 @@ TrajoptMPCReference drop-in) against the reference's own recorded solves
 
 Integer outputs -- exit codes, SQP iteration counts, the PCG iteration count
 of every QP, line-search iterations and the alpha sequence -- must be
-identical.  Trajectories and merit values: relative tolerance 1e-7.
+identical.  Trajectories and merit values: relative tolerance 1e-7.  Method N
+(the dense KKT solve, the reference's default) runs the direct Schur path:
+same solution, pinned by the reference's own method-N solves.
 
 PCG-J exception (documented in DESIGN.md): Jacobi-preconditioned CG on these
 ill-conditioned Schur complements (cond ~1e6-1e7) is not converging smoothly
@@ -48,7 +50,10 @@ def test_sqp_matches_reference(f):
     name, N, seed, method = _parse(f)
     d = np.load(f)
     solver = _solver(name)
-    x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(d["x0"], d["u0"], N, float(d["dt"]), method, {})
+    if method == "N":   # the reference's default method: called without naming it, as its callers do
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(d["x0"], d["u0"], N, float(d["dt"]))
+    else:
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(d["x0"], d["u0"], N, float(d["dt"]), method, {})
     assert exit_sqp == int(d["exit_sqp"])
     assert exit_soft == int(d["exit_soft"])
     assert outer_iter == int(d["outer_iter"])
@@ -59,7 +64,9 @@ def test_sqp_matches_reference(f):
     assert [t["line_search_iteration"] for t in tr] == list(d["tr_line_search_iteration"].astype(int))
     assert [t["succeeded_line_search"] for t in tr] == list(d["tr_succeeded_line_search"].astype(bool))
     ours = [t["inner_iters"] for t in tr[1:]]
-    if method == "S":
+    if "tr_singular" in d:
+        assert [t["singular"] for t in tr] == list(d["tr_singular"].astype(bool))
+    if method in ("S", "N"):
         assert ours == [0] * len(ours)   # direct solve: no PCG iterations
     elif method == "PCG-J":
         assert ours[0] == int(d["pcg_iters"][0])

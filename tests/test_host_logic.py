@@ -51,8 +51,6 @@ def test_invalid_method_and_unsupported_paths_raise():
     with pytest.raises(ValueError):
         s.SQP(x, u, 8, 0.1, "CG", {})
     with pytest.raises(NotImplementedError):
-        s.SQP(x, u, 8, 0.1, "N", {})
-    with pytest.raises(NotImplementedError):
         s.SQP(x, u, 8, 0.1, "PCG-SS", {"overloading": True})
 
 

@@ -13,12 +13,13 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TMPC_LIBRARY") or os.path.join(_HERE, "libtmpc.so")
 
-LINSYS = {"S": 1, "PCG-J": 2, "PCG-BJ": 3, "PCG-SS": 4, "PCG-0": 5}
+LINSYS = {"S": 1, "PCG-J": 2, "PCG-BJ": 3, "PCG-SS": 4, "PCG-0": 5, "N": 6}
 SOLVER_ILQR = 16
 PRECOND = {"J": 1, "BJ": 2, "SS": 3, "0": 4}
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
+_up = C.POINTER(C.c_uint64)
 
 
 class tmpc_options(C.Structure):
@@ -60,7 +61,7 @@ class tmpc_trace(C.Structure):
     _fields_ = [
         ("iteration", _ip), ("line_search_iteration", _ip), ("alpha", _dp), ("rho", _dp), ("J", _dp),
         ("c", _dp), ("merit", _dp), ("D", _dp), ("reduction_ratio", _dp), ("succeeded_line_search", _ip),
-        ("pcg_iters", _ip),
+        ("pcg_iters", _ip), ("singular", _ip), ("hard_active", _up),
     ]
 
 
@@ -94,8 +95,11 @@ SIGNATURES = {
     "tmpc_rollout_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p]),
     "tmpc_fd_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
     "tmpc_fd_grad_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
-    "tmpc_qp_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _dp, _dp, _dp, _ip, _dp,
-                                _dp, _dp, _dp]),
+    "tmpc_qp_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _ip,
+                                _dp, _dp, _dp, _dp]),
+    "tmpc_qp_hard_info": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _up, _dp, _dp, _dp, _ip]),
+    "tmpc_hard_pcg_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _ip, C.c_int, _dp, _dp,
+                                      C.c_double, C.c_int, _dp, _ip]),
     "tmpc_pcg_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, C.c_double,
                                  C.c_int, _dp, _ip, _dp, _dp, _dp]),
     "tmpc_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
@@ -158,6 +162,8 @@ def _ptr(a):
         return a.ctypes.data_as(_dp)
     if a.dtype == np.int32:
         return a.ctypes.data_as(_ip)
+    if a.dtype == np.uint64:
+        return a.ctypes.data_as(_up)
     raise TypeError(a.dtype)
 
 
@@ -289,24 +295,27 @@ class Context:
         return mu, lam, phi
 
     # ---------------------------------------------------------------- solves
-    def _trace_arrays(self, B):
+    def _trace_arrays(self, B, N=None, hard_active=False):
         W = int(self.options.max_iter_SQP_DDP) + 1
         arrays = {}
         for name, dt_ in [("iteration", np.int32), ("line_search_iteration", np.int32), ("alpha", np.float64),
                           ("rho", np.float64), ("J", np.float64), ("c", np.float64), ("merit", np.float64),
                           ("D", np.float64), ("reduction_ratio", np.float64),
-                          ("succeeded_line_search", np.int32), ("pcg_iters", np.int32)]:
+                          ("succeeded_line_search", np.int32), ("pcg_iters", np.int32), ("singular", np.int32)]:
             arrays[name] = np.zeros((B, W), dtype=dt_)
+        if hard_active:
+            arrays["hard_active"] = np.zeros((B, W, N), dtype=np.uint64)
         return arrays, tmpc_trace(**{k: _ptr(v) for k, v in arrays.items()})
 
-    def sqp_solve_batch(self, x, u, N, dt, method="PCG-SS", with_trace=True):
-        """x [B][nx][N], u [B][nu][N-1] -> dict of results (arrays per problem)."""
+    def sqp_solve_batch(self, x, u, N, dt, method="PCG-SS", with_trace=True, hard_active=False):
+        """x [B][nx][N], u [B][nu][N-1] -> dict of results (arrays per problem).  hard_active: also the
+        per-QP active-set bitmasks of the hard box limits, trace["hard_active"] [B][max_iter+1][N]."""
         x = _c64(x).copy()
         u = _c64(u).copy()
         self._check_traj(x, u, N)
         B = x.shape[0]
         out = {k: np.zeros(B, dtype=np.int32) for k in ("exit_sqp", "exit_soft", "outer_iter", "sqp_iter")}
-        arrays, tr = self._trace_arrays(B) if with_trace else ({}, None)
+        arrays, tr = self._trace_arrays(B, N, hard_active) if with_trace else ({}, None)
         self._check(self.lib.tmpc_sqp_solve_batch(
             self.h, B, int(N), float(dt), LINSYS[method], _ptr(x), _ptr(u), _ptr(out["exit_sqp"]),
             _ptr(out["exit_soft"]), _ptr(out["outer_iter"]), _ptr(out["sqp_iter"]),
@@ -379,8 +388,9 @@ class Context:
                     "tmpc_fd_grad_batch")
         return A, Bm, dq
 
-    def qp_batch(self, x, u, N, dt, rho, method="PCG-SS", want_blocks=True, guess=None):
-        """guess [B][N nx]: the PCG initial iterate (solveKKTSystem_Schur's options['guess']).
+    def qp_batch(self, x, u, N, dt, rho, method="PCG-SS", want_blocks=True, guess=None, xs=None):
+        """guess [B][N nx]: the PCG initial iterate (solveKKTSystem_Schur's options['guess']); xs [B][nx]: the
+        SQP's initial state (default x[:, :, 0]).
         With hard box limits set, want_blocks must be False and the lambda part of dxul holds the
         dynamics-row multipliers only (include/tmpc.h)."""
         x, u = _c64(x), _c64(u)
@@ -389,6 +399,8 @@ class Context:
         nu = u.shape[1]
         if guess is not None:
             guess = _c64(guess).reshape(B, N * nx)
+        if xs is not None:
+            xs = _c64(np.broadcast_to(np.asarray(xs, dtype=np.float64), (B, nx)))
         rho = _c64(np.broadcast_to(np.asarray(rho, dtype=np.float64), (B,)))
         L = (nx + nu) * (N - 1) + nx + nx * N
         dxul = np.zeros((B, L))
@@ -398,9 +410,38 @@ class Context:
         g = np.zeros((B, N * nx)) if want_blocks else None
         Pd = np.zeros((B, N, nx, nx)) if want_blocks else None
         self._check(self.lib.tmpc_qp_batch(self.h, B, int(N), float(dt), LINSYS[method], _ptr(rho), _ptr(x), _ptr(u),
-                                           _ptr(guess), _ptr(dxul), _ptr(iters), _ptr(Sd), _ptr(Sl), _ptr(g), _ptr(Pd)),
+                                           _ptr(xs), _ptr(guess), _ptr(dxul), _ptr(iters), _ptr(Sd), _ptr(Sl), _ptr(g),
+                                           _ptr(Pd)),
                     "tmpc_qp_batch")
         return dict(dxul=dxul, pcg_iters=iters, S_diag=Sd, S_lo=Sl, gamma=g, P_diag=Pd)
+
+    def qp_hard_info(self, B, N):
+        """Hard-limit detail of the last qp_batch (tmpc_qp_hard_info): dict with dim [B], active [B][N]
+        (uint64 bitmasks), lambda_hard [B][N][6n], S_band [B][dmax][2W+1], gamma [B][dmax], singular [B], W."""
+        sizes = np.zeros(2, dtype=np.int32)
+        self._check(self.lib.tmpc_qp_hard_info(self.h, int(B), int(N), _ptr(sizes), None, None, None, None, None,
+                                               None), "tmpc_qp_hard_info")
+        dmax, W = int(sizes[0]), int(sizes[1])
+        out = dict(dim=np.zeros(B, dtype=np.int32), active=np.zeros((B, N), dtype=np.uint64),
+                   lambda_hard=np.zeros((B, N, 6 * self.model.n)), S_band=np.zeros((B, dmax, 2 * W + 1)),
+                   gamma=np.zeros((B, dmax)), singular=np.zeros(B, dtype=np.int32))
+        self._check(self.lib.tmpc_qp_hard_info(self.h, int(B), int(N), _ptr(sizes), _ptr(out["dim"]),
+                                               _ptr(out["active"]), _ptr(out["lambda_hard"]), _ptr(out["S_band"]),
+                                               _ptr(out["gamma"]), _ptr(out["singular"])), "tmpc_qp_hard_info")
+        out["W"] = W
+        return out
+
+    def hard_pcg_batch(self, S_band, gamma, dim, nx, precond="SS", tol=1e-6, max_iter=100):
+        """The hard-limit QP's banded PCG (tmpc_hard_pcg_batch) on given S_band [B][dmax][2W+1]."""
+        S_band, gamma = _c64(S_band), _c64(gamma)
+        B, dmax, BW = S_band.shape
+        dim = np.ascontiguousarray(dim, dtype=np.int32)
+        lam = np.zeros((B, dmax))
+        it = np.zeros(B, dtype=np.int32)
+        self._check(self.lib.tmpc_hard_pcg_batch(self.h, B, int(nx), dmax, (BW - 1) // 2, _ptr(dim), PRECOND[precond],
+                                                 _ptr(S_band), _ptr(gamma), float(tol), int(max_iter), _ptr(lam),
+                                                 _ptr(it)), "tmpc_hard_pcg_batch")
+        return lam, it
 
     def pcg_batch(self, S_diag, S_lo, gamma, precond="SS", S_up=None, guess=None, tol=1e-6, max_iter=100,
                   trace=True):

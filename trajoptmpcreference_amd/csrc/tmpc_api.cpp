@@ -61,6 +61,8 @@ struct tmpc_ctx {
   std::vector<hipEvent_t> event_pool;
   int* h_count = nullptr;  // pinned
   int64_t last_counters[4] = {0, 0, 0, 0};
+  // shape of the last tmpc_qp_batch with hard box limits (tmpc_qp_hard_info); B = 0: none
+  struct { int B, N, dmax, W; } hard_last{0, 0, 0, 0};
 };
 
 static int fail(tmpc_ctx* c, const char* fmt, ...) {
@@ -200,10 +202,12 @@ static std::vector<double> alpha_list(const tmpc_options& o) {
   return a;
 }
 
-// 0 = method S (direct block-tridiagonal solve, k_btsolve)
+// 0 = method S (direct block-tridiagonal solve, k_btsolve); method N (the dense KKT solve) has the
+// same solution and takes the same direct path (include/tmpc.h)
 static int precond_of(int linsys) {
   switch (linsys) {
     case TMPC_LINSYS_S: return 0;
+    case TMPC_LINSYS_N: return 0;
     case TMPC_LINSYS_PCG_J: return PRECOND_J;
     case TMPC_LINSYS_PCG_BJ: return PRECOND_BJ;
     case TMPC_LINSYS_PCG_SS: return PRECOND_SS;
@@ -237,6 +241,8 @@ struct Work {
   double* lam_keep;                  // where the PCG path stores lambda (nullable; warm start)
   HardArgs* hard;                    // hard box constraints: the variable-row QP (tmpc_hard.hip)
   double* Sg;                        // S / P^-1 rows in HBM past 1024 rows (k_qp<..., GM>), else null
+  unsigned long long* tr_active;     // hard limits: per-QP active-set bitmasks into the trace (nullable)
+  int Wtr;                           // trace row stride
 };
 
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
@@ -284,6 +290,9 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     h.du = w.du;
     h.tol = ctx->opts.exit_tolerance_linSys;
     h.max_iter = ctx->opts.max_iter_linSys;
+    h.iter = st.iter;
+    h.Wtr = w.Wtr;
+    h.tr_active = w.tr_active;
     HIP_OK(hipMemsetAsync(w.iters, 0, sizeof(int) * B, ctx->stream));
     const char* names[3] = {"hard_schur", precond == 0 ? "hard_direct" : "hard_pcg", "dxu"};
     for (int ph = 0; ph < 3; ++ph) {
@@ -336,7 +345,7 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   BUF(double, du, (size_t)B * K * nj);
   BUF(int, iters, (size_t)B);
   w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters,
-           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
   if (N * nx >= qp_gm_min_rows()) {   // the GM QP kernel's rows of S / P^-1
     BUF(double, qp_gm, qp_gm_doubles(B, N, nx));
     w.Sg = qp_gm;
@@ -386,7 +395,10 @@ static int alloc_trace(tmpc_ctx* ctx, int B, int W, TraceDev& tr) {
   BUF(double, tr_ratio, (size_t)B * W);
   BUF(int, tr_acc, (size_t)B * W);
   BUF(int, tr_pcg, (size_t)B * W);
-  tr = TraceDev{tr_iteration, tr_ls, tr_alpha, tr_rho, tr_J, tr_c, tr_merit, tr_D, tr_ratio, tr_acc, tr_pcg};
+  BUF(int, tr_sing, (size_t)B * W);
+  HIP_OK(hipMemsetAsync(tr_sing, 0, (size_t)B * W * sizeof(int), ctx->stream));   // iLQR never sets it
+  tr = TraceDev{tr_iteration, tr_ls, tr_alpha, tr_rho, tr_J, tr_c, tr_merit, tr_D, tr_ratio, tr_acc, tr_pcg, tr_sing,
+                nullptr};
   return 0;
 }
 
@@ -438,6 +450,11 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
   BUF(int, hd_rknot, (size_t)B * hard.dmax);
   BUF(int, hd_ridx, (size_t)B * hard.dmax);
   BUF(int, hd_pk, (size_t)B * hard.dmax * 2);
+  BUF(int, hd_slot, (size_t)B * N * hard.rmax);
+  BUF(unsigned long long, hd_amask, (size_t)B * N);
+  BUF(int, hd_sing, (size_t)B);
+  HIP_OK(hipMemsetAsync(hd_sing, 0, (size_t)B * sizeof(int), ctx->stream));
+  hard.hslot = hd_slot; hard.amask = hd_amask; hard.sing = hd_sing;
   BUF(double, hd_Y, (size_t)B * hard.dmax * 2 * (nx + nj));
   BUF(double, hd_Sb, (size_t)B * hard.dmax * BW);
   BUF(double, hd_gam, (size_t)B * hard.dmax);
@@ -510,7 +527,7 @@ static int lockstep_loop(tmpc_ctx* ctx, long cap, int* active_count, Body body) 
 }
 
 static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
-                      TraceDev* tr_out, bool keep_warm = false) {
+                      TraceDev* tr_out, bool keep_warm = false, bool hard_trace = false) {
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
   const int precond = precond_of(linsys);
@@ -563,6 +580,13 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     if ((rc = setup_hard(ctx, B, N, T, precond, hard))) return rc;
     hterms = hard.hterms;
     w.hard = &hard;
+    w.Wtr = W;
+    if (hard_trace) {   // per-QP active-set bitmasks in the trace (tmpc_trace.hard_active)
+      BUF(unsigned long long, tr_hard, (size_t)B * W * N);
+      HIP_OK(hipMemsetAsync(tr_hard, 0, (size_t)B * W * N * sizeof(unsigned long long), ctx->stream));
+      w.tr_active = tr_hard;
+      tr.hard_active = tr_hard;
+    }
   }
   if (o.pcg_warm_start && precond != 0 && ctx->hlim.any_hard)
     return fail(ctx, "pcg_warm_start with hard box constraints: the Schur dimension changes with the active set "
@@ -609,7 +633,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     }
     Timed t(ctx, "ls_decide");
     launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
-                     st, w.iters, tr, ac, prob_counters, hterms);
+                     st, w.iters, tr, ac, prob_counters, hterms, (w.hard && precond == 0) ? hard.sing : nullptr);
     HIP_OK(hipGetLastError());
     return 0;
   };
@@ -1071,7 +1095,8 @@ int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, dou
   HIP_OK(hipMemcpyAsync(io_x, x, xn * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(io_u, u, un * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   TraceDev tr;
-  if ((rc = sqp_device(ctx, B, N, dt, linsys, io_x, io_u, &tr))) return rc;
+  const bool hard_trace = trace && trace->hard_active && ctx->hlim.any_hard;
+  if ((rc = sqp_device(ctx, B, N, dt, linsys, io_x, io_u, &tr, false, hard_trace))) return rc;
   HIP_OK(hipMemcpy(x, io_x, xn * sizeof(double), hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(u, io_u, un * sizeof(double), hipMemcpyDeviceToHost));
   if (exit_sqp) HIP_OK(hipMemcpy(exit_sqp, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
@@ -1093,7 +1118,14 @@ int tmpc_sqp_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, dou
     CP(reduction_ratio, ratio, double)
     CP(succeeded_line_search, accepted, int)
     CP(pcg_iters, pcg_iters, int)
+    CP(singular, singular, int)
 #undef CP
+    if (trace->hard_active) {
+      if (hard_trace)
+        HIP_OK(hipMemcpy(trace->hard_active, tr.hard_active, n * N * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      else
+        memset(trace->hard_active, 0, n * N * sizeof(uint64_t));
+    }
   }
   return 0;
 }
@@ -1134,7 +1166,9 @@ int tmpc_ilqr_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, double* x, dou
     CP(reduction_ratio, ratio, double)
     CP(succeeded_line_search, accepted, int)
     CP(pcg_iters, pcg_iters, int)
+    CP(singular, singular, int)
 #undef CP
+    if (trace->hard_active) memset(trace->hard_active, 0, n * N * sizeof(uint64_t));
   }
   return 0;
 }
@@ -1302,8 +1336,8 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
 }
 
 int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
-                  const double* u, const double* guess, double* dxul, int32_t* pcg_iters, double* S_diag,
-                  double* S_lo, double* gamma, double* P_diag) {
+                  const double* u, const double* xs, const double* guess, double* dxul, int32_t* pcg_iters,
+                  double* S_diag, double* S_lo, double* gamma, double* P_diag) {
   if (!ctx) return -1;
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
@@ -1328,8 +1362,11 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   HIP_OK(hipMemcpyAsync(st.rho, rho, sizeof(double) * B, hipMemcpyHostToDevice, ctx->stream));
   launch_init_state(ctx->stream, B, 0.0, ProbState{st.drho, st.drho, st.J, st.c, st.merit, st.iter, st.active,
                                                    st.need_grad, st.exit_sqp}, nullptr);
-  HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), io_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
-                          hipMemcpyDeviceToDevice, ctx->stream));
+  if (xs)   // the SQP's initial state (solveKKTSystem_Schur's xs argument, :361): c_0 = x_0 - xs
+    HIP_OK(hipMemcpyAsync(w.xs, xs, sizeof(double) * B * nx, hipMemcpyHostToDevice, ctx->stream));
+  else
+    HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), io_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
+                            hipMemcpyDeviceToDevice, ctx->stream));
   if (guess && precond != 0) {
     BUF(double, io_guess, (size_t)B * N * nx);
     HIP_OK(hipMemcpyAsync(io_guess, guess, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
@@ -1342,9 +1379,11 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
     if ((rc = setup_hard(ctx, B, N, 0, precond, hard))) return rc;
     w.hard = &hard;
   }
+  ctx->hard_last = {0, 0, 0, 0};
   if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, !ctx->hlim.any_hard))) return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (ctx->hlim.any_hard) {
+    ctx->hard_last = {B, N, hard.dmax, hard.W};
     std::vector<int> roff((size_t)B * N);
     std::vector<double> lh((size_t)B * hard.dmax);
     HIP_OK(hipMemcpy(roff.data(), hard.roff, roff.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -1378,6 +1417,105 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   if (gamma) HIP_OK(hipMemcpy(gamma, w.gam, sizeof(double) * B * N * nx, hipMemcpyDeviceToHost));
   if (P_diag && precond != PRECOND_J && precond != 0)
     HIP_OK(hipMemcpy(P_diag, w.Pd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim, uint64_t* active,
+                      double* lambda_hard, double* S_band, double* gamma, int32_t* singular) {
+  if (!ctx) return -1;
+  const auto& hl = ctx->hard_last;
+  if (hl.B == 0) return fail(ctx, "tmpc_qp_hard_info: the last tmpc_qp_batch ran without hard box limits");
+  if (hl.B != B || hl.N != N)
+    return fail(ctx, "tmpc_qp_hard_info: the last hard-limit QP was B=%d N=%d, asked for B=%d N=%d", hl.B, hl.N, B, N);
+  hipSetDevice(ctx->device);
+  const int nj = ctx->hmodel.n, S6 = 6 * nj;
+  if (sizes) {
+    sizes[0] = hl.dmax;
+    sizes[1] = hl.W;
+  }
+  auto dev = [&](const char* name) { return ctx->bufs[name].ptr; };
+  if (dim) HIP_OK(hipMemcpy(dim, dev("hd_dim"), sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (active) HIP_OK(hipMemcpy(active, dev("hd_amask"), sizeof(uint64_t) * B * N, hipMemcpyDeviceToHost));
+  if (singular) HIP_OK(hipMemcpy(singular, dev("hd_sing"), sizeof(int) * B, hipMemcpyDeviceToHost));
+  const size_t BW = 2 * (size_t)hl.W + 1;
+  if (S_band) HIP_OK(hipMemcpy(S_band, dev("hd_Sb"), sizeof(double) * B * hl.dmax * BW, hipMemcpyDeviceToHost));
+  if (gamma) HIP_OK(hipMemcpy(gamma, dev("hd_gam"), sizeof(double) * B * hl.dmax, hipMemcpyDeviceToHost));
+  if (lambda_hard) {
+    // the hard rows' multipliers by slot t * 2n + e (0 where the slot has no row)
+    int rmax = 0;
+    for (int t = 0; t < 3; ++t) rmax += ctx->hlim.hard[t] != HARD_NONE ? 2 * nj : 0;
+    std::vector<int> cnt((size_t)B * N), hoff((size_t)B * N), slot((size_t)B * N * rmax);
+    std::vector<double> lam((size_t)B * hl.dmax);
+    HIP_OK(hipMemcpy(cnt.data(), dev("hd_cnt"), cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(hoff.data(), dev("hd_hoff"), hoff.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(slot.data(), dev("hd_slot"), slot.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(lam.data(), dev("hd_lam"), lam.size() * sizeof(double), hipMemcpyDeviceToHost));
+    memset(lambda_hard, 0, sizeof(double) * B * N * S6);
+    for (int b = 0; b < B; ++b)
+      for (int k = 0; k < N; ++k) {
+        const size_t bk = (size_t)b * N + k;
+        for (int r = 0; r < cnt[bk] && r < rmax; ++r)
+          lambda_hard[bk * S6 + slot[bk * rmax + r]] = lam[(size_t)b * hl.dmax + hoff[bk] + r];
+      }
+  }
+  return 0;
+}
+
+int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int32_t* dim, int precond,
+                        const double* S_band, const double* gamma, double tol, int max_iter, double* lambda,
+                        int32_t* iters) {
+  if (!ctx) return -1;
+  if (B < 1 || nx < 2 || nx > 14 || (nx & 1) || dmax < 1 || W < 0)
+    return fail(ctx, "bad sizes B=%d nx=%d dmax=%d W=%d", B, nx, dmax, W);
+  if (precond != PRECOND_J && precond != PRECOND_BJ && precond != PRECOND_SS && precond != PRECOND_NONE)
+    return fail(ctx, "preconditioner %d: valid are J=1, BJ=2, SS=3, 0=4 (PCG.py:52-55)", precond);
+  if ((5 * (size_t)dmax + 16) * sizeof(double) > 160 * 1024)
+    return fail(ctx, "dmax = %d exceeds the PCG's LDS vectors (max 4092)", dmax);
+  if (max_iter < 0) return fail(ctx, "max_iter must be >= 0");
+  if (!dim || !S_band || !gamma) return fail(ctx, "null input");
+  for (int b = 0; b < B; ++b)
+    if (dim[b] < 1 || dim[b] > dmax) return fail(ctx, "dim[%d] = %d outside [1, %d]", b, dim[b], dmax);
+  hipSetDevice(ctx->device);
+  const size_t BW = 2 * (size_t)W + 1, nbmax = dmax / nx + 1;
+  BUF(double, hp_Sb, (size_t)B * dmax * BW);
+  BUF(double, hp_gam, (size_t)B * dmax);
+  BUF(double, hp_lam, (size_t)B * dmax);
+  BUF(int, hp_dim, (size_t)B);
+  BUF(int, hp_act, (size_t)B);
+  BUF(int, hp_it, (size_t)B);
+  BUF(double, hp_Pd, (size_t)B * nbmax * nx * nx);
+  BUF(double, hp_Pl, (size_t)B * nbmax * nx * nx);
+  BUF(double, hp_Pt, (size_t)B * nbmax * nx * nx);
+  HIP_OK(hipMemcpyAsync(hp_Sb, S_band, sizeof(double) * B * dmax * BW, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hp_gam, gamma, sizeof(double) * B * dmax, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hp_dim, dim, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+  std::vector<int> ones(B, 1);
+  HIP_OK(hipMemcpyAsync(hp_act, ones.data(), sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+  HardArgs h{};
+  h.B = B;
+  h.phase = 1;
+  h.precond = precond;
+  h.dmax = dmax;
+  h.W = W;
+  h.tol = tol;
+  h.max_iter = max_iter;
+  h.active = hp_act;
+  h.dim = hp_dim;
+  h.Sb = hp_Sb;
+  h.gam = hp_gam;
+  h.Pd = hp_Pd;
+  h.Pl = hp_Pl;
+  h.Ptmp = hp_Pt;
+  h.lam = hp_lam;
+  h.iters = hp_it;
+  {
+    Timed t(ctx, "hard_pcg");
+    LAUNCH_OK(launch_hard(ctx->stream, nx / 2, h));
+  }
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  resolve_timings(ctx);
+  if (lambda) HIP_OK(hipMemcpy(lambda, hp_lam, sizeof(double) * B * dmax, hipMemcpyDeviceToHost));
+  if (iters) HIP_OK(hipMemcpy(iters, hp_it, sizeof(int) * B, hipMemcpyDeviceToHost));
   return 0;
 }
 

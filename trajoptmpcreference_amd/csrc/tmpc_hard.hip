@@ -27,7 +27,16 @@
 //   k_hard_dxu      dxu_k = Ghat_k (g_k - (C^T lambda)_k)
 //   k_hard_ls       the hard terms of totalHardConstraintViolation (:286-293) per trial point
 // Parity of these semantics is pinned for the 1-link arm by tests/golden/hard_*.npz.
+//
+// Summation order.  PCG on these Schur complements is order sensitive (the trailing dim mod nx rows
+// have no preconditioner rows): two valid orders stop up to 5 iterations apart on the same S.  Every
+// kernel of this file therefore rounds each product and sum on its own (fp contraction off below) and
+// k_hard_pcg sums in the canonical order that oracle/hard.py pcg_canonical restates -- sequential
+// sums from 0.0, per-thread dot partials over 256 threads, a 64-lane xor butterfly, a fan-in over the
+// 4 waves -- so that on identical S and gamma the two are bitwise equal (tests/test_gpu_hard.py).
 #include "tmpc_internal.h"
+
+#pragma clang fp contract(off)
 
 namespace tmpc {
 
@@ -35,11 +44,15 @@ __device__ __forceinline__ bool h_use_QF(const CostDev* C, int k, int N) {
   return (k == N - 1) || (C->QF_start >= 0 && k >= C->QF_start);
 }
 
-// the knot's rows in the reference order; returns the count (<= rmax)
+// the knot's rows in the reference order; returns the count (<= rmax).  slot (nullable) = t * 2 NJ + e,
+// the row's (limit kind, entry of [z - lb; ub - z]); *mask (nullable) = the active-set bitmask of the
+// knot, bit slot set for every violated entry (ACTIVE_SET's rows, FULL_SET's nonzero rows)
 template <int NJ>
 __device__ __forceinline__ int hard_knot_rows(const ConstrDev* __restrict__ Cs, const double* z, bool terminal,
-                                              int rmax, int* col, double* sgn, double* val) {
+                                              int rmax, int* col, double* sgn, double* val, int* slot = nullptr,
+                                              unsigned long long* mask = nullptr) {
   int m = 0;
+  unsigned long long bits = 0ull;
   for (int t = 0; t < 3; ++t) {
     const int hm = Cs->hard[t];
     if (hm == HARD_NONE || (t == 2 && terminal)) continue;
@@ -49,14 +62,17 @@ __device__ __forceinline__ int hard_knot_rows(const ConstrDev* __restrict__ Cs, 
       const double v = e < NJ ? zi - Cs->lb[t][i] : Cs->ub[t][i] - zi;
       const bool act = v < 0.0;
       if (hm == HARD_ACTIVE && !act) continue;
+      if (act) bits |= 1ull << (t * 2 * NJ + e);
       if (m < rmax) {
         col[m] = t * NJ + i;
         sgn[m] = act ? (e < NJ ? 1.0 : -1.0) : 0.0;
         val[m] = v;
+        if (slot) slot[m] = t * 2 * NJ + e;
       }
       ++m;
     }
   }
+  if (mask) *mask = bits;
   return m;
 }
 
@@ -65,7 +81,10 @@ __global__ void __launch_bounds__(256) k_hard_rows(const ConstrDev* __restrict__
                                                    const double* __restrict__ x, const double* __restrict__ u,
                                                    const int* __restrict__ active, int* __restrict__ cnt,
                                                    int* __restrict__ hcol, double* __restrict__ hsgn,
-                                                   double* __restrict__ hval) {
+                                                   double* __restrict__ hval, int* __restrict__ hslot,
+                                                   unsigned long long* __restrict__ amask,
+                                                   const int* __restrict__ iter, int Wtr,
+                                                   unsigned long long* __restrict__ tr_active) {
   constexpr int NX = 2 * NJ;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * N) return;
@@ -76,7 +95,11 @@ __global__ void __launch_bounds__(256) k_hard_rows(const ConstrDev* __restrict__
   for (int m = 0; m < NX; ++m) z[m] = x[((size_t)b * NX + m) * N + k];
   for (int m = 0; m < NJ; ++m) z[NX + m] = k < K ? u[((size_t)b * NJ + m) * K + k] : 0.0;
   const size_t o = (size_t)gid * rmax;
-  cnt[gid] = hard_knot_rows<NJ>(Cs, z, k == K, rmax, hcol + o, hsgn + o, hval + o);
+  unsigned long long bits;
+  cnt[gid] = hard_knot_rows<NJ>(Cs, z, k == K, rmax, hcol + o, hsgn + o, hval + o, hslot + o, &bits);
+  amask[gid] = bits;
+  // the QP's active set in the trace row of this SQP iteration (row iter + 1, as k_ls_decide's)
+  if (tr_active) tr_active[((size_t)b * Wtr + iter[b] + 1) * N + k] = bits;
 }
 
 // Row layout of one problem: roff[j] = first row of R_j, hoff[k] = first row of H_k, dim;
@@ -473,13 +496,24 @@ __global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int pr
   if (threadIdx.x == 0) iters[b] = it_done;
 }
 
-// Method S: S lambda = gamma by banded elimination (S is negative definite: no pivoting).  Rows
-// that are identically zero (FULL_SET's inactive constraints) get lambda = 0: the minimum-norm
-// least-squares answer of the reference's lstsq fallback (:431-436).
-__global__ void __launch_bounds__(256) k_hard_direct(int B, int W, int dmax, const int* __restrict__ active,
-                                                     const int* __restrict__ dim, const double* __restrict__ Sb,
-                                                     const double* __restrict__ gam, double* __restrict__ M,
-                                                     double* __restrict__ rhs, double* __restrict__ lam) {
+// Method S (and N): S lambda = gamma by banded elimination (S is negative definite: no pivoting).
+// Where S is singular the reference's np.linalg.solve raises and it takes lstsq's minimum-norm
+// least-squares answer, setting `singular` (:353-357, 431-436).  S is singular in exactly two
+// structural ways here, both handled in closed form before the elimination:
+//   * identically zero rows (FULL_SET's inactive constraints): lambda = 0 for them, the minimum norm;
+//   * a knot-0 hard row on a state entry (xs violates a joint / velocity limit) duplicates the
+//     initial-state row R_0 of that entry up to its sign s: S row / column b = s row / column a
+//     exactly.  The least-squares equations for the pair reduce to one, row a with gamma_a' =
+//     (gamma_a + s gamma_b) / 2 on lambda' = lambda_a + s lambda_b, and the minimum-norm split is
+//     lambda_a = lambda' / 2, lambda_b = s lambda' / 2 (the null vector e_b - s e_a is orthogonal).
+// sing[b] = 1 when either happened (the trace's `singular`).
+__global__ void __launch_bounds__(256) k_hard_direct(int B, int N, int NX, int W, int dmax, int rmax,
+                                                     const int* __restrict__ active, const int* __restrict__ dim,
+                                                     const int* __restrict__ hoff, const int* __restrict__ cnt,
+                                                     const int* __restrict__ hcol, const double* __restrict__ hsgn,
+                                                     const double* __restrict__ Sb, const double* __restrict__ gam,
+                                                     double* __restrict__ M, double* __restrict__ rhs,
+                                                     double* __restrict__ lam, int* __restrict__ sing) {
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
@@ -489,8 +523,47 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int W, int dmax, con
   double* y = rhs + (size_t)b * dmax;
   __shared__ double fcol[1024];
   __shared__ double red[16];
+  __shared__ int s_dup_a[64], s_dup_b[64];
+  __shared__ double s_dup_s[64];
+  __shared__ int s_ndup, s_sing;
   for (int e = threadIdx.x; e < D * BW; e += blockDim.x) Mb[e] = S[e];
   for (int a = threadIdx.x; a < D; a += blockDim.x) y[a] = gam[(size_t)b * dmax + a];
+  if (threadIdx.x == 0) {
+    // knot-0 hard rows on state entries: duplicates of R_0 rows (rows 0..NX-1)
+    int nd = 0;
+    const int c0 = cnt[(size_t)b * N], h0 = hoff[(size_t)b * N];
+    const size_t hb = (size_t)b * N * rmax;
+    for (int s = 0; s < c0 && s < rmax && nd < 64; ++s) {
+      const double sg = hsgn[hb + s];
+      const int col = hcol[hb + s];
+      if (sg != 0.0 && col < NX) {
+        s_dup_a[nd] = col;
+        s_dup_b[nd] = h0 + s;
+        s_dup_s[nd] = sg;
+        ++nd;
+      }
+    }
+    s_ndup = nd;
+    s_sing = nd > 0;
+  }
+  __syncthreads();
+  const int nd = s_ndup;
+  if (nd > 0 && threadIdx.x == 0) {
+    for (int i = 0; i < nd; ++i) {
+      const int a = s_dup_a[i], bb = s_dup_b[i];
+      y[a] = 0.5 * (y[a] + s_dup_s[i] * y[bb]);
+      y[bb] = 0.0;
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < nd; ++i) {   // row and column b -> identity
+    const int bb = s_dup_b[i];
+    for (int o = threadIdx.x; o < BW; o += blockDim.x) {
+      Mb[(size_t)bb * BW + o] = o == W ? 1.0 : 0.0;
+      const int r = bb - W + o;    // column bb of row r sits at offset bb - r + W = 2W - o
+      if (r >= 0 && r < D && r != bb) Mb[(size_t)r * BW + (2 * W - o)] = 0.0;
+    }
+  }
   __syncthreads();
   // zero rows -> identity rows with a zero right-hand side
   for (int a = threadIdx.x; a < D; a += blockDim.x) {
@@ -499,6 +572,7 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int W, int dmax, con
     if (zero) {
       Mb[(size_t)a * BW + W] = 1.0;
       y[a] = 0.0;
+      s_sing = 1;
     }
   }
   __syncthreads();
@@ -527,6 +601,15 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int W, int dmax, con
     if (threadIdx.x == 0) y[p] = (y[p] - s) / Mb[(size_t)p * BW + W];
     __syncthreads();
   }
+  if (threadIdx.x == 0) {   // the minimum-norm split of the merged duplicate pairs
+    for (int i = 0; i < nd; ++i) {
+      const double l = y[s_dup_a[i]];
+      y[s_dup_a[i]] = 0.5 * l;
+      y[s_dup_b[i]] = s_dup_s[i] * (0.5 * l);
+    }
+    sing[b] = s_sing;
+  }
+  __syncthreads();
   for (int a = threadIdx.x; a < D; a += blockDim.x) lam[(size_t)b * dmax + a] = y[a];
 }
 
@@ -635,7 +718,7 @@ struct LaunchHard {
     const int B = h.B, N = h.N;
     if (h.phase == 0) {
       hipLaunchKernelGGL((k_hard_rows<NJ>), HGRID(B * N, 256), 0, s, h.Cs, B, N, h.rmax, h.x, h.u, h.active, h.cnt,
-                         h.hcol, h.hsgn, h.hval);
+                         h.hcol, h.hsgn, h.hval, h.hslot, h.amask, h.iter, h.Wtr, h.tr_active);
       hipLaunchKernelGGL(k_hard_layout, dim3(B), dim3(64), 0, s, B, N, NX, h.rmax, h.active, h.cnt, h.roff, h.hoff,
                          h.dim, h.rkind, h.rknot, h.ridx, h.dmax);
       hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), 0, s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
@@ -643,8 +726,8 @@ struct LaunchHard {
                          h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam);
     } else if (h.phase == 1) {
       if (h.precond == 0) {
-        hipLaunchKernelGGL(k_hard_direct, dim3(B), dim3(256), 0, s, B, h.W, h.dmax, h.active, h.dim, h.Sb, h.gam, h.M,
-                           h.rhs, h.lam);
+        hipLaunchKernelGGL(k_hard_direct, dim3(B), dim3(256), 0, s, B, N, NX, h.W, h.dmax, h.rmax, h.active, h.dim,
+                           h.hoff, h.cnt, h.hcol, h.hsgn, h.Sb, h.gam, h.M, h.rhs, h.lam, h.sing);
       } else {
         const size_t lds = ((size_t)5 * h.dmax + 16) * sizeof(double);
         hipLaunchKernelGGL((k_hard_pcg<NX>), dim3(B), dim3(256), lds, s, B, h.W, h.dmax, h.precond, h.active, h.dim,

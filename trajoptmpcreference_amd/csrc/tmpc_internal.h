@@ -65,6 +65,8 @@ struct TraceDev {
   double* ratio;
   int* accepted;
   int* pcg_iters;
+  int* singular;                  // the QP took the least-squares answer (reference: self.singular)
+  unsigned long long* hard_active;   // [B][W][N] per-knot active-set bitmasks of the QP (nullable)
 };
 
 // f32: rigid-body dynamics (and, for launch_ilqr_backward, the Riccati sweep) in fp32 --
@@ -117,7 +119,8 @@ void launch_sum_counters(hipStream_t s, int B, const unsigned long long* pc, uns
 void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
-                      int* active_count, unsigned long long* counters, const double* hterms);
+                      int* active_count, unsigned long long* counters, const double* hterms,
+                      const int* qp_singular = nullptr);
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active);
 // st / act_init / rho_init: the per-problem outer loop (null act_init: lock-step, tmpc_kernels.hip)
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
@@ -159,6 +162,12 @@ struct HardArgs {
   const int* active;
   int *cnt, *hcol, *roff, *hoff, *dim, *rkind, *rknot, *ridx, *PK, *iters;
   double *hsgn, *hval, *Y, *Sb, *gam, *Pd, *Pl, *Ptmp, *M, *rhs, *lam, *dx, *du, *hterms;
+  int* hslot;                     // [B][N][rmax] t * 2n + e of each row
+  unsigned long long* amask;      // [B][N] active-set bitmask per knot (bit t * 2n + e)
+  int* sing;                      // [B] the direct solve took the least-squares answer (singular S)
+  const int* iter;                // per-problem SQP iteration (trace row iter + 1)
+  int Wtr;                        // trace row stride (max_iter_SQP_DDP + 1)
+  unsigned long long* tr_active;  // [B][Wtr][N] trace copy of amask (nullable)
 };
 int launch_hard(hipStream_t s, int nj, const HardArgs& h);
 int hard_set_max_lds();

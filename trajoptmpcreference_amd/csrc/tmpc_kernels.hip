@@ -1411,7 +1411,8 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
                                                   const int* __restrict__ pcg_iters, TraceDev tr,
                                                   int* __restrict__ active_count,
                                                   unsigned long long* __restrict__ counters,
-                                                  const double* __restrict__ hterms) {
+                                                  const double* __restrict__ hterms,
+                                                  const int* __restrict__ qp_singular) {
   const int b = blockIdx.x;
   if (!st.active[b]) return;
   __shared__ double sJ[64], sC[64], sD[64];
@@ -1449,7 +1450,7 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
       const size_t e = (size_t)b * W;
       tr.iteration[e] = 0; tr.ls_iter[e] = 0; tr.alpha[e] = 1.0; tr.rho[e] = st.rho[b];
       tr.J[e] = J; tr.c[e] = c; tr.merit[e] = J + o.mu * c; tr.D[e] = __builtin_nan(""); tr.ratio[e] = __builtin_nan("");
-      tr.accepted[e] = 0; tr.pcg_iters[e] = 0;
+      tr.accepted[e] = 0; tr.pcg_iters[e] = 0; tr.singular[e] = 0;
       s_choice = -2;
     } else {
       const double J = st.J[b], c = st.c[b], merit = st.merit[b];
@@ -1497,6 +1498,7 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
       tr.J[e] = error ? J : Jn; tr.c[e] = error ? c : cn; tr.merit[e] = error ? merit : mn;
       tr.D[e] = D; tr.ratio[e] = ratio; tr.accepted[e] = error ? 0 : 1;
       tr.pcg_iters[e] = pcg_iters ? pcg_iters[b] : 0;
+      tr.singular[e] = qp_singular ? qp_singular[b] : 0;
       // check_for_exit_or_error
       bool done = false;
       if (error) {
@@ -1767,9 +1769,10 @@ int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* S
 void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
-                      int* active_count, unsigned long long* counters, const double* hterms) {
+                      int* active_count, unsigned long long* counters, const double* hterms,
+                      const int* qp_singular) {
   hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u, dx, du,
-                     st, pcg_iters, tr, active_count, counters, hterms);
+                     st, pcg_iters, tr, active_count, counters, hterms, qp_singular);
 }
 
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active) {

@@ -10,9 +10,13 @@ the initial states broadcast from rank 0 and the per-problem result summaries
 gathered back; the max over ranks of the timed region uses the same
 communicator.
 
-The RCCL unique id is handed from rank 0 to the other ranks through a file
-next to the launcher: its name includes MASTER_PORT and the parent (launcher)
-pid that the ranks of one launch share.
+The RCCL unique id travels from rank 0 to the other ranks over a TCP socket at
+MASTER_ADDR : MASTER_PORT + 1 (TMPC_COMM_PORT overrides the port), so any
+launcher that exports the usual rendezvous variables works, whatever the
+process tree.  Every rank sends a hash of its run configuration (batch size,
+horizon, model, cost, options, limits) with its request; rank 0 refuses a
+mismatch and every rank fails fast instead of solving different problems.
+A launcher that prefers a shared file sets TMPC_COMM_ID_FILE.
 """
 import os
 import time
@@ -34,18 +38,97 @@ def shard_range(rank: int, B: int):
     return rank * B, (rank + 1) * B
 
 
-def _id_path():
-    p = os.environ.get("TMPC_COMM_ID_FILE")
-    if p:
-        return p
-    return f"/tmp/tmpc_rccl_id_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+def config_hash(*parts) -> bytes:
+    """sha256 over the run configuration: numpy arrays (shape, dtype, bytes), bytes, or anything JSON-able."""
+    import hashlib
+    import json
+    h = hashlib.sha256()
+    for p in parts:
+        if isinstance(p, np.ndarray):
+            h.update(repr((p.shape, p.dtype.str)).encode())
+            h.update(np.ascontiguousarray(p).tobytes())
+        elif isinstance(p, (bytes, bytearray)):
+            h.update(bytes(p))
+        else:
+            h.update(json.dumps(p, sort_keys=True, default=str).encode())
+    return h.digest()
 
 
-def exchange_unique_id(rank: int, timeout_s: float = 120.0) -> bytes:
-    """Rank 0 creates the RCCL unique id and publishes it atomically; the others wait for it."""
-    path = _id_path()
+def _comm_addr():
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("TMPC_COMM_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
+    return host, port
+
+
+def _recv_exact(sock, n):
+    buf = b""
+    while len(buf) < n:
+        chunk = sock.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError("peer closed the RCCL id exchange")
+        buf += chunk
+    return buf
+
+
+def exchange_unique_id(rank: int, world: int, cfg: bytes = b"\0" * 32, timeout_s: float = 120.0,
+                       make_id=None) -> bytes:
+    """Rank 0 creates the RCCL unique id (make_id, default ncclGetUniqueId) and serves it over TCP to
+    the world - 1 other ranks, each of which first sends (rank, cfg); a rank whose cfg differs from rank
+    0's gets a refusal and raises, and rank 0 raises after answering everyone.  With TMPC_COMM_ID_FILE
+    set, the id goes through that file instead (no config check)."""
+    import socket
+    import struct
+    make_id = make_id or _native.comm_unique_id
+    if len(cfg) != 32:
+        raise ValueError("cfg must be a 32-byte digest (config_hash)")
+    path = os.environ.get("TMPC_COMM_ID_FILE")
+    if path:
+        return _exchange_via_file(rank, path, timeout_s, make_id)
+    host, port = _comm_addr()
+    n_id = _native.COMM_ID_BYTES
     if rank == 0:
-        uid = _native.comm_unique_id()
+        uid = make_id()
+        bad = []
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as srv:
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((host, port))
+            srv.listen(max(1, world))
+            srv.settimeout(timeout_s)
+            for _ in range(world - 1):
+                conn, _ = srv.accept()
+                with conn:
+                    conn.settimeout(timeout_s)
+                    r, peer_cfg = struct.unpack("<i32s", _recv_exact(conn, 36))
+                    if peer_cfg == cfg:
+                        conn.sendall(b"\x00" + uid)
+                    else:
+                        bad.append(r)
+                        conn.sendall(b"\x01" + cfg + b"\0" * (n_id - 32))
+        if bad:
+            raise RuntimeError(f"rank 0: ranks {sorted(bad)} run a different configuration "
+                               "(batch / horizon / model / cost / options / limits); refusing to start")
+        return uid
+    t0 = time.time()
+    while True:
+        try:
+            with socket.create_connection((host, port), timeout=5.0) as c:
+                c.settimeout(timeout_s)
+                c.sendall(struct.pack("<i32s", rank, cfg))
+                reply = _recv_exact(c, 1 + n_id)
+            break
+        except (ConnectionRefusedError, socket.timeout, OSError):
+            if time.time() - t0 > timeout_s:
+                raise TimeoutError(f"rank {rank}: no RCCL id server at {host}:{port} after {timeout_s} s")
+            time.sleep(0.05)
+    if reply[0] != 0:
+        raise RuntimeError(f"rank {rank}: rank 0 runs a different configuration "
+                           "(batch / horizon / model / cost / options / limits); refusing to start")
+    return reply[1:]
+
+
+def _exchange_via_file(rank, path, timeout_s, make_id):
+    if rank == 0:
+        uid = make_id()
         tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "wb") as f:
             f.write(uid)
@@ -85,16 +168,18 @@ class LocalComm:
         pass
 
 
-def make_comm(ctx, rank: int, world: int):
-    """RCCL communicator for world > 1 (one rank per GPU), LocalComm otherwise."""
+def make_comm(ctx, rank: int, world: int, cfg: bytes = b"\0" * 32):
+    """RCCL communicator for world > 1 (one rank per GPU), LocalComm otherwise.  cfg: config_hash of
+    the run; every rank must pass the same one."""
     if world == 1:
         return LocalComm()
-    uid = exchange_unique_id(rank)
+    uid = exchange_unique_id(rank, world, cfg)
     comm = _native.Comm(ctx, world, rank, uid)
     comm.barrier()
-    if rank == 0:
+    path = os.environ.get("TMPC_COMM_ID_FILE")
+    if rank == 0 and path:
         try:
-            os.remove(_id_path())
+            os.remove(path)
         except OSError:
             pass
     return comm

@@ -80,6 +80,7 @@ class TrajoptMPCReference:
         self.exit_soft = 0
         self.exit_sqp = 0
         self.singular = False
+        self.active_sets = []
 
     def update_cost(self, costObj: TrajoptCost):
         if not isinstance(costObj, TrajoptCost):
@@ -133,7 +134,7 @@ class TrajoptMPCReference:
                                       "device implementation)")
         if not isinstance(self.cost, QuadraticCost):
             raise NotImplementedError("the GPU solver supports QuadraticCost and UrdfCost")
-        spec = self.other_constraints.gpu_spec()   # raises for the hard modes
+        spec = self.other_constraints.gpu_spec()   # raises for ADMM_PROJECTION (the reference exits too)
         if options.get("overloading"):
             raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
         ctx = self.plant._ctx()
@@ -156,17 +157,17 @@ class TrajoptMPCReference:
         return ctx
 
     def SQP_batch(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.PCG_SS, options=None,
-                  soft_state=None):
+                  soft_state=None, hard_active=False):
         """B problems at once: x [B][nx][N], u [B][nu][N-1] -> dict of per-problem results.
         With soft limits every problem starts from the constraint objects' mu / lambda / phi
         (or from soft_state = (mu, lam, phi), each [B][N][6n]); the final per-problem
-        constants are returned as r["soft_state"]."""
+        constants are returned as r["soft_state"].  hard_active: with hard limits, also every QP's
+        active set (r["trace"]["hard_active"] [B][max_iter+1][N] bitmasks, include/tmpc.h)."""
         options = {} if options is None else options
         self.set_default_options(options)
+        # method N (solveKKTSystem, the dense KKT solve, :313-359) has the Schur complement's solution and
+        # runs the direct Schur path with the same least-squares fallback (include/tmpc.h TMPC_LINSYS_N)
         method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
-        if method == "N":
-            raise NotImplementedError("the dense KKT solve (method N) is not offered on the GPU; "
-                                      "use S, PCG-J, PCG-BJ or PCG-SS")
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
@@ -180,7 +181,7 @@ class TrajoptMPCReference:
             if soft_state is None:
                 soft_state = [np.broadcast_to(a, (B,) + a.shape) for a in self.other_constraints.pack_state(N)]
             ctx.set_soft_state(B, N, *soft_state)
-        r = ctx.sqp_solve_batch(x, u, N, dt, method)
+        r = ctx.sqp_solve_batch(x, u, N, dt, method, hard_active=hard_active)
         if soft:
             r["soft_state"] = ctx.get_soft_state(B, N)
         return r
@@ -189,7 +190,8 @@ class TrajoptMPCReference:
         """TrajoptMPCReference.SQP (:510-760) for one problem."""
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
-        r = self.SQP_batch(x[None], u[None], N, dt, LINEAR_SYSTEM_SOLVER_METHOD, options)
+        hard = any(c.is_hard_constraint_mode() for _, c in self.other_constraints.limits())
+        r = self.SQP_batch(x[None], u[None], N, dt, LINEAR_SYSTEM_SOLVER_METHOD, options, hard_active=hard)
         method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
         it = int(r["sqp_iter"][0])
         t = r["trace"]
@@ -202,8 +204,12 @@ class TrajoptMPCReference:
         last_pass = outer if ex_soft == 2 else outer - 1
         if "soft_state" in r:
             self.other_constraints.unpack_state(*[a[0] for a in r["soft_state"]])
+        # self.singular is sticky over the object's life, as the reference's (:74, :356, :435)
+        sing_rows = [bool(v) for v in t["singular"][0, :rows]]
         self.trace = []
         for i in range(rows):
+            if i:
+                self.singular = self.singular or sing_rows[i]
             self.trace.append({
                 "outer_iteration": last_pass,
                 "iteration": int(t["iteration"][0, i]),
@@ -217,9 +223,12 @@ class TrajoptMPCReference:
                 "reduction_ratio": None if i == 0 else float(t["reduction_ratio"][0, i]),
                 # the true PCG iteration count (the reference stores len((trace, trace2)) == 2: SURVEY F7)
                 "inner_iters": int(t["pcg_iters"][0, i]) if method.startswith("PCG") else 0,
-                "singular": False,
+                "singular": self.singular if i else False,
                 "succeeded_line_search": bool(t["succeeded_line_search"][0, i]),
             })
+        # with hard limits: each QP's active set, per knot a bitmask (bit t * 2n + e; include/tmpc.h) --
+        # the rows the reference appends to C (TrajoptMPCReference.py:238-248), one list per trace row
+        self.active_sets = [[int(v) for v in t["hard_active"][0, i]] for i in range(1, rows)] if hard else []
         self.exit_sqp = int(r["exit_sqp"][0])
         self.exit_soft = int(r["exit_soft"][0])
         return (r["x"][0], r["u"][0], self.exit_sqp, self.exit_soft, int(r["outer_iter"][0]), it)
@@ -319,16 +328,15 @@ class TrajoptMPCReference:
         return r["x_exec"][0], r["u_exec"][0], r["exit_codes"][0], r["iters"][0]
 
     def solveKKTSystem_Schur(self, x, u, xs, N, dt, rho=0.0, use_PCG=True, options=None):
-        """One QP (formKKTSystemBlocks + solveKKTSystem_Schur, :361-455) -> dxul column.
-        xs must equal x[:, 0] (the SQP always passes the initial state)."""
+        """One QP (formKKTSystemBlocks + solveKKTSystem_Schur, :361-455) -> dxul column; xs is the SQP's
+        initial state (the initial-state row's c_0 = x_0 - xs)."""
         options = {} if options is None else dict(options)
         self.set_default_options(options)
         ptype = options.get("preconditioner_type", "BJ")
         method = "PCG-" + ptype if use_PCG else "S"
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
-        if not np.array_equal(np.asarray(xs), x[:, 0]):
-            raise NotImplementedError("xs != x[:, 0] is not supported by the batched QP entry point")
+        xs = np.asarray(xs, dtype=np.float64).reshape(1, -1)
         u = np.asarray(u, dtype=np.float64)
         self._check_xu(x[None], u[None], N)
         # options['guess'] -> PCG.update_guess (:439-440): the PCG's initial iterate
@@ -337,6 +345,7 @@ class TrajoptMPCReference:
             guess = np.asarray(guess, dtype=np.float64).reshape(1, -1)
             if guess.shape[1] != N * x.shape[0]:
                 raise ValueError(f"options['guess'] must have N * nx = {N * x.shape[0]} entries, got {guess.shape[1]}")
-        r = ctx.qp_batch(x[None], u[None], N, dt, rho, method, want_blocks=False, guess=guess if use_PCG else None)
+        r = ctx.qp_batch(x[None], u[None], N, dt, rho, method, want_blocks=False, guess=guess if use_PCG else None,
+                         xs=xs)
         self.n_inner_iter = int(r["pcg_iters"][0])
         return r["dxul"][0].reshape(-1, 1)
