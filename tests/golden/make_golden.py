@@ -333,11 +333,15 @@ def run_sqp(args):
             "succeeded_line_search", "inner_iters", "singular"]
     rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(t[k]) for t in tr]) for k in keys}
     pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
+    # the |nu| trace of every QP's PCG (PCG.py:79-111), NaN-padded: where the exit test |nu'| < tol fell
+    nu = np.full((len(pcg_iters), int(max(pcg_iters, default=0)) + 1), np.nan)
+    for q, t in enumerate(solver.saved_inner_traces):
+        nu[q, :len(t[0][0])] = np.asarray(t[0][0], dtype=float)
     dxul = np.array([d["value"][:, 0] for d in solver.saved_dxul])
     np.savez_compressed(os.path.join(OUT, f"sqp_{name}_N{N}_s{seed}_{method}.npz"),
                         x0=x0, u0=u0, x=np.asarray(x), u=np.asarray(u), dt=dt,
                         exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer_iter, sqp_iter=sqp_iter,
-                        pcg_iters=pcg_iters, dxul=dxul, wall_s=wall, **rec)
+                        pcg_iters=pcg_iters, nu_traces=nu, dxul=dxul, wall_s=wall, **rec)
     return f"[golden] sqp {name} N={N} seed={seed} {method}: exit={exit_sqp} iters={sqp_iter} " \
            f"pcg={list(pcg_iters)} wall={wall:.1f}s"
 
@@ -663,6 +667,11 @@ def main():
                 ("AUGMENTED_LAGRANGIAN", "S", 20, 7.0)]
         with mp.get_context("fork").Pool(len(jobs)) as pool:
             for msg in pool.imap_unordered(run_pendulum, jobs):
+                print(msg, flush=True)
+    if a.only == "sqpJ":   # the PCG-J solves again, now with their |nu| traces
+        jobs = [("arm3", 8, 2, "PCG-J", 0.1), ("arm3", 32, 0, "PCG-J", 0.1)]
+        with mp.get_context("fork").Pool(len(jobs)) as pool:
+            for msg in pool.imap_unordered(run_sqp, jobs):
                 print(msg, flush=True)
     if a.only in (None, "hooks"):
         gen_soft_hooks()
