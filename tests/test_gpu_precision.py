@@ -78,8 +78,12 @@ def test_reduced_precision_ilqr_tracks_fp64(name, n, N, prec):
 
 
 def test_config3_fp32_ilqr_al_converged_problems():
-    """BASELINE config 3 in fp32 (arm6 N = 64 iLQR, augmented-Lagrangian torque limits): the problems
-    the fp64 oracle solves to convergence (exit 1) are solved by the fp32 path to the same optimum."""
+    """BASELINE config 3 in fp32 (arm6 N = 64 iLQR, augmented-Lagrangian torque limits), 8 problems:
+    the one the fp64 oracle solves to convergence (exit 1, seed 803) is solved by the fp32 path to the same
+    optimum (trajectory at 2e-3); the other 7 end on the rho schedule or the iteration caps (exit 2 / 3)
+    in fp64 too, after different rho paths in fp32 (fp32 rollouts cannot meet dJ < 1e-6), so
+    for every problem the fp32 run must end with a finite trajectory and a final cost within 10 % of the
+    fp64 oracle's (parity unpinned: the reference has no fp32 path)."""
     d = golden("oracle_config3_arm6_N64_ilqr_al.npz")
     N = int(d["N"])
     lb, ub = float(d["lb"]), float(d["ub"])
@@ -89,11 +93,17 @@ def test_config3_fp32_ilqr_al_converged_problems():
             "max_iter_SQP_DDP": int(d["max_iter_SQP_DDP"]), "precision": "fp32"}
     r = s.iLQR_batch(x, u, N, 0.1, opts)
     conv = [i for i in range(len(x)) if int(d["exit_code_0"][i]) == 1]
-    assert conv
+    assert len(conv) == 1 and len(x) == 8
     for i in conv:
         assert int(r["exit_code"][i]) == 1, i
         assert _rel(r["x"][i], d["x_0"][i]) < 2e-3, i
     assert all(np.isfinite(r["x"]).ravel())
+    from oracle import sqp as osqp
+    cost = osqp.QuadCost(np.eye(12), 100 * np.eye(12), 0.1 * np.eye(6), np.zeros(12))
+    for i in range(len(x)):   # the quadratic cost of the final trajectory, against the fp64 oracle's
+        J32 = osqp.total_cost(cost, r["x"][i], r["u"][i], N)
+        J64 = osqp.total_cost(cost, d["x_0"][i], d["u_0"][i], N)
+        assert abs(J32 - J64) <= 0.1 * abs(J64), (i, J32, J64)
 
 
 def test_config5_mixed_mpc_sqp_n128():
