@@ -453,7 +453,8 @@ def main():
     headline = a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and not limits and \
         a.cost == "quadratic" and N == 64 and a.precision == "fp64"
     if a.limits != "none":
-        name += f", soft box constraints {a.limits}"
+        hard = any(v["mode"] in ("ACTIVE_SET", "FULL_SET") for v in LIMIT_PRESETS[a.limits].values())
+        name += f", {'hard' if hard else 'soft'} box constraints {a.limits}"
     if a.cost == "ee":
         name += ", UrdfCost end-effector cost (twolinks.py goal)"
     if a.mpc_steps > 0:

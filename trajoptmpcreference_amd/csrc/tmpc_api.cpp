@@ -8,6 +8,7 @@
 // (k_ls_decide); the host reads back one integer per iteration.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -245,33 +246,36 @@ struct Work {
   int Wtr;                           // trace row stride
 };
 
+// P / nb: the problems the batch launches visit (tmpc_internal.h PList; the identity and B outside the
+// lock-step loop)
 static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const double* d_x, const double* d_u,
-                  const ProbState& st, Work& w, bool keep_blocks) {
+                  const ProbState& st, Work& w, bool keep_blocks, PList P, int nb) {
   const int nj = ctx->hmodel.n;
   const bool chain = ctx->hmodel.chain != 0;
   const bool soft = w.jsoft != nullptr;
   const double* G = soft ? w.Gk : w.G;
   {
     Timed t(ctx, "qp_fd");
-    LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs, st.need_grad, w.qdd,
-                           w.cvec));
+    LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, P, nb, N, dt, d_x, d_u, w.xs, st.need_grad,
+                           w.qdd, w.cvec));
   }
   {
     Timed t(ctx, "qp_minv");
-    LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad, w.minv));
+    LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, P, nb, N, d_x, st.need_grad,
+                             w.minv));
   }
   {
     Timed t(ctx, "qp_grad");
-    LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad, w.qdd, w.minv, w.A,
-                             w.Bm));
+    LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, P, nb, N, dt, d_x, st.need_grad, w.qdd, w.minv,
+                             w.A, w.Bm));
   }
   if (soft) {
     Timed t(ctx, "ginv");
-    LAUNCH_OK(launch_ginv_soft(ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, st.rho, st.active, d_x, d_u, w.smu,
+    LAUNCH_OK(launch_ginv_soft(ctx->stream, nj, ctx->dcost, ctx->dlim, P, nb, N, st.rho, st.active, d_x, d_u, w.smu,
                                w.slam, w.Gk, w.jsoft));
   } else {
     Timed t(ctx, "ginv");
-    LAUNCH_OK(launch_ginv(ctx->stream, nj, ctx->dcost, B, st.rho, st.active, w.G));
+    LAUNCH_OK(launch_ginv(ctx->stream, nj, ctx->dcost, P, nb, st.rho, st.active, w.G));
   }
   if (w.hard) {   // hard box constraints: rows of C per knot, banded S (tmpc_hard.hip)
     HardArgs h = *w.hard;
@@ -305,7 +309,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   if (precond == 0) {   // method S: Schur blocks -> direct solve -> dxu
     {
       Timed t(ctx, "schur");
-      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, G,
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, G,
                           w.A, w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, nullptr, w.Sd, w.Sl, w.gam, nullptr,
                           w.jsoft, nullptr, nullptr));
     }
@@ -315,7 +319,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     }
     {
       Timed t(ctx, "dxu");
-      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, G, w.A,
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, G, w.A,
                           w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, w.lam, nullptr, nullptr, nullptr, nullptr,
                           w.jsoft, nullptr, nullptr));
     }
@@ -323,7 +327,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   }
   {
     Timed t(ctx, "qp");
-    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, B, N, precond, QP_MODE_PCG, d_x, d_u, st.active, G, w.A,
+    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, precond, QP_MODE_PCG, d_x, d_u, st.active, G, w.A,
                         w.Bm, w.cvec, ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx,
                         w.du, keep_blocks ? w.lam : w.lam_keep, keep_blocks ? w.Sd : nullptr,
                         keep_blocks ? w.Sl : nullptr, keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr,
@@ -455,6 +459,8 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
   BUF(int, hd_sing, (size_t)B);
   HIP_OK(hipMemsetAsync(hd_sing, 0, (size_t)B * sizeof(int), ctx->stream));
   hard.hslot = hd_slot; hard.amask = hd_amask; hard.sing = hd_sing;
+  BUF(int, hd_rng, (size_t)B * hard.dmax * 2);
+  hard.rng = hd_rng;
   BUF(double, hd_Y, (size_t)B * hard.dmax * 2 * (nx + nj));
   BUF(double, hd_Sb, (size_t)B * hard.dmax * BW);
   BUF(double, hd_gam, (size_t)B * hard.dmax);
@@ -496,31 +502,63 @@ static int hard_ls(tmpc_ctx* ctx, int nj, const HardArgs& base, int B, int N, in
   return launch_hard(ctx->stream, nj, h);
 }
 
+// The problem list of the lock-step loop: mask = the per-problem "may still do work" flag (st.active
+// without soft limits, outer_active with them: both only ever go 1 -> 0 inside the loop), idx / cnt
+// its device list, P / nb what the iteration's launches take (tmpc_internal.h PList).
+struct AliveList {
+  const int* mask;
+  int* idx;
+  int* cnt;
+  int B;
+  PList P;
+  int nb;
+};
+
+static int alloc_alive(tmpc_ctx* ctx, int B, const int* mask, AliveList& al) {
+  BUF(int, alive_idx, B);
+  BUF(int, alive_cnt, 1);
+  al = AliveList{mask, alive_idx, alive_cnt, B, PList{nullptr, nullptr}, B};
+  return 0;
+}
+
 // keep_warm: the PCG warm-start buffer already holds this batch's starting lambdas (MPC loop)
 // Lock-step batch loop with a lag-1 termination test.  Each batch iteration writes its two flags
-// (some problem continues its inner loop / some problem restarted an outer pass) into its own half
-// of active_count[2][2]; the host copies them to pinned memory and tests iteration `it` only after
-// iteration `it + 1` has been enqueued, so the GPU never idles while the host decides.  Every kernel
-// masks itself with the per-problem state, so the one iteration enqueued after the batch finished
-// is a no-op for every problem (need_grad / active / outer_active are all 0).
+// (some problem continues its inner loop / some problem restarted an outer pass) and the length of
+// the rebuilt problem list into its own slot of active_count[2][4]; the host copies them to pinned
+// memory and tests iteration `it` only after iteration `it + 1` has been enqueued, so the GPU never
+// idles while the host decides.  Every kernel masks itself with the per-problem state, so the one
+// iteration enqueued after the batch finished is a no-op for every problem (need_grad / active /
+// outer_active are all 0).  The launches of iteration `it` visit the problem list built at the end
+// of `it - 1` (on the stream, so exact), with the grid sized by the list length the host last read,
+// the one of iteration `it - 2` (an upper bound: the list only shrinks); the tail of a batch whose
+// problems converge at different iterations then dispatches only its live problems' workgroups.
 template <class Body>
-static int lockstep_loop(tmpc_ctx* ctx, long cap, int* active_count, Body body) {
+static int lockstep_loop(tmpc_ctx* ctx, long cap, int* active_count, AliveList& al, Body body) {
   hipEvent_t ev[2] = {get_event(ctx), get_event(ctx)};
   if (!ev[0] || !ev[1]) return fail(ctx, "hipEventCreate failed");
   int rc = 0;
+  launch_alive_list(ctx->stream, al.B, al.mask, al.idx, al.cnt, nullptr);
+  HIP_OK(hipGetLastError());
+  al.P = PList{al.idx, al.cnt};
+  al.nb = al.B;
   for (long it = 0; it < cap; ++it) {
     const int p = (int)(it & 1);
-    int* ac = active_count + 2 * p;
-    HIP_OK(hipMemsetAsync(ac, 0, 2 * sizeof(int), ctx->stream));
+    int* ac = active_count + 4 * p;
+    if (it >= 2) al.nb = std::max(1, std::min(al.nb, ctx->h_count[4 * p + 2]));   // synced at it - 1
+    HIP_OK(hipMemsetAsync(ac, 0, 3 * sizeof(int), ctx->stream));
     if ((rc = body(ac))) break;
-    HIP_OK(hipMemcpyAsync(ctx->h_count + 2 * p, ac, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    launch_alive_list(ctx->stream, al.B, al.mask, al.idx, al.cnt, ac + 2);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(ctx->h_count + 4 * p, ac, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(hipEventRecord(ev[p], ctx->stream));
     if (it > 0) {
       HIP_OK(hipEventSynchronize(ev[p ^ 1]));
-      const int* h = ctx->h_count + 2 * (p ^ 1);
+      const int* h = ctx->h_count + 4 * (p ^ 1);
       if (h[0] == 0 && h[1] == 0) break;
     }
   }
+  al.P = PList{nullptr, nullptr};
+  al.nb = al.B;
   ctx->event_pool.push_back(ev[0]);
   ctx->event_pool.push_back(ev[1]);
   return rc;
@@ -548,13 +586,15 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   if ((rc = alloc_trace(ctx, B, W, tr))) return rc;
   BUF(double, alphas, T + 1);
   BUF(double, terms, (size_t)B * T * N * 4);   // [B][T][N][cost, violation, D, soft value]
-  BUF(int, active_count, 4);   // [2][2] (lag-1 double buffer): [0] some problem in its inner loop, [1] some problem restarted a pass
+  BUF(int, active_count, 8);   // [2][4] (lag-1 double buffer): [0] some problem in its inner loop, [1] some problem restarted a pass, [2] problem-list length
   BUF(unsigned long long, counters, 4);
   BUF(unsigned long long, prob_counters, (size_t)B * 3);   // per-problem tallies of k_ls_decide
   BUF(int, outer_active, B);
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
   const bool soft = ctx->hlim.any != 0;
+  AliveList alv;
+  if ((rc = alloc_alive(ctx, B, soft ? outer_active : st.active, alv))) return rc;
   // UrdfCost has a state-dependent Hessian: it takes the per-knot Ghat path of the soft limits
   const bool perknot = soft || ctx->hcost.kind == COST_EE;
   double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
@@ -613,38 +653,38 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   auto init_merit = [&](int* mask, int* ac) -> int {
     ProbState sti = st;
     sti.active = mask;
-    LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, 1,
-                              dt, alphas + T, d_x, d_u, w.xs, nullptr, nullptr, mask, terms));
+    LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
+                              alv.P, alv.nb, N, 1, dt, alphas + T, d_x, d_u, w.xs, nullptr, nullptr, mask, terms));
     if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, mask));
-    launch_ls_decide(ctx->stream, B, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
+    launch_ls_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
                      sti, nullptr, tr, ac, nullptr, hterms);
     HIP_OK(hipGetLastError());
     return 0;
   };
   // one SQP iteration (:550-757) of every problem in its inner loop; flags[0] = some problem continues
   auto sqp_iteration = [&](int* ac) -> int {
-    int rc2 = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false);
+    int rc2 = run_qp(ctx, B, N, dt, precond, d_x, d_u, st, w, false, alv.P, alv.nb);
     if (rc2) return rc2;
     {
       Timed t(ctx, "ls_terms");
-      LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam, B, N, T, dt,
-                                alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
+      LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
+                                alv.P, alv.nb, N, T, dt, alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
       if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, T, alphas, d_x, d_u, w.dx, w.du, st.active));
     }
     Timed t(ctx, "ls_decide");
-    launch_ls_decide(ctx->stream, B, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
+    launch_ls_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, T, LS_MODE_STEP, soft, alphas, so, terms, d_x, d_u, w.dx, w.du,
                      st, w.iters, tr, ac, prob_counters, hterms, (w.hard && precond == 0) ? hard.sing : nullptr);
     HIP_OK(hipGetLastError());
     return 0;
   };
-  HIP_OK(hipMemsetAsync(active_count, 0, 4 * sizeof(int), ctx->stream));
+  HIP_OK(hipMemsetAsync(active_count, 0, 8 * sizeof(int), ctx->stream));
   if ((rc = init_merit(st.active, active_count))) return rc;
   if (!soft) {
     // unconstrained: one inner loop (at most max_iter iterations, + 1 for the lag of the exit test);
     // check_and_update_soft_constraints then exits 1 (:531-757)
-    rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, [&](int* ac) { return sqp_iteration(ac); });
+    rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, alv, [&](int* ac) { return sqp_iteration(ac); });
     if (rc) return rc;
-    launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints, o.max_iter_softConstraints,
+    launch_soft_outer(ctx->stream, ctx->dlim, PList{nullptr, nullptr}, B, N, nj, o.exit_tolerance_softConstraints, o.max_iter_softConstraints,
                       d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft, active_count);
     HIP_OK(hipGetLastError());
   } else {
@@ -657,17 +697,17 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     BUF(int, act_init, B);
     HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
     const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
-    rc = lockstep_loop(ctx, cap, active_count, [&](int* ac) -> int {
+    rc = lockstep_loop(ctx, cap, active_count, alv, [&](int* ac) -> int {
       int r = sqp_iteration(ac);
       if (r) return r;
-      launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
+      launch_soft_outer(ctx->stream, ctx->dlim, alv.P, alv.nb, N, nj, o.exit_tolerance_softConstraints,
                         o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
                         ac + 1, &st, act_init, o.rho_init_SQP_DDP);
       HIP_OK(hipGetLastError());
       // restarted passes (act_init, set by k_soft_outer): initial merit, then into the inner loop;
       // masked by act_init, so a no-op when no pass restarted
       if ((r = init_merit(act_init, ac))) return r;
-      launch_activate(ctx->stream, B, act_init, st.active);
+      launch_activate(ctx->stream, alv.P, alv.nb, act_init, st.active);
       HIP_OK(hipGetLastError());
       return 0;
     });
@@ -714,13 +754,15 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   BUF(double, il_xt, (size_t)B * T * nx * N);
   BUF(double, il_ut, (size_t)B * T * nj * K);
   BUF(double, il_J, (size_t)B * T);
-  BUF(int, active_count, 4);   // [2][2], as sqp_device
+  BUF(int, active_count, 8);   // [2][4], as sqp_device
   BUF(int, outer_active, B);
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
   BUF(unsigned long long, counters, 4);
   HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
   const bool soft = ctx->hlim.any != 0;
+  AliveList alv;
+  if ((rc = alloc_alive(ctx, B, soft ? outer_active : st.active, alv))) return rc;
   double *smu = nullptr, *slam = nullptr, *sphi = nullptr, *il_jac = nullptr;
   if (soft) {
     if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
@@ -744,8 +786,9 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   auto init_cost = [&](int* mask, int* ac) -> int {
     ProbState sti = st;
     sti.active = mask;
-    LAUNCH_OK(launch_ilqr_init_cost(ctx->stream, nj, ctx->dcost, ctx->dlim, smu, slam, B, N, d_x, d_u, mask, il_J));
-    launch_ilqr_decide(ctx->stream, B, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, sti,
+    LAUNCH_OK(launch_ilqr_init_cost(ctx->stream, nj, ctx->dcost, ctx->dlim, smu, slam, alv.P, alv.nb, N, d_x, d_u,
+                                    mask, il_J));
+    launch_ilqr_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, sti,
                        tr, ac, nullptr);
     HIP_OK(hipGetLastError());
     return 0;
@@ -754,42 +797,43 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   auto ilqr_iteration = [&](int* ac) -> int {
     {
       Timed t(ctx, "qp_fd");
-      LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u, w.xs,
-                             st.need_grad, w.qdd, w.cvec));
+      LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, alv.P, alv.nb, N, dt, d_x, d_u,
+                             w.xs, st.need_grad, w.qdd, w.cvec));
     }
     {
       Timed t(ctx, "qp_minv");
-      LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, d_x, st.need_grad,
-                               w.minv));
+      LAUNCH_OK(launch_qp_minv(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, alv.P, alv.nb, N, d_x,
+                               st.need_grad, w.minv));
     }
     {
       Timed t(ctx, "qp_grad");
-      LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, st.need_grad,
-                               w.qdd, w.minv, w.A, w.Bm));
+      LAUNCH_OK(launch_qp_grad(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, alv.P, alv.nb, N, dt, d_x,
+                               st.need_grad, w.qdd, w.minv, w.A, w.Bm));
     }
     {
       Timed t(ctx, "ilqr_backward");
-      LAUNCH_OK(launch_ilqr_backward(ric32(ctx), ctx->stream, nj, ctx->dcost, ctx->dlim, B, N, d_x, d_u, st.rho, st.active,
+      LAUNCH_OK(launch_ilqr_backward(ric32(ctx), ctx->stream, nj, ctx->dcost, ctx->dlim, alv.P, alv.nb, N, d_x, d_u,
+                                     st.rho, st.active,
                                      w.A, w.Bm, smu, slam, il_jac, il_K, il_d, il_dV, il_ok));
     }
     {
       Timed t(ctx, "ilqr_forward");
       LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu,
-                                    slam, B, N, T, dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut,
+                                    slam, alv.P, alv.nb, N, T, dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut,
                                     il_J));
     }
     Timed t(ctx, "ilqr_decide");
-    launch_ilqr_decide(ctx->stream, B, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st, tr,
+    launch_ilqr_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st, tr,
                        ac, counters);
     HIP_OK(hipGetLastError());
     return 0;
   };
-  HIP_OK(hipMemsetAsync(active_count, 0, 4 * sizeof(int), ctx->stream));
+  HIP_OK(hipMemsetAsync(active_count, 0, 8 * sizeof(int), ctx->stream));
   if ((rc = init_cost(st.active, active_count))) return rc;
   if (!soft) {
-    rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, [&](int* ac) { return ilqr_iteration(ac); });
+    rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, alv, [&](int* ac) { return ilqr_iteration(ac); });
     if (rc) return rc;
-    launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
+    launch_soft_outer(ctx->stream, ctx->dlim, PList{nullptr, nullptr}, B, N, nj, o.exit_tolerance_softConstraints,
                       o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
                       active_count);
     HIP_OK(hipGetLastError());
@@ -799,15 +843,15 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     BUF(int, act_init, B);
     HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
     const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
-    rc = lockstep_loop(ctx, cap, active_count, [&](int* ac) -> int {
+    rc = lockstep_loop(ctx, cap, active_count, alv, [&](int* ac) -> int {
       int r = ilqr_iteration(ac);
       if (r) return r;
-      launch_soft_outer(ctx->stream, ctx->dlim, B, N, nj, o.exit_tolerance_softConstraints,
+      launch_soft_outer(ctx->stream, ctx->dlim, alv.P, alv.nb, N, nj, o.exit_tolerance_softConstraints,
                         o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
                         ac + 1, &st, act_init, o.rho_init_SQP_DDP);
       HIP_OK(hipGetLastError());
       if ((r = init_cost(act_init, ac))) return r;   // masked by act_init: a no-op when no pass restarted
-      launch_activate(ctx->stream, B, act_init, st.active);
+      launch_activate(ctx->stream, alv.P, alv.nb, act_init, st.active);
       HIP_OK(hipGetLastError());
       return 0;
     });
@@ -935,6 +979,14 @@ int tmpc_set_cost_quadratic(tmpc_ctx* ctx, int nx, int nu, const double* Q, cons
   memcpy(c.QF, QF, sizeof(double) * nx * nx);
   memcpy(c.R, R, sizeof(double) * nu * nu);
   memcpy(c.xg, xg, sizeof(double) * nx);
+  // diagonal Q, QF, R: the kernels' cost products take their exact-zero-free form (CostDev.diag)
+  c.diag = 1;
+  for (int r = 0; r < nx; ++r)
+    for (int k = 0; k < nx; ++k)
+      if (r != k && (Q[r * nx + k] != 0.0 || QF[r * nx + k] != 0.0)) c.diag = 0;
+  for (int r = 0; r < nu; ++r)
+    for (int k = 0; k < nu; ++k)
+      if (r != k && R[r * nu + k] != 0.0) c.diag = 0;
   hipSetDevice(ctx->device);
   HIP_OK(hipMemcpyAsync(ctx->dcost, &c, sizeof(c), hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -1380,7 +1432,8 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
     w.hard = &hard;
   }
   ctx->hard_last = {0, 0, 0, 0};
-  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, !ctx->hlim.any_hard))) return rc;
+  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, !ctx->hlim.any_hard, PList{nullptr, nullptr}, B)))
+    return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (ctx->hlim.any_hard) {
     ctx->hard_last = {B, N, hard.dmax, hard.W};
@@ -1438,7 +1491,22 @@ int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim,
   if (active) HIP_OK(hipMemcpy(active, dev("hd_amask"), sizeof(uint64_t) * B * N, hipMemcpyDeviceToHost));
   if (singular) HIP_OK(hipMemcpy(singular, dev("hd_sing"), sizeof(int) * B, hipMemcpyDeviceToHost));
   const size_t BW = 2 * (size_t)hl.W + 1;
-  if (S_band) HIP_OK(hipMemcpy(S_band, dev("hd_Sb"), sizeof(double) * B * hl.dmax * BW, hipMemcpyDeviceToHost));
+  if (S_band) {
+    // the kernels write S only inside each row's structural range (k_hard_schur): zero the rest
+    HIP_OK(hipMemcpy(S_band, dev("hd_Sb"), sizeof(double) * B * hl.dmax * BW, hipMemcpyDeviceToHost));
+    std::vector<int> rg((size_t)B * hl.dmax * 2), dm(B);
+    HIP_OK(hipMemcpy(rg.data(), dev("hd_rng"), rg.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(dm.data(), dev("hd_dim"), B * sizeof(int), hipMemcpyDeviceToHost));
+    for (int b = 0; b < B; ++b)
+      for (int a = 0; a < hl.dmax; ++a) {
+        double* row = S_band + ((size_t)b * hl.dmax + a) * BW;
+        const int* r = rg.data() + ((size_t)b * hl.dmax + a) * 2;
+        for (size_t o = 0; o < BW; ++o) {
+          const int c = a - hl.W + (int)o;
+          if (a >= dm[b] || c < r[0] || c > r[1]) row[o] = 0.0;
+        }
+      }
+  }
   if (gamma) HIP_OK(hipMemcpy(gamma, dev("hd_gam"), sizeof(double) * B * hl.dmax, hipMemcpyDeviceToHost));
   if (lambda_hard) {
     // the hard rows' multipliers by slot t * 2n + e (0 where the slot has no row)
@@ -1486,6 +1554,23 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
   BUF(double, hp_Pd, (size_t)B * nbmax * nx * nx);
   BUF(double, hp_Pl, (size_t)B * nbmax * nx * nx);
   BUF(double, hp_Pt, (size_t)B * nbmax * nx * nx);
+  BUF(int, hp_rng, (size_t)B * dmax * 2);
+  // each row's first / last nonzero column: the range the kernel's products visit (tmpc_hard.hip)
+  std::vector<int> rg((size_t)B * dmax * 2);
+  for (int b = 0; b < B; ++b)
+    for (int a = 0; a < dmax; ++a) {
+      const double* row = S_band + ((size_t)b * dmax + a) * BW;
+      int lo = a, hi = a;
+      for (size_t o = 0; o < BW; ++o) {
+        const int c = a - W + (int)o;
+        if (c < 0 || c >= dim[b] || row[o] == 0.0) continue;
+        lo = std::min(lo, c);
+        hi = std::max(hi, c);
+      }
+      rg[((size_t)b * dmax + a) * 2] = lo;
+      rg[((size_t)b * dmax + a) * 2 + 1] = hi;
+    }
+  HIP_OK(hipMemcpyAsync(hp_rng, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(hp_Sb, S_band, sizeof(double) * B * dmax * BW, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(hp_gam, gamma, sizeof(double) * B * dmax, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(hp_dim, dim, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
@@ -1508,6 +1593,7 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
   h.Ptmp = hp_Pt;
   h.lam = hp_lam;
   h.iters = hp_it;
+  h.rng = hp_rng;
   {
     Timed t(ctx, "hard_pcg");
     LAUNCH_OK(launch_hard(ctx->stream, nx / 2, h));

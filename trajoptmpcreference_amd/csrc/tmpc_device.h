@@ -51,6 +51,11 @@ struct CostDev {            // QuadraticCost (TrajoptCost.py:24-104) or UrdfCost
   int nx, nu;
   int QF_start;             // -1 = None
   int kind;                 // COST_*
+  // QuadraticCost with diagonal Q, QF and R (set by tmpc_set_cost_quadratic; the reference's own
+  // workloads).  A dot product against such a row adds fma(0, y, acc) = acc for every
+  // off-diagonal entry, so it reduces to its diagonal term bit for bit -- for finite y: a
+  // non-finite entry makes every generic sum NaN (0 * inf) and diag_dot keeps that explicitly.
+  int diag;
   double Q[NXMAX * NXMAX];
   double QF[NXMAX * NXMAX];
   double R[NJMAX * NJMAX];
@@ -59,6 +64,16 @@ struct CostDev {            // QuadraticCost (TrajoptCost.py:24-104) or UrdfCost
   // row-major 4x4, joints 0 and 1 of the 2-link chain
   double eeH0[2][16], eeHa[2][16], eeHb[2][16];
 };
+
+// sum_c M[r][c] y[c] for a diagonal M of order n (CostDev.diag): the generic chain's value.
+// poison: NaN when some y[c] is non-finite and n > 1 (then 0 * y[c] enters every generic row sum
+// but the diagonal one), else 0 -- callers add it to the result the generic form would have poisoned
+template <class T>
+__device__ __forceinline__ T diag_poison(const T* y, int n) {
+  bool fin = true;
+  for (int c = 0; c < n; ++c) fin = fin && isfinite(y[c]);
+  return (fin || n < 2) ? T(0) : T(NAN);
+}
 
 // UrdfCost task-space terms at one knot (2-link arms only, as the reference: SURVEY F5).
 //   y = [p(q); J(q) qd] - xg          delta_x           TrajoptCost.py:425-435

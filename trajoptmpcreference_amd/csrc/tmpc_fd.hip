@@ -17,7 +17,7 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
 // c_{k+1} = x_{k+1} - f(x_k, u_k) (formKKTSystemBlocks :227-231); lane k = 0
 // also writes c_0 = x_0 - xs (:213-214).
 template <int NJ, bool CHAIN, class MT, class R>
-__global__ void __launch_bounds__(256) k_qp_fd(MT M, int B, int N, double dt,
+__global__ void __launch_bounds__(256) k_qp_fd(MT M, PList P, int B, int N, double dt,
                                                const double* __restrict__ x, const double* __restrict__ u,
                                                const double* __restrict__ xs, const int* __restrict__ need,
                                                double* __restrict__ qdd_out, double* __restrict__ cvec) {
@@ -25,7 +25,9 @@ __global__ void __launch_bounds__(256) k_qp_fd(MT M, int B, int N, double dt,
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int K = N - 1;
   if (gid >= B * K) return;
-  const int b = gid / K, k = gid - b * K;
+  const int p = gid / K, k = gid - p * K;
+  if (!P.has(p, B)) return;
+  const int b = P.at(p);
   if (!need[b]) return;
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NJ * K;
@@ -72,7 +74,7 @@ template <int NJ, bool CHAIN, bool SOFT, class MT, class R>
 __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restrict__ C,
                                                   const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                   const double* __restrict__ lam,
-                                                  int B, int N, int T, double dt, const double* __restrict__ alphas,
+                                                  PList P, int B, int N, int T, double dt, const double* __restrict__ alphas,
                                                   const double* __restrict__ x, const double* __restrict__ u,
                                                   const double* __restrict__ xs, const double* __restrict__ dx,
                                                   const double* __restrict__ du, const int* __restrict__ active,
@@ -81,9 +83,12 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * T * N) return;
   const int k = gid % N;
-  const int bt = gid / N;
-  const int b = bt / T, t = bt - b * T;
+  const int pt = gid / N;
+  const int p = pt / T, t = pt - p * T;
+  if (!P.has(p, B)) return;
+  const int b = P.at(p);
   if (!active[b]) return;
+  const size_t bt = (size_t)b * T + t;
   const int K = N - 1;
   const double al = alphas[t];
   const double* xb = x + (size_t)b * NX * N;
@@ -111,6 +116,16 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
   for (int m = 0; m < NX; ++m) d[m] = xk[m] - C->xg[m];
   // value: 0.5 dx^T (Q dx) [+ 0.5 u^T (R u)]; gradient: [dx^T Q, u^T R]
   double vq = 0.0;
+  if (C->diag) {   // the same chains without their exact-zero terms (CostDev.diag)
+    const double pz = diag_poison(d, NX);
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+      const double qd = __fma_rn(Qk[r * NX + r], d[r], 0.0);
+      vq = __fma_rn(d[r], qd, vq);
+      Dk = __fma_rn(qd + pz, dxk[r], Dk);
+    }
+    vq = vq + pz;
+  } else {
 #pragma unroll
   for (int r = 0; r < NX; ++r) {
     double qd = 0.0, gq = 0.0;
@@ -121,6 +136,7 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
     }
     vq += d[r] * qd;
     Dk += gq * dxk[r];
+  }
   }
   cost = 0.5 * vq;
   }
@@ -136,6 +152,16 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
       uk[m] = dub ? ub[m * K + k] - al * duk[m] : ub[m * K + k];
     }
     double vr = 0.0;
+    if (C->diag) {
+      const double pz = diag_poison(uk, NU);
+#pragma unroll
+      for (int r = 0; r < NU; ++r) {
+        const double ru = __fma_rn(C->R[r * NU + r], uk[r], 0.0);
+        vr = __fma_rn(uk[r], ru, vr);
+        Dk = __fma_rn(ru + pz, duk[r], Dk);
+      }
+      vr = vr + pz;
+    } else {
 #pragma unroll
     for (int r = 0; r < NU; ++r) {
       double ru = 0.0, gr = 0.0;
@@ -146,6 +172,7 @@ __global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restric
       }
       vr += uk[r] * ru;
       Dk += gr * duk[r];
+    }
     }
     cost += 0.5 * vr;
     // dynamics defect at the trial point
@@ -320,22 +347,22 @@ __global__ void __launch_bounds__(64) k_mpc_shift(MT M, int B, int N, double dt,
 
 template <int NJ, bool CHAIN, class MT>
 struct LaunchFD {
-  static void qp_fd(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x, const double* u,
-                    const double* xs, const int* need, double* qdd, double* cvec) {
+  static void qp_fd(bool f32, hipStream_t s, const ModelDev* M, PList P, int B, int N, double dt, const double* x,
+                    const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
     if (f32)
-      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), B, N, dt, x, u, xs,
-                         need, qdd, cvec);
+      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), P, B, N, dt, x, u,
+                         xs, need, qdd, cvec);
     else
-      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), B, N, dt, x, u, xs,
-                         need, qdd, cvec);
+      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), P, B, N, dt, x, u,
+                         xs, need, qdd, cvec);
   }
   static void ls_terms(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
-                       const double* lam, int B, int N, int T, double dt, const double* alphas, const double* x,
+                       const double* lam, PList P, int B, int N, int T, double dt, const double* alphas, const double* x,
                        const double* u, const double* xs, const double* dx, const double* du, const int* active,
                        double* terms) {
 #define TMPC_LS(SOFTV, RV)                                                                                        \
     hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, SOFTV, MT, RV>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, \
-                       lam, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms);
+                       lam, P, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms);
     if (mu) { if (f32) { TMPC_LS(true, float) } else { TMPC_LS(true, double) } }
     else { if (f32) { TMPC_LS(false, float) } else { TMPC_LS(false, double) } }
 #undef TMPC_LS
@@ -378,15 +405,17 @@ struct LaunchFD {
   }                                                                                                    \
   return 0;
 
-int launch_qp_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt,
-                 const double* x, const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
-  TMPC_DISPATCH_NJ(nj, chain, qp_fd(f32, s, M, B, N, dt, x, u, xs, need, qdd, cvec))
+int launch_qp_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, PList P, int B, int N,
+                 double dt, const double* x, const double* u, const double* xs, const int* need, double* qdd,
+                 double* cvec) {
+  TMPC_DISPATCH_NJ(nj, chain, qp_fd(f32, s, M, P, B, N, dt, x, u, xs, need, qdd, cvec))
 }
 int launch_ls_terms(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C,
-                    const ConstrDev* Cs, const double* mu, const double* lam, int B, int N, int T, double dt,
+                    const ConstrDev* Cs, const double* mu, const double* lam, PList P, int B, int N, int T, double dt,
                     const double* alphas, const double* x, const double* u, const double* xs, const double* dx,
                     const double* du, const int* active, double* terms) {
-  TMPC_DISPATCH_NJ(nj, chain, ls_terms(f32, s, M, C, Cs, mu, lam, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms))
+  TMPC_DISPATCH_NJ(nj, chain, ls_terms(f32, s, M, C, Cs, mu, lam, P, B, N, T, dt, alphas, x, u, xs, dx, du, active,
+                                       terms))
 }
 int launch_unit_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt,
                    const double* x, const double* u, double* xnext, double* qdd) {

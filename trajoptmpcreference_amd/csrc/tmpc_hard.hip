@@ -244,8 +244,11 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
                                                     const int* __restrict__ hoff, const int* __restrict__ hcol,
                                                     const double* __restrict__ hsgn, const double* __restrict__ hval,
                                                     double* __restrict__ Y, int* __restrict__ PK,
-                                                    double* __restrict__ Sb, double* __restrict__ gam) {
+                                                    double* __restrict__ Sb, double* __restrict__ gam,
+                                                    int* __restrict__ rng) {
   constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
+  extern __shared__ int s_piece[];   // [N] first row, [N] last row touching each knot piece
+  __shared__ int s_wt;
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int K = N - 1;
@@ -284,15 +287,51 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     else ca = hval[hb + (size_t)knot * rmax + idx];
     gam[(size_t)b * dmax + a] = ca - g_dot;
   }
+  // the rows of each knot piece: S_ac is structurally nonzero only where rows a and c share a piece,
+  // so row a's nonzeros lie in [min, max] of the rows of its pieces -- a much narrower range than
+  // the worst-case band W, which the PCG's products and the elimination then stay inside
+  for (int k = threadIdx.x; k < N; k += blockDim.x) {
+    s_piece[k] = D;
+    s_piece[N + k] = -1;
+  }
+  if (threadIdx.x == 0) s_wt = 1;
   __syncthreads();
-  // phase 2: the band, row a, column c = a - W + o
+  for (int a = threadIdx.x; a < D; a += blockDim.x)
+    for (int p = 0; p < 2; ++p) {
+      const int kp = PKb[a * 2 + p];
+      if (kp < 0) continue;
+      atomicMin(&s_piece[kp], a);
+      atomicMax(&s_piece[N + kp], a);
+    }
+  __syncthreads();
+  int* rb = rng + (size_t)b * dmax * 2;
+  for (int a = threadIdx.x; a < D; a += blockDim.x) {
+    int lo = a, hi = a;
+    for (int p = 0; p < 2; ++p) {
+      const int kp = PKb[a * 2 + p];
+      if (kp < 0) continue;
+      lo = min(lo, s_piece[kp]);
+      hi = max(hi, s_piece[N + kp]);
+    }
+    lo = max(lo, max(0, a - W));
+    hi = min(hi, min(D - 1, a + W));
+    rb[2 * a] = lo;
+    rb[2 * a + 1] = hi;
+    atomicMax(&s_wt, hi - lo + 1);
+  }
+  __syncthreads();
+  // phase 2: the band inside the row ranges, row a, column c = lo_a + o (stored at offset c - a + W);
+  // entries outside the ranges are never read (band_at / the PCG product / k_hard_direct's copy)
   const int BW = 2 * W + 1;
+  const int Wt = s_wt;
   double* S = Sb + (size_t)b * dmax * BW;
-  for (int e = threadIdx.x; e < D * BW; e += blockDim.x) {
-    const int a = e / BW, o = e - a * BW;
-    const int c = a - W + o;
+  for (int e = threadIdx.x; e < D * Wt; e += blockDim.x) {
+    const int a = e / Wt;
+    const int c = rb[2 * a] + (e - a * Wt);
+    if (c > rb[2 * a + 1]) continue;
+    const int o = c - a + W;
     double s = 0.0;
-    if (c >= 0 && c < D) {
+    {
       const int kind = rk[a], knot = rn[a], idx = ri[a];
       const int* hc = hcol + hb + (size_t)knot * rmax;
       const double* hs = hsgn + hb + (size_t)knot * rmax;
@@ -326,9 +365,9 @@ __device__ __forceinline__ double h_block_sum(double v, double* red) {
   return s;
 }
 
-__device__ __forceinline__ double band_at(const double* S, int BW, int W, int r, int c) {
-  const int o = c - r + W;
-  return (o >= 0 && o < BW) ? S[(size_t)r * BW + o] : 0.0;
+// S_rc from the band; zero outside row r's structural range rg[2r .. 2r+1]
+__device__ __forceinline__ double band_at(const double* S, const int* rg, int BW, int W, int r, int c) {
+  return (c >= rg[2 * r] && c <= rg[2 * r + 1]) ? S[(size_t)r * BW + (c - r + W)] : 0.0;
 }
 
 // In-place Gauss-Jordan inverse of a small block (global memory, one thread), the operation order of
@@ -369,13 +408,14 @@ __global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int pr
                                                   const double* __restrict__ gam, double tol, int max_iter,
                                                   double* __restrict__ Pd, double* __restrict__ Pl,
                                                   double* __restrict__ Ptmp, double* __restrict__ lam,
-                                                  int* __restrict__ iters) {
+                                                  int* __restrict__ iters, const int* __restrict__ rng) {
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
   const int BW = 2 * W + 1;
   const int nb = D / NX;
   const double* S = Sb + (size_t)b * dmax * BW;
+  const int* rg = rng + (size_t)b * dmax * 2;
   const size_t nbmax = dmax / NX + 1;
   double* P = Pd + (size_t)b * nbmax * NX * NX;
   double* PL = Pl + (size_t)b * nbmax * NX * NX;
@@ -392,7 +432,7 @@ __global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int pr
     for (int k = threadIdx.x; k < nb; k += blockDim.x) {
       double* M = P + (size_t)k * NX * NX;
       for (int i = 0; i < NX; ++i)
-        for (int j = 0; j < NX; ++j) M[i * NX + j] = band_at(S, BW, W, k * NX + i, k * NX + j);
+        for (int j = 0; j < NX; ++j) M[i * NX + j] = band_at(S, rg, BW, W, k * NX + i, k * NX + j);
       h_gj_inverse(M, NX);
     }
     __syncthreads();
@@ -401,11 +441,11 @@ __global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int pr
         double* Sk = T + (size_t)k * NX * NX;
         if (k & 1) {   // P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1})
           for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, BW, W, k * NX + i, (k - 1) * NX + j);
+            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, BW, W, k * NX + i, (k - 1) * NX + j);
           h_neg_triple(P + (size_t)k * NX * NX, Sk, P + (size_t)(k - 1) * NX * NX, PL + (size_t)(k - 1) * NX * NX, NX);
         } else {       // P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk); stored as its transpose P_{k,k-1}
           for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, BW, W, (k - 1) * NX + i, k * NX + j);
+            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, BW, W, (k - 1) * NX + i, k * NX + j);
           double prod[NX * NX];
           h_neg_triple(P + (size_t)(k - 1) * NX * NX, Sk, P + (size_t)k * NX * NX, prod, NX);
           for (int i = 0; i < NX; ++i)
@@ -422,7 +462,7 @@ __global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int pr
       if (precond == PRECOND_NONE) {
         s = r[a];
       } else if (precond == PRECOND_J) {
-        s = (1.0 / band_at(S, BW, W, a, a)) * r[a];
+        s = (1.0 / band_at(S, rg, BW, W, a, a)) * r[a];
       } else if (a >= nb * NX) {
         s = 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
       } else {
@@ -446,9 +486,11 @@ __global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int pr
   };
   auto spmv = [&](const double* v, double* out) {
     for (int a = threadIdx.x; a < D; a += blockDim.x) {
+      // the row's structural range only: the terms left out are exact zeros
       double s = 0.0;
-      const int c0 = a - W > 0 ? a - W : 0, c1 = a + W < D - 1 ? a + W : D - 1;
-      for (int c = c0; c <= c1; ++c) s += S[(size_t)a * BW + (c - a + W)] * v[c];
+      const int c0 = rg[2 * a], c1 = rg[2 * a + 1];
+      const double* Sa = S + (size_t)a * BW + (W - a);
+      for (int c = c0; c <= c1; ++c) s += Sa[c] * v[c];
       out[a] = s;
     }
   };
@@ -513,20 +555,30 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int N, int NX, int W
                                                      const int* __restrict__ hcol, const double* __restrict__ hsgn,
                                                      const double* __restrict__ Sb, const double* __restrict__ gam,
                                                      double* __restrict__ M, double* __restrict__ rhs,
-                                                     double* __restrict__ lam, int* __restrict__ sing) {
+                                                     double* __restrict__ lam, int* __restrict__ sing,
+                                                     const int* __restrict__ rng) {
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
   const int BW = 2 * W + 1;
   const double* S = Sb + (size_t)b * dmax * BW;
+  const int* rg = rng + (size_t)b * dmax * 2;
   double* Mb = M + (size_t)b * dmax * BW;
   double* y = rhs + (size_t)b * dmax;
   __shared__ double fcol[1024];
   __shared__ double red[16];
   __shared__ int s_dup_a[64], s_dup_b[64];
   __shared__ double s_dup_s[64];
-  __shared__ int s_ndup, s_sing;
-  for (int e = threadIdx.x; e < D * BW; e += blockDim.x) Mb[e] = S[e];
+  __shared__ int s_ndup, s_sing, s_wr;
+  if (threadIdx.x == 0) s_wr = 0;
+  __syncthreads();
+  // M = S inside the row ranges, zero elsewhere; Wr = the half-bandwidth of those ranges, which the
+  // elimination's fill-in never leaves (no pivoting)
+  for (int e = threadIdx.x; e < D * BW; e += blockDim.x) {
+    const int a = e / BW, c = a - W + (e - a * BW);
+    Mb[e] = (c >= rg[2 * a] && c <= rg[2 * a + 1]) ? S[e] : 0.0;
+  }
+  for (int a = threadIdx.x; a < D; a += blockDim.x) atomicMax(&s_wr, max(a - rg[2 * a], rg[2 * a + 1] - a));
   for (int a = threadIdx.x; a < D; a += blockDim.x) y[a] = gam[(size_t)b * dmax + a];
   if (threadIdx.x == 0) {
     // knot-0 hard rows on state entries: duplicates of R_0 rows (rows 0..NX-1)
@@ -576,8 +628,9 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int N, int NX, int W
     }
   }
   __syncthreads();
+  const int Wr = s_wr;
   for (int p = 0; p < D; ++p) {
-    const int r1 = p + W < D - 1 ? p + W : D - 1;
+    const int r1 = p + Wr < D - 1 ? p + Wr : D - 1;
     const double piv = Mb[(size_t)p * BW + W];
     for (int r = p + 1 + threadIdx.x; r <= r1; r += blockDim.x) fcol[r - p - 1] = Mb[(size_t)r * BW + (p - r + W)] / piv;
     __syncthreads();
@@ -594,7 +647,7 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int N, int NX, int W
   }
   // back substitution
   for (int p = D - 1; p >= 0; --p) {
-    const int c1 = p + W < D - 1 ? p + W : D - 1;
+    const int c1 = p + Wr < D - 1 ? p + Wr : D - 1;
     double part = 0.0;
     for (int c = p + 1 + threadIdx.x; c <= c1; c += blockDim.x) part += Mb[(size_t)p * BW + (c - p + W)] * y[c];
     const double s = h_block_sum(part, red);
@@ -721,17 +774,18 @@ struct LaunchHard {
                          h.hcol, h.hsgn, h.hval, h.hslot, h.amask, h.iter, h.Wtr, h.tr_active);
       hipLaunchKernelGGL(k_hard_layout, dim3(B), dim3(64), 0, s, B, N, NX, h.rmax, h.active, h.cnt, h.roff, h.hoff,
                          h.dim, h.rkind, h.rknot, h.ridx, h.dmax);
-      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), 0, s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
+      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), 2 * N * sizeof(int), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
                          h.per_knot, h.A, h.Bm, h.cvec, h.x, h.u, h.jsoft, h.dim, h.rkind, h.rknot, h.ridx, h.hoff,
-                         h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam);
+                         h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam, h.rng);
     } else if (h.phase == 1) {
       if (h.precond == 0) {
         hipLaunchKernelGGL(k_hard_direct, dim3(B), dim3(256), 0, s, B, N, NX, h.W, h.dmax, h.rmax, h.active, h.dim,
-                           h.hoff, h.cnt, h.hcol, h.hsgn, h.Sb, h.gam, h.M, h.rhs, h.lam, h.sing);
+                           h.hoff, h.cnt, h.hcol, h.hsgn, h.Sb, h.gam, h.M, h.rhs, h.lam, h.sing,
+                           h.rng);
       } else {
         const size_t lds = ((size_t)5 * h.dmax + 16) * sizeof(double);
         hipLaunchKernelGGL((k_hard_pcg<NX>), dim3(B), dim3(256), lds, s, B, h.W, h.dmax, h.precond, h.active, h.dim,
-                           h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, h.Ptmp, h.lam, h.iters);
+                           h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, h.Ptmp, h.lam, h.iters, h.rng);
       }
     } else if (h.phase == 2) {
       hipLaunchKernelGGL((k_hard_dxu<NJ>), HGRID(B * N, 64), 0, s, h.C, B, N, h.dmax, h.rmax, h.active, h.Ghat,

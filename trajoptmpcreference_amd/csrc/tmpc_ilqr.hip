@@ -40,6 +40,7 @@ struct IlqrLds {
   double z[2][NX + NU];                 // knot k's [x_k; u_k] and the prefetched knot's (fp64: the soft terms)
   R dv[2];
   int fail;
+  R trash[64];                          // the stores of lanes without an output land here
 };
 
 // One 64-lane workgroup = one wave: LDS written by one lane is visible to the others once the
@@ -47,6 +48,16 @@ struct IlqrLds {
 // alone.  __syncthreads() would also drain the wave's outstanding global memory operations
 // (vmcnt(0)): the K_k / d_k stores of the previous knot and the next knot's prefetch loads.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// lane l's value of v, on every lane (v_readlane: no LDS round trip)
+__device__ __forceinline__ double lane_val(double v, int l) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)bits, l), hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float lane_val(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 
 // Diagnostic build only (-DTMPC_ILQR_STAMPS): per-phase s_memtime cycle totals of block 0's
 // backward sweep, printed at its end (tools/debug/ilqr_stamps.py).
@@ -72,7 +83,7 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 template <int NJ, class R, bool MF>
 __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
-                                                      int B, int N, const double* __restrict__ x,
+                                                      PList P, int B, int N, const double* __restrict__ x,
                                                       const double* __restrict__ u, const double* __restrict__ rho_in,
                                                       const int* __restrict__ active, const double* __restrict__ Aall,
                                                       const double* __restrict__ Ball, const double* __restrict__ mu,
@@ -82,7 +93,8 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
                                                       int* __restrict__ ok) {
   constexpr int NX = 2 * NJ, NU = NJ, NC = NX + 1;
   constexpr int NA = (NX * NX + 63) / 64, NB = (NX * NU + 63) / 64;   // prefetch slots per lane
-  const int b = blockIdx.x;
+  if (!P.has(blockIdx.x, B)) return;
+  const int b = P.at(blockIdx.x);
   if (!active[b]) return;
   __shared__ IlqrLds<NJ, R> L;
   const int t = threadIdx.x;
@@ -92,6 +104,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   const double* ub = u + (size_t)b * NU * K;
   const bool soft = jsoft != nullptr;   // soft limits: their jacobians precomputed (k_ilqr_soft_jac)
   const int qf_start = C->QF_start;
+  const bool diag = C->diag != 0;
 
   // the cost blocks once (QuadraticCost, TrajoptCost.py:71-83)
   for (int e = t; e < NX * NX; e += 64) {
@@ -142,16 +155,31 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     if (t < 3 * NJ) L.jac[t] = R(pj);   // 0 without soft limits
     wave_lds_sync();
     const R* Qk = use_qf(k) ? L.QF : L.Q;
-    if (t < NX) {
-      R g = 0.0;
-      for (int m = 0; m < NX; ++m) g += R(zk[m] - L.xg[m]) * Qk[m * NX + t];
-      L.lx[t] = g + L.jac[t];
-    } else if (t < NX + NU && !term) {
-      const int c = t - NX;
-      R g = 0.0;
-      for (int m = 0; m < NU; ++m) g += R(zk[NX + m]) * L.Rc[m * NU + c];
-      L.lu[c] = g + L.jac[NX + c];
+    // lanes < NX: l_x[t], lanes NX .. NX + NU - 1: l_u[t - NX].  Both dot products on every lane and
+    // one store: the wave would execute both sides of a divergent branch anyway, plus its exec
+    // bookkeeping (one wave per problem: every instruction is on the critical path)
+    const int tx = t < NX ? t : NX - 1;
+    const bool isu = t >= NX && t < NX + NU;
+    const int tu = isu ? t - NX : 0;
+    R g = 0.0, gu = 0.0;
+    if (diag) {   // the same chains without their exact-zero terms (CostDev.diag)
+      R y[NX], w[NU];
+#pragma unroll
+      for (int m = 0; m < NX; ++m) y[m] = R(zk[m] - L.xg[m]);
+#pragma unroll
+      for (int m = 0; m < NU; ++m) w[m] = R(zk[NX + m]);
+      g = fma_r(y[tx], Qk[tx * NX + tx], R(0)) + diag_poison(y, NX);
+      gu = fma_r(w[tu], L.Rc[tu * NU + tu], R(0)) + diag_poison(w, NU);
+    } else {
+#pragma unroll
+      for (int m = 0; m < NX; ++m) g += R(zk[m] - L.xg[m]) * Qk[m * NX + tx];
+#pragma unroll
+      for (int m = 0; m < NU; ++m) gu += R(zk[NX + m]) * L.Rc[m * NU + tu];
     }
+    const R vx = g + L.jac[tx];
+    const R vu = gu + L.jac[NX + tu];
+    R* dst = t < NX ? &L.lx[t] : ((isu && !term) ? &L.lu[tu] : &L.trash[t]);
+    *dst = t < NX ? vx : vu;
   };
   // l_xx (+ per-type outer products on the q / qd diagonal blocks)
   auto lxx = [&](int k, int r, int c) -> R {
@@ -225,15 +253,16 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
 #pragma unroll
         for (int s = 0; s < KS; ++s) pv[tl] = __builtin_amdgcn_mfma_f64_16x16x4f64(vf[s], abf[tl][s], pv[tl], 0, 0, 0);
       }
+      // row NX of the product (the [A B]^T V_x row) sits in reg NX / 4 of the lanes with hi = NX % 4
+      constexpr int IR = NX / 4, HR = NX % 4;
 #pragma unroll
-      for (int tl = 0; tl < 2; ++tl)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (hi + 4 * i == NX) {
-            const int c = 16 * tl + lo;
-            if (c < NX) L.Qx[c] = L.lx[c] + R(pv[tl][i]);
-            else if (c < NX + NU) L.Qu[c - NX] = L.lu[c - NX] + R(pv[tl][i]);
-          }
+      for (int tl = 0; tl < 2; ++tl) {
+        const int c = 16 * tl + lo;
+        const bool isx = c < NX, isu = !isx && c < NX + NU;
+        const R base = isx ? L.lx[isx ? c : 0] : L.lu[isu ? c - NX : 0];
+        R* dst = (hi == HR && isx) ? &L.Qx[isx ? c : 0] : ((hi == HR && isu) ? &L.Qu[isu ? c - NX : 0] : &L.trash[t]);
+        *dst = base + R(pv[tl][IR]);
+      }
       // [A B]^T [P VB]: tile (tr, tc); B operand of k-step s = reg s of pv[tc] (rows >= NX zeroed)
 #pragma unroll
       for (int tr = 0; tr < 2; ++tr)
@@ -245,18 +274,33 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
             const double bop = 4 * s + hi < NX ? pv[tc][s] : 0.0;
             q = __builtin_amdgcn_mfma_f64_16x16x4f64(abf[tr][s], bop, q, 0, 0, 0);
           }
+          // element i of the tile: row 16 tr + hi + 4 i, column 16 tc + lo.  Which of Q_xx / Q_ux /
+          // Q_uu it can belong to is fixed per (tr, tc, i) up to the lane's hi / lo: the impossible
+          // cases drop out at compile time, the rest is one select-and-store (same expressions)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int r = 16 * tr + hi + 4 * i, c = 16 * tc + lo;
+            const int r0 = 16 * tr + 4 * i, c0 = 16 * tc;          // compile-time after unrolling
+            const bool can_rx = r0 < NX, can_ru = r0 + 3 >= NX && r0 < NX + NU;
+            const bool can_cx = c0 < NX, can_cu = c0 + 15 >= NX && c0 < NX + NU;
+            const bool can_xx = can_rx && can_cx, can_ux = can_ru && can_cx, can_uu = can_ru && can_cu;
+            if (!(can_xx || can_ux || can_uu)) continue;
+            const int r = r0 + hi, c = c0 + lo;
             const R v = R(q[i]);
-            if (r < NX && c < NX) {
-              L.Qxx[r * NX + c] = lxx(k, r, c) + v;
-            } else if (r >= NX && r < NX + NU && c < NX) {
-              L.Qux[(r - NX) * NX + c] = v;
-            } else if (r >= NX && r < NX + NU && c >= NX && c < NX + NU) {
-              const int rr = r - NX, cc = c - NX;
-              L.Quu[rr * NU + cc] = (L.Rc[rr * NU + cc] + L.jac[NX + rr] * L.jac[NX + cc]) + v + (rr == cc ? rho : R(0));
+            const bool rx = r < NX, ru = r >= NX && r < NX + NU, cx = c < NX, cu = c >= NX && c < NX + NU;
+            const bool xx = can_xx && rx && cx, ux = can_ux && ru && cx, uu = can_uu && ru && cu;
+            const int rr = ru ? r - NX : 0, cc = cu ? c - NX : 0;
+            R val = v;
+            if (can_xx) {
+              const R vxx = lxx(k, rx ? r : 0, cx ? c : 0) + v;
+              val = xx ? vxx : val;
             }
+            if (can_uu) {
+              const R vuu = (L.Rc[rr * NU + cc] + L.jac[NX + rr] * L.jac[NX + cc]) + v + (rr == cc ? rho : R(0));
+              val = uu ? vuu : val;
+            }
+            R* dst = xx ? &L.Qxx[(rx ? r : 0) * NX + (cx ? c : 0)]
+                        : (ux ? &L.Qux[rr * NX + (cx ? c : 0)] : (uu ? &L.Quu[rr * NU + cc] : &L.trash[t]));
+            *dst = val;
           }
         }
       wave_lds_sync();
@@ -319,7 +363,9 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     IL_STAMP(2);
     // [K | d] = -Q_uu^-1 [Q_ux | Q_u]: Cholesky Q_uu = L L^T (every lane, from LDS), then lane c
     // solves its right-hand-side column c; Q_uu not positive definite -> backward failure
-    if (t < NC) {
+    {
+      // every lane factors (the wave would anyway); lanes >= NC solve a copy of column NC - 1
+      const int tc = t < NC ? t : NC - 1;
       R Lc[NU][NU];
       bool pd = true;
 #pragma unroll
@@ -341,7 +387,8 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       R y[NU];
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
-        R v = t < NX ? L.Qux[i * NX + t] : L.Qu[i];
+        const R vx = L.Qux[i * NX + (tc < NX ? tc : 0)], vu = L.Qu[i];
+        R v = tc < NX ? vx : vu;
 #pragma unroll
         for (int m = 0; m < i; ++m) v -= Lc[i][m] * y[m];
         y[i] = v / Lc[i][i];
@@ -354,7 +401,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
         y[i] = v / Lc[i][i];
       }
 #pragma unroll
-      for (int i = 0; i < NU; ++i) L.KD[i * NC + t] = -y[i];
+      for (int i = 0; i < NU; ++i) *(t < NC ? &L.KD[i * NC + tc] : &L.trash[t]) = -y[i];
       if (t == 0 && !pd) L.fail = 1;
     }
     wave_lds_sync();
@@ -375,9 +422,13 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if (4 * i >= NX) continue;   // rows past NX: none
         const int r = hi + 4 * i, c = lo;
-        if (r < NX && c < NX) L.P[r * NX + c] = L.Qxx[r * NX + c] + R(mv[i]);
-        else if (r < NX && c == NX) L.Vx[r] = L.Qx[r] + R(mv[i]);
+        const bool rx = r < NX, cx = c < NX, cv = c == NX;
+        const int rs = rx ? r : 0;
+        const R base = cx ? L.Qxx[rs * NX + (cx ? c : 0)] : L.Qx[rs];
+        R* dst = (rx && cx) ? &L.P[rs * NX + (cx ? c : 0)] : ((rx && cv) ? &L.Vx[rs] : &L.trash[t]);
+        *dst = base + R(mv[i]);
       }
     } else
     for (int e = t; e < NX * NX + NX; e += 64) {
@@ -395,42 +446,44 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
         L.Vx[r] = L.Qx[r] + s;
       }
     }
-    if (t == 63) {
-      // operands to registers first (one wave alone: each LDS read in the chain would expose its latency)
-      R dd[NU], qu[NU], quu[NU * NU];
+    {
+      // dV: lane i forms (Q_uu d)_i, then the two sums run in i order on values every lane holds
+      // (the same chains as one lane computing everything, without its serial 6 x 6 product)
+      R dd[NU], qu[NU];
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
         dd[i] = L.KD[i * NC + NX];
         qu[i] = L.Qu[i];
       }
+      const int iq = t < NU ? t : NU - 1;
+      R qd = 0.0;
 #pragma unroll
-      for (int i = 0; i < NU * NU; ++i) quu[i] = L.Quu[i];
+      for (int m = 0; m < NU; ++m) qd += L.Quu[iq * NU + m] * dd[m];
       R s1 = 0.0, s2 = 0.0;
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
         const R di = dd[i];
         s1 += di * qu[i];
-        R qd = 0.0;
-#pragma unroll
-        for (int m = 0; m < NU; ++m) qd += quu[i * NU + m] * dd[m];
-        s2 += di * qd;
+        s2 += di * lane_val(qd, i);
       }
-      L.dv[0] += s1;
-      L.dv[1] += R(0.5) * s2;
+      if (t == 0) {
+        L.dv[0] += s1;
+        L.dv[1] += R(0.5) * s2;
+      }
     }
     IL_STAMP(4);
     // K_k, d_k to HBM ([B][K][NU][NX], [B][K][NU]); not waited for (wave_lds_sync)
-    for (int e = t; e < NU * NC; e += 64) {
-      const int i = e / NC, c = e % NC;
-      if (c < NX)
-        Kout[(((size_t)b * K + k) * NU + i) * NX + c] = double(L.KD[e]);
-      else
-        dout[((size_t)b * K + k) * NU + i] = double(L.KD[e]);
+#pragma unroll
+    for (int j = 0; j < (NU * NC + 63) / 64; ++j) {
+      const int e = t + 64 * j, i = e / NC, c = e % NC;
+      double* dst = c < NX ? Kout + (((size_t)b * K + k) * NU + i) * NX + c : dout + ((size_t)b * K + k) * NU + i;
+      if (e < NU * NC) *dst = double(L.KD[e]);
     }
     wave_lds_sync();
-    for (int e = t; e < NX * NX; e += 64) {
-      const int r = e / NX, c = e % NX;
-      L.Vxx[e] = R(0.5) * (L.P[r * NX + c] + L.P[c * NX + r]);
+#pragma unroll
+    for (int j = 0; j < (NX * NX + 63) / 64; ++j) {
+      const int e = t + 64 * j, r = e / NX, c = e % NX;
+      if (e < NX * NX) L.Vxx[e] = R(0.5) * (L.P[r * NX + c] + L.P[c * NX + r]);
     }
     IL_STAMP(5);
     if (k > 0) {
@@ -461,6 +514,22 @@ __device__ __forceinline__ double knot_quad_cost(const CostDev* __restrict__ C, 
                                                  const double* uh, bool term) {
   constexpr int NX = 2 * NJ, NU = NJ;
   const double* Qk = use_QF(C, k, N) ? C->QF : C->Q;
+  if (C->diag) {   // the same chains without their exact-zero terms (CostDev.diag)
+    double y[NX];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) y[r] = xh[r] - C->xg[r];
+    double vq = 0.0;
+#pragma unroll
+    for (int r = 0; r < NX; ++r) vq = __fma_rn(y[r], __fma_rn(Qk[r * NX + r], y[r], 0.0), vq);
+    double cost = 0.5 * (vq + diag_poison(y, NX));
+    if (!term) {
+      double vr = 0.0;
+#pragma unroll
+      for (int r = 0; r < NU; ++r) vr = __fma_rn(uh[r], __fma_rn(C->R[r * NU + r], uh[r], 0.0), vr);
+      cost = __fma_rn(0.5, vr + diag_poison(uh, NU), cost);
+    }
+    return cost;
+  }
   double vq = 0.0;
 #pragma unroll
   for (int r = 0; r < NX; ++r) {
@@ -493,11 +562,12 @@ __device__ __forceinline__ double knot_quad_cost(const CostDev* __restrict__ C, 
 template <int NJ, bool SOFT>
 __global__ void __launch_bounds__(64) k_ilqr_init_cost(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
                                                        const double* __restrict__ mu, const double* __restrict__ lam,
-                                                       int N, const double* __restrict__ x,
+                                                       PList P, int B, int N, const double* __restrict__ x,
                                                        const double* __restrict__ u, const int* __restrict__ mask,
                                                        double* __restrict__ Jt) {
   constexpr int NX = 2 * NJ, NU = NJ;
-  const int b = blockIdx.x;
+  if (!P.has(blockIdx.x, B)) return;
+  const int b = P.at(blockIdx.x);
   if (!mask[b]) return;
   extern __shared__ double sc[];   // [2][N]
   const int K = N - 1;
@@ -559,8 +629,8 @@ struct FwdPf {
 template <int NJ, bool CHAIN, bool SOFT, class MT, class R, bool PF>
 __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __restrict__ C,
                                                      const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
-                                                     const double* __restrict__ lam, int B, int N, int T, double dt,
-                                                     int init, const double* __restrict__ alphas,
+                                                     const double* __restrict__ lam, PList P, int B, int N, int T,
+                                                     double dt, int init, const double* __restrict__ alphas,
                                                      const double* __restrict__ x, const double* __restrict__ u,
                                                      const double* __restrict__ Kg, const double* __restrict__ dg,
                                                      const int* __restrict__ active, const int* __restrict__ ok,
@@ -571,13 +641,17 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
   MT M = Mg;
   if constexpr (!MT::STATIC) M = ModelRef{stage_model(Mg.p, &sM)};
   constexpr int NX = 2 * NJ, NU = NJ;
-  using P = FwdPf<NJ>;
+  using PF_ = FwdPf<NJ>;
   extern __shared__ __align__(16) double pfb[];
   const int lane = threadIdx.x;
   const int gid = blockIdx.x * blockDim.x + lane;
-  const int bl = min(gid, B * T - 1) / T;   // (dead lanes of the last group: the last problem, unused)
-  const int b = bl, tr = min(gid, B * T - 1) - b * T;
-  const bool live = gid < B * T && active[b] && (init || ok[b]);
+  // lanes over (listed problem p, trial); the problem list's last entry stands in for dead lanes
+  const int np = P.cnt ? min(B, *P.cnt) : B;
+  if (np <= 0) return;
+  const int pt = min(gid, np * T - 1);
+  const int pp = pt / T, tr = pt - pp * T;
+  const int b = P.at(pp);
+  const bool live = gid < np * T && active[b] && (init || ok[b]);
   const bool pf = PF && !init;
   if (pf) {
     if (__ballot(live) == 0) return;   // the whole wave: no work, no prefetch to share
@@ -588,28 +662,38 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
   const double al = init ? 0.0 : alphas[tr];
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NU * K;
-  double* xo = xt + (size_t)gid * NX * N;
-  double* uo = ut + (size_t)gid * NU * K;
-  // prefetch bookkeeping: problems [p0, p0 + nprob) of this group, this lane's problem slot pl
+  const size_t bt = (size_t)b * T + tr;   // this lane's trial slot
+  double* xo = xt + bt * NX * N;
+  double* uo = ut + bt * NU * K;
+  // prefetch bookkeeping: listed problems [p0, p0 + nprob) of this group, this lane's problem slot pl.
+  // Their batch indices are read from the problem list once, into LDS: an index load per piece
+  // inside the knot loop would make every LDS-DMA issue wait for the one before it (vmcnt counts
+  // both in issue order).
   const int p0 = (int)(blockIdx.x * blockDim.x) / T;
-  const int npf = P::nprob(T);
-  const int pl = b - p0;
+  const int npf = PF_::nprob(T);
+  const int pl = pp - p0;
+  __shared__ int s_pb[64];
+  const int npt = min(npf, 64);   // the slots a lane can own (pl < 64); higher ones only pad
+  if (pf) {
+    if (lane < npt) s_pb[lane] = P.at(min(p0 + lane, np - 1));
+    __syncthreads();
+  }
   auto prefetch = [&](int kn, int slot) {
-    double* buf = pfb + (size_t)slot * (P::rk(T) + P::rs(T));
+    double* buf = pfb + (size_t)slot * (PF_::rk(T) + PF_::rs(T));
     // K_kn: 16-byte pieces, lane-linear destinations
-    for (int j = 0; j * 64 < npf * P::CK; ++j) {
+    for (int j = 0; j * 64 < npf * PF_::CK; ++j) {
       const int c = j * 64 + lane;
-      const int p = c / P::CK, w = c - p * P::CK;
-      const int bb = min(p0 + p, B - 1);
-      const double* src = Kg + ((size_t)bb * K + kn) * P::SK + 2 * w;
+      const int p = c / PF_::CK, w = c - p * PF_::CK;
+      const int bb = s_pb[min(p, npt - 1)];
+      const double* src = Kg + ((size_t)bb * K + kn) * PF_::SK + 2 * w;
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + (size_t)j * 128), 16, 0, 0);
     }
     // d_kn, x_kn, u_kn: dwords
-    double* sb = buf + P::rk(T);
-    for (int j = 0; j * 64 < npf * 2 * P::SS; ++j) {
+    double* sb = buf + PF_::rk(T);
+    for (int j = 0; j * 64 < npf * 2 * PF_::SS; ++j) {
       const int q = j * 64 + lane;
-      const int p = q / (2 * P::SS), r = q - p * (2 * P::SS), item = r >> 1, half = r & 1;
-      const int bb = min(p0 + p, B - 1);
+      const int p = q / (2 * PF_::SS), r = q - p * (2 * PF_::SS), item = r >> 1, half = r & 1;
+      const int bb = s_pb[min(p, npt - 1)];
       const double* src = item < NU ? dg + ((size_t)bb * K + kn) * NU + item
                         : item < NU + NX ? x + ((size_t)bb * NX + (item - NU)) * N + kn
                                          : u + ((size_t)bb * NU + (item - NU - NX)) * K + kn;
@@ -646,9 +730,9 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
 #pragma unroll
         for (int i = 0; i < NU; ++i) uh[i] = ub[i * K + k];
       } else if (pf) {
-        const double* buf = pfb + (size_t)(k & 1) * (P::rk(T) + P::rs(T));
-        const double* Kk = buf + (size_t)pl * P::SK;
-        const double* sk = buf + P::rk(T) + (size_t)pl * P::SS;   // d_k | x_k | u_k
+        const double* buf = pfb + (size_t)(k & 1) * (PF_::rk(T) + PF_::rs(T));
+        const double* Kk = buf + (size_t)pl * PF_::SK;
+        const double* sk = buf + PF_::rk(T) + (size_t)pl * PF_::SS;   // d_k | x_k | u_k
         double dx[NX];
 #pragma unroll
         for (int m = 0; m < NX; ++m) dx[m] = xh[m] - sk[NU + m];
@@ -721,7 +805,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
     printf("ilqr_fwd_stamps K=%d loads+feedback %llu cost %llu aba %llu euler %llu soft %llu\n", K, st_[0], st_[1],
            st_[2], st_[3] + st_[7], 0ull);
 #endif
-  Jt[gid] = J;
+  Jt[bt] = J;
 }
 
 // The soft-limit values of the trial trajectories (value_soft_constraints, summed after the cost
@@ -732,13 +816,16 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
 // 1.0 ms forward launches).
 template <int NJ>
 __global__ void __launch_bounds__(64) k_ilqr_soft_add(const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
-                                                      const double* __restrict__ lam, int B, int N, int T,
+                                                      const double* __restrict__ lam, PList P, int B, int N, int T,
                                                       const double* __restrict__ xt, const double* __restrict__ ut,
                                                       const int* __restrict__ active, const int* __restrict__ ok,
                                                       double* __restrict__ Jt) {
   constexpr int NX = 2 * NJ, NU = NJ;
-  const int gid = blockIdx.x, b = gid / T;
+  const int pp = blockIdx.x / T, tr = blockIdx.x - pp * T;
+  if (!P.has(pp, B)) return;
+  const int b = P.at(pp);
   if (!active[b] || !ok[b]) return;
+  const size_t gid = (size_t)b * T + tr;
   extern __shared__ double sv[];   // [N]
   const int K = N - 1;
   const double* xo = xt + (size_t)gid * NX * N;
@@ -766,14 +853,17 @@ __global__ void __launch_bounds__(64) k_ilqr_soft_add(const ConstrDev* __restric
 // to mu / lambda in HBM per knot on its critical path; it now prefetches row k - 1 with A_{k-1}.
 template <int NJ>
 __global__ void __launch_bounds__(256) k_ilqr_soft_jac(const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
-                                                       const double* __restrict__ lam, int B, int N,
+                                                       const double* __restrict__ lam, PList P, int B, int N,
                                                        const double* __restrict__ x, const double* __restrict__ u,
                                                        const int* __restrict__ active, double* __restrict__ jout) {
   constexpr int NX = 2 * NJ, NU = NJ;
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= B * N) return;
-  const int b = gid / N, k = gid - b * N;
+  const int pk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pk >= B * N) return;
+  const int p = pk / N, k = pk - p * N;
+  if (!P.has(p, B)) return;
+  const int b = P.at(p);
   if (!active[b]) return;
+  const size_t gid = (size_t)b * N + k;
   const int K = N - 1;
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NU * K;
@@ -792,7 +882,7 @@ __global__ void __launch_bounds__(256) k_ilqr_soft_jac(const ConstrDev* __restri
 // One 64-lane workgroup per problem.  Acceptance ratio (J - J^) / (-alpha (dV1 + alpha dV2)) in
 // [exp_red_min, exp_red_max] in the reference's alpha order (oracle/ilqr.py), rho schedule and exit
 // codes of reduce_regularization / check_for_exit_or_error (:457-481), trace row, trajectory copy.
-__global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU, int T, int init,
+__global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int NX, int NU, int T, int init,
                                                     const double* __restrict__ alphas, SolverOpts o,
                                                     const double* __restrict__ Jt, const double* __restrict__ dV,
                                                     const int* __restrict__ okb, const double* __restrict__ xt,
@@ -800,7 +890,8 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
                                                     double* __restrict__ u, ProbState st, TraceDev tr,
                                                     int* __restrict__ active_count,
                                                     unsigned long long* __restrict__ counters) {
-  const int b = blockIdx.x;
+  if (!P.has(blockIdx.x, B)) return;
+  const int b = P.at(blockIdx.x);
   if (!st.active[b]) return;
   __shared__ int s_choice;
   const int t = threadIdx.x;
@@ -894,7 +985,7 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(int B, int N, int NX, int NU
 
 template <int NJ, bool CHAIN, class MT>
 struct LaunchIlqr {
-  static void backward(bool f32, hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
+  static void backward(bool f32, hipStream_t s, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N, const double* x,
                        const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                        const double* mu, const double* lam, double* jscratch, double* K, double* d, double* dV,
                        int* ok) {
@@ -904,21 +995,21 @@ struct LaunchIlqr {
     // soft limits: every knot's jacobian first, in parallel ([B][N][3 NJ] in jscratch)
     const double* js = nullptr;
     if (mu) {
-      hipLaunchKernelGGL((k_ilqr_soft_jac<NJ>), TMPC_GRID(B * N, 256), 0, s, Cs, mu, lam, B, N, x, u, active, jscratch);
+      hipLaunchKernelGGL((k_ilqr_soft_jac<NJ>), TMPC_GRID(B * N, 256), 0, s, Cs, mu, lam, P, B, N, x, u, active, jscratch);
       js = jscratch;
     }
     if (f32)
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, float, false>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, float, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
                          Bm, mu, lam, js, K, d, dV, ok);
     else if (mf)
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, true>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, true>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
                          Bm, mu, lam, js, K, d, dV, ok);
     else
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, false>), dim3(B), dim3(64), 0, s, C, Cs, B, N, x, u, rho, active, A,
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
                          Bm, mu, lam, js, K, d, dV, ok);
   }
   static void forward(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
-                      const double* lam, int B, int N, int T, double dt, int init, const double* alphas,
+                      const double* lam, PList P, int B, int N, int T, double dt, int init, const double* alphas,
                       const double* x, const double* u, const double* K, const double* d, const int* active,
                       const int* ok, double* xt, double* ut, double* Jt) {
     // the prefetching instance when its LDS buffers fit (T >= 2: <= 33 problems per group); init
@@ -929,17 +1020,17 @@ struct LaunchIlqr {
 #define TMPC_FWD(SOFTV, RV)                                                                                          \
     if (pf)                                                                                                          \
       hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV, true>), TMPC_GRID(B * T, 64), pf_lds, s,           \
-                         MT::make(M), C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt); \
+                         MT::make(M), C, Cs, mu, lam, P, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt); \
     else                                                                                                             \
       hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV, false>), TMPC_GRID(B * T, 64), 0, s, MT::make(M),  \
-                         C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
+                         C, Cs, mu, lam, P, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
     // soft limits: the rollouts sum the cost terms, k_ilqr_soft_add the soft values (INIT: in the kernel)
     if (mu && init) { if (f32) { TMPC_FWD(true, float) } else { TMPC_FWD(true, double) } }
     else { if (f32) { TMPC_FWD(false, float) } else { TMPC_FWD(false, double) } }
 #undef TMPC_FWD
     if (mu && !init)
-      hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B * T), dim3(64), N * sizeof(double), s, Cs, mu, lam, B, N, T, xt,
-                         ut, active, ok, Jt);
+      hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B * T), dim3(64), N * sizeof(double), s, Cs, mu, lam, P, B, N, T,
+                         xt, ut, active, ok, Jt);
   }
 };
 
@@ -960,33 +1051,34 @@ struct LaunchIlqr {
   }                                                                                                    \
   return 0;
 
-int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N,
+int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N,
                          const double* x, const double* u, const double* rho, const int* active, const double* A,
                          const double* Bm, const double* mu, const double* lam, double* jscratch, double* K,
                          double* d, double* dV, int* ok) {
   const int mid = 0;
-  TMPC_DISPATCH_ILQR(nj, true, backward(f32, s, C, Cs, B, N, x, u, rho, active, A, Bm, mu, lam, jscratch, K, d, dV, ok))
+  TMPC_DISPATCH_ILQR(nj, true, backward(f32, s, C, Cs, P, B, N, x, u, rho, active, A, Bm, mu, lam, jscratch, K, d, dV,
+                                        ok))
 }
 
 int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C,
-                        const ConstrDev* Cs, const double* mu, const double* lam, int B, int N, int T, double dt,
-                        int init, const double* alphas, const double* x, const double* u, const double* K,
+                        const ConstrDev* Cs, const double* mu, const double* lam, PList P, int B, int N, int T,
+                        double dt, int init, const double* alphas, const double* x, const double* u, const double* K,
                         const double* d, const int* active, const int* ok, double* xt, double* ut, double* Jt) {
-  TMPC_DISPATCH_ILQR(nj, chain, forward(f32, s, M, C, Cs, mu, lam, B, N, T, dt, init, alphas, x, u, K, d, active, ok,
+  TMPC_DISPATCH_ILQR(nj, chain, forward(f32, s, M, C, Cs, mu, lam, P, B, N, T, dt, init, alphas, x, u, K, d, active, ok,
                                         xt, ut, Jt))
 }
 
 int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, const double* mu,
-                          const double* lam, int B, int N, const double* x, const double* u, const int* mask,
+                          const double* lam, PList P, int B, int N, const double* x, const double* u, const int* mask,
                           double* Jt) {
   const size_t lds = (size_t)2 * N * sizeof(double);
   if (lds > 64 * 1024) return -1;
 #define TMPC_INIT_COST(V)                                                                                      \
   case V:                                                                                                      \
     if (mu)                                                                                                    \
-      hipLaunchKernelGGL((k_ilqr_init_cost<V, true>), dim3(B), dim3(64), lds, s, C, Cs, mu, lam, N, x, u, mask, Jt); \
+      hipLaunchKernelGGL((k_ilqr_init_cost<V, true>), dim3(B), dim3(64), lds, s, C, Cs, mu, lam, P, B, N, x, u, mask, Jt); \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_ilqr_init_cost<V, false>), dim3(B), dim3(64), lds, s, C, Cs, mu, lam, N, x, u, mask, Jt); \
+      hipLaunchKernelGGL((k_ilqr_init_cost<V, false>), dim3(B), dim3(64), lds, s, C, Cs, mu, lam, P, B, N, x, u, mask, Jt); \
     return 0;
   switch (nj) {
     TMPC_INIT_COST(1) TMPC_INIT_COST(2) TMPC_INIT_COST(3) TMPC_INIT_COST(4) TMPC_INIT_COST(5) TMPC_INIT_COST(6)
@@ -996,11 +1088,11 @@ int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrD
 #undef TMPC_INIT_COST
 }
 
-void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,
+void launch_ilqr_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int T, int init, const double* alphas,
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
                         int* active_count, unsigned long long* counters) {
-  hipLaunchKernelGGL(k_ilqr_decide, dim3(B), dim3(64), 0, s, B, N, NX, NU, T, init, alphas, o, Jt, dV, ok, xt, ut, x,
+  hipLaunchKernelGGL(k_ilqr_decide, dim3(B), dim3(64), 0, s, P, B, N, NX, NU, T, init, alphas, o, Jt, dV, ok, xt, ut, x,
                      u, st, tr, active_count, counters);
 }
 

@@ -17,6 +17,21 @@ int ctx_fail(tmpc_ctx* ctx, const char* fmt, ...);
 int ctx_device(const tmpc_ctx* ctx);
 hipStream_t ctx_stream(const tmpc_ctx* ctx);
 
+// The problems a batch-iteration launch visits: launches over B problems take (PList, nb) and visit
+// problems P.at(p) for p < nb (and p < *P.cnt).  idx null: the identity, nb = B.  Otherwise idx is the
+// ascending list of the problems still alive in the lock-step loop (k_alive_list, rebuilt at the end of
+// every batch iteration on the stream, so exact when a launch reads it) and nb the host's upper bound
+// of its length (the count of two iterations before: aliveness only ever ends).  Every kernel still
+// tests its own per-problem mask (active / need_grad / ...): the list only drops the problems that can
+// no longer be active, so the lock-step tail stops dispatching thousands of early-exit workgroups.
+struct PList {
+  const int* idx;
+  const int* cnt;
+  __device__ __forceinline__ int at(int p) const { return idx ? idx[p] : p; }
+  __device__ __forceinline__ bool has(int p, int nb) const { return p < nb && (!cnt || p < *cnt); }
+};
+void launch_alive_list(hipStream_t s, int B, const int* alive, int* idx, int* cnt, int* host_slot);
+
 // PRECOND_NONE: the identity preconditioner '0' (PCG.py:114-118)
 enum { PRECOND_J = 1, PRECOND_BJ = 2, PRECOND_SS = 3, PRECOND_NONE = 4 };
 enum { LS_MODE_INIT = 0, LS_MODE_STEP = 1 };
@@ -71,14 +86,14 @@ struct TraceDev {
 
 // f32: rigid-body dynamics (and, for launch_ilqr_backward, the Riccati sweep) in fp32 --
 // tmpc_options.precision F32 / MIXED; every buffer stays fp64
-int launch_qp_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
+int launch_qp_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, PList P, int B, int N, double dt, const double* x,
                  const double* u, const double* xs, const int* need, double* qdd, double* cvec);
-int launch_qp_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, const double* x,
+int launch_qp_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, PList P, int B, int N, const double* x,
                    const int* need, double* minv);
-int launch_qp_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, const double* x,
+int launch_qp_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, PList P, int B, int N, double dt, const double* x,
                    const int* need, const double* qdd, const double* minv, double* A, double* Bm);
 int launch_ls_terms(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
-                    const double* mu, const double* lam, int B, int N, int T, double dt, const double* alphas,
+                    const double* mu, const double* lam, PList P, int B, int N, int T, double dt, const double* alphas,
                     const double* x, const double* u, const double* xs, const double* dx, const double* du,
                     const int* active, double* terms);
 int launch_unit_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
@@ -88,8 +103,8 @@ int launch_unit_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const
                      const double* qdd, const double* minv, double* A, double* Bm, double* dqdd);
 int launch_rollout(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
                    const double* u);
-int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G);
-int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, int mode, const double* x,
+int launch_ginv(hipStream_t s, int nj, const CostDev* C, PList P, int B, const double* rho, const int* active, double* G);
+int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, int precond, int mode, const double* x,
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
@@ -106,7 +121,7 @@ inline int qp_gm_min_rows() {
   const int v = e ? atoi(e) : 0;
   return v > 0 ? v : 1025;
 }
-int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
+int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N, const double* rho,
                      const int* active, const double* x, const double* u, const double* mu, const double* lam,
                      double* Gk, double* jsoft);
 int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
@@ -116,30 +131,30 @@ int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const
                    const double* gam, double* U, double* Y, double* lam);
 int pcg_set_max_lds();
 void launch_sum_counters(hipStream_t s, int B, const unsigned long long* pc, unsigned long long* out);
-void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
+void launch_ls_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
                       int* active_count, unsigned long long* counters, const double* hterms,
                       const int* qp_singular = nullptr);
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active);
 // st / act_init / rho_init: the per-problem outer loop (null act_init: lock-step, tmpc_kernels.hip)
-void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
+void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, PList P, int B, int N, int nj, double tol, int max_iter,
                        const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
                        int* outer_iter, int* exit_soft, int* outer_count, const ProbState* st = nullptr,
                        int* act_init = nullptr, double rho_init = 0.0);
-void launch_activate(hipStream_t s, int B, int* act_init, int* active);
-int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* x,
+void launch_activate(hipStream_t s, PList P, int B, int* act_init, int* active);
+int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N, const double* x,
                          const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                          const double* mu, const double* lam, double* jscratch, double* K, double* d, double* dV,
                          int* ok);
 int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, const CostDev* C, const ConstrDev* Cs,
-                        const double* mu, const double* lam, int B, int N, int T, double dt, int init,
+                        const double* mu, const double* lam, PList P, int B, int N, int T, double dt, int init,
                         const double* alphas, const double* x, const double* u, const double* K, const double* d,
                         const int* active, const int* ok, double* xt, double* ut, double* Jt);
 int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, const double* mu,
-                          const double* lam, int B, int N, const double* x, const double* u, const int* mask,
+                          const double* lam, PList P, int B, int N, const double* x, const double* u, const int* mask,
                           double* Jt);
-void launch_ilqr_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int init, const double* alphas,
+void launch_ilqr_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int T, int init, const double* alphas,
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
                         int* active_count, unsigned long long* counters);
@@ -165,6 +180,7 @@ struct HardArgs {
   int* hslot;                     // [B][N][rmax] t * 2n + e of each row
   unsigned long long* amask;      // [B][N] active-set bitmask per knot (bit t * 2n + e)
   int* sing;                      // [B] the direct solve took the least-squares answer (singular S)
+  int* rng;                       // [B][dmax][2] first / last structurally nonzero column of each row of S
   const int* iter;                // per-problem SQP iteration (trace row iter + 1)
   int Wtr;                        // trace row stride (max_iter_SQP_DDP + 1)
   unsigned long long* tr_active;  // [B][Wtr][N] trace copy of amask (nullable)

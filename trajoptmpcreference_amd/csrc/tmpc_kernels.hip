@@ -42,7 +42,7 @@ __device__ __forceinline__ void minv_lane_store(const MT& M, const double q[NJ],
 }
 
 template <int NJ, bool CHAIN, class MT, class R>
-__global__ void __launch_bounds__(256) k_qp_minv(MT M, int B, int N,
+__global__ void __launch_bounds__(256) k_qp_minv(MT M, PList P, int B, int N,
                                                  const double* __restrict__ x, const int* __restrict__ need,
                                                  double* __restrict__ minv_out) {
   constexpr int NX = 2 * NJ;
@@ -50,9 +50,12 @@ __global__ void __launch_bounds__(256) k_qp_minv(MT M, int B, int N,
   const int K = N - 1;
   if (gid >= B * K * NJ) return;
   const int col = gid % NJ;
-  const int bk = gid / NJ;
-  const int b = bk / K, k = bk - b * K;
+  const int pk = gid / NJ;
+  const int p = pk / K, k = pk - p * K;
+  if (!P.has(p, B)) return;
+  const int b = P.at(p);
   if (!need[b]) return;
+  const size_t bk = (size_t)b * K + k;
   const double* xb = x + (size_t)b * NX * N;
   double q[NJ];
 #pragma unroll
@@ -101,7 +104,7 @@ __device__ __forceinline__ void grad_lane_store(const MT& M, double dt, const do
 }
 
 template <int NJ, bool CHAIN, class MT, class R>
-__global__ void __launch_bounds__(256) k_qp_grad(MT M, int B, int N, double dt,
+__global__ void __launch_bounds__(256) k_qp_grad(MT M, PList P, int B, int N, double dt,
                                                  const double* __restrict__ x, const int* __restrict__ need,
                                                  const double* __restrict__ qdd_in, const double* __restrict__ minv_in,
                                                  double* __restrict__ Aout, double* __restrict__ Bout) {
@@ -110,9 +113,12 @@ __global__ void __launch_bounds__(256) k_qp_grad(MT M, int B, int N, double dt,
   const int K = N - 1;
   if (gid >= B * K * NX) return;
   const int col = gid % NX;
-  const int bk = gid / NX;
-  const int b = bk / K, k = bk - b * K;
+  const int pk = gid / NX;
+  const int p = pk / K, k = pk - p * K;
+  if (!P.has(p, B)) return;
+  const int b = P.at(p);
   if (!need[b]) return;
+  const size_t bk = (size_t)b * K + k;
   const double* xb = x + (size_t)b * NX * N;
   double q[NJ], qd[NJ], qdd[NJ];
 #pragma unroll
@@ -181,14 +187,16 @@ struct GjSweep<NX, NX> {
 // adds rho in place and inverts (TrajoptMPCReference.py:419-422).
 // One 16-lane group per matrix, one row per lane (GjSweep).
 template <int NJ>
-__global__ void __launch_bounds__(64) k_ginv(const CostDev* __restrict__ C, int B, const double* __restrict__ rho,
-                                             const int* __restrict__ active, double* __restrict__ Ginv) {
+__global__ void __launch_bounds__(64) k_ginv(const CostDev* __restrict__ C, PList P, int B,
+                                             const double* __restrict__ rho, const int* __restrict__ active,
+                                             double* __restrict__ Ginv) {
   constexpr int NX = 2 * NJ;
   const int lane = threadIdx.x & 63;
   const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;   // one matrix per 16 lanes
   const int r = lane & 15;
-  const bool in_range = slot < B * 3;
-  const int b = in_range ? slot / 3 : 0, which = in_range ? slot - 3 * b : 0;
+  const int ps = slot / 3;
+  const bool in_range = slot < B * 3 && P.has(ps, B);
+  const int b = in_range ? P.at(ps) : 0, which = in_range ? slot - 3 * ps : 0;
   const bool act = in_range && active[b];
   const int n = which == 2 ? NJ : NX;
   const double* src = which == 0 ? C->Q : (which == 1 ? C->QF : C->R);
@@ -221,24 +229,26 @@ __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
 // knot, x|u block), one row per lane, Gauss-Jordan as k_ginv.  Also writes the
 // summed jacobian (the g_k increment) to jsoft [B][N][NX + NU].
 // Layout of Gk: [B][N][NX*NX + NU*NU] (x block, then the packed u block).
-constexpr int GINV_SOFT_GROUPS = 8;
+constexpr int GINV_SOFT_GROUPS = 2;
 template <int NJ>
 __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C, const ConstrDev* __restrict__ Cs,
-                                                  int B, int N, const double* __restrict__ rho,
+                                                  PList P, int B, int N, const double* __restrict__ rho,
                                                   const int* __restrict__ active, const double* __restrict__ x,
                                                   const double* __restrict__ u, const double* __restrict__ mu,
                                                   const double* __restrict__ lam, double* __restrict__ Gk,
                                                   double* __restrict__ jsoft) {
   constexpr int NX = 2 * NJ, NU = NJ, MC = 6 * NJ;
-  // one workgroup per (problem, GINV_SOFT_GROUPS x 4 of its 2N matrices): an inactive problem costs a
-  // handful of workgroups, not 2N / 4 (config 4 runs most of its 528 batch iterations with a few
-  // percent of the problems active, and dispatching 131k early-exit workgroups took 0.1 ms)
+  // one workgroup per (problem, GINV_SOFT_GROUPS x 4 of its 2N matrices), over the launch's problem list
+  // (PList: the lock-step tail no longer dispatches workgroups for problems that have finished, so the
+  // groups per workgroup can stay few -- the tail's latency is one workgroup's sequential groups)
   const int lane = threadIdx.x & 63;
   const int r = lane & 15;
   const int wpp = (2 * N + 4 * GINV_SOFT_GROUPS - 1) / (4 * GINV_SOFT_GROUPS);
-  const int b = blockIdx.x / wpp;
-  if (b >= B || !active[b]) return;   // workgroup-uniform exit
-  const int c0 = (blockIdx.x - b * wpp) * 4 * GINV_SOFT_GROUPS;
+  const int pb = blockIdx.x / wpp;
+  if (pb >= B || !P.has(pb, B)) return;   // workgroup-uniform exit
+  const int b = P.at(pb);
+  if (!active[b]) return;
+  const int c0 = (blockIdx.x - pb * wpp) * 4 * GINV_SOFT_GROUPS;
   for (int grp = 0; grp < GINV_SOFT_GROUPS; ++grp) {
   const int rem = c0 + 4 * grp + (lane >> 4);
   const bool in_range = rem < 2 * N;
@@ -1109,7 +1119,7 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
 //       GM: more than 1024 rows -- S and P^-1 rows in HBM (Sg, [B][4][NX][rows], PcgRowG), two rows
 //           per lane, LDS vectors of QP_MAX_ROWS rows.
 template <int NJ, int RPL, int MAXT, bool PK, int MODE, bool GM = false>
-__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int B, int N, int precond,
+__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PList P, int B, int N, int precond,
                                              const double* __restrict__ x, const double* __restrict__ u,
                                              const int* __restrict__ active, const double* __restrict__ Ginv,
                                              const double* __restrict__ Aall, const double* __restrict__ Ball,
@@ -1122,7 +1132,8 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, int 
                                              double* __restrict__ Sg) {
   constexpr int NX = 2 * NJ, NU = NJ;
   constexpr int VR = GM ? QP_MAX_ROWS : 1024;
-  const int b = blockIdx.x;
+  if (!P.has(blockIdx.x, B)) return;
+  const int b = P.at(blockIdx.x);
   if (!active[b]) return;
   extern __shared__ __align__(16) double lds[];
   const int rows = N * NX;
@@ -1403,7 +1414,7 @@ int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const
 // alpha schedule (:712-718), reduce_regularization (:457-461) and
 // check_for_exit_or_error (:463-481), applies the accepted step and records
 // the trace row (:691-705 / :729-743).
-__global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, int T, int mode, int soft,
+__global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX, int NU, int T, int mode, int soft,
                                                   const double* __restrict__ alphas, SolverOpts o,
                                                   const double* __restrict__ terms, double* __restrict__ x,
                                                   double* __restrict__ u, const double* __restrict__ dx,
@@ -1413,7 +1424,8 @@ __global__ void __launch_bounds__(64) k_ls_decide(int B, int N, int NX, int NU, 
                                                   unsigned long long* __restrict__ counters,
                                                   const double* __restrict__ hterms,
                                                   const int* __restrict__ qp_singular) {
-  const int b = blockIdx.x;
+  if (!P.has(blockIdx.x, B)) return;
+  const int b = P.at(blockIdx.x);
   if (!st.active[b]) return;
   __shared__ double sJ[64], sC[64], sD[64];
   __shared__ int s_choice;
@@ -1620,23 +1632,23 @@ __global__ void __launch_bounds__(256) k_unit_grad(MT M, int K, double dt,
 // f32: the dynamics in fp32 (tmpc_options.precision F32 / MIXED), fp64 in and out
 template <int NJ, bool CHAIN, class MT>
 struct Launch {
-  static void qp_minv(bool f32, hipStream_t s, const ModelDev* M, int B, int N, const double* x, const int* need,
-                      double* minv) {
+  static void qp_minv(bool f32, hipStream_t s, const ModelDev* M, PList P, int B, int N, const double* x,
+                      const int* need, double* minv) {
     if (f32)
-      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), B, N, x,
-                         need, minv);
+      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), P, B, N,
+                         x, need, minv);
     else
-      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), B, N, x,
-                         need, minv);
+      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), P, B, N,
+                         x, need, minv);
   }
-  static void qp_grad(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, const double* x,
+  static void qp_grad(bool f32, hipStream_t s, const ModelDev* M, PList P, int B, int N, double dt, const double* x,
                       const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
     if (f32)
-      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), B, N,
-                         dt, x, need, qdd, minv, A, Bm);
+      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P, B,
+                         N, dt, x, need, qdd, minv, A, Bm);
     else
-      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), B, N,
-                         dt, x, need, qdd, minv, A, Bm);
+      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P,
+                         B, N, dt, x, need, qdd, minv, A, Bm);
   }
   static void unit_minv(bool f32, hipStream_t s, const ModelDev* M, int K, const double* x, double* minv) {
     if (f32)
@@ -1657,10 +1669,11 @@ struct Launch {
 
 template <int NJ>
 struct LaunchNJ {
-  static void ginv(hipStream_t s, const CostDev* C, int B, const double* rho, const int* active, double* G) {
-    hipLaunchKernelGGL((k_ginv<NJ>), TMPC_GRID(B * 3 * 16, 64), 0, s, C, B, rho, active, G);
+  static void ginv(hipStream_t s, const CostDev* C, PList P, int B, const double* rho, const int* active, double* G) {
+    hipLaunchKernelGGL((k_ginv<NJ>), TMPC_GRID(B * 3 * 16, 64), 0, s, C, P, B, rho, active, G);
   }
-  static void qp(hipStream_t s, const CostDev* C, int B, int N, int precond, int mode, const double* x, const double* u,
+  static void qp(hipStream_t s, const CostDev* C, PList P, int B, int N, int precond, int mode, const double* x,
+                 const double* u,
                  const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
                  int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
                  double* Pd, const double* jsoft, const double* guess, double* Sg) {
@@ -1672,7 +1685,7 @@ struct LaunchNJ {
     const int rpl = gm ? 2 : pcg_rpl(N, NX);
     const int threads = ((rows / rpl + 63) / 64) * 64;
     const size_t lds = qp_lds_doubles(N, NX, NJ, gm ? QP_MAX_ROWS : 1024) * sizeof(double);
-#define TMPC_QP_ARGS s, C, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, \
+#define TMPC_QP_ARGS s, C, P, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, \
                      Sl, gam, Pd, jsoft, guess, Sg
 #define TMPC_QP_LAUNCH(PKV, MODEV)                                                                        \
     if (gm)                                                                                                \
@@ -1692,11 +1705,11 @@ struct LaunchNJ {
 #undef TMPC_QP_LAUNCH
 #undef TMPC_QP_ARGS
   }
-  static void ginv_soft(hipStream_t s, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
+  static void ginv_soft(hipStream_t s, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N, const double* rho,
                         const int* active, const double* x, const double* u, const double* mu, const double* lam,
                         double* Gk, double* jsoft) {
     const int wpp = (2 * N + 4 * GINV_SOFT_GROUPS - 1) / (4 * GINV_SOFT_GROUPS);
-    hipLaunchKernelGGL((k_ginv_soft<NJ>), dim3(B * wpp), dim3(64), 0, s, C, Cs, B, N, rho, active, x, u, mu, lam, Gk,
+    hipLaunchKernelGGL((k_ginv_soft<NJ>), dim3(B * wpp), dim3(64), 0, s, C, Cs, P, B, N, rho, active, x, u, mu, lam, Gk,
                        jsoft);
   }
 };
@@ -1766,13 +1779,45 @@ int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* S
   }
 }
 
-void launch_ls_decide(hipStream_t s, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
-                      const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
-                      const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
-                      int* active_count, unsigned long long* counters, const double* hterms,
+void launch_ls_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int T, int mode, int soft,
+                      const double* alphas, const SolverOpts& o, const double* terms, double* x, double* u,
+                      const double* dx, const double* du, const ProbState& st, const int* pcg_iters,
+                      const TraceDev& tr, int* active_count, unsigned long long* counters, const double* hterms,
                       const int* qp_singular) {
-  hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u, dx, du,
-                     st, pcg_iters, tr, active_count, counters, hterms, qp_singular);
+  hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, P, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u, dx,
+                     du, st, pcg_iters, tr, active_count, counters, hterms, qp_singular);
+}
+
+// The problems still alive in the lock-step loop (mask != 0), ascending, and their count: one
+// 1024-lane workgroup, each lane a contiguous chunk of the batch, a block prefix sum of the chunk
+// counts.  host_slot (nullable): the count also lands in the iteration's flag slot the host reads back.
+__global__ void __launch_bounds__(1024) k_alive_list(int B, const int* __restrict__ alive, int* __restrict__ idx,
+                                                     int* __restrict__ cnt, int* __restrict__ host_slot) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int chunk = (B + nt - 1) / nt;
+  const int lo = t * chunk, hi = min(B, lo + chunk);
+  int c = 0;
+  for (int b = lo; b < hi; ++b) c += alive[b] != 0;
+  part[t] = c;
+  __syncthreads();
+  for (int off = 1; off < nt; off <<= 1) {   // inclusive Hillis-Steele scan
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int o = part[t] - c;
+  for (int b = lo; b < hi; ++b)
+    if (alive[b]) idx[o++] = b;
+  if (t == nt - 1) {
+    *cnt = part[t];
+    if (host_slot) *host_slot = part[t];
+  }
+}
+
+void launch_alive_list(hipStream_t s, int B, const int* alive, int* idx, int* cnt, int* host_slot) {
+  hipLaunchKernelGGL(k_alive_list, dim3(1), dim3(1024), 0, s, B, alive, idx, cnt, host_slot);
 }
 
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active) {
@@ -1799,14 +1844,15 @@ __device__ __forceinline__ double soft_v(const ConstrDev* Cs, int t, int e, int 
   return e < n ? z - Cs->lb[t][i] : Cs->ub[t][i] - z;
 }
 
-__global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__ Cs, int B, int N, int NJ,
+__global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__ Cs, PList P, int B, int N, int NJ,
                                                    double tol, int max_iter, const double* __restrict__ x,
                                                    const double* __restrict__ u, double* __restrict__ mu,
                                                    double* __restrict__ lam, double* __restrict__ phi,
                                                    int* __restrict__ outer_active, int* __restrict__ outer_iter,
                                                    int* __restrict__ exit_soft, int* __restrict__ outer_count,
                                                    ProbState st, int* __restrict__ act_init, double rho_init) {
-  const int b = blockIdx.x;
+  if (!P.has(blockIdx.x, B)) return;
+  const int b = P.at(blockIdx.x);
   if (!outer_active[b]) return;
   const bool per_problem = act_init != nullptr;
   if (per_problem && (st.active[b] || act_init[b])) return;
@@ -1886,23 +1932,25 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
 }
 
 // act_init -> active once the initial merit of a restarted pass is set
-__global__ void k_activate(int B, int* __restrict__ act_init, int* __restrict__ active) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || !act_init[b]) return;
+__global__ void k_activate(PList P, int B, int* __restrict__ act_init, int* __restrict__ active) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!P.has(p, B)) return;
+  const int b = P.at(p);
+  if (!act_init[b]) return;
   act_init[b] = 0;
   active[b] = 1;
 }
 
-void launch_activate(hipStream_t s, int B, int* act_init, int* active) {
-  hipLaunchKernelGGL(k_activate, TMPC_GRID(B, 256), 0, s, B, act_init, active);
+void launch_activate(hipStream_t s, PList P, int B, int* act_init, int* active) {
+  hipLaunchKernelGGL(k_activate, TMPC_GRID(B, 256), 0, s, P, B, act_init, active);
 }
 
-void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double tol, int max_iter,
+void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, PList P, int B, int N, int nj, double tol, int max_iter,
                        const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
                        int* outer_iter, int* exit_soft, int* outer_count, const ProbState* st, int* act_init,
                        double rho_init) {
   ProbState none{};
-  hipLaunchKernelGGL(k_soft_outer, dim3(B), dim3(64), 0, s, Cs, B, N, nj, tol, max_iter, x, u, mu, lam, phi,
+  hipLaunchKernelGGL(k_soft_outer, dim3(B), dim3(64), 0, s, Cs, P, B, N, nj, tol, max_iter, x, u, mu, lam, phi,
                      outer_active, outer_iter, exit_soft, outer_count, st ? *st : none, act_init, rho_init);
 }
 
@@ -2007,13 +2055,14 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
   return 0;
 #endif
 
-int launch_qp_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N,
+int launch_qp_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, PList P, int B, int N,
                    const double* x, const int* need, double* minv) {
-  TMPC_DISPATCH_NJ(nj, chain, qp_minv(f32, s, M, B, N, x, need, minv))
+  TMPC_DISPATCH_NJ(nj, chain, qp_minv(f32, s, M, P, B, N, x, need, minv))
 }
-int launch_qp_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt,
-                   const double* x, const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
-  TMPC_DISPATCH_NJ(nj, chain, qp_grad(f32, s, M, B, N, dt, x, need, qdd, minv, A, Bm))
+int launch_qp_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, PList P, int B, int N,
+                   double dt, const double* x, const int* need, const double* qdd, const double* minv, double* A,
+                   double* Bm) {
+  TMPC_DISPATCH_NJ(nj, chain, qp_grad(f32, s, M, P, B, N, dt, x, need, qdd, minv, A, Bm))
 }
 int launch_unit_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, const double* x,
                      double* minv) {
@@ -2023,10 +2072,11 @@ int launch_unit_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const
                      const double* x, const double* qdd, const double* minv, double* A, double* Bm, double* dqdd) {
   TMPC_DISPATCH_NJ(nj, chain, unit_grad(f32, s, M, K, dt, x, qdd, minv, A, Bm, dqdd))
 }
-int launch_ginv(hipStream_t s, int nj, const CostDev* C, int B, const double* rho, const int* active, double* G) {
-  TMPC_DISPATCH_NJ2(nj, ginv(s, C, B, rho, active, G))
+int launch_ginv(hipStream_t s, int nj, const CostDev* C, PList P, int B, const double* rho, const int* active,
+                double* G) {
+  TMPC_DISPATCH_NJ2(nj, ginv(s, C, P, B, rho, active, G))
 }
-int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond, int mode, const double* x,
+int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, int precond, int mode, const double* x,
               const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
@@ -2036,13 +2086,13 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, int B, int N, int precond
   const bool gm = rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG);
   if (gm && mode == QP_MODE_PCG && !Sg) return -4;
   if (qp_lds_doubles(N, 2 * nj, nj, gm ? QP_MAX_ROWS : 1024) * sizeof(double) > 160 * 1024) return -3;
-  TMPC_DISPATCH_NJ2(nj, qp(s, C, B, N, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd,
-                           Sl, gam, Pd, jsoft, guess, Sg))
+  TMPC_DISPATCH_NJ2(nj, qp(s, C, P, B, N, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam,
+                           Sd, Sl, gam, Pd, jsoft, guess, Sg))
 }
-int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, int B, int N, const double* rho,
-                     const int* active, const double* x, const double* u, const double* mu, const double* lam,
-                     double* Gk, double* jsoft) {
-  TMPC_DISPATCH_NJ2(nj, ginv_soft(s, C, Cs, B, N, rho, active, x, u, mu, lam, Gk, jsoft))
+int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N,
+                     const double* rho, const int* active, const double* x, const double* u, const double* mu,
+                     const double* lam, double* Gk, double* jsoft) {
+  TMPC_DISPATCH_NJ2(nj, ginv_soft(s, C, Cs, P, B, N, rho, active, x, u, mu, lam, Gk, jsoft))
 }
 
 }  // namespace tmpc
