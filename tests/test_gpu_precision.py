@@ -78,12 +78,13 @@ def test_reduced_precision_ilqr_tracks_fp64(name, n, N, prec):
 
 
 def test_config3_fp32_ilqr_al_converged_problems():
-    """BASELINE config 3 in fp32 (arm6 N = 64 iLQR, augmented-Lagrangian torque limits), 8 problems:
-    the one the fp64 oracle solves to convergence (exit 1, seed 803) is solved by the fp32 path to the same
-    optimum (trajectory at 2e-3); the other 7 end on the rho schedule or the iteration caps (exit 2 / 3)
-    in fp64 too, after different rho paths in fp32 (fp32 rollouts cannot meet dJ < 1e-6), so
-    for every problem the fp32 run must end with a finite trajectory and a final cost within 10 % of the
-    fp64 oracle's (parity unpinned: the reference has no fp32 path)."""
+    """BASELINE config 3 in fp32 (arm6 N = 64 iLQR, augmented-Lagrangian torque limits), all 8 problems
+    of the oracle fixture: every fp32 run ends with a finite trajectory whose quadratic cost is within
+    10 % of the fp64 oracle's; on the one problem the fp64 oracle solves to convergence (exit 1, seed 803)
+    the fp32 trajectory is that optimum at 2e-3.  Its exit code is not asserted: the exit test
+    dJ < 1e-6 sits below the fp32 rounding of a rollout cost (~1e-7 relative of J ~ 10..100), so
+    whether an fp32 run meets it before the rho schedule ends it (exit 2) is decided by rounding
+    (module docstring; parity unpinned: the reference has no fp32 path)."""
     d = golden("oracle_config3_arm6_N64_ilqr_al.npz")
     N = int(d["N"])
     lb, ub = float(d["lb"]), float(d["ub"])
@@ -95,7 +96,7 @@ def test_config3_fp32_ilqr_al_converged_problems():
     conv = [i for i in range(len(x)) if int(d["exit_code_0"][i]) == 1]
     assert len(conv) == 1 and len(x) == 8
     for i in conv:
-        assert int(r["exit_code"][i]) == 1, i
+        assert int(r["exit_code"][i]) in (1, 2), i
         assert _rel(r["x"][i], d["x_0"][i]) < 2e-3, i
     assert all(np.isfinite(r["x"]).ravel())
     from oracle import sqp as osqp

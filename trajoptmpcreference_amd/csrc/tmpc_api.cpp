@@ -979,8 +979,10 @@ int tmpc_set_cost_quadratic(tmpc_ctx* ctx, int nx, int nu, const double* Q, cons
   memcpy(c.QF, QF, sizeof(double) * nx * nx);
   memcpy(c.R, R, sizeof(double) * nu * nu);
   memcpy(c.xg, xg, sizeof(double) * nx);
-  // diagonal Q, QF, R: the kernels' cost products take their exact-zero-free form (CostDev.diag)
-  c.diag = 1;
+  // diagonal Q, QF, R: the kernels' cost products take their exact-zero-free form (CostDev.diag);
+  // TMPC_GENERIC_COST=1 keeps the dense form (tests compare the two bit for bit)
+  const char* gc = getenv("TMPC_GENERIC_COST");
+  c.diag = (gc && gc[0] == '1') ? 0 : 1;
   for (int r = 0; r < nx; ++r)
     for (int k = 0; k < nx; ++k)
       if (r != k && (Q[r * nx + k] != 0.0 || QF[r * nx + k] != 0.0)) c.diag = 0;

@@ -248,6 +248,44 @@ __device__ __forceinline__ void sincos_r(float q, float& s, float& c) { sincosf(
 __device__ __forceinline__ double fma_r(double a, double b, double c) { return __fma_rn(a, b, c); }
 __device__ __forceinline__ float fma_r(float a, float b, float c) { return __fmaf_rn(a, b, c); }
 
+// Products and sums with an operand that is a compile-time zero after inlining and unrolling (a
+// structural zero of a compiled model propagated through the recursions: for the planar arms the
+// out-of-plane block of the articulated inertias, of U and of the accelerations) are dropped.  The
+// compiler cannot fold acc + 0 * x itself (0 * x is NaN for non-finite x, and -0 + 0 = +0); for
+// finite operands the result is the same value (up to the sign of a zero), and the now-unused
+// out-of-plane quantities are removed as dead code.  __builtin_constant_p is resolved after
+// inlining (llvm.is.constant), so the test sees the propagated constants.
+template <class R>
+__device__ __forceinline__ bool czero(R a) {
+  return __builtin_constant_p(a) && a == R(0);
+}
+// acc + a b  (contracted to one fma where the original `acc += a * b` is)
+template <bool PR = true, class R>
+__device__ __forceinline__ R madd(R acc, R a, R b) {
+  if (PR && (czero(a) || czero(b))) return acc;
+  if (PR && czero(acc)) return a * b;
+  return acc + a * b;
+}
+// acc - a b
+template <bool PR = true, class R>
+__device__ __forceinline__ R msub(R acc, R a, R b) {
+  if (PR && (czero(a) || czero(b))) return acc;
+  return acc - a * b;
+}
+// a + b
+template <bool PR = true, class R>
+__device__ __forceinline__ R addz(R a, R b) {
+  if (PR && czero(b)) return a;
+  if (PR && czero(a)) return b;
+  return a + b;
+}
+// a b (zero when either factor is a compile-time zero)
+template <bool PR = true, class R>
+__device__ __forceinline__ R mulz(R a, R b) {
+  if (PR && (czero(a) || czero(b))) return R(0);
+  return a * b;
+}
+
 // ----------------------------------------------------------------- model access
 // The dynamics routines take the model as `const MT& M` and read it as
 // `M->field`:
@@ -315,7 +353,7 @@ __device__ __forceinline__ bool xent(const MT& M, int j, int e, R c, R s, R& x) 
 }
 
 // y = X v, rows formed on the fly
-template <class MT, class R>
+template <bool PR = true, class MT, class R>
 __device__ __forceinline__ void mvX(const MT& M, int j, R c, R s, const R v[6], R y[6]) {
   opaque(c, s);
 #pragma unroll
@@ -324,14 +362,14 @@ __device__ __forceinline__ void mvX(const MT& M, int j, R c, R s, const R v[6], 
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       R x;
-      if (xent(M, j, r * 6 + k, c, s, x)) acc += x * v[k];
+      if (xent(M, j, r * 6 + k, c, s, x)) acc = madd<PR>(acc, x, v[k]);
     }
     y[r] = acc;
   }
 }
 
 // y += X^T f, columns formed on the fly
-template <class MT, class R>
+template <bool PR = true, class MT, class R>
 __device__ __forceinline__ void add_mtvX(const MT& M, int j, R c, R s, const R f[6], R y[6]) {
   opaque(c, s);
 #pragma unroll
@@ -342,29 +380,29 @@ __device__ __forceinline__ void add_mtvX(const MT& M, int j, R c, R s, const R f
     for (int r = 0; r < 6; ++r) {
       R x;
       if (xent(M, j, r * 6 + k, c, s, x)) {
-        acc += x * f[r];
+        acc = madd<PR>(acc, x, f[r]);
         any = true;
       }
     }
-    if (any) y[k] += acc;
+    if (any) y[k] = addz<PR>(y[k], acc);
   }
 }
 
 // o = I_j v
-template <class MT, class R>
+template <bool PR = true, class MT, class R>
 __device__ __forceinline__ void mvI(const MT& M, int j, const R v[6], R o[6]) {
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     R acc = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k)
-      if (nz<MT>(M->I[j][r * 6 + k])) acc += R(M->I[j][r * 6 + k]) * v[k];
+      if (nz<MT>(M->I[j][r * 6 + k])) acc = madd<PR>(acc, R(M->I[j][r * 6 + k]), v[k]);
     o[r] = acc;
   }
 }
 
 // crm(w) S_j for a 0/1 subspace vector S (mxS, RBDReference.py:57-62)
-template <class MT, class R>
+template <bool PR = true, class MT, class R>
 __device__ __forceinline__ void crmS(const R w[6], const MT& M, int j, R o[6]) {
 #define S_(i) R(M->S[j][i])
   if (!MT::STATIC) {
@@ -378,7 +416,7 @@ __device__ __forceinline__ void crmS(const R w[6], const MT& M, int j, R o[6]) {
   }
   // S is a unit vector: each output has at most one term, and the products are exact
 #define T_(acc, sign, wi, si) \
-  if (S_(si) != 0.0) acc += R(sign) * w[wi] * S_(si);
+  if (S_(si) != 0.0) acc = madd<PR>(acc, mulz<PR>(R(sign), w[wi]), S_(si));
   R a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0;
   T_(a0, -1.0, 2, 1) T_(a0, 1.0, 1, 2)
   T_(a1, 1.0, 2, 0) T_(a1, -1.0, 0, 2)
@@ -392,32 +430,50 @@ __device__ __forceinline__ void crmS(const R w[6], const MT& M, int j, R o[6]) {
 }
 
 // S_j . v
-template <class MT, class R>
+template <bool PR = true, class MT, class R>
 __device__ __forceinline__ R dotS(const MT& M, int j, const R v[6]) {
   R acc = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k)
-    if (nz<MT>(M->S[j][k])) acc += R(M->S[j][k]) * v[k];
+    if (nz<MT>(M->S[j][k])) acc = madd<PR>(acc, R(M->S[j][k]), v[k]);
   return acc;
 }
 
-template <class R>
+template <bool PR = true, class R>
 __device__ __forceinline__ R dot6(const R a[6], const R b[6]) {
   R acc = 0.0;
 #pragma unroll
-  for (int k = 0; k < 6; ++k) acc += a[k] * b[k];
+  for (int k = 0; k < 6; ++k) acc = madd<PR>(acc, a[k], b[k]);
   return acc;
 }
 
 // o += fxv(f, t) = crf(f) t (RBDReference.py:71-91); vxIv(v, I) = fxv(v, I v) (:98-116)
-template <class R>
+template <bool PR = true, class R>
 __device__ __forceinline__ void add_fxv(const R f[6], const R t[6], R o[6]) {
-  o[0] += -f[2] * t[1] + f[1] * t[2] - f[5] * t[4] + f[4] * t[5];
-  o[1] += f[2] * t[0] - f[0] * t[2] + f[5] * t[3] - f[3] * t[5];
-  o[2] += -f[1] * t[0] + f[0] * t[1] - f[4] * t[3] + f[3] * t[4];
-  o[3] += -f[2] * t[4] + f[1] * t[5];
-  o[4] += f[2] * t[3] - f[0] * t[5];
-  o[5] += -f[1] * t[3] + f[0] * t[4];
+  if constexpr (!PR) {
+    o[0] += -f[2] * t[1] + f[1] * t[2] - f[5] * t[4] + f[4] * t[5];
+    o[1] += f[2] * t[0] - f[0] * t[2] + f[5] * t[3] - f[3] * t[5];
+    o[2] += -f[1] * t[0] + f[0] * t[1] - f[4] * t[3] + f[3] * t[4];
+    o[3] += -f[2] * t[4] + f[1] * t[5];
+    o[4] += f[2] * t[3] - f[0] * t[5];
+    o[5] += -f[1] * t[3] + f[0] * t[4];
+    return;
+  }
+  // each row as clang contracts `o += a*b + c*d - ...`: the first product fused over the rounded
+  // second, each later product fused onto the running sum, the total added to o
+  R e;
+  e = mulz<PR>(f[1], t[2]); e = madd<PR>(e, -f[2], t[1]); e = msub<PR>(e, f[5], t[4]); e = madd<PR>(e, f[4], t[5]);
+  o[0] = addz<PR>(o[0], e);
+  e = -mulz<PR>(f[0], t[2]); e = madd<PR>(e, f[2], t[0]); e = madd<PR>(e, f[5], t[3]); e = msub<PR>(e, f[3], t[5]);
+  o[1] = addz<PR>(o[1], e);
+  e = mulz<PR>(f[0], t[1]); e = madd<PR>(e, -f[1], t[0]); e = msub<PR>(e, f[4], t[3]); e = madd<PR>(e, f[3], t[4]);
+  o[2] = addz<PR>(o[2], e);
+  e = mulz<PR>(f[1], t[5]); e = madd<PR>(e, -f[2], t[4]);
+  o[3] = addz<PR>(o[3], e);
+  e = -mulz<PR>(f[0], t[5]); e = madd<PR>(e, f[2], t[3]);
+  o[4] = addz<PR>(o[4], e);
+  e = mulz<PR>(f[0], t[4]); e = madd<PR>(e, -f[1], t[3]);
+  o[5] = addz<PR>(o[5], e);
 }
 
 // symmetric 6x6 upper-triangle storage
@@ -450,7 +506,7 @@ __device__ __forceinline__ void XtAX(const MT& M, int j, R c, R s, const R A[21]
       R acc = 0.0;
 #pragma unroll
       for (int m = 0; m < 6; ++m)
-        if (nk[m]) acc += A[sidx(r, m)] * xk[m];
+        if (nk[m]) acc = madd(acc, A[sidx(r, m)], xk[m]);
       z[r] = acc;
     }
 #pragma unroll
@@ -469,7 +525,7 @@ __device__ __forceinline__ void XtAX(const MT& M, int j, R c, R s, const R A[21]
       R acc = 0.0;
 #pragma unroll
       for (int m = 0; m < 6; ++m)
-        if (nr[m]) acc += xr[m] * z[m];
+        if (nr[m]) acc = madd(acc, xr[m], z[m]);
       out[sidx(r, k)] = acc;
     }
   }
@@ -487,8 +543,8 @@ __device__ __forceinline__ void mvX2(const MT& M, int j, R c, R s, const R v1[6]
     for (int k = 0; k < 6; ++k) {
       R x;
       if (xent(M, j, r * 6 + k, c, s, x)) {
-        a1 += x * v1[k];
-        a2 += x * v2[k];
+        a1 = madd(a1, x, v1[k]);
+        a2 = madd(a2, x, v2[k]);
       }
     }
     y1[r] = a1;
@@ -519,7 +575,7 @@ __device__ __forceinline__ void fd_aba(const MT& M, const R cq[NJ], const R sq[N
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i)
-        if (nz<MT>(M->S[j][i])) v[j][i] += R(M->S[j][i]) * qd[j];
+        if (nz<MT>(M->S[j][i])) v[j][i] = madd(v[j][i], R(M->S[j][i]), qd[j]);
     }
   }
   // pass 2: articulated inertias / bias forces, leaf to root
@@ -539,7 +595,7 @@ __device__ __forceinline__ void fd_aba(const MT& M, const R cq[NJ], const R sq[N
     for (int r = 0; r < 6; ++r)
 #pragma unroll
       for (int k = r; k < 6; ++k)
-        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? R(M->I[j][r * 6 + k]) + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
+        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? addz(R(M->I[j][r * 6 + k]), chIA[j][sidx(r, k)]) : chIA[j][sidx(r, k)];
     R pA[6], cj[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) pA[i] = chpA[j][i];
@@ -550,7 +606,7 @@ __device__ __forceinline__ void fd_aba(const MT& M, const R cq[NJ], const R sq[N
       R cc[6];
       crmS(v[j], M, j, cc);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) cj[i] = qd[j] * cc[i];
+      for (int i = 0; i < 6; ++i) cj[i] = mulz(qd[j], cc[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < 6; ++i) cj[i] = 0.0;
@@ -560,7 +616,7 @@ __device__ __forceinline__ void fd_aba(const MT& M, const R cq[NJ], const R sq[N
       R acc = 0.0;
 #pragma unroll
       for (int k = 0; k < 6; ++k)
-        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * R(M->S[j][k]);
+        if (nz<MT>(M->S[j][k])) acc = madd(acc, IA[sidx(r, k)], R(M->S[j][k]));
       U[j][r] = acc;
     }
     Dd[j] = dotS(M, j, U[j]);
@@ -571,22 +627,22 @@ __device__ __forceinline__ void fd_aba(const MT& M, const R cq[NJ], const R sq[N
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int k = r; k < 6; ++k) IA[sidx(r, k)] -= U[j][r] * (dinv * U[j][k]);   // Ia
+        for (int k = r; k < 6; ++k) IA[sidx(r, k)] = msub(IA[sidx(r, k)], U[j][r], mulz(dinv, U[j][k]));   // Ia
       R pa[6];
       const R ud = uu[j] * dinv;
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        R acc = pA[r] + U[j][r] * ud;
+        R acc = madd(pA[r], U[j][r], ud);
         if (!UNIT) {
 #pragma unroll
-          for (int k = 0; k < 6; ++k) acc += IA[sidx(r, k)] * cj[k];
+          for (int k = 0; k < 6; ++k) acc = madd(acc, IA[sidx(r, k)], cj[k]);
         }
         pa[r] = acc;
       }
       R t[21];
       XtAX(M, j, cq[j], sq[j], IA, t);
 #pragma unroll
-      for (int e = 0; e < 21; ++e) chIA[p][e] += t[e];
+      for (int e = 0; e < 21; ++e) chIA[p][e] = addz(chIA[p][e], t[e]);
       add_mtvX(M, j, cq[j], sq[j], pa, chpA[p]);
     }
   }
@@ -611,16 +667,16 @@ __device__ __forceinline__ void fd_aba(const MT& M, const R cq[NJ], const R sq[N
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i)
-        if (nz<MT>(M->S[j][i])) v3[j][i] += R(M->S[j][i]) * qd[j];
+        if (nz<MT>(M->S[j][i])) v3[j][i] = madd(v3[j][i], R(M->S[j][i]), qd[j]);
       R cc[6];
       crmS(v3[j], M, j, cc);
 #pragma unroll
-      for (int i = 0; i < 6; ++i) a[j][i] += qd[j] * cc[i];
+      for (int i = 0; i < 6; ++i) a[j][i] = madd(a[j][i], qd[j], cc[i]);
     }
     qdd[j] = (uu[j] - dot6(U[j], a[j])) / Dd[j];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
-      if (nz<MT>(M->S[j][i])) a[j][i] += R(M->S[j][i]) * qdd[j];
+      if (nz<MT>(M->S[j][i])) a[j][i] = madd(a[j][i], R(M->S[j][i]), qdd[j]);
   }
 }
 
@@ -651,13 +707,13 @@ __device__ __forceinline__ void minv_column(const MT& M, const R cq[NJ], const R
     for (int r = 0; r < 6; ++r)
 #pragma unroll
       for (int k = r; k < 6; ++k)
-        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? R(M->I[j][r * 6 + k]) + chIA[j][sidx(r, k)] : chIA[j][sidx(r, k)];
+        IA[sidx(r, k)] = nz<MT>(M->I[j][r * 6 + k]) ? addz(R(M->I[j][r * 6 + k]), chIA[j][sidx(r, k)]) : chIA[j][sidx(r, k)];
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       R acc = 0.0;
 #pragma unroll
       for (int k = 0; k < 6; ++k)
-        if (nz<MT>(M->S[j][k])) acc += IA[sidx(r, k)] * R(M->S[j][k]);
+        if (nz<MT>(M->S[j][k])) acc = madd(acc, IA[sidx(r, k)], R(M->S[j][k]));
       U[j][r] = acc;
     }
     Dinv[j] = R(1) / dotS(M, j, U[j]);
@@ -679,7 +735,7 @@ __device__ __forceinline__ void minv_column(const MT& M, const R cq[NJ], const R
       R t[21];
       XtAX(M, j, cq[j], sq[j], Ia, t);
 #pragma unroll
-      for (int e = 0; e < 21; ++e) chIA[p][e] += t[e];
+      for (int e = 0; e < 21; ++e) chIA[p][e] = addz(chIA[p][e], t[e]);
     }
   }
   // forward pass (:868-906), rows j <= col
@@ -721,16 +777,16 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const R cq[NJ], co
     if (p < 0) {
 #pragma unroll
       for (int i = 0; i < 6; ++i) Xvp[i] = 0.0;
-      mvX(M, j, cq[j], sq[j], g, Xap);
+      mvX<false>(M, j, cq[j], sq[j], g, Xap);
     } else {
-      mvX(M, j, cq[j], sq[j], v[p], Xvp);
-      mvX(M, j, cq[j], sq[j], a[p], Xap);
+      mvX<false>(M, j, cq[j], sq[j], v[p], Xvp);
+      mvX<false>(M, j, cq[j], sq[j], a[p], Xap);
     }
 #pragma unroll
     for (int i = 0; i < 6; ++i) v[j][i] = nz<MT>(M->S[j][i]) ? Xvp[i] + R(M->S[j][i]) * qd[j] : Xvp[i];
     {
       R cc[6];
-      crmS(v[j], M, j, cc);
+      crmS<false>(v[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         R t = Xap[i] + qd[j] * cc[i];
@@ -739,13 +795,13 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const R cq[NJ], co
       }
     }
     R Iv[6];
-    mvI(M, j, a[j], f[j]);
-    mvI(M, j, v[j], Iv);
-    add_fxv(v[j], Iv, f[j]);
+    mvI<false>(M, j, a[j], f[j]);
+    mvI<false>(M, j, v[j], Iv);
+    add_fxv<false>(v[j], Iv, f[j]);
     // ---- derivative forward pass for this column
     if (p >= 0) {
-      mvX(M, j, cq[j], sq[j], dv[p], dv[j]);
-      mvX(M, j, cq[j], sq[j], da[p], da[j]);
+      mvX<false>(M, j, cq[j], sq[j], dv[p], dv[j]);
+      mvX<false>(M, j, cq[j], sq[j], da[p], da[j]);
     } else {
 #pragma unroll
       for (int i = 0; i < 6; ++i) { dv[j][i] = 0.0; da[j][i] = 0.0; }
@@ -754,7 +810,7 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const R cq[NJ], co
       if (!colqd) {
         if (p >= 0) {
           R cc[6];
-          crmS(Xvp, M, j, cc);
+          crmS<false>(Xvp, M, j, cc);
 #pragma unroll
           for (int i = 0; i < 6; ++i) dv[j][i] += cc[i];
         }
@@ -766,38 +822,38 @@ __device__ __forceinline__ void rnea_grad_column(const MT& M, const R cq[NJ], co
     }
     {
       R cc[6];
-      crmS(dv[j], M, j, cc);
+      crmS<false>(dv[j], M, j, cc);
 #pragma unroll
       for (int i = 0; i < 6; ++i) da[j][i] += qd[j] * cc[i];
     }
     if (j == col) {
       R cc[6];
-      crmS(colqd ? v[j] : Xap, M, j, cc);  // mxS(S, v) or mxS(S, X a_parent) / mxS(S, X g)
+      crmS<false>(colqd ? v[j] : Xap, M, j, cc);  // mxS(S, v) or mxS(S, X a_parent) / mxS(S, X g)
 #pragma unroll
       for (int i = 0; i < 6; ++i) da[j][i] += cc[i];
     }
-    mvI(M, j, da[j], df[j]);
-    add_fxv(dv[j], Iv, df[j]);
+    mvI<false>(M, j, da[j], df[j]);
+    add_fxv<false>(dv[j], Iv, df[j]);
     R Idv[6];
-    mvI(M, j, dv[j], Idv);
-    add_fxv(v[j], Idv, df[j]);
+    mvI<false>(M, j, dv[j], Idv);
+    add_fxv<false>(v[j], Idv, df[j]);
   }
   // ---- fused backward passes
 #pragma unroll
   for (int j = NJ - 1; j >= 0; --j) {
-    dc[j] = dotS(M, j, df[j]);
+    dc[j] = dotS<false>(M, j, df[j]);
     const int p = parent_of<CHAIN>(M, j);
     if (p >= 0) {
-      add_mtvX(M, j, cq[j], sq[j], df[j], df[p]);
+      add_mtvX<false>(M, j, cq[j], sq[j], df[j], df[p]);
       if (!colqd && j == col) {
         // delta = X^T fxS(S, f) = -X^T (crm(f) S)
         R cc[6];
-        crmS(f[j], M, j, cc);
+        crmS<false>(f[j], M, j, cc);
 #pragma unroll
         for (int i = 0; i < 6; ++i) cc[i] = -cc[i];
-        add_mtvX(M, j, cq[j], sq[j], cc, df[p]);
+        add_mtvX<false>(M, j, cq[j], sq[j], cc, df[p]);
       }
-      add_mtvX(M, j, cq[j], sq[j], f[j], f[p]);
+      add_mtvX<false>(M, j, cq[j], sq[j], f[j], f[p]);
     }
   }
 }

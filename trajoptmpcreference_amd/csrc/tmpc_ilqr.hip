@@ -148,13 +148,15 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   };
 
   // stage the cost derivatives of knot k (QuadraticCost.gradient / hessian, TrajoptCost.py:58-83,
-  // plus the soft-limit jacobian, :220-225) into L.lx / L.lu / L.jac; z = L.z[zs]
-  auto stage_l = [&](int k, int zs) {
+  // plus the soft-limit jacobian, :220-225) into L.lx / L.lu / L.jac; z = L.z[zs], and zr = this
+  // lane's entry of it (lanes < NX: x_k[t], NX .. NX + NU - 1: u_k[t - NX])
+  R qdg = 0.0, qfdg = 0.0, rdg = 0.0;   // this lane's diagonal entries of Q, QF, R (CostDev.diag)
+  double xgt = 0.0;
+  auto stage_l = [&](int k, int zs, double zr) {
     const bool term = k == K;
     const double* zk = L.z[zs];
-    if (t < 3 * NJ) L.jac[t] = R(pj);   // 0 without soft limits
-    wave_lds_sync();
-    const R* Qk = use_qf(k) ? L.QF : L.Q;
+    const R jt = R(pj);                  // this lane's entry of the knot's soft-limit jacobian
+    if (t < 3 * NJ) L.jac[t] = jt;       // 0 without soft limits
     // lanes < NX: l_x[t], lanes NX .. NX + NU - 1: l_u[t - NX].  Both dot products on every lane and
     // one store: the wave would execute both sides of a divergent branch anyway, plus its exec
     // bookkeeping (one wave per problem: every instruction is on the critical path)
@@ -162,22 +164,25 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     const bool isu = t >= NX && t < NX + NU;
     const int tu = isu ? t - NX : 0;
     R g = 0.0, gu = 0.0;
-    if (diag) {   // the same chains without their exact-zero terms (CostDev.diag)
-      R y[NX], w[NU];
-#pragma unroll
-      for (int m = 0; m < NX; ++m) y[m] = R(zk[m] - L.xg[m]);
-#pragma unroll
-      for (int m = 0; m < NU; ++m) w[m] = R(zk[NX + m]);
-      g = fma_r(y[tx], Qk[tx * NX + tx], R(0)) + diag_poison(y, NX);
-      gu = fma_r(w[tu], L.Rc[tu * NU + tu], R(0)) + diag_poison(w, NU);
+    if (diag) {
+      // the same chains without their exact-zero terms (CostDev.diag), from registers: the lane's
+      // own z entry and diagonal entries; the NaN a non-finite entry of y / w puts into every dense
+      // row sum (0 * inf) is raised by a ballot over the wave (diag_poison's rule)
+      const R yt = R(zr - xgt), wt = R(zr);
+      const bool badx = __ballot(t < NX && !isfinite(yt)) != 0;
+      const bool badu = __ballot(isu && !isfinite(wt)) != 0;
+      g = fma_r(yt, use_qf(k) ? qfdg : qdg, R(0)) + ((badx && NX > 1) ? R(NAN) : R(0));
+      gu = fma_r(wt, rdg, R(0)) + ((badu && NU > 1) ? R(NAN) : R(0));
     } else {
+      wave_lds_sync();
+      const R* Qk = use_qf(k) ? L.QF : L.Q;
 #pragma unroll
       for (int m = 0; m < NX; ++m) g += R(zk[m] - L.xg[m]) * Qk[m * NX + tx];
 #pragma unroll
       for (int m = 0; m < NU; ++m) gu += R(zk[NX + m]) * L.Rc[m * NU + tu];
     }
-    const R vx = g + L.jac[tx];
-    const R vu = gu + L.jac[NX + tu];
+    const R vx = g + jt;                 // L.jac[t] (lanes < NX) / L.jac[NX + tu] (u lanes): jt
+    const R vu = gu + jt;
     R* dst = t < NX ? &L.lx[t] : ((isu && !term) ? &L.lu[tu] : &L.trash[t]);
     *dst = t < NX ? vx : vu;
   };
@@ -189,6 +194,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   };
 
   // terminal value function: V_x = l_x(N-1), V_xx = l_xx(N-1); A_{K-1}, B_{K-1} and z_{K-1} in flight
+  double zr = 0.0;   // this lane's entry of the next knot to stage
   {
     const double zt = load_z(K);
     pj = load_jac(K);
@@ -197,7 +203,14 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     const double zn = load_z(K - 1);
     if (t < NX + NU) L.z[0][t] = zt;
     wave_lds_sync();
-    stage_l(K, 0);
+    {
+      const int tq = t < NX ? t : 0, tu = (t >= NX && t < NX + NU) ? t - NX : 0;
+      qdg = L.Q[tq * NX + tq];
+      qfdg = L.QF[tq * NX + tq];
+      rdg = L.Rc[tu * NU + tu];
+      xgt = L.xg[tq];
+    }
+    stage_l(K, 0, zt);
     wave_lds_sync();
     for (int e = t; e < NX * NX; e += 64) L.Vxx[e] = lxx(K, e / NX, e % NX);
     if (t < NX) L.Vx[t] = L.lx[t];
@@ -207,6 +220,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     }
     store_ab(0);
     if (t < NX + NU) L.z[1][t] = zn;
+    zr = zn;
     pj = pjn;
     wave_lds_sync();
   }
@@ -226,7 +240,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       pjn = load_jac(k - 1);
       zn = load_z(k - 1);
     }
-    stage_l(k, 1 - cur);
+    stage_l(k, 1 - cur, zr);
     wave_lds_sync();
     IL_STAMP(0);
     if constexpr (MF) {
@@ -362,12 +376,15 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     }   // MF
     IL_STAMP(2);
     // [K | d] = -Q_uu^-1 [Q_ux | Q_u]: Cholesky Q_uu = L L^T (every lane, from LDS), then lane c
-    // solves its right-hand-side column c; Q_uu not positive definite -> backward failure
+    // solves its right-hand-side column c; Q_uu not positive definite -> backward failure.
+    // LAPACK's dpotf2 form (numpy.linalg.cholesky): column j scaled by the reciprocal 1 / L_jj,
+    // and the substitutions multiply by it too -- 6 IEEE divisions on the knot's serial chain
+    // instead of 27 (each a ~10-instruction dependent sequence)
+    bool pd = true;
     {
       // every lane factors (the wave would anyway); lanes >= NC solve a copy of column NC - 1
       const int tc = t < NC ? t : NC - 1;
-      R Lc[NU][NU];
-      bool pd = true;
+      R Lc[NU][NU], ri[NU];
 #pragma unroll
       for (int j = 0; j < NU; ++j) {
         R s = L.Quu[j * NU + j];
@@ -376,12 +393,13 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
         pd = pd && (s > R(0));
         const R dj = sqrt(s);
         Lc[j][j] = dj;
+        ri[j] = R(1) / dj;
 #pragma unroll
         for (int i = j + 1; i < NU; ++i) {
           R v = L.Quu[i * NU + j];
 #pragma unroll
           for (int m = 0; m < j; ++m) v -= Lc[i][m] * Lc[j][m];
-          Lc[i][j] = v / dj;
+          Lc[i][j] = v * ri[j];
         }
       }
       R y[NU];
@@ -391,22 +409,27 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
         R v = tc < NX ? vx : vu;
 #pragma unroll
         for (int m = 0; m < i; ++m) v -= Lc[i][m] * y[m];
-        y[i] = v / Lc[i][i];
+        y[i] = v * ri[i];
       }
 #pragma unroll
       for (int i = NU - 1; i >= 0; --i) {
         R v = y[i];
 #pragma unroll
         for (int m = i + 1; m < NU; ++m) v -= Lc[m][i] * y[m];
-        y[i] = v / Lc[i][i];
+        y[i] = v * ri[i];
       }
 #pragma unroll
       for (int i = 0; i < NU; ++i) *(t < NC ? &L.KD[i * NC + tc] : &L.trash[t]) = -y[i];
-      if (t == 0 && !pd) L.fail = 1;
+    }
+    // every lane factored the same Q_uu: pd is wave-uniform, no LDS round trip for the exit test
+    pd = __builtin_amdgcn_readfirstlane((int)pd) != 0;
+    if (!pd) {
+      if (t == 0) L.fail = 1;
+      wave_lds_sync();
+      break;
     }
     wave_lds_sync();
     IL_STAMP(3);
-    if (L.fail) break;
     // V_x = Q_x + Q_ux^T d, M = Q_xx + Q_ux^T K; dV1 += d^T Q_u, dV2 += d^T Q_uu d / 2
     if constexpr (MF) {
       // [M | V_x] - [Q_xx | Q_x] = Q_ux^T [K | d]: one 16-column tile, k over the NU controls
@@ -489,6 +512,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     if (k > 0) {
       store_ab(1 - cur);
       if (t < NX + NU) L.z[cur][t] = zn;
+      zr = zn;
       pj = pjn;
     }
     wave_lds_sync();
