@@ -150,8 +150,6 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
   // stage the cost derivatives of knot k (QuadraticCost.gradient / hessian, TrajoptCost.py:58-83,
   // plus the soft-limit jacobian, :220-225) into L.lx / L.lu / L.jac; z = L.z[zs], and zr = this
   // lane's entry of it (lanes < NX: x_k[t], NX .. NX + NU - 1: u_k[t - NX])
-  R qdg = 0.0, qfdg = 0.0, rdg = 0.0;   // this lane's diagonal entries of Q, QF, R (CostDev.diag)
-  double xgt = 0.0;
   auto stage_l = [&](int k, int zs, double zr) {
     const bool term = k == K;
     const double* zk = L.z[zs];
@@ -168,10 +166,12 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       // the same chains without their exact-zero terms (CostDev.diag), from registers: the lane's
       // own z entry and diagonal entries; the NaN a non-finite entry of y / w puts into every dense
       // row sum (0 * inf) is raised by a ballot over the wave (diag_poison's rule)
-      const R yt = R(zr - xgt), wt = R(zr);
+      const int tq = t < NX ? t : 0;
+      const R qdg = (use_qf(k) ? L.QF : L.Q)[tq * NX + tq], rdg = L.Rc[tu * NU + tu];
+      const R yt = R(zr - L.xg[tq]), wt = R(zr);
       const bool badx = __ballot(t < NX && !isfinite(yt)) != 0;
       const bool badu = __ballot(isu && !isfinite(wt)) != 0;
-      g = fma_r(yt, use_qf(k) ? qfdg : qdg, R(0)) + ((badx && NX > 1) ? R(NAN) : R(0));
+      g = fma_r(yt, qdg, R(0)) + ((badx && NX > 1) ? R(NAN) : R(0));
       gu = fma_r(wt, rdg, R(0)) + ((badu && NU > 1) ? R(NAN) : R(0));
     } else {
       wave_lds_sync();
@@ -203,13 +203,6 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     const double zn = load_z(K - 1);
     if (t < NX + NU) L.z[0][t] = zt;
     wave_lds_sync();
-    {
-      const int tq = t < NX ? t : 0, tu = (t >= NX && t < NX + NU) ? t - NX : 0;
-      qdg = L.Q[tq * NX + tq];
-      qfdg = L.QF[tq * NX + tq];
-      rdg = L.Rc[tu * NU + tu];
-      xgt = L.xg[tq];
-    }
     stage_l(K, 0, zt);
     wave_lds_sync();
     for (int e = t; e < NX * NX; e += 64) L.Vxx[e] = lxx(K, e / NX, e % NX);
@@ -627,8 +620,9 @@ __global__ void __launch_bounds__(64) k_ilqr_init_cost(const CostDev* __restrict
 
 // ======================================================================= forward sweep (closed-loop rollouts)
 // lane = (b, trial t).  INIT: J at the current trajectory (no rollout).  Trial
-// trajectories are kept ([B][T][nx][N], [B][T][nu][N-1]) so the decision kernel
-// copies the accepted one.  Cost sums in totalCost's order (:296-310): the
+// trajectories are kept knot-major ([B][T][N][nx], [B][T][N-1][nu]: a lane's knot is one
+// contiguous 96 + 48-byte run, where the reference's [nx][N] order made every knot 18 partial
+// cache-line writes per lane) so the decision kernel copies (and transposes) the accepted one.  Cost sums in totalCost's order (:296-310): the
 // QuadraticCost terms, then the soft values.
 // Prefetch (PF) of the feedback law's operands: the knot loop is one serial chain per lane
 // (~25k cycles per knot at one wave per SIMD, profiles/r02: ~40 % of it the loads of K_k, d_k,
@@ -744,7 +738,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
     if (live) {
     if (!init) {
 #pragma unroll
-      for (int m = 0; m < NX; ++m) xo[m * N + k] = xh[m];
+      for (int m = 0; m < NX; ++m) xo[k * NX + m] = xh[m];
     } else {
 #pragma unroll
       for (int m = 0; m < NX; ++m) xh[m] = xb[m * N + k];
@@ -766,7 +760,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
 #pragma unroll
           for (int m = 0; m < NX; ++m) fb += Kk[i * NX + m] * dx[m];
           uh[i] = (sk[NU + NX + i] + al * sk[i]) + fb;
-          uo[i * K + k] = uh[i];
+          uo[k * NU + i] = uh[i];
         }
       } else {
         const double* Kk = Kg + ((size_t)b * K + k) * NU * NX;
@@ -777,7 +771,7 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
 #pragma unroll
           for (int m = 0; m < NX; ++m) fb += Kk[i * NX + m] * (xh[m] - xb[m * N + k]);
           uh[i] = (ub[i * K + k] + al * dk[i]) + fb;
-          uo[i * K + k] = uh[i];
+          uo[k * NU + i] = uh[i];
         }
       }
     }
@@ -817,9 +811,9 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
     for (int k = 0; k <= K; ++k) {
       double z[3 * NJ], jac[3 * NJ];
 #pragma unroll
-      for (int m = 0; m < NX; ++m) z[m] = xs_[m * N + k];
+      for (int m = 0; m < NX; ++m) z[m] = init ? xs_[m * N + k] : xs_[k * NX + m];
 #pragma unroll
-      for (int m = 0; m < NU; ++m) z[NX + m] = k < K ? us_[m * K + k] : 0.0;
+      for (int m = 0; m < NU; ++m) z[NX + m] = k < K ? (init ? us_[m * K + k] : us_[k * NU + m]) : 0.0;
       const size_t ko = ((size_t)b * N + k) * 6 * NJ;
       J = J + soft_knot<NJ>(Cs, mu + ko, lam + ko, k == K, z, jac);
     }
@@ -832,42 +826,62 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
   Jt[bt] = J;
 }
 
+// trials per pass of k_ilqr_soft_add: as many [N + 1] LDS rows as fit in 48 KB
+__host__ __device__ inline int soft_add_group(int T, int N) {
+  const int g = (48 * 1024) / ((N + 1) * (int)sizeof(double));
+  return g < 1 ? 1 : (g < T ? g : T);
+}
+
 // The soft-limit values of the trial trajectories (value_soft_constraints, summed after the cost
-// terms as totalCost does, :296-310): one 64-lane workgroup per (problem, trial), lanes over knots
-// for soft_knot (z from the trial trajectory, mu / lambda of the knot), then lane 0 adds them to
-// the rollout's cost sum in knot order -- the serial tail of k_ilqr_forward operand for operand,
-// which paid one dependent round trip to HBM per knot inside a single lane (0.4 ms of config 3's
-// 1.0 ms forward launches).
+// terms as totalCost does, :296-310): one 64-lane workgroup per problem, lanes over knots.  A lane
+// reads its knot's mu / lambda once and evaluates soft_knot for every trial's trajectory (the trials
+// share the constants: one workgroup per (problem, trial) read them T times); then lane tr adds
+// trial tr's values to its rollout's cost sum in knot order -- the serial tail of k_ilqr_forward
+// operand for operand, the T trials' chains side by side.
 template <int NJ>
 __global__ void __launch_bounds__(64) k_ilqr_soft_add(const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                       const double* __restrict__ lam, PList P, int B, int N, int T,
                                                       const double* __restrict__ xt, const double* __restrict__ ut,
                                                       const int* __restrict__ active, const int* __restrict__ ok,
                                                       double* __restrict__ Jt) {
-  constexpr int NX = 2 * NJ, NU = NJ;
-  const int pp = blockIdx.x / T, tr = blockIdx.x - pp * T;
-  if (!P.has(pp, B)) return;
-  const int b = P.at(pp);
+  constexpr int NX = 2 * NJ, NU = NJ, MC = 6 * NJ;
+  if (!P.has(blockIdx.x, B)) return;
+  const int b = P.at(blockIdx.x);
   if (!active[b] || !ok[b]) return;
-  const size_t gid = (size_t)b * T + tr;
-  extern __shared__ double sv[];   // [N]
-  const int K = N - 1;
-  const double* xo = xt + (size_t)gid * NX * N;
-  const double* uo = ut + (size_t)gid * NU * K;
-  for (int k = threadIdx.x; k < N; k += 64) {
-    double z[3 * NJ], jac[3 * NJ];
+  extern __shared__ double sv[];   // [TG][N + 1] (the pad puts the trials' rows on different banks)
+  const int K = N - 1, ld = N + 1;
+  const int TG = soft_add_group(T, N);   // trials per pass (the LDS rows of one pass)
+  for (int t0 = 0; t0 < T; t0 += TG) {
+    const int tn = min(TG, T - t0);
+    for (int k = threadIdx.x; k < N; k += 64) {
+      const size_t ko = ((size_t)b * N + k) * MC;
+      double mk[MC], lk[MC];
 #pragma unroll
-    for (int m = 0; m < NX; ++m) z[m] = xo[m * N + k];
+      for (int e = 0; e < MC; ++e) {
+        mk[e] = mu[ko + e];
+        lk[e] = lam[ko + e];
+      }
+      for (int q = 0; q < tn; ++q) {
+        const size_t gid = (size_t)b * T + t0 + q;
+        const double* xo = xt + gid * NX * N;
+        const double* uo = ut + gid * NU * K;
+        double z[3 * NJ], jac[3 * NJ];
 #pragma unroll
-    for (int m = 0; m < NU; ++m) z[NX + m] = k < K ? uo[m * K + k] : 0.0;
-    const size_t ko = ((size_t)b * N + k) * 6 * NJ;
-    sv[k] = soft_knot<NJ>(Cs, mu + ko, lam + ko, k == K, z, jac);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double J = Jt[gid];
-    for (int k = 0; k < N; ++k) J = J + sv[k];
-    Jt[gid] = J;
+        for (int m = 0; m < NX; ++m) z[m] = xo[k * NX + m];
+#pragma unroll
+        for (int m = 0; m < NU; ++m) z[NX + m] = k < K ? uo[k * NU + m] : 0.0;
+        sv[q * ld + k] = soft_knot<NJ>(Cs, mk, lk, k == K, z, jac);
+      }
+    }
+    __syncthreads();
+    const int q = threadIdx.x;
+    if (q < tn) {
+      const size_t gid = (size_t)b * T + t0 + q;
+      double J = Jt[gid];
+      for (int k = 0; k < N; ++k) J = J + sv[q * ld + k];
+      Jt[gid] = J;
+    }
+    __syncthreads();
   }
 }
 
@@ -999,8 +1013,15 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int N
   if (choice >= 0) {
     const double* xs_ = xt + ((size_t)b * T + choice) * NX * N;
     const double* us_ = ut + ((size_t)b * T + choice) * NU * K;
-    for (int e = t; e < NX * N; e += 64) x[(size_t)b * NX * N + e] = xs_[e];
-    for (int e = t; e < NU * K; e += 64) u[(size_t)b * NU * K + e] = us_[e];
+    // trial trajectories are knot-major ([k][m], see k_ilqr_forward); x / u the reference's [m][k]
+    for (int e = t; e < NX * N; e += 64) {
+      const int m = e / N, k = e - m * N;
+      x[(size_t)b * NX * N + e] = xs_[k * NX + m];
+    }
+    for (int e = t; e < NU * K; e += 64) {
+      const int m = e / K, k = e - m * K;
+      u[(size_t)b * NU * K + e] = us_[k * NU + m];
+    }
   }
 }
 
@@ -1053,8 +1074,8 @@ struct LaunchIlqr {
     else { if (f32) { TMPC_FWD(false, float) } else { TMPC_FWD(false, double) } }
 #undef TMPC_FWD
     if (mu && !init)
-      hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B * T), dim3(64), N * sizeof(double), s, Cs, mu, lam, P, B, N, T,
-                         xt, ut, active, ok, Jt);
+      hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B), dim3(64), (size_t)soft_add_group(T, N) * (N + 1) * sizeof(double), s, Cs, mu, lam,
+                         P, B, N, T, xt, ut, active, ok, Jt);
   }
 };
 
