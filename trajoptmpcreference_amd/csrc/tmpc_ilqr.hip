@@ -827,8 +827,11 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
 }
 
 // trials per pass of k_ilqr_soft_add: as many [N + 1] LDS rows as fit in 48 KB
-__host__ __device__ inline int soft_add_group(int T, int N) {
-  const int g = (48 * 1024) / ((N + 1) * (int)sizeof(double));
+// (TMPC_SOFT_ADD_GROUP=g caps it: tests run the multi-pass form at small sizes)
+static inline int soft_add_group(int T, int N) {
+  int g = (48 * 1024) / ((N + 1) * (int)sizeof(double));
+  const char* e = getenv("TMPC_SOFT_ADD_GROUP");
+  if (e && atoi(e) > 0 && atoi(e) < g) g = atoi(e);
   return g < 1 ? 1 : (g < T ? g : T);
 }
 
@@ -841,16 +844,16 @@ __host__ __device__ inline int soft_add_group(int T, int N) {
 template <int NJ>
 __global__ void __launch_bounds__(64) k_ilqr_soft_add(const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                       const double* __restrict__ lam, PList P, int B, int N, int T,
-                                                      const double* __restrict__ xt, const double* __restrict__ ut,
-                                                      const int* __restrict__ active, const int* __restrict__ ok,
-                                                      double* __restrict__ Jt) {
+                                                      int TG, const double* __restrict__ xt,
+                                                      const double* __restrict__ ut, const int* __restrict__ active,
+                                                      const int* __restrict__ ok, double* __restrict__ Jt) {
   constexpr int NX = 2 * NJ, NU = NJ, MC = 6 * NJ;
   if (!P.has(blockIdx.x, B)) return;
   const int b = P.at(blockIdx.x);
   if (!active[b] || !ok[b]) return;
   extern __shared__ double sv[];   // [TG][N + 1] (the pad puts the trials' rows on different banks)
   const int K = N - 1, ld = N + 1;
-  const int TG = soft_add_group(T, N);   // trials per pass (the LDS rows of one pass)
+  // TG: trials per pass (the LDS rows of one pass, soft_add_group)
   for (int t0 = 0; t0 < T; t0 += TG) {
     const int tn = min(TG, T - t0);
     for (int k = threadIdx.x; k < N; k += 64) {
@@ -1073,9 +1076,11 @@ struct LaunchIlqr {
     if (mu && init) { if (f32) { TMPC_FWD(true, float) } else { TMPC_FWD(true, double) } }
     else { if (f32) { TMPC_FWD(false, float) } else { TMPC_FWD(false, double) } }
 #undef TMPC_FWD
-    if (mu && !init)
-      hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B), dim3(64), (size_t)soft_add_group(T, N) * (N + 1) * sizeof(double), s, Cs, mu, lam,
-                         P, B, N, T, xt, ut, active, ok, Jt);
+    if (mu && !init) {
+      const int tg = soft_add_group(T, N);
+      hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B), dim3(64), (size_t)tg * (N + 1) * sizeof(double), s, Cs, mu, lam,
+                         P, B, N, T, tg, xt, ut, active, ok, Jt);
+    }
   }
 };
 
