@@ -38,7 +38,6 @@ struct IlqrLds {
   R Q[NX * NX], QF[NX * NX], Rc[NU * NU];   // the cost's Hessian blocks, staged once
   double xg[NX];
   double z[2][NX + NU];                 // knot k's [x_k; u_k] and the prefetched knot's (fp64: the soft terms)
-  R dv[2];
   int fail;
   R trash[64];                          // the stores of lanes without an output land here
 };
@@ -195,6 +194,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
 
   // terminal value function: V_x = l_x(N-1), V_xx = l_xx(N-1); A_{K-1}, B_{K-1} and z_{K-1} in flight
   double zr = 0.0;   // this lane's entry of the next knot to stage
+  R dv0 = 0.0, dv1 = 0.0;   // the expected-reduction sums dV1, dV2 (lane NX)
   {
     const double zt = load_z(K);
     pj = load_jac(K);
@@ -208,7 +208,6 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     for (int e = t; e < NX * NX; e += 64) L.Vxx[e] = lxx(K, e / NX, e % NX);
     if (t < NX) L.Vx[t] = L.lx[t];
     if (t == 0) {
-      L.dv[0] = L.dv[1] = 0.0;
       L.fail = 0;
     }
     store_ab(0);
@@ -374,6 +373,7 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
     // and the substitutions multiply by it too -- 6 IEEE divisions on the knot's serial chain
     // instead of 27 (each a ~10-instruction dependent sequence)
     bool pd = true;
+    R ds1 = 0.0, ds2 = 0.0;   // this knot's dV terms (meaningful on lane NX)
     {
       // every lane factors (the wave would anyway); lanes >= NC solve a copy of column NC - 1
       const int tc = t < NC ? t : NC - 1;
@@ -395,10 +395,11 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
           Lc[i][j] = v * ri[j];
         }
       }
-      R y[NU];
+      R y[NU], qv[NU];
 #pragma unroll
       for (int i = 0; i < NU; ++i) {
         const R vx = L.Qux[i * NX + (tc < NX ? tc : 0)], vu = L.Qu[i];
+        qv[i] = vu;
         R v = tc < NX ? vx : vu;
 #pragma unroll
         for (int m = 0; m < i; ++m) v -= Lc[i][m] * y[m];
@@ -413,6 +414,21 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       }
 #pragma unroll
       for (int i = 0; i < NU; ++i) *(t < NC ? &L.KD[i * NC + tc] : &L.trash[t]) = -y[i];
+      // dV terms on the lane of column NX, whose -y is d (dV1 += d^T Q_u, dV2 += d^T Q_uu d / 2): the
+      // chains the wave formed from LDS copies after the next phase (d from KD, (Q_uu d)_i on lane i,
+      // read back lane by lane), now from this lane's registers, operand for operand
+      R s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int i = 0; i < NU; ++i) {
+        R qd = 0.0;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) qd += L.Quu[i * NU + m] * (-y[m]);
+        const R di = -y[i];
+        s1 += di * qv[i];
+        s2 += di * qd;
+      }
+      ds1 = s1;
+      ds2 = s2;
     }
     // every lane factored the same Q_uu: pd is wave-uniform, no LDS round trip for the exit test
     pd = __builtin_amdgcn_readfirstlane((int)pd) != 0;
@@ -421,9 +437,11 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       wave_lds_sync();
       break;
     }
+    dv0 += ds1;
+    dv1 += R(0.5) * ds2;
     wave_lds_sync();
     IL_STAMP(3);
-    // V_x = Q_x + Q_ux^T d, M = Q_xx + Q_ux^T K; dV1 += d^T Q_u, dV2 += d^T Q_uu d / 2
+    // V_x = Q_x + Q_ux^T d, M = Q_xx + Q_ux^T K
     if constexpr (MF) {
       // [M | V_x] - [Q_xx | Q_x] = Q_ux^T [K | d]: one 16-column tile, k over the NU controls
       constexpr int KU = (NU + 3) / 4;
@@ -462,31 +480,6 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
         L.Vx[r] = L.Qx[r] + s;
       }
     }
-    {
-      // dV: lane i forms (Q_uu d)_i, then the two sums run in i order on values every lane holds
-      // (the same chains as one lane computing everything, without its serial 6 x 6 product)
-      R dd[NU], qu[NU];
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        dd[i] = L.KD[i * NC + NX];
-        qu[i] = L.Qu[i];
-      }
-      const int iq = t < NU ? t : NU - 1;
-      R qd = 0.0;
-#pragma unroll
-      for (int m = 0; m < NU; ++m) qd += L.Quu[iq * NU + m] * dd[m];
-      R s1 = 0.0, s2 = 0.0;
-#pragma unroll
-      for (int i = 0; i < NU; ++i) {
-        const R di = dd[i];
-        s1 += di * qu[i];
-        s2 += di * lane_val(qd, i);
-      }
-      if (t == 0) {
-        L.dv[0] += s1;
-        L.dv[1] += R(0.5) * s2;
-      }
-    }
     IL_STAMP(4);
     // K_k, d_k to HBM ([B][K][NU][NX], [B][K][NU]); not waited for (wave_lds_sync)
 #pragma unroll
@@ -517,10 +510,10 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
            "Kstore/Vxx %llu store_ab %llu loop %llu\n", K, st_[0], st_[1], st_[2], st_[3], st_[4], st_[5], st_[6],
            st_[7]);
 #endif
-  if (t == 0) {
-    ok[b] = L.fail ? 0 : 1;
-    dV[2 * b] = double(L.dv[0]);
-    dV[2 * b + 1] = double(L.dv[1]);
+  if (t == 0) ok[b] = L.fail ? 0 : 1;
+  if (t == NX) {
+    dV[2 * b] = double(dv0);
+    dV[2 * b + 1] = double(dv1);
   }
 }
 
