@@ -32,6 +32,8 @@ from typing import List
 
 import numpy as np
 
+from ._options import NO_OPTIONS, fresh
+
 HARD_MODES = ("ACTIVE_SET", "FULL_SET")
 SOFT_MODES = ("QUADRATIC_PENALTY", "AUGMENTED_LAGRANGIAN", "ADMM_PROJECTION")
 GPU_SOFT_MODES = ("QUADRATIC_PENALTY", "AUGMENTED_LAGRANGIAN")
@@ -41,8 +43,8 @@ class BoxConstraint:
     """lb <= z <= ub on a constraint_size slice (TrajoptConstraint.py:5-176)."""
 
     def __init__(self, constraint_size: int = 0, num_timesteps: int = 0, upper_bounds: List[float] = (),
-                 lower_bounds: List[float] = (), mode: str = "NONE", options=None):
-        options = {} if options is None else options
+                 lower_bounds: List[float] = (), mode: str = "NONE", options=NO_OPTIONS):
+        options = fresh(options)
         self.constraint_size = constraint_size
         self.num_timesteps = num_timesteps
         self.num_constraints = 2 * constraint_size * num_timesteps
@@ -52,6 +54,16 @@ class BoxConstraint:
         self.bounds = np.zeros(2 * constraint_size)
         self.bounds[:constraint_size] = lower_bounds
         self.bounds[constraint_size:] = upper_bounds
+        self.validate_constraint_mode(mode, options)
+        T, m = num_timesteps, 2 * constraint_size
+        self.quadratic_penalty_mu = options["quadratic_penalty_mu_init"] * np.ones((m, T))
+        self.augmented_lagrangian_lambda = np.zeros((m, T))
+        self.augmented_lagrangian_phi = options["augmentated_lagrangian_phi_init"] * np.ones((m, T))
+
+    def validate_constraint_mode(self, mode: str, options=NO_OPTIONS):
+        """TrajoptConstraint.py:37-51: set the mode and the option defaults (raises where the reference
+        prints + exits)."""
+        options = fresh(options)
         if mode not in HARD_MODES + SOFT_MODES:
             raise ValueError("Invalid Constraint Mode. Options are [ACTIVE_SET, FULL_SET, QUADRATIC_PENALTY, "
                              "AUGMENTED_LAGRANGIAN, ADMM_PROJECTION]")
@@ -64,10 +76,6 @@ class BoxConstraint:
         options.setdefault("jacobian_extra_columns_head", 0)
         options.setdefault("jacobian_extra_columns_tail", 0)
         self.options = options
-        T, m = num_timesteps, 2 * constraint_size
-        self.quadratic_penalty_mu = options["quadratic_penalty_mu_init"] * np.ones((m, T))
-        self.augmented_lagrangian_lambda = np.zeros((m, T))
-        self.augmented_lagrangian_phi = options["augmentated_lagrangian_phi_init"] * np.ones((m, T))
 
     def is_hard_constraint_mode(self, mode=None):
         return (self.mode if mode is None else mode) in HARD_MODES
@@ -88,9 +96,9 @@ class BoxConstraint:
         z = np.asarray(z, dtype=np.float64).reshape(-1)[:self.constraint_size]
         return np.concatenate([z - self.lower, self.upper - z])
 
-    def value(self, z, timestep: int = None, mode: str = None):
+    def value(self, xk, timestep: int = None, mode: str = None):
         mode = self.mode if mode is None else mode
-        v = self.full_value(z)
+        v = self.full_value(xk)
         if mode == "ACTIVE_SET":
             return v[v < 0]
         if mode == "FULL_SET":
@@ -104,10 +112,10 @@ class BoxConstraint:
             return val
         raise NotImplementedError("ADMM_PROJECTION is not implemented (the reference exits too, :81-83)")
 
-    def jacobian(self, z, timestep: int = None, mode: str = None):
+    def jacobian(self, xk, timestep: int = None, mode: str = None):
         """Soft modes: the jacobian column (head + constraint_size + tail entries)."""
         mode = self.mode if mode is None else mode
-        v = self.full_value(z)
+        v = self.full_value(xk)
         cs = self.constraint_size
         sign = np.concatenate([np.ones(cs), -np.ones(cs)]) * (v < 0)
         full = np.zeros((2 * cs, cs))
@@ -126,18 +134,19 @@ class BoxConstraint:
             jac = jac + np.matmul(self.augmented_lagrangian_lambda[:, timestep], full)
         return jac.reshape(-1, 1)
 
-    def max_soft_constraint_value(self, z_of_t):
+    def max_soft_constraint_value(self, x):
+        """TrajoptConstraint.py:131-136 on the limited slice x (constraint_size x num_timesteps)."""
         m = 0
         for t in range(self.num_timesteps):
-            m = max(m, abs(min(self.full_value(z_of_t[:, t]))))
+            m = max(m, abs(min(self.full_value(x[:, t]))))
         return m
 
-    def update_soft_constraint_constants(self, z_of_t):
+    def update_soft_constraint_constants(self, x):
         """BoxConstraint.update_soft_constraint_constants (:138-166) on the limited slice z_of_t
         (constraint_size x num_timesteps, one column per knot): per entry of [z - lb; ub - z] < 0,
         mu *= mu_factor (capped at mu_max) when |value| >= phi, else lambda += mu value and
         phi /= phi_factor.  Returns True when no constant changed (every violated mu at its cap)."""
-        z_of_t = np.asarray(z_of_t, dtype=np.float64)
+        z_of_t = np.asarray(x, dtype=np.float64)
         o = self.options
         flag = True
         for t in range(self.num_timesteps):
@@ -178,20 +187,20 @@ class TrajoptConstraint:
         self.velocity_limits = None
         self.torque_limits = None
 
-    def set_joint_limits(self, upper_bounds, lower_bounds, mode, options=None):
-        options = {} if options is None else dict(options)
+    def set_joint_limits(self, upper_bounds, lower_bounds, mode, options=NO_OPTIONS):
+        options = dict(options)
         options["jacobian_extra_columns_tail"] = self.nv + self.nu
         # all N knots (the reference sizes joint limits N-1 and then indexes knot N-1: oracle/soft.py)
         self.joint_limits = BoxConstraint(self.nq, self.num_timesteps, upper_bounds, lower_bounds, mode, options)
 
-    def set_velocity_limits(self, upper_bounds, lower_bounds, mode, options=None):
-        options = {} if options is None else dict(options)
+    def set_velocity_limits(self, upper_bounds, lower_bounds, mode, options=NO_OPTIONS):
+        options = dict(options)
         options["jacobian_extra_columns_head"] = self.nq
         options["jacobian_extra_columns_tail"] = self.nu
         self.velocity_limits = BoxConstraint(self.nv, self.num_timesteps, upper_bounds, lower_bounds, mode, options)
 
-    def set_torque_limits(self, upper_bounds, lower_bounds, mode, options=None):
-        options = {} if options is None else dict(options)
+    def set_torque_limits(self, upper_bounds, lower_bounds, mode, options=NO_OPTIONS):
+        options = dict(options)
         options["jacobian_extra_columns_head"] = self.nq + self.nv
         self.torque_limits = BoxConstraint(self.nu, self.num_timesteps - 1, upper_bounds, lower_bounds, mode, options)
 
@@ -259,7 +268,11 @@ class TrajoptConstraint:
         T = self.num_timesteps
         return J[:, :self.nq + self.nv] if (timestep is not None and timestep >= T - 1) else J
 
-    def total_hard_constraints(self, x=None, u=None, timestep=None):
+    def len_or_none(self, x):
+        """TrajoptConstraint.py:276-279."""
+        return 0 if x is None else len(x)
+
+    def total_hard_constraints(self, x, u, timestep=None):
         """TrajoptConstraint.total_hard_constraints (:281-293)."""
         if not any(c.is_hard_constraint_mode() for _, c in self.limits()):
             return 0

@@ -115,9 +115,28 @@ class UrdfCost(QuadraticCost):
         J = np.column_stack(((dH[0] @ H[1] @ self.OFFSET)[:2], (H[0] @ dH[1] @ self.OFFSET)[:2]))
         return pos, J
 
+    def compute_J(self, q):
+        """The end-effector Jacobian d p / d q (TrajoptCost.py:398-400 -> RBDReference.Jacobian)."""
+        return self._kin(np.asarray(q, dtype=np.float64))[1]
+
+    def dJtotdq(self, q, qd):
+        """TrajoptCost.py:460-480: d jacobian_tot_state / d q as a (2n, 2n, 2n) array, from the
+        reference's hard-coded 2-link patterns of dJdq / d2Jdq2 (RBDReference.py:219-316)."""
+        J = self.compute_J(q)
+        n = self.n
+        dJdq = np.array([-J[1, :], [-J[1, 1], -J[1, 1]], -J[0, :], [J[0, 1], J[0, 1]]])
+        ddJdq = np.array([-J[0, :], [-J[0, 1], -J[0, 1]], -J[1, :], [-J[1, 1], -J[1, 1]]])
+        A = np.hstack((dJdq, np.zeros((2 * n, n)))).reshape(n, n, 2 * n)
+        Bm = np.hstack((dJdq, ddJdq)).reshape(n, n, 2 * n)
+        out = np.zeros((2 * n, 2 * n, 2 * n))
+        out[0:n, 0:n, :] = A
+        out[n:2 * n, 0:n, :] = Bm
+        out[n:2 * n, n:2 * n, :] = A
+        return out
+
     def jacobian_tot_state(self, q, qd):
         """RBDReference.py:313-331 with the hand-coded dJdq pattern (:252-259)."""
-        _, J = self._kin(q)
+        J = self.compute_J(q)
         dJdq = np.array([[-J[1, 0], -J[1, 1]], [-J[1, 1], -J[1, 1]], [-J[0, 0], -J[0, 1]], [J[0, 1], J[0, 1]]])
         J2 = (dJdq @ qd).reshape(2, 2)
         return np.vstack((np.hstack((J, np.zeros((2, 2)))), np.hstack((J2, J))))

@@ -1426,6 +1426,24 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
     HIP_OK(hipMemcpyAsync(io_guess, guess, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
     w.guess = io_guess;
   }
+  // soft limits: the QP of formKKTSystemBlocks carries their jacobian terms (:220-225, :255-259) at the
+  // context's soft state (tmpc_set_soft_state; defaults if it was never set for this B, N)
+  if (ctx->hlim.any) {
+    double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
+    if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
+    if (ctx->soft_B != B || ctx->soft_N != N) {
+      launch_soft_init(ctx->stream, ctx->dlim, (size_t)B * N * 6 * nj, 6 * nj, smu, slam, sphi);
+      HIP_OK(hipGetLastError());
+      ctx->soft_B = B;
+      ctx->soft_N = N;
+    }
+    BUF(double, soft_Gk, (size_t)B * N * (nx * nx + nj * nj));
+    BUF(double, soft_j, (size_t)B * N * (nx + nj));
+    w.Gk = soft_Gk;
+    w.jsoft = soft_j;
+    w.smu = smu;
+    w.slam = slam;
+  }
   // hard box constraints: the QP with the knots' constraint rows (tmpc_hard.hip); the lambda part of
   // dxul then holds the multipliers of the N nx dynamics / initial-state rows, in knot order
   HardArgs hard{};

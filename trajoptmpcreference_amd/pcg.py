@@ -12,6 +12,7 @@ per-system kernel.  Invalid options raise ValueError instead of exit().
 import numpy as np
 
 from . import _native
+from ._options import NO_OPTIONS, fresh
 
 VALID_PRECONDITIONERS = ("0", "J", "BJ", "SS")
 
@@ -37,13 +38,13 @@ def extract_blocks(A, block_size):
 
 
 class PCG:
-    def __init__(self, A, b, block_size, Nblocks, guess=None, options=None, overloading=False, device=0):
+    def __init__(self, A, b, block_size, Nblocks, guess=None, options=NO_OPTIONS, overloading=False, device=0):
         self.A = A
         self.b = b
         self.block_size = int(block_size)
         self.Nblocks = Nblocks
         self.guess = guess
-        self.options = {} if options is None else options
+        self.options = fresh(options)
         self.overloading = overloading
         self.device = device
         self.set_default_options(self.options)
@@ -88,51 +89,74 @@ class PCG:
     def update_RETURN_TRACE(self, mode):
         self.options["RETURN_TRACE"] = mode
 
-    def solve(self):
-        Dg, Lo, Up = extract_blocks(self.A, self.block_size)
-        N, nx = Dg.shape[0], self.block_size
-        b = np.asarray(self.b, dtype=np.float64).reshape(1, -1)
-        guess = None
-        if self.guess is not None:
-            g = np.asarray(self.guess, dtype=np.float64).reshape(1, -1)
-            if np.any(g != 0):
-                guess = g
-        max_iter = int(self.options["max_iter"])
+    def _run(self, A, b, guess, options):
+        Dg, Lo, Up = extract_blocks(A, self.block_size)
+        b = np.asarray(b, dtype=np.float64).reshape(1, -1)
+        if guess is not None:
+            g = np.asarray(guess, dtype=np.float64).reshape(1, -1)
+            guess = g if np.any(g != 0) else None
+        max_iter = int(options["max_iter"])
         ctx = _native.default_context(self.device)
-        lam, it, tn, tr, Pd = ctx.pcg_batch(Dg[None], Lo[None], b, precond=self.options["preconditioner_type"],
-                                            S_up=Up[None], guess=guess, tol=float(self.options["exit_tolerance"]),
+        lam, it, tn, tr, Pd = ctx.pcg_batch(Dg[None], Lo[None], b, precond=options["preconditioner_type"],
+                                            S_up=Up[None], guess=guess, tol=float(options["exit_tolerance"]),
                                             max_iter=max_iter, trace=True)
-        self._Pd = Pd[0]
         n_it = int(it[0])
         self.iterations = n_it
         trace = [float(v) for v in tn[0, :n_it + 1]]
         trace2 = [float(v) for v in tr[0, :n_it + 1]]
-        return lam[0].reshape(-1, 1), (trace, trace2)
+        return lam[0].reshape(-1, 1), (trace, trace2), Pd[0]
+
+    def solve(self):
+        """PCG.solve (PCG.py:214-215): pcg(A, b, Pinv, guess, options) with this object's preconditioner."""
+        x, traces, self._Pd = self._run(self.A, self.b, self.guess, self.options)
+        return x, traces
+
+    def pcg(self, A, b, Pinv, guess, options=NO_OPTIONS):
+        """PCG.pcg (PCG.py:66-111).  The GPU applies the preconditioner of options['preconditioner_type']
+        from A's blocks; Pinv must be that preconditioner (compute_preconditioner(A, block_size, type),
+        to 1e-10 relative) -- an arbitrary dense Pinv has no device path and raises."""
+        options = fresh(options)
+        self.set_default_options(options)
+        want = self.compute_preconditioner(A, self.block_size, options["preconditioner_type"])
+        Pinv = np.asarray(Pinv, dtype=np.float64)
+        if Pinv.shape != want.shape or not np.allclose(Pinv, want, rtol=1e-10, atol=1e-300):
+            raise NotImplementedError("PCG.pcg: Pinv is not the block preconditioner of type "
+                                      f"{options['preconditioner_type']!r} of A (the GPU builds it from A's blocks)")
+        x, traces, _ = self._run(A, b, guess, options)
+        return x, traces
+
+    def compute_preconditioner(self, A, block_size, preconditioner_type):
+        """PCG.compute_preconditioner (PCG.py:113-212) as a dense matrix: '0' identity, J diag(A)^-1, BJ the
+        diagonal block inverses, SS the symmetric stair (odd block rows carry -P_k A_k,k+-1 P_k+-1, mirrored
+        to the even ones).  The block inverses come from the GPU's Gauss-Jordan (the solver's own P)."""
+        self.validate_precon_type(preconditioner_type)
+        A = np.asarray(A, dtype=np.float64)
+        b = int(block_size)
+        if preconditioner_type == "0":
+            return np.identity(A.shape[0])
+        if preconditioner_type == "J":
+            return np.diag(1.0 / np.diag(A))
+        Dg, Lo, Up = extract_blocks(A, b)
+        N = Dg.shape[0]
+        ctx = _native.default_context(self.device)
+        _, _, _, _, Pd = ctx.pcg_batch(Dg[None], Lo[None], np.zeros((1, N * b)), precond=preconditioner_type,
+                                       S_up=Up[None], tol=1.0, max_iter=0, trace=False)
+        Pd = Pd[0]
+        P = np.zeros((N * b, N * b))
+        for k in range(N):
+            P[k * b:(k + 1) * b, k * b:(k + 1) * b] = Pd[k]
+        if preconditioner_type == "SS":
+            for k in range(1, N, 2):
+                lo = -Pd[k] @ (Lo[k - 1] @ Pd[k - 1])
+                P[k * b:(k + 1) * b, (k - 1) * b:k * b] = lo
+                P[(k - 1) * b:k * b, k * b:(k + 1) * b] = lo.T
+                if k < N - 1:
+                    up = -Pd[k] @ (Up[k] @ Pd[k + 1])
+                    P[k * b:(k + 1) * b, (k + 1) * b:(k + 2) * b] = up
+                    P[(k + 1) * b:(k + 2) * b, k * b:(k + 1) * b] = up.T
+        return P
 
     @property
     def Pinv(self):
-        """Dense preconditioner as compute_preconditioner builds it (PCG.py:166-212)."""
-        Dg, Lo, Up = extract_blocks(self.A, self.block_size)
-        N, b = Dg.shape[0], self.block_size
-        ptype = self.options["preconditioner_type"]
-        P = np.zeros((N * b, N * b))
-        if ptype == "J":
-            return np.diag(1.0 / np.diag(np.asarray(self.A, dtype=np.float64)))
-        if ptype == "0":   # identity (PCG.py:114-118)
-            return np.identity(N * b)
-        if self._Pd is None:
-            self.solve()
-        Pd = self._Pd
-        for k in range(N):
-            P[k * b:(k + 1) * b, k * b:(k + 1) * b] = Pd[k]
-        if ptype == "SS":
-            for k in range(N):
-                if k % 2:
-                    lo = -Pd[k] @ (Lo[k - 1] @ Pd[k - 1])
-                    P[k * b:(k + 1) * b, (k - 1) * b:k * b] = lo
-                    P[(k - 1) * b:k * b, k * b:(k + 1) * b] = lo.T
-                    if k < N - 1:
-                        up = -Pd[k] @ (Up[k] @ Pd[k + 1])
-                        P[k * b:(k + 1) * b, (k + 1) * b:(k + 2) * b] = up
-                        P[(k + 1) * b:(k + 2) * b, k * b:(k + 1) * b] = up.T
-        return P
+        """The dense preconditioner (the reference's self.Pinv, PCG.py:16)."""
+        return self.compute_preconditioner(self.A, self.block_size, self.options["preconditioner_type"])

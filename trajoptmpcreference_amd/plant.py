@@ -11,6 +11,7 @@ gradients are inconsistent in the reference, TrajoptPlant.py:189,193,235-243).
 import numpy as np
 
 from . import _native
+from ._options import NO_OPTIONS, fresh
 from .urdf import parse_urdf, pendulum_urdf
 
 
@@ -22,10 +23,10 @@ class _RBDReferenceShim:
 class TrajoptPlant:
     """Base plant (TrajoptPlant.py:10-108)."""
 
-    def __init__(self, integrator_type: int = 0, options=None, need_path: bool = False):
+    def __init__(self, integrator_type: int = 0, options=NO_OPTIONS, need_path: bool = False):
         self.validate_integrator_type(integrator_type)
         self.integrator_type = integrator_type
-        options = {} if options is None else options
+        options = fresh(options)
         self.set_default_options(options, need_path)
         self.options = options
 
@@ -69,12 +70,25 @@ class TrajoptPlant:
         top = np.hstack((np.zeros((nq, nq)), np.eye(nv), np.zeros((nq, m))))
         return np.vstack((top, dqdd))
 
+    def integrator(self, xk, uk, dt, return_gradient=False, iter_1=0, iter_2=0, iter_3=0):
+        """TrajoptPlant.integrator, explicit Euler (TrajoptPlant.py:83-108) on this plant's own
+        forward_dynamics / forward_dynamics_gradient hooks: x+ = x + dt [v; qdd], A = I + dt dxdot_x,
+        B = dt dxdot_u.  URDFPlant overrides it with the GPU's batched kernels."""
+        xk = np.asarray(xk, dtype=np.float64)
+        n = len(xk)
+        qdd = self.forward_dynamics(xk, uk, iter_1, iter_2, iter_3)
+        xkp1 = xk + dt * self.qdd_to_xdot(xk, qdd)
+        if not return_gradient:
+            return xkp1
+        dxdot = self.dqdd_to_dxdot(self.forward_dynamics_gradient(xk, uk, iter_1, iter_2, iter_3))
+        return np.eye(n) + dt * dxdot[:, 0:n], dt * dxdot[:, n:]
+
 
 class URDFPlant(TrajoptPlant):
     """URDF rigid-body plant (TrajoptPlant.py:274-331) on the GPU."""
 
-    def __init__(self, integrator_type: int = 0, options=None, device: int = 0):
-        options = {} if options is None else options
+    def __init__(self, integrator_type: int = 0, options=NO_OPTIONS, device: int = 0):
+        options = fresh(options)
         super().__init__(integrator_type, options, True)
         path = options["path_to_urdf"]
         self.model = parse_urdf(path)
@@ -143,10 +157,10 @@ class PendulumPlant(URDFPlant):
     upright (examples/pendulum.py's goal xg = [3.14159, 0]).  It is a URDF model (urdf.pendulum_urdf)
     behind the URDFPlant surface, so it runs on the same GPU kernels as every other plant."""
 
-    def __init__(self, integrator_type: int = 0, options=None, device: int = 0, mass: float = 1.0,
+    def __init__(self, integrator_type: int = 0, options=NO_OPTIONS, device: int = 0, mass: float = 1.0,
                  length: float = 1.0):
         # a copy: the caller's dict must not come back pointing at the pendulum model
-        options = dict(options or {})
+        options = dict(options)
         options["path_to_urdf"] = pendulum_urdf(mass, length)
         super().__init__(integrator_type, options, device)
 

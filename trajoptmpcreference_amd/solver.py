@@ -13,6 +13,7 @@ import enum
 import numpy as np
 
 from . import _native
+from ._options import NO_OPTIONS, fresh
 from .constraint import TrajoptConstraint
 from .cost import QuadraticCost, TrajoptCost, UrdfCost
 from .plant import TrajoptPlant, URDFPlant
@@ -186,8 +187,9 @@ class TrajoptMPCReference:
             r["soft_state"] = ctx.get_soft_state(B, N)
         return r
 
-    def SQP(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.N, options=None):
+    def SQP(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.N, options=NO_OPTIONS):
         """TrajoptMPCReference.SQP (:510-760) for one problem."""
+        options = fresh(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
         hard = any(c.is_hard_constraint_mode() for _, c in self.other_constraints.limits())
@@ -298,10 +300,10 @@ class TrajoptMPCReference:
         m = SOLVER_METHOD.value if isinstance(SOLVER_METHOD, MPCSolverMethods) else str(SOLVER_METHOD)
         if m == "iLQR":
             solver = "iLQR"
-        elif m.startswith("QP-") and m[3:] in ("S", "PCG-J", "PCG-BJ", "PCG-SS"):
-            solver = m[3:]
+        elif m.startswith("QP-") and m[3:] in ("N", "S", "PCG-J", "PCG-BJ", "PCG-SS"):
+            solver = m[3:]   # QP-N: the dense KKT solve, the Schur complement's solution (method N of SQP)
         else:
-            raise NotImplementedError(f"MPC solver {m}: use iLQR, QP-S, QP-PCG-J, QP-PCG-BJ or QP-PCG-SS")
+            raise NotImplementedError(f"MPC solver {m}: use iLQR, QP-N, QP-S, QP-PCG-J, QP-PCG-BJ or QP-PCG-SS")
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
@@ -327,25 +329,232 @@ class TrajoptMPCReference:
             self.other_constraints.unpack_state(*[a[0] for a in r["soft_state"]])
         return r["x_exec"][0], r["u_exec"][0], r["exit_codes"][0], r["iters"][0]
 
-    def solveKKTSystem_Schur(self, x, u, xs, N, dt, rho=0.0, use_PCG=True, options=None):
-        """One QP (formKKTSystemBlocks + solveKKTSystem_Schur, :361-455) -> dxul column; xs is the SQP's
-        initial state (the initial-state row's c_0 = x_0 - xs)."""
-        options = {} if options is None else dict(options)
-        self.set_default_options(options)
-        ptype = options.get("preconditioner_type", "BJ")
-        method = "PCG-" + ptype if use_PCG else "S"
-        ctx = self._context(options)
+    # ------------------------------------------------------------------ the reference's QP-level methods
+    # formKKTSystemBlocks / solveKKTSystem / solveKKTSystem_Schur / totalCost / totalHardConstraintViolation /
+    # reduce_regularization / check_for_exit_or_error / check_and_update_soft_constraints
+    # (TrajoptMPCReference.py:118-508) for callers that drive the SQP steps themselves.  The dynamics and the
+    # QP solve run on the GPU (tmpc_fd_batch / tmpc_fd_grad_batch / tmpc_qp_batch); the dense matrices these
+    # methods return are assembled from the device's blocks at this boundary, in the reference's layout.
+    def _dims(self):
+        nq, nv, nu = self.plant.get_num_pos(), self.plant.get_num_vel(), self.plant.get_num_cntrl()
+        return nq + nv, nu
+
+    def _gpu_plant(self):
+        if not isinstance(self.plant, URDFPlant):
+            raise NotImplementedError("the GPU solver needs a URDFPlant (custom TrajoptPlant subclasses have no "
+                                      "device implementation)")
+        return self.plant
+
+    def formKKTSystemBlocks(self, x, u, xs, N: int, dt: float):
+        """formKKTSystemBlocks (:118-271, the NumPy branch :200-271): dense G, g, C, c of the QP at (x, u).
+        A_k, B_k and f(x_k, u_k) of all N - 1 knots come from one GPU launch each; cost hessian / gradient,
+        the soft-limit jacobian terms (:220-225, :255-259) and the hard-limit rows appended after each
+        knot's dynamics rows (:238-248, :262-270) are the plugins' own hooks, placed as the reference
+        places them."""
+        plant = self._gpu_plant()
+        nx, nu = self._dims()
+        n = nx + nu
         x = np.asarray(x, dtype=np.float64)
-        xs = np.asarray(xs, dtype=np.float64).reshape(1, -1)
         u = np.asarray(u, dtype=np.float64)
+        xs = np.asarray(xs, dtype=np.float64).reshape(-1)
+        X, U = x[:, :N - 1].T, u[:, :N - 1].T
+        A, B = plant.integrator_batch(X, U, dt, return_gradient=True)
+        xkp1 = plant.integrator_batch(X, U, dt)
+        con = self.other_constraints
+        nz = n * (N - 1) + nx
+        n_other = con.total_hard_constraints(x, u)
+        G = np.zeros((nz, nz))
+        g = np.zeros((nz, 1))
+        C = np.zeros((nx * N + n_other, nz))
+        c = np.zeros((nx * N + n_other, 1))
+        ci, si = 0, 0
+        C[ci:ci + nx, si:si + nx] = np.eye(nx)
+        c[ci:ci + nx, 0] = x[:, 0] - xs
+        ci += nx
+        for k in range(N - 1):
+            G[si:si + n, si:si + n] = self.cost.hessian(x[:, k], u[:, k], k)
+            g[si:si + n, 0] = self.cost.gradient(x[:, k], u[:, k], k)
+            if con.total_soft_constraints(timestep=k) > 0:
+                gck = con.jacobian_soft_constraints(x[:, k], u[:, k], k)
+                g[si:si + n, :] = g[si:si + n, :] + gck
+                G[si:si + n, si:si + n] += np.outer(gck, gck)
+            C[ci:ci + nx, si:si + n + nx] = np.hstack((-A[k], -B[k], np.eye(nx)))
+            c[ci:ci + nx, 0] = x[:, k + 1] - xkp1[k]
+            ci += nx
+            if n_other > 0 and con.total_hard_constraints(x, u, k):
+                jac = con.jacobian_hard_constraints(x[:, k], u[:, k], k)
+                val = con.value_hard_constraints(x[:, k], u[:, k], k)
+                if val is not None and len(val):
+                    m = len(val)
+                    C[ci:ci + m, si:si + n] = np.reshape(jac, (m, n))
+                    c[ci:ci + m] = np.reshape(val, (m, 1))
+                    ci += m
+            si += n
+        G[si:si + nx, si:si + nx] = self.cost.hessian(x[:, N - 1], timestep=N - 1)
+        g[si:si + nx, 0] = self.cost.gradient(x[:, N - 1], timestep=N - 1)
+        if con.total_soft_constraints(timestep=N - 1) > 0:
+            gc = con.jacobian_soft_constraints(x[:, N - 1], timestep=N - 1)
+            g[si:si + nx, :] = g[si:si + nx, :] + gc
+            G[si:si + nx, si:si + nx] = G[si:si + nx, si:si + nx] + np.outer(gc, gc)
+        if n_other > 0 and con.total_hard_constraints(x, u, N - 1):
+            jac = con.jacobian_hard_constraints(x[:, N - 1], timestep=N - 1)
+            val = con.value_hard_constraints(x[:, N - 1], timestep=N - 1)
+            if val is not None and len(val):
+                m = len(val)
+                C[ci:ci + m, si:si + nx] = np.reshape(jac, (m, nx))
+                c[ci:ci + m] = np.reshape(val, (m, 1))
+        return G, g, C, c
+
+    def totalHardConstraintViolation(self, x, u, xs, N: int, dt: float, mode=None):
+        """totalHardConstraintViolation (:273-294): |x_0 - xs|_1 + sum_k |x_{k+1} - f(x_k, u_k)|_1 (+ the hard
+        limits' |values|), each term summed as the reference sums it; mode "MAX" takes max instead of sum.
+        f of all knots is one GPU launch."""
+        plant = self._gpu_plant()
+        mode_func = max if mode == "MAX" else sum
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        xs = np.asarray(xs, dtype=np.float64).reshape(-1)
+        xkp1 = plant.integrator_batch(x[:, :N - 1].T, u[:, :N - 1].T, dt)
+        c = mode_func(list(map(abs, x[:, 0] - xs)))
+        for k in range(N - 1):
+            c = c + mode_func(list(map(abs, x[:, k + 1] - xkp1[k])))
+        con = self.other_constraints
+        if con.total_hard_constraints(x, u) > 0:
+            for k in range(N - 1):
+                if con.total_hard_constraints(x, u, k):
+                    c = c + mode_func(list(map(abs, con.value_hard_constraints(x[:, k], u[:, k], k))))
+            if con.total_hard_constraints(x, u, N - 1):
+                # the reference passes N - 1 as uk here (:292), which value_hard_constraints then ignores for
+                # the terminal knot's state limits
+                c = c + mode_func(list(map(abs, con.value_hard_constraints(x[:, N - 1], timestep=N - 1))))
+        return c
+
+    def totalCost(self, x, u, N: int):
+        """totalCost (:296-310): sum of the cost hook over the knots (terminal: u = None), plus the soft
+        limits' values, in the reference's order."""
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        J = 0
+        for k in range(N - 1):
+            J = J + self.cost.value(x[:, k], u[:, k], k)
+        J = J + self.cost.value(x[:, N - 1], timestep=N - 1)
+        con = self.other_constraints
+        if con.total_soft_constraints() > 0:
+            for k in range(N - 1):
+                J = J + con.value_soft_constraints(x[:, k], u[:, k], k)
+            J = J + con.value_soft_constraints(x[:, N - 1], timestep=N - 1)
+        return J
+
+    def _qp(self, x, u, xs, N, dt, rho, method, options):
+        """One QP on the GPU (tmpc_qp_batch) -> the reference's dxul column [dxu; lambda], lambda in the
+        reference's row order (initial state, then per knot its dynamics rows and its active hard rows).
+        options are the reference's linear-system options (solveKKTSystem_Schur passes PCG's keys:
+        exit_tolerance, max_iter, preconditioner_type, guess -- PCG.py:19-25, :439-440); the caller's dict
+        is not modified."""
+        opts = dict(options)
+        self.set_default_options(opts)
+        if "exit_tolerance" in opts:
+            opts["exit_tolerance_linSys"] = opts["exit_tolerance"]
+        if "max_iter" in opts:
+            opts["max_iter_linSys"] = opts["max_iter"]
+        ctx = self._context(opts)
+        nx, nu = self._dims()
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        xs = np.asarray(xs, dtype=np.float64).reshape(1, -1)
         self._check_xu(x[None], u[None], N)
-        # options['guess'] -> PCG.update_guess (:439-440): the PCG's initial iterate
-        guess = options.get("guess")
-        if guess is not None:
+        guess = opts.get("guess") if method.startswith("PCG") else None
+        if guess is not None:   # options['guess'] -> PCG.update_guess (:439-440)
             guess = np.asarray(guess, dtype=np.float64).reshape(1, -1)
-            if guess.shape[1] != N * x.shape[0]:
-                raise ValueError(f"options['guess'] must have N * nx = {N * x.shape[0]} entries, got {guess.shape[1]}")
-        r = ctx.qp_batch(x[None], u[None], N, dt, rho, method, want_blocks=False, guess=guess if use_PCG else None,
-                         xs=xs)
+            if guess.shape[1] != N * nx:
+                raise ValueError(f"options['guess'] must have N * nx = {N * nx} entries, got {guess.shape[1]}")
+        con = self.other_constraints
+        if any(c.is_soft_constraint_mode() for _, c in con.limits()):   # the objects' current mu / lambda
+            ctx.set_soft_state(1, N, *[a[None] for a in con.pack_state(N)])
+        r = ctx.qp_batch(x[None], u[None], N, dt, rho, method, want_blocks=False, guess=guess, xs=xs)
         self.n_inner_iter = int(r["pcg_iters"][0])
-        return r["dxul"][0].reshape(-1, 1)
+        dxul = r["dxul"][0]
+        if not any(c.is_hard_constraint_mode() for _, c in con.limits()):
+            return dxul.reshape(-1, 1)
+        info = ctx.qp_hard_info(1, N)
+        if int(info["singular"][0]):
+            self.singular = True
+        nz = (nx + nu) * (N - 1) + nx
+        lam_dyn = dxul[nz:].reshape(N, nx)
+        lam_h = info["lambda_hard"][0]
+        n = nx // 2
+        lam = [lam_dyn[0]]
+        for k in range(N):
+            if k < N - 1:
+                lam.append(lam_dyn[k + 1])
+            slots = []
+            for kind, cobj, z in con._hard_slices(x[:, k], u[:, k] if k < N - 1 else None,
+                                                  k if k < N - 1 else N - 1):
+                t = {"joint_limits": 0, "velocity_limits": 1, "torque_limits": 2}[kind]
+                v = cobj.full_value(z)
+                for e in range(2 * cobj.constraint_size):
+                    if cobj.mode == "FULL_SET" or v[e] < 0:
+                        slots.append(t * 2 * n + e)
+            lam.append(lam_h[k, slots])
+        return np.concatenate([dxul[:nz]] + lam).reshape(-1, 1)
+
+    def solveKKTSystem(self, x, u, xs, N: int, dt: float, rho: float = 0.0, options=NO_OPTIONS):
+        """solveKKTSystem (:313-359): the dense KKT [G + rho I, C^T; C, 0] dxul = [g; c].  Its solution is
+        the Schur complement's, so the GPU solves it blockwise by the direct path (method N: block-Thomas,
+        or the banded elimination with hard limits) with the reference's least-squares fallback for a
+        singular system (self.singular)."""
+        return self._qp(x, u, xs, N, dt, rho, "N", fresh(options))
+
+    def solveKKTSystem_Schur(self, x, u, xs, N: int, dt: float, rho: float = 0.0, use_PCG=False, options=NO_OPTIONS):
+        """solveKKTSystem_Schur (:361-455): S = -C G^-1 C^T, gamma = c - C G^-1 g, lambda by the direct solve
+        (use_PCG False, the reference's default) or PCG with options['preconditioner_type'] (default BJ,
+        PCG.py:24) and options['guess'] as the initial iterate; dxu = G^-1 (g - C^T lambda)."""
+        options = fresh(options)
+        method = "PCG-" + options.get("preconditioner_type", "BJ") if use_PCG else "S"
+        return self._qp(x, u, xs, N, dt, rho, method, options)
+
+    def reduce_regularization(self, rho: float, drho: float, options: dict):
+        """reduce_regularization (:457-461)."""
+        self.set_default_options(options)
+        drho = min(drho / options["rho_factor_SQP_DDP"], 1 / options["rho_factor_SQP_DDP"])
+        rho = max(rho * drho, options["rho_min_SQP_DDP"])
+        return rho, drho
+
+    def check_for_exit_or_error(self, error: bool, delta_J: float, iteration: int, rho: float, drho: float, options):
+        """check_for_exit_or_error (:463-481): the error branch raises rho (exit 2 past rho_max), a cost
+        decrease below the tolerance exits 1 (signed: any increase exits too), the last iteration exits 3."""
+        self.set_default_options(options)
+        exit_flag = False
+        if error:
+            drho = max(drho * options["rho_factor_SQP_DDP"], options["rho_factor_SQP_DDP"])
+            rho = max(rho * drho, options["rho_min_SQP_DDP"])
+            if rho > options["rho_max_SQP_DDP"]:
+                self.exit_sqp = 2
+                exit_flag = True
+        elif delta_J < options["exit_tolerance_SQP_DDP"]:
+            self.exit_sqp = 1
+            exit_flag = True
+        if iteration == options["max_iter_SQP_DDP"] - 1:
+            self.exit_sqp = 3
+            exit_flag = True
+        else:
+            iteration += 1
+        return exit_flag, iteration, rho, drho
+
+    def check_and_update_soft_constraints(self, x, u, iteration: int, options):
+        """check_and_update_soft_constraints (:483-508): exit_soft 1 (converged), 2 (max outer passes),
+        3 (every violated mu at its cap), else the AL update of the constraint objects' constants."""
+        exit_flag = False
+        if self.other_constraints.max_soft_constraint_value(x, u) < options["exit_tolerance_softConstraints"]:
+            self.exit_soft = 1
+            exit_flag = True
+        if iteration == options["max_iter_softConstraints"] - 1:
+            self.exit_soft = 2
+            exit_flag = True
+        else:
+            iteration += 1
+        if not exit_flag:
+            if self.other_constraints.update_soft_constraint_constants(x, u):
+                self.exit_soft = 3
+                exit_flag = True
+        return exit_flag, iteration
