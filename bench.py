@@ -9,10 +9,14 @@ every problem's exit) of B independent problems of the §8d workload:
 Inputs are resident in HBM before the timed region (each step restores the
 initial trajectories with a device-to-device copy, inside the timed region).
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N,
-or any launcher that sets RANK / WORLD_SIZE / LOCAL_RANK): one process per GPU,
-rank r solves global problems [r B, (r+1) B) -- independent problems, no
-collective inside a solve, weak scaling.  RCCL over xGMI through libtmpc's
+Multi-GPU: `python bench.py --gpus N` starts the N ranks itself (one child
+process per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
+set; the parent touches no GPU, prints rank 0's line and fails if any rank
+fails); under a launcher that sets those variables (python -m
+torch.distributed.run --nproc-per-node N bench.py --gpus N) each process is one
+rank and WORLD_SIZE must equal --gpus.  Rank r solves global problems
+[r B, (r+1) B) -- independent problems, no collective inside a solve, weak
+scaling.  RCCL over xGMI through libtmpc's
 tmpc_comm_* C ABI (trajoptmpcreference_amd/dist.py; no PyTorch) broadcasts the
 initial states from rank 0, times the region with a barrier and the max over
 ranks, and gathers every problem's exit code / iteration count to rank 0.
@@ -324,8 +328,81 @@ def gm_roofline(a, N, nx, qp, per_launch_iters, per_launch_qps, traffic, src):
     return out
 
 
+def _free_port_pair():
+    """A free TCP port P with P + 1 free too (P: MASTER_PORT; P + 1: the RCCL id exchange, dist.py)."""
+    import socket
+    for _ in range(64):
+        with socket.socket() as s0:
+            s0.bind(("127.0.0.1", 0))
+            p = s0.getsockname()[1]
+            if p >= 65535:
+                continue
+            try:
+                with socket.socket() as s1:
+                    s1.bind(("127.0.0.1", p + 1))
+                return p
+            except OSError:
+                continue
+    raise RuntimeError("no free port pair for the rank rendezvous")
+
+
+def launch_ranks(a, argv):
+    """--gpus N > 1 with no launcher: one child process per GPU (rank r on GPU r), this process touching no
+    GPU.  Rank 0's stdout (the JSON line) is forwarded; the exit status is non-zero if any rank fails (the
+    others are then stopped)."""
+    import subprocess
+    import tempfile
+    port = _free_port_pair()
+    procs = []
+    with tempfile.TemporaryFile(mode="w+") as out0:
+        for r in range(a.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                       LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                          stdout=out0 if r == 0 else subprocess.DEVNULL))
+        rcs = [None] * len(procs)
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+            if any(rc not in (None, 0) for rc in rcs):   # a rank failed: stop the others, fail
+                for r, p in enumerate(procs):
+                    if rcs[r] is None:
+                        p.kill()
+                        rcs[r] = p.wait()
+                        rcs[r] = rcs[r] if rcs[r] else -9
+                break
+            time.sleep(0.2)
+        out0.seek(0)
+        sys.stdout.write(out0.read())
+        sys.stdout.flush()
+    bad = [r for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        print(f"bench.py: ranks {bad} failed (exit codes {[rcs[r] for r in bad]})", file=sys.stderr)
+        return 1
+    return 0
+
+
+def _standin():
+    """TMPC_BENCH_STANDIN=<path>: a test stand-in module (tests/bench_standin.py) supplying Context and
+    make_comm, so the CPU test suite can run the multi-rank launch path without a GPU.  Never set by the
+    driver's runs: unset, the bench runs libtmpc (and fails without a GPU)."""
+    path = os.environ.get("TMPC_BENCH_STANDIN")
+    if not path:
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("tmpc_bench_standin", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != a.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {a.gpus}: pass the same N")
     from trajoptmpcreference_amd import _native, dist
     from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
 
@@ -333,11 +410,12 @@ def main():
     n, N, B, dt = a.links, a.N, a.batch, 0.1
     nx, nu = 2 * n, n
     model = parse_urdf(planar_arm_urdf(n))
-    ctx = _native.Context(local_rank)
+    standin = _standin()
+    ctx = standin.Context(local_rank) if standin else _native.Context(local_rank)
     # every rank must run the same configuration: its hash rides on the RCCL id exchange (dist.py)
     cfg = dist.config_hash({k: v for k, v in sorted(vars(a).items()) if k != "cpu_procs"}, model.X0, model.Xa,
                            model.Xb, model.I, np.asarray(model.parent), bytes(ctx.options))
-    comm = dist.make_comm(ctx, rank, world, cfg)
+    comm = standin.make_comm(ctx, rank, world, cfg) if standin else dist.make_comm(ctx, rank, world, cfg)
     ctx.set_model(model)
     if a.cost == "ee":
         if n != 2:

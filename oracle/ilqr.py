@@ -72,10 +72,48 @@ def derivatives(cost, x, u, N, soft=None):
     return lx, lu, lxx, luu
 
 
-def backward(A, B, lx, lu, lxx, luu, rho, solve="cholesky"):
-    """Riccati sweep; returns (K, d, dV1, dV2, ok).  solve = "lu" solves for [K | d] with
-    np.linalg.solve instead of the Cholesky factor: the same algorithm with different
-    rounding, used by the tests to tell rounding-sensitive problems from real mismatches."""
+def chol_solve(Quu, rhs):
+    """[K | d] = Q_uu^-1 rhs in ONE canonical order -- the GPU's (k_ilqr_backward, tmpc_ilqr.hip):
+    LAPACK dpotf2's Cholesky Q_uu = L L^T with the column below each pivot scaled by the pivot's
+    reciprocal (numpy.linalg.cholesky's form), then per right-hand-side column the forward and back
+    substitutions, each sum sequential in m and scaled by the same reciprocal.  Returns None when Q_uu
+    is not positive definite (a pivot <= 0: the backward pass fails, as LinAlgError does).  The GPU
+    contracts each update into a fused multiply-add; the integers (exit codes, iteration and line-search
+    counts, alpha paths) of every tested workload are identical to this restatement's."""
+    n = Quu.shape[0]
+    L = np.zeros((n, n))
+    ri = np.zeros(n)
+    for j in range(n):
+        s = Quu[j, j]
+        for m in range(j):
+            s = s - L[j, m] * L[j, m]
+        if not s > 0:
+            return None
+        L[j, j] = np.sqrt(s)
+        ri[j] = 1.0 / L[j, j]
+        for i in range(j + 1, n):
+            v = Quu[i, j]
+            for m in range(j):
+                v = v - L[i, m] * L[j, m]
+            L[i, j] = v * ri[j]
+    y = np.array(rhs, dtype=np.float64, copy=True)
+    for i in range(n):                       # L y = rhs (all columns at once, the same order per column)
+        v = y[i].copy()
+        for m in range(i):
+            v = v - L[i, m] * y[m]
+        y[i] = v * ri[i]
+    for i in range(n - 1, -1, -1):           # L^T z = y
+        v = y[i].copy()
+        for m in range(i + 1, n):
+            v = v - L[m, i] * y[m]
+        y[i] = v * ri[i]
+    return y
+
+
+def backward(A, B, lx, lu, lxx, luu, rho, solve="canonical"):
+    """Riccati sweep; returns (K, d, dV1, dV2, ok).  [K | d] by chol_solve (the one canonical order the
+    GPU follows); solve = "lu" (np.linalg.solve) and "numpy-cholesky" (np.linalg.cholesky + two
+    np.linalg.solve) are kept only for the history of tests/golden/make_oracle_fixtures.py."""
     N = len(lx)
     nu = lu[0].shape[0]
     Vx = lx[N - 1].copy()
@@ -90,12 +128,18 @@ def backward(A, B, lx, lu, lxx, luu, rho, solve="cholesky"):
         Qxx = lxx[k] + Ak.T @ (Vxx @ Ak)
         Quu = luu[k] + Bk.T @ (Vxx @ Bk) + rho * np.eye(nu)
         Qux = Bk.T @ (Vxx @ Ak)
-        try:
-            L = np.linalg.cholesky(Quu)
-        except np.linalg.LinAlgError:
-            return None, None, 0.0, 0.0, False
         rhs = np.hstack([Qux, Qu[:, None]])
-        sol = np.linalg.solve(L.T, np.linalg.solve(L, rhs)) if solve == "cholesky" else np.linalg.solve(Quu, rhs)
+        if solve == "canonical":
+            sol = chol_solve(Quu, rhs)
+            if sol is None:
+                return None, None, 0.0, 0.0, False
+        else:
+            try:
+                L = np.linalg.cholesky(Quu)
+            except np.linalg.LinAlgError:
+                return None, None, 0.0, 0.0, False
+            sol = np.linalg.solve(L.T, np.linalg.solve(L, rhs)) if solve == "numpy-cholesky" else \
+                np.linalg.solve(Quu, rhs)
         K[k] = -sol[:, :-1]
         d[k] = -sol[:, -1]
         dV1 += d[k] @ Qu
@@ -117,7 +161,39 @@ def forward(model, x, u, K, d, alpha, dt):
     return xn, un
 
 
-def ilqr(model, cost, x, u, N, dt, options=None, soft=None, solve="cholesky"):
+def step(model, cost, x, u, N, dt, rho, J, o, soft=None, solve="canonical"):
+    """One iLQR iteration from the iterate (x, u) with cost J and regularisation rho: backward sweep, then
+    the line search alpha = 1, f, f^2, ... until the ratio test accepts or alpha <= alpha_min.  Returns
+    dict(x, u, J, error, delta_J, succeeded, ls, alpha, ratio, dV1, trials) -- the new iterate on acceptance,
+    the old one otherwise (error: Q_uu not positive definite, or no alpha accepted); trials lists each
+    line-search trial's (alpha, J_new, ratio)."""
+    A, B = rbd.euler_gradient(model, x[:, :N - 1].T, u.T, dt)
+    lx, lu, lxx, luu = derivatives(cost, x, u, N, soft)
+    K, d, dV1, dV2, ok = backward(A, B, lx, lu, lxx, luu, rho, solve)
+    if not ok:
+        return dict(x=x, u=u, J=J, error=True, delta_J=0.0, succeeded=False, ls=0, alpha=0.0, ratio=None, dV1=None,
+                    trials=[])
+    alpha, ls = 1, 0
+    trials = []
+    while True:
+        xn, un = forward(model, x, u, K, d, alpha, dt)
+        J_new = total_cost(cost, xn, un, N, soft)
+        delta_J = J - J_new
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = np.float64(delta_J) / np.float64(-alpha * (dV1 + alpha * dV2))
+        trials.append((alpha, J_new, ratio))
+        if ratio >= o["expected_reduction_min_SQP_DDP"] and ratio <= o["expected_reduction_max_SQP_DDP"]:
+            return dict(x=xn, u=un, J=J_new, error=False, delta_J=delta_J, succeeded=True, ls=ls, alpha=alpha,
+                        ratio=ratio, dV1=dV1, trials=trials)
+        if alpha > o["alpha_min_SQP_DDP"]:
+            alpha *= o["alpha_factor_SQP_DDP"]
+            ls += 1
+        else:
+            return dict(x=x, u=u, J=J, error=True, delta_J=delta_J, succeeded=False, ls=ls, alpha=alpha,
+                        ratio=ratio, dV1=dV1, trials=trials)
+
+
+def ilqr(model, cost, x, u, N, dt, options=None, soft=None, solve="canonical"):
     """Returns dict(x, u, exit_code, exit_soft, outer_iter, iter, trace)."""
     o = default_options(options)
     x = rollout(model, np.array(x, dtype=float)[:, 0], np.array(u, dtype=float), dt)
@@ -133,38 +209,14 @@ def ilqr(model, cost, x, u, N, dt, options=None, soft=None, solve="cholesky"):
         it = 0
         exit_code = 0
         while True:
-            A, B = rbd.euler_gradient(model, x[:, :N - 1].T, u.T, dt)
-            lx, lu, lxx, luu = derivatives(cost, x, u, N, soft)
-            K, d, dV1, dV2, ok = backward(A, B, lx, lu, lxx, luu, rho, solve)
-            error = not ok
-            delta_J = 0.0
-            if ok:
-                alpha = 1
-                ls = 0
-                while True:
-                    xn, un = forward(model, x, u, K, d, alpha, dt)
-                    J_new = total_cost(cost, xn, un, N, soft)
-                    delta_J = J - J_new
-                    with np.errstate(divide="ignore", invalid="ignore"):
-                        ratio = np.float64(delta_J) / np.float64(-alpha * (dV1 + alpha * dV2))
-                    if ratio >= o["expected_reduction_min_SQP_DDP"] and ratio <= o["expected_reduction_max_SQP_DDP"]:
-                        x, u, J = xn, un, J_new
-                        drho = min(drho / o["rho_factor_SQP_DDP"], 1 / o["rho_factor_SQP_DDP"])
-                        rho = max(rho * drho, o["rho_min_SQP_DDP"])
-                        trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=ls, alpha=alpha,
-                                          rho=rho, J=J, dV1=dV1, reduction_ratio=ratio, succeeded_line_search=True))
-                        break
-                    elif alpha > o["alpha_min_SQP_DDP"]:
-                        alpha *= o["alpha_factor_SQP_DDP"]
-                        ls += 1
-                    else:
-                        error = True
-                        trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=ls, alpha=alpha,
-                                          rho=rho, J=J, dV1=dV1, reduction_ratio=ratio, succeeded_line_search=False))
-                        break
-            else:
-                trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=0, alpha=0.0, rho=rho,
-                                  J=J, dV1=None, reduction_ratio=None, succeeded_line_search=False))
+            st = step(model, cost, x, u, N, dt, rho, J, o, soft, solve)
+            x, u, J, error, delta_J = st["x"], st["u"], st["J"], st["error"], st["delta_J"]
+            if st["succeeded"]:
+                drho = min(drho / o["rho_factor_SQP_DDP"], 1 / o["rho_factor_SQP_DDP"])
+                rho = max(rho * drho, o["rho_min_SQP_DDP"])
+            trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=st["ls"],
+                              alpha=st["alpha"], rho=rho, J=J, dV1=st["dV1"], reduction_ratio=st["ratio"],
+                              succeeded_line_search=st["succeeded"]))
             exit_flag = False
             if error:
                 drho = max(drho * o["rho_factor_SQP_DDP"], o["rho_factor_SQP_DDP"])

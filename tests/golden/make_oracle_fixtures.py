@@ -133,22 +133,21 @@ def main():
     pool = mp.get_context("fork").Pool(a.procs)
     if a.only in (None, "config3"):
         t = time.time()
-        jobs = [(C3["seed0"] + i, s) for i in range(C3["B"]) for s in ("cholesky", "lu")]
-        res = pool.map(job_config3, jobs, chunksize=1)
+        # one restatement: the [K | d] solve in the GPU's canonical order (oracle/ilqr.py chol_solve)
+        jobs = [(C3["seed0"] + i, "canonical") for i in range(C3["B"])]
+        rs = pool.map(job_config3, jobs, chunksize=1)
         rec = {"N": C3["N"], "seeds": np.arange(C3["seed0"], C3["seed0"] + C3["B"]), "lb": C3["lb"], "ub": C3["ub"],
                "max_iter_softConstraints": C3["opts"]["max_iter_softConstraints"],
                "max_iter_SQP_DDP": C3["opts"]["max_iter_SQP_DDP"]}
-        for v, s in enumerate(("cholesky", "lu")):
-            rs = [r for r in res if r["solve"] == s]
-            for k in ("exit_code", "iter", "exit_soft", "outer_iter", "J"):
-                rec[f"{k}_{v}"] = np.array([r[k] for r in rs])
-            for k in ("x", "u", "mu"):
-                rec[f"{k}_{v}"] = np.array([r[k] for r in rs])
-            W = max(len(r["alpha"]) for r in rs)
-            rec[f"alpha_{v}"] = np.array([r["alpha"] + [np.nan] * (W - len(r["alpha"])) for r in rs])
+        for k in ("exit_code", "iter", "exit_soft", "outer_iter", "J"):
+            rec[k] = np.array([r[k] for r in rs])
+        for k in ("x", "u", "mu"):
+            rec[k] = np.array([r[k] for r in rs])
+        W = max(len(r["alpha"]) for r in rs)
+        rec["alpha"] = np.array([r["alpha"] + [np.nan] * (W - len(r["alpha"])) for r in rs])
         np.savez_compressed(os.path.join(OUT, "oracle_config3_arm6_N64_ilqr_al.npz"), **rec)
-        print(f"[oracle] config3: {time.time() - t:.0f} s; chol (exit, iter, soft, outer) "
-              f"{list(zip(rec['exit_code_0'], rec['iter_0'], rec['exit_soft_0'], rec['outer_iter_0']))}", flush=True)
+        print(f"[oracle] config3: {time.time() - t:.0f} s; (exit, iter, soft, outer) "
+              f"{list(zip(rec['exit_code'], rec['iter'], rec['exit_soft'], rec['outer_iter']))}", flush=True)
     if a.only in (None, "config4"):
         t = time.time()
         res = pool.map(job_config4, [C4["seed0"] + i for i in range(C4["B"])], chunksize=1)
@@ -164,16 +163,13 @@ def main():
               f"{list(zip(rec['exit_sqp'], rec['sqp_iter'], rec['exit_soft'], rec['outer_iter']))}", flush=True)
     if a.only in (None, "config5"):
         t = time.time()
-        jobs = [(C5["seed0"] + i, s) for i in range(C5["B"]) for s in ("cholesky", "lu")]
-        res = pool.map(job_config5, jobs, chunksize=1)
+        jobs = [(C5["seed0"] + i, "canonical") for i in range(C5["B"])]
+        rs = pool.map(job_config5, jobs, chunksize=1)
         rec = {"N": C5["N"], "steps": C5["steps"], "seeds": np.arange(C5["seed0"], C5["seed0"] + C5["B"])}
-        for v, s in enumerate(("cholesky", "lu")):
-            rs = [r for r in res if r["solve"] == s]
-            for k in ("exit_codes", "iters", "x_exec", "u_exec"):
-                rec[f"{k}_{v}"] = np.array([r[k] for r in rs])
+        for k in ("exit_codes", "iters", "x_exec", "u_exec"):
+            rec[k] = np.array([r[k] for r in rs])
         np.savez_compressed(os.path.join(OUT, "oracle_config5_arm6_N128_mpc_ilqr.npz"), **rec)
-        print(f"[oracle] config5: {time.time() - t:.0f} s; chol iters {rec['iters_0'].tolist()} "
-              f"lu {rec['iters_1'].tolist()}", flush=True)
+        print(f"[oracle] config5: {time.time() - t:.0f} s; iters {rec['iters'].tolist()}", flush=True)
     if a.only in (None, "sqp128"):
         t = time.time()
         res = pool.map(job_sqp128, [C5S["seed0"] + i for i in range(C5S["B"])], chunksize=1)

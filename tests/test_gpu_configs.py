@@ -7,9 +7,9 @@ tests/golden/make_oracle_fixtures.py and are compared here:
   config 4  arm6 N=64 SQP PCG-SS, torque + joint limits by augmented Lagrangian, 8 problems
   config 5  arm6 N=128 receding-horizon MPC loop (iLQR horizon solves), 2 problems x 3 steps
 Integer outputs must be identical (exit codes, iteration counts, outer passes, per-QP PCG
-counts, line-search alpha paths); iLQR may match either of the oracle's two [K | d] solves
-(test_gpu_ilqr.py explains why); trajectories within 1e-6 relative (1e-5 for iLQR + AL, whose
-two CPU restatements already differ by 4e-7)."""
+counts, line-search alpha paths) to the one oracle restatement (iLQR: the [K | d] solve in the
+GPU's canonical order, oracle/ilqr.py chol_solve); trajectories within 1e-6 relative (1e-5 for
+iLQR + AL: its sweeps amplify rounding along the horizon, test_gpu_ilqr.py)."""
 import numpy as np
 import pytest
 
@@ -51,16 +51,14 @@ def test_config3_ilqr_augmented_lagrangian_arm6_n64():
     mu = r["soft_state"][0]
     for i in range(len(d["seeds"])):
         got = (int(r["exit_code"][i]), int(r["iter"][i]), int(r["exit_soft"][i]), int(r["outer_iter"][i]))
-        ok = [v for v in (0, 1) if got == (int(d[f"exit_code_{v}"][i]), int(d[f"iter_{v}"][i]),
-                                           int(d[f"exit_soft_{v}"][i]), int(d[f"outer_iter_{v}"][i]))]
-        assert ok, (i, got)
-        v = ok[0]
-        al = d[f"alpha_{v}"][i]
+        assert got == (int(d["exit_code"][i]), int(d["iter"][i]), int(d["exit_soft"][i]),
+                       int(d["outer_iter"][i])), (i, got)
+        al = d["alpha"][i]
         al = list(al[~np.isnan(al)])
         assert list(r["trace"]["alpha"][i, 1:len(al) + 1]) == al, i
-        assert _rel(r["x"][i], d[f"x_{v}"][i]) < 1e-5, i
-        assert _rel(r["u"][i], d[f"u_{v}"][i]) < 1e-5, i
-        assert np.array_equal(mu[i, :N - 1, 24:36].T, d[f"mu_{v}"][i]), i
+        assert _rel(r["x"][i], d["x"][i]) < 1e-5, i
+        assert _rel(r["u"][i], d["u"][i]) < 1e-5, i
+        assert np.array_equal(mu[i, :N - 1, 24:36].T, d["mu"][i]), i
 
 
 def test_config4_sqp_pcg_torque_and_joint_limits_arm6_n64():
@@ -92,8 +90,6 @@ def test_config5_mpc_loop_arm6_n128():
     r = solver.MPC_batch(x, u, N, 0.1, "iLQR", {}, mpc_steps=steps)
     for i in range(len(d["seeds"])):
         got = (list(r["exit_codes"][i]), list(r["iters"][i]))
-        ok = [v for v in (0, 1) if got == (list(d[f"exit_codes_{v}"][i]), list(d[f"iters_{v}"][i]))]
-        assert ok, (i, got)
-        v = ok[0]
-        assert np.allclose(r["x_exec"][i], d[f"x_exec_{v}"][i], rtol=1e-6, atol=1e-8), i
-        assert np.allclose(r["u_exec"][i], d[f"u_exec_{v}"][i], rtol=1e-6, atol=1e-8), i
+        assert got == (list(d["exit_codes"][i]), list(d["iters"][i])), (i, got)
+        assert np.allclose(r["x_exec"][i], d["x_exec"][i], rtol=1e-6, atol=1e-8), i
+        assert np.allclose(r["u_exec"][i], d["u_exec"][i], rtol=1e-6, atol=1e-8), i

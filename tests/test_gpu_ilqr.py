@@ -3,18 +3,26 @@ drop-in against the oracle's restatement (oracle/ilqr.py).
 
 The reference has no iLQR, so parity is against this build's own
 definition ("parity unpinned" w.r.t. the reference); the dynamics, cost and
-soft-limit hooks it consumes are pinned (test_oracle_golden.py).  Integer
-outputs -- exit code, iteration count, line-search iteration and the alpha
-path -- must be identical; final trajectories within 1e-6 relative and the
-final J within 1e-8.  Intermediate J values are not compared: two equally
-valid CPU restatements (Cholesky vs LU solve for [K | d]) already differ by up
-to 3e-4 in intermediate iLQR costs of arm6 N=64 while their final iterates
-agree to 1e-13 (measured on seeds 500-505); where even their integer outputs
-differ (a ratio test of two ~1e-12 decreases at convergence, e.g. arm3 seed
-515: (1, 6) vs (2, 9)) the GPU must match one of the two.  With the augmented
-Lagrangian at mu ~ 1e7 (10 outer passes) even the iteration counts of the two
-CPU restatements diverge, so the soft-limit case runs 4 outer passes (where
-they agree exactly).
+soft-limit hooks it consumes are pinned (test_oracle_golden.py).  ONE
+restatement: the [K | d] solve in the GPU's canonical order (oracle/ilqr.py
+chol_solve: dpotf2's reciprocal pivots, sequential substitutions).
+
+Integers are compared with no tolerance where the inputs are identical: every
+iteration of the GPU's own run is replayed at the GPU's own iterate (the same
+solve stopped after j iterations, rho_j from the trace's schedule) through the
+oracle's iteration (oracle/ilqr.py step), whose line-search count, alpha and
+acceptance must be the trace's; the exit code and iteration count must follow
+from those rows by check_for_exit_or_error's rules (TrajoptMPCReference.py:
+463-481).  The one exemption is a decision taken at the rounding floor of the
+cost: at convergence the ratio test compares two ~1e-15 decreases (arm3 seed
+515: the GPU accepts alpha = 1 with dJ = 1.8e-15, the oracle's trial from the
+same iterate rises by 2 ulp and is rejected), which only a bitwise restatement
+could reproduce; such a row must move the cost by less than 1e-12 of J in both
+runs.  The Riccati recursion amplifies rounding along the horizon: one sweep
+from identical iterates gives costs 2e-8 (arm6 N = 64) to 1.8e-4 (N = 128)
+apart, and two CPU orders of the same sweep reach intermediate costs 1e-2
+apart on arm6 seed 505 -- so whole runs are compared at convergence only: the
+final cost within 1e-7, trajectories within 1e-4.
 """
 import numpy as np
 import pytest
@@ -34,36 +42,120 @@ def _solver(n, N, spec=None):
     return TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(n)), con)
 
 
-def _oracle(m, cost, x, u, N, opts=None, soft_factory=None):
-    """The oracle run twice: Cholesky and LU solves for [K | d] (same algorithm, different
-    rounding).  Where the two disagree the problem is rounding-sensitive (its last steps
-    test a reduction ratio of two ~1e-12 numbers) and the GPU must match one of them."""
-    from oracle import ilqr as oilqr
-    runs = []
-    for solve in ("cholesky", "lu"):
-        soft = soft_factory() if soft_factory else (None, None)
-        runs.append((oilqr.ilqr(m, cost, x, u, N, 0.1, dict(opts or {}), soft[0], solve=solve), soft[1]))
-    return runs
-
-
 def _key(o):
     return (o["exit_code"], o["iter"], o["exit_soft"], o["outer_iter"])
 
 
-def _check(r, i, runs):
-    got = (int(r["exit_code"][i]), int(r["iter"][i]), int(r["exit_soft"][i]), int(r["outer_iter"][i]))
-    matches = [run for run in runs if _key(run[0]) == got]
-    assert matches, (i, got, [_key(run[0]) for run in runs])
-    o = matches[0][0]
-    tr = o["trace"]
-    rows = len(tr)
-    assert list(r["trace"]["alpha"][i, 1:rows]) == [t["alpha"] for t in tr[1:]]
-    assert list(r["trace"]["line_search_iteration"][i, 1:rows]) == [t["line_search_iteration"] for t in tr[1:]]
-    assert np.isclose(r["trace"]["J"][i, rows - 1], tr[-1]["J"], rtol=1e-8, atol=1e-12)
-    scale = max(1.0, float(np.max(np.abs(o["x"]))))
-    assert float(np.max(np.abs(r["x"][i] - o["x"]))) < 1e-6 * scale
-    scale = max(1.0, float(np.max(np.abs(o["u"]))))
-    assert float(np.max(np.abs(r["u"][i] - o["u"]))) < 1e-6 * scale
+def _rows(r, i):
+    return int(r["iter"][i]) + 1 + (int(r["exit_code"][i]) == 3)
+
+
+def _check_full(r, i, o):
+    """The converged solution against the oracle's full run (its exit code can differ where the last
+    decision is taken at the rounding floor of the cost: see _replay)."""
+    J = float(r["trace"]["J"][i, _rows(r, i) - 1])
+    assert abs(J - o["trace"][-1]["J"]) <= 1e-7 * max(1.0, abs(o["trace"][-1]["J"])), (i, J, o["trace"][-1]["J"])
+    for a, b in ((r["x"][i], o["x"]), (r["u"][i], o["u"])):
+        assert float(np.max(np.abs(a - b))) < 1e-4 * max(1.0, float(np.max(np.abs(b)))), i
+
+
+def _gpu_rollout(solver, x0s, u0s, N, dt=0.1):
+    """x = the device's rollout of u from x[:, :, 0] (tmpc_rollout_batch_device, the iLQR's start)."""
+    opts = {}
+    solver.set_default_options(opts)
+    ctx = solver._context(opts)
+    x = np.ascontiguousarray(x0s, dtype=np.float64).copy()
+    u = np.ascontiguousarray(u0s, dtype=np.float64)
+    dx, du = ctx.alloc(x.nbytes), ctx.alloc(u.nbytes)
+    try:
+        ctx.h2d(dx, x)
+        ctx.h2d(du, u)
+        ctx.rollout_device(x.shape[0], N, dt, dx, du)
+        ctx.d2h(x, dx)
+        ctx.synchronize()
+    finally:
+        ctx.free(dx)
+        ctx.free(du)
+    return x
+
+
+def _replay(solver, r, m, cost, x0s, u0s, N, opts=None, dt=0.1):
+    """Every iteration of the GPU's own run, from the GPU's own iterate, through the oracle's iteration:
+    identical line-search count, alpha and acceptance, except where the decision is taken at the rounding
+    floor of the cost (both runs' trial costs within 1e-12 of J: a reduction ratio of two ~1e-15 numbers at
+    convergence, which no restatement short of a bitwise one reproduces); the accepted cost within 1e-3
+    (the sweep's own rounding amplification); and the GPU's exit code / iteration count as
+    check_for_exit_or_error (:463-481) derives them from those rows.  Returns the floor-decided rows."""
+    from oracle import ilqr as oilqr
+    from oracle import sqp as osqp
+    o = osqp.default_options(opts)
+    B = x0s.shape[0]
+    rows = [_rows(r, i) for i in range(B)]
+    t = r["trace"]
+    floor_rows = []
+    f = float(o["rho_factor_SQP_DDP"])
+    for j in range(max(rows) - 1):
+        live = [i for i in range(B) if j + 1 < rows[i]]
+        if j == 0:   # iteration 0 starts from the GPU's rollout of u0 (the solver replaces x by it)
+            xj, uj = list(_gpu_rollout(solver, x0s, u0s, N, dt)), list(u0s)
+        else:
+            rj = solver.iLQR_batch(x0s, u0s, N, dt, dict(opts or {}, max_iter_SQP_DDP=j))
+            xj, uj = list(rj["x"]), list(rj["u"])
+        for i in live:
+            rho, drho = o["rho_init_SQP_DDP"], 1.0
+            for q in range(j):   # rho before iteration j (the trace's schedule, oracle/ilqr.py)
+                if t["succeeded_line_search"][i, q + 1]:
+                    drho = min(drho / f, 1.0 / f)
+                else:
+                    drho = max(drho * f, f)
+                rho = max(rho * drho, o["rho_min_SQP_DDP"])
+            J = float(t["J"][i, j])
+            with np.errstate(all="ignore"):
+                st = oilqr.step(m, cost, xj[i], uj[i], N, dt, rho, J, o)
+            row = j + 1
+            same = (int(t["line_search_iteration"][i, row]), float(t["alpha"][i, row]),
+                    bool(t["succeeded_line_search"][i, row])) == (st["ls"], st["alpha"], st["succeeded"])
+            if not same:
+                # only at the rounding floor: the first trial whose outcome differs must change the cost by
+                # less than 1e-12 of J in the oracle's run, and the GPU's row by as little
+                floor = 1e-12 * max(1.0, abs(J))
+                ls_gpu = int(t["line_search_iteration"][i, row])
+                q = min(ls_gpu, len(st["trials"]) - 1)
+                assert abs(J - st["trials"][q][1]) <= floor, (i, j, "decision differs above the rounding floor",
+                                                              st["trials"][q], J)
+                assert abs(float(t["J"][i, row]) - J) <= floor, (i, j, float(t["J"][i, row]), J)
+                floor_rows.append((i, j))
+                continue
+            if st["succeeded"]:
+                # one sweep from identical iterates: the Riccati recursion amplifies rounding along the
+                # horizon (measured 2e-8 of J at arm6 N = 64, 1.8e-4 at N = 128 over one step)
+                assert abs(float(t["J"][i, row]) - st["J"]) <= 1e-3 * max(1.0, abs(st["J"])), (i, j)
+    for i in range(B):   # the exit rule on the GPU's own rows
+        it, code = 0, 0
+        rho, drho = o["rho_init_SQP_DDP"], 1.0
+        for q in range(1, rows[i]):
+            ok = bool(t["succeeded_line_search"][i, q])
+            if ok:
+                drho = min(drho / f, 1.0 / f)
+                rho = max(rho * drho, o["rho_min_SQP_DDP"])
+                dJ = float(t["J"][i, q - 1]) - float(t["J"][i, q])
+            stop = False
+            if not ok:
+                drho = max(drho * f, f)
+                rho = max(rho * drho, o["rho_min_SQP_DDP"])
+                if rho > o["rho_max_SQP_DDP"]:
+                    code, stop = 2, True
+            elif dJ < o["exit_tolerance_SQP_DDP"]:
+                code, stop = 1, True
+            if it == o["max_iter_SQP_DDP"] - 1:
+                code, stop = 3, True
+            else:
+                it += 1
+            if stop:
+                assert q == rows[i] - 1, (i, q, rows[i])
+                break
+        assert (code, it) == (int(r["exit_code"][i]), int(r["iter"][i])), (i, code, it)
+    return floor_rows
 
 
 @pytest.mark.parametrize("name,N,B", [("arm3", 32, 16), ("arm6fix", 64, 6), ("arm2", 16, 8)])
@@ -76,7 +168,9 @@ def test_ilqr_batch_matches_oracle(name, N, B):
     r = solver.iLQR_batch(np.array(xs), np.array(us), N, 0.1, {})
     cost = osqp.QuadCost(*quad_cost_arrays(m.n))
     for i in range(B):
-        _check(r, i, _oracle(m, cost, xs[i], us[i], N))
+        with np.errstate(all="ignore"):
+            _check_full(r, i, oilqr.ilqr(m, cost, xs[i], us[i], N, 0.1, {}))
+    _replay(solver, r, m, cost, np.array(xs), np.array(us), N)
 
 
 def test_ilqr_nonfinite_trials_rejected(monkeypatch):
@@ -107,19 +201,22 @@ def test_ilqr_nonfinite_trials_rejected(monkeypatch):
     r = solver.iLQR_batch(np.array(xs), np.array(us), N, 0.1, {})
     cost = osqp.QuadCost(*quad_cost_arrays(m.n))
     runs = []
-    with np.errstate(over="ignore", invalid="ignore"):
+    with np.errstate(all="ignore"):
         for i in range(B):
             cur["i"] = i
-            runs.append(_oracle(m, cost, xs[i], us[i], N))
+            runs.append(oilqr.ilqr(m, cost, xs[i], us[i], N, 0.1, {}))
     assert flagged, "no diverging trial in this workload: the test no longer exercises non-finite rejection"
     for i in sorted(flagged):
-        _check(r, i, runs[i])
+        _check_full(r, i, runs[i])
         assert np.all(np.isfinite(r["x"][i])) and np.all(np.isfinite(r["u"][i]))
-        assert np.isfinite(r["trace"]["J"][i, len(runs[i][0][0]["trace"]) - 1])
+        assert np.isfinite(r["trace"]["J"][i, _rows(r, i) - 1])
+    monkeypatch.setattr(oilqr, "forward", fwd)
+    _replay(solver, r, m, cost, np.array(xs), np.array(us), N)
 
 
 def test_ilqr_soft_limits_match_oracle():
-    """iLQR with soft torque limits (augmented Lagrangian outer loop)."""
+    """iLQR with soft torque limits (augmented Lagrangian outer loop, 4 passes): every integer (exit codes,
+    iterations, outer passes, the last pass's alpha path) and the final mu equal to the oracle's run."""
     from oracle import ilqr as oilqr
     from oracle import sqp as osqp
     from oracle.soft import SoftConstraints, SoftLimit
@@ -136,10 +233,14 @@ def test_ilqr_soft_limits_match_oracle():
         return SoftConstraints([lim]), lim
 
     for i in range(B):
-        runs = _oracle(m, cost, xs[i], us[i], N, opts, factory)
-        _check(r, i, runs)
+        soft, lim = factory()
+        with np.errstate(all="ignore"):
+            o = oilqr.ilqr(m, cost, xs[i], us[i], N, 0.1, dict(opts), soft)
         got = (int(r["exit_code"][i]), int(r["iter"][i]), int(r["exit_soft"][i]), int(r["outer_iter"][i]))
-        lim = [run[1] for run in runs if _key(run[0]) == got][0]
+        assert got == _key(o), (i, got, _key(o))
+        rows = len(o["trace"])
+        assert list(r["trace"]["alpha"][i, 1:rows]) == [t["alpha"] for t in o["trace"][1:]], i
+        _check_full(r, i, o)
         assert np.array_equal(r["soft_state"][0][i, :N - 1, 12:18].T, lim.mu)
 
 

@@ -65,9 +65,10 @@ def test_mpc_soft_limits_shift_like_the_reference():
 
 
 def test_ilqr_long_horizon_n128():
-    """iLQR has no horizon limit (the MPC config is arm6 N = 128).  Compared at convergence:
-    intermediate iterates of a 128-step closed-loop rollout amplify rounding differences along the
-    horizon (two CPU restatements differ there too), the converged trajectory does not."""
+    """iLQR has no horizon limit (the MPC config is arm6 N = 128).  Exit code and the converged
+    trajectory against the oracle's run; intermediate iterates of a 128-step sweep amplify rounding
+    along the horizon (test_gpu_ilqr.py), so the iteration count is checked by replay: every
+    iteration from the GPU's own iterate takes the GPU's line-search decision (test_gpu_ilqr._replay)."""
     from oracle import ilqr as oilqr
     from oracle import sqp as osqp
     m = arm_model("arm6fix")
@@ -75,12 +76,13 @@ def test_ilqr_long_horizon_n128():
     solver = _setup(6, N)
     x, u = osqp.initial_problem(m, N, 0.05, 3)
     r = solver.iLQR_batch(x[None], u[None], N, 0.05, {})
-    runs = [oilqr.ilqr(m, osqp.QuadCost(*quad_cost_arrays(6)), x, u, N, 0.05, {}, solve=s) for s in ("cholesky", "lu")]
-    got = (int(r["exit_code"][0]), int(r["iter"][0]))
-    match = [o for o in runs if (o["exit_code"], o["iter"]) == got]
-    assert match, (got, [(o["exit_code"], o["iter"]) for o in runs])
-    assert got[0] == 1
-    assert np.allclose(r["x"][0], match[0]["x"], rtol=1e-6, atol=1e-7)
+    cost = osqp.QuadCost(*quad_cost_arrays(6))
+    with np.errstate(all="ignore"):
+        o = oilqr.ilqr(m, cost, x, u, N, 0.05, {})
+    assert int(r["exit_code"][0]) == o["exit_code"] == 1
+    assert np.allclose(r["x"][0], o["x"], rtol=1e-6, atol=1e-7)
+    from test_gpu_ilqr import _replay
+    _replay(solver, r, m, cost, x[None], u[None], N, dt=0.05)
 
 
 def test_mpc_pcg_warm_start_matches_oracle():

@@ -38,6 +38,24 @@ def test_pcg_on_reference_blocks(ctx, name, N, pre):
 
 
 @pytest.mark.parametrize("name,N", CASES)
+@pytest.mark.parametrize("pre", ["J", "BJ", "SS", "0"])
+def test_pcg_bitwise_canonical(ctx, name, N, pre):
+    """The kernel is the canonical-order restatement (oracle/canon.c) bit for bit on identical inputs:
+    iteration count, lambda, the |nu| trace and the preconditioner blocks (S_{k,k+1} = S_{k+1,k}^T, as the
+    fused QP kernel forms it)."""
+    from oracle import canon
+    d = golden(f"qp_{name}_N{N}.npz")
+    lam, it, tn, _, Pd = ctx.pcg_batch(d["S_diag"][None], d["S_lo"][None], d["gamma"][None], precond=pre,
+                                       tol=1e-6, max_iter=100)
+    lam_c, it_c, tn_c = canon.pcg(d["S_diag"], d["S_lo"], d["gamma"], pre)
+    assert int(it[0]) == it_c == int(d[f"iters_{pre}"])
+    assert np.array_equal(lam[0], lam_c)
+    assert np.array_equal(tn[0, :it_c + 1], tn_c)
+    if pre in ("BJ", "SS"):
+        assert np.array_equal(Pd[0], canon.block_inverse(d["S_diag"]))
+
+
+@pytest.mark.parametrize("name,N", CASES)
 @pytest.mark.parametrize("pre", ["BJ", "SS"])
 def test_pcg_guess_matches_reference(ctx, name, N, pre):
     """PCG.update_guess (TrajoptMPCReference.py:439-440): the reference's solve from a given x0."""

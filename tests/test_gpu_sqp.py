@@ -8,15 +8,21 @@ identical.  Trajectories and merit values: relative tolerance 1e-7.  Method N
 (the dense KKT solve, the reference's default) runs the direct Schur path:
 same solution, pinned by the reference's own method-N solves.
 
-PCG-J exception (documented in DESIGN.md): Jacobi-preconditioned CG on these
-ill-conditioned Schur complements (cond ~1e6-1e7) is not converging smoothly
--- its |rho| trace drops by two decades per iteration near the exit -- so the
-~1e-16 differences between this build's dynamics / Schur arithmetic and
-NumPy's are amplified within an SQP run and a QP after the first may stop one
-CG iteration earlier or later (sqp_arm3_N8_s2: 58 vs 59 in QPs 1-2; the
-reference's own trace there reads 8.5e-6 then 3.2e-8 around the 1e-6 exit).
-On identical S (test_gpu_pcg.py) PCG-J iteration counts are exact.  For PCG-J
-the per-QP counts may differ by +-1 and trajectories are compared at 1e-4.
+PCG counts with no tolerance: every QP of the GPU's own run is replayed at the
+GPU's own iterate (the same solve stopped after j iterations, rho_j from the
+trace's schedule) through tmpc_qp_batch, which must take the trace's count, and
+the canonical-order PCG (oracle/canon.c: the fused kernel's operation order,
+pinned to the reference's counts on the reference's own S in
+test_oracle_canon.py) on that QP's S must take the same count and return the
+GPU's lambda bit for bit.  Against the reference's recorded counts: every QP for
+PCG-BJ / SS, QP 0 for PCG-J.  Jacobi-preconditioned CG on these ill-conditioned
+Schur complements (cond ~1e6-1e7) does not converge smoothly -- its |nu| trace
+drops by two decades per iteration near the exit (sqp_arm3_N8_s2: 8.5e-6 then
+3.2e-8 around the 1e-6 exit) -- so after QP 0 the S of the two runs (~1e-13
+apart: ABA vs RNEA + M^-1 dynamics, blockwise vs dense Schur formation) can
+decide the count: QPs 1-2 of sqp_arm3_N8_s2 take 58 on the GPU's S (and 58 in the
+canonical order on it) where the reference's NumPy order took 59 on its own.
+PCG-J trajectories are compared at 1e-4.
 """
 import glob
 import os
@@ -70,9 +76,10 @@ def test_sqp_matches_reference(f):
         assert ours == [0] * len(ours)   # direct solve: no PCG iterations
     elif method == "PCG-J":
         assert ours[0] == int(d["pcg_iters"][0])
-        assert all(abs(a - int(b)) <= 1 for a, b in zip(ours, d["pcg_iters"]))
     else:
         assert ours == list(d["pcg_iters"])
+    if method.startswith("PCG"):
+        _replay_counts(solver, d, N, method, ours)
     rtol = 1e-4 if method == "PCG-J" else 1e-7
     for key in ("J", "c", "merit", "rho"):
         ours = np.array([t[key] for t in tr])
@@ -82,6 +89,34 @@ def test_sqp_matches_reference(f):
     assert float(np.max(np.abs(x - d["x"]))) < rtol * scale
     scale = max(1.0, float(np.max(np.abs(d["u"]))))
     assert float(np.max(np.abs(u - d["u"]))) < rtol * scale
+
+
+def _replay_counts(solver, d, N, method, counts):
+    """Every QP j of the GPU's run at the GPU's own iterate: tmpc_qp_batch takes the trace's PCG count, and
+    the canonical-order PCG (oracle/canon.py) on the QP's own S takes it too and returns the GPU's lambda
+    bit for bit (the reference's TrajoptMPCReference.py:415-445 + PCG.py:66-111 on identical inputs)."""
+    from oracle import canon
+    x0, u0, dt = d["x0"][None], d["u0"][None], float(d["dt"])
+    opts = {}
+    solver.set_default_options(opts)
+    f = float(opts["rho_factor_SQP_DDP"])
+    rho, drho = opts["rho_init_SQP_DDP"], 1.0
+    ok = [t["succeeded_line_search"] for t in solver.trace[1:]]
+    for j, want in enumerate(counts):
+        if j == 0:
+            xj, uj = x0, u0
+        else:
+            rj = solver.SQP_batch(x0, u0, N, dt, method, {"max_iter_SQP_DDP": j})
+            xj, uj = rj["x"], rj["u"]
+        ctx = solver._context(dict(opts))
+        q = ctx.qp_batch(xj, uj, N, dt, rho, method, want_blocks=True, xs=x0[:, :, 0])
+        assert int(q["pcg_iters"][0]) == want, (j, int(q["pcg_iters"][0]), want)
+        lam, it, _ = canon.pcg(q["S_diag"][0], q["S_lo"][0], q["gamma"][0], method[4:])
+        assert it == want, (j, it, want)
+        nx = q["S_diag"].shape[2]
+        assert np.array_equal(lam, q["dxul"][0][-N * nx:]), j
+        drho = min(drho / f, 1.0 / f) if ok[j] else max(drho * f, f)
+        rho = max(rho * drho, opts["rho_min_SQP_DDP"])
 
 
 @pytest.mark.parametrize("name,N,B,method", [("arm3", 32, 64, "PCG-SS"), ("arm6fix", 64, 16, "PCG-SS"),

@@ -73,8 +73,9 @@ def _recv_exact(sock, n):
 def exchange_unique_id(rank: int, world: int, cfg: bytes = b"\0" * 32, timeout_s: float = 120.0,
                        make_id=None) -> bytes:
     """Rank 0 creates the RCCL unique id (make_id, default ncclGetUniqueId) and serves it over TCP to
-    the world - 1 other ranks, each of which first sends (rank, cfg); a rank whose cfg differs from rank
-    0's gets a refusal and raises, and rank 0 raises after answering everyone.  With TMPC_COMM_ID_FILE
+    the world - 1 other ranks, each of which first sends (rank, cfg).  Rank 0 reads every request before
+    it answers any: if every cfg equals its own, every rank gets the id; if any differs, every rank gets
+    a refusal and raises (rank 0 too), so no rank is left waiting in the communicator init.  With TMPC_COMM_ID_FILE
     set, the id goes through that file instead (no config check)."""
     import socket
     import struct
@@ -89,21 +90,28 @@ def exchange_unique_id(rank: int, world: int, cfg: bytes = b"\0" * 32, timeout_s
     if rank == 0:
         uid = make_id()
         bad = []
+        conns = []
         with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as srv:
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind((host, port))
             srv.listen(max(1, world))
             srv.settimeout(timeout_s)
-            for _ in range(world - 1):
-                conn, _ = srv.accept()
-                with conn:
+            try:
+                # every request first (connections held open), then one verdict for all: the id to every
+                # rank, or a refusal to every rank -- no rank may go on to the communicator init alone
+                for _ in range(world - 1):
+                    conn, _ = srv.accept()
+                    conns.append(conn)
                     conn.settimeout(timeout_s)
                     r, peer_cfg = struct.unpack("<i32s", _recv_exact(conn, 36))
-                    if peer_cfg == cfg:
-                        conn.sendall(b"\x00" + uid)
-                    else:
+                    if peer_cfg != cfg:
                         bad.append(r)
-                        conn.sendall(b"\x01" + cfg + b"\0" * (n_id - 32))
+                reply = (b"\x01" + cfg + b"\0" * (n_id - 32)) if bad else (b"\x00" + uid)
+                for conn in conns:
+                    conn.sendall(reply)
+            finally:
+                for conn in conns:
+                    conn.close()
         if bad:
             raise RuntimeError(f"rank 0: ranks {sorted(bad)} run a different configuration "
                                "(batch / horizon / model / cost / options / limits); refusing to start")
