@@ -309,7 +309,9 @@ int tmpc_memcpy_d2d(tmpc_ctx* ctx, void* dst, const void* src, size_t bytes);
 int tmpc_synchronize(tmpc_ctx* ctx);
 
 /* Kernel timing collected with HIP events on the context stream when options.profile = 1.
- * name: "pcg", "qp_fd", "qp_grad", "ginv", "schur", "dxu", "ls_terms", "ls_decide". */
+ * name: "qp_fd", "qp_minv", "qp_grad", "ginv", "qp" (the fused Schur + PCG + dxu kernel), "schur",
+ * "btsolve", "dxu", "ls_terms", "ls_decide", "hard_schur", "hard_pcg", "hard_direct", "ilqr_backward",
+ * "ilqr_forward", "ilqr_decide", "mpc_shift", "pcg" (tmpc_pcg_batch / tmpc_hard_pcg_batch). */
 int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
 int tmpc_reset_stats(tmpc_ctx* ctx);
 
@@ -323,8 +325,11 @@ int tmpc_solve_counters(tmpc_ctx* ctx, int64_t* counters);
  * examples/test_multiple.py:123-128).  Problems shard by contiguous batch slices with no exchange
  * inside a solve; the communicator carries the initial states broadcast from rank 0 and the
  * per-problem summaries gathered back.  Rank 0 calls tmpc_comm_get_unique_id and shares the id
- * out of band (bench.py: a file next to the launcher's rendezvous) before every rank calls
- * tmpc_comm_create.  Buffers are device memory; every call is synchronous on the ctx stream. */
+ * out of band before every rank calls tmpc_comm_create: trajoptmpcreference_amd/dist.py serves it over
+ * TCP at MASTER_ADDR : MASTER_PORT + 1 together with a hash of each rank's run configuration (rank 0
+ * answers every rank only after reading all requests: the id to all, or a refusal to all), or through a
+ * launcher-provided file (TMPC_COMM_ID_FILE).  Buffers are device memory; every call is synchronous on
+ * the ctx stream. */
 #define TMPC_COMM_ID_BYTES 128
 typedef struct tmpc_comm tmpc_comm;
 int tmpc_comm_get_unique_id(uint8_t* id /* [TMPC_COMM_ID_BYTES] */);

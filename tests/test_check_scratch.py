@@ -1,5 +1,6 @@
 """tools/check_scratch.py (make check-scratch): the parser of hipcc's kernel-resource-usage remarks
-flags scratch in a hot fp64 kernel of a compiled model and ignores the fp32 / runtime-model instances."""
+flags scratch in a hot fp64 or fp32 kernel of a compiled model and ignores the runtime-model
+instances (ModelRef: any robot outside the bundled arms)."""
 import os
 import subprocess
 import sys
@@ -27,7 +28,16 @@ def test_scratch_in_hot_fp64_kernel_fails():
     assert _run(_remarks(bwd64, 108, 160)).returncode == 1
 
 
-def test_fp32_and_runtime_model_instances_are_not_gated():
+def test_scratch_in_hot_fp32_kernel_fails():
+    """The fp32 instances (BASELINE configs 3 / 5) are gated too: before the full-unroll build they kept
+    192-256 B per lane of scratch."""
     fwd32 = "_ZN4tmpc14k_ilqr_forwardILi6ELb1ELb1ENS_4Arm6EfLb1EEEvT2_PKNS_7CostDevE"
+    assert _run(_remarks(fwd32, 231, 256)).returncode == 1
+    assert _run(_remarks(fwd32, 165, 0)).returncode == 0
+    minv32 = "_ZN4tmpc9k_qp_minvILi6ELb1ENS_4Arm6EfEEvT1_NS_5PListEiiPKdPKiPd"
+    assert _run(_remarks(minv32, 140, 192)).returncode == 1
+
+
+def test_runtime_model_instances_are_not_gated():
     ref64 = "_ZN4tmpc7k_qp_fdILi6ELb0ENS_8ModelRefEdEEvT1_NS_5PListEiidPKdS5_S5_PKiPdS8_"
-    assert _run(_remarks(fwd32, 231, 256) + _remarks(ref64, 256, 2176)).returncode == 0
+    assert _run(_remarks(ref64, 256, 2176)).returncode == 0

@@ -83,14 +83,15 @@ def test_reduced_precision_ilqr_tracks_fp64(name, n, N, prec):
 def test_config3_fp32_ilqr_al_all_problems():
     """BASELINE config 3 at its declared precision (fp32; arm6 N = 64 iLQR, augmented-Lagrangian torque
     limits), all 8 problems of the oracle fixture against the fp64 oracle (parity unpinned: the reference
-    has no fp32 path).  Bounds, with the values measured on MI355X in round 4 in brackets
-    (gpurun_out/r04b, tools/debug/r04_dump.py): every problem's final quadratic cost within 5e-3 relative
-    of the fp64 run's [max 1.6e-3] and its state trajectory within 6e-2 of max|x| [max 2.7e-2]; the one
-    problem the fp64 oracle solves to convergence (exit 1) at 2e-3 [2.4e-4].  The fp64 runs of the other
-    seven end on the rho schedule or the outer-pass limit (exit 2 / 3) at points fp32 rounding moves (its
-    controls differ up to 0.37 of max|u| there), and the exit test dJ < 1e-6 is below fp32 rounding of a
-    rollout cost (~1e-7 of J ~ 10..100), so exit codes are not compared.  The measured maxima are reported
-    as a warning in the test output."""
+    has no fp32 path).  Bounds, with the values measured on MI355X in round 4 in brackets (two binaries:
+    the round-3 build / the full-unroll build of DESIGN.md 4e; gpurun_out/r04b, r04e): every problem's final
+    quadratic cost within 1e-2 relative of the fp64 run's [max 1.6e-3 / 2.2e-3] and its state trajectory
+    within 1e-1 of max|x| [max 2.7e-2 / 4.6e-2]; the one problem the fp64 oracle solves to convergence
+    (exit 1) at 2e-3 [2.4e-4 / 1.3e-4].  The fp64 runs of the other seven end on the rho schedule or the
+    outer-pass limit (exit 2 / 3) at points fp32 rounding moves (their controls differ up to 0.37 of max|u|
+    there, and the two binaries' fp32 runs differ from each other as much), and the exit test dJ < 1e-6 is
+    below fp32 rounding of a rollout cost (~1e-7 of J ~ 10..100), so exit codes are not compared.  The
+    measured maxima are reported as a warning in the test output."""
     import warnings
     d = golden("oracle_config3_arm6_N64_ilqr_al.npz")
     N = int(d["N"])
@@ -111,12 +112,12 @@ def test_config3_fp32_ilqr_al_all_problems():
         xerr.append(_rel(r["x"][i], d["x"][i]))
     conv = [i for i in range(len(x)) if int(d["exit_code"][i]) == 1]
     cerr = [_rel(r["x"][i], d["x"][i]) for i in conv]
-    warnings.warn(f"config 3 fp32 vs fp64 oracle, 8 problems: max cost rel err {max(jerr):.2e} (bound 5e-3), "
-                  f"max state rel err {max(xerr):.2e} (bound 6e-2), converged problem(s) {conv}: "
+    warnings.warn(f"config 3 fp32 vs fp64 oracle, 8 problems: max cost rel err {max(jerr):.2e} (bound 1e-2), "
+                  f"max state rel err {max(xerr):.2e} (bound 1e-1), converged problem(s) {conv}: "
                   f"{[f'{e:.2e}' for e in cerr]} (bound 2e-3)")
     assert len(conv) == 1
-    assert max(jerr) < 5e-3, jerr
-    assert max(xerr) < 6e-2, xerr
+    assert max(jerr) < 1e-2, jerr
+    assert max(xerr) < 1e-1, xerr
     assert max(cerr) < 2e-3, cerr
 
 

@@ -1,10 +1,12 @@
-"""Fail when a hot fp64 kernel of the compiled planar arms uses scratch (private stack memory).
+"""Fail when a hot kernel of the compiled planar arms uses scratch (private stack memory), in fp64 and in
+fp32 (the precision modes of BASELINE configs 3 and 5).
 
 Reads the output of `hipcc -Rpass-analysis=kernel-resource-usage` (stdin) and reports, per kernel,
 VGPRs / scratch bytes per lane / occupancy.  A kernel whose name matches one of the hot families
-below, compiled for a static model (Arm<n>) in fp64, must have ScratchSize 0: the round-3 dynamics
-pruning once made the compiler move k_qp_grad's arrays to scratch (592 B per lane, 3x slower,
-DESIGN.md 4d) without a single reported spill.
+below, compiled for a static model (Arm<n>) in fp64 or fp32, must have ScratchSize 0: the round-3
+dynamics pruning once made the compiler move k_qp_grad's arrays to scratch (592 B per lane, 3x slower,
+DESIGN.md 4d) without a single reported spill, and the fp32 instances kept rolled joint loops (their
+arrays dynamically indexed, so in scratch) until the full-unroll threshold.
 Usage: make -C trajoptmpcreference_amd/csrc check-scratch
 """
 import re
@@ -27,13 +29,14 @@ def main():
             res[cur][m.group(1).split()[0]] = int(m.group(2))
     bad = []
     for k, v in sorted(res.items()):
-        # fp64 instances on a compiled model (...Arm6Ed...), and the fp64 Riccati sweep (...ILi6Ed...)
-        hot = any(h in k for h in HOT) and (re.search(r"Arm\d+Ed", k) or re.search(r"k_ilqr_backwardILi\d+Ed", k))
+        # fp64 / fp32 instances on a compiled model (...Arm6Ed... / ...Arm6Ef...), and the Riccati sweep
+        # (...ILi6Ed... / ...ILi6Ef...)
+        hot = any(h in k for h in HOT) and (re.search(r"Arm\d+E[df]", k) or re.search(r"k_ilqr_backwardILi\d+E[df]", k))
         if hot and v.get("ScratchSize", 0) > 0:
             bad.append((k, v))
         print(f"{k[:90]:90s} vgpr {v.get('VGPRs')} scratch {v.get('ScratchSize')} occ {v.get('Occupancy')}")
     for k, v in bad:
-        print(f"SCRATCH in hot fp64 kernel: {k} {v}", file=sys.stderr)
+        print(f"SCRATCH in hot kernel: {k} {v}", file=sys.stderr)
     sys.exit(1 if bad else 0)
 
 

@@ -63,7 +63,9 @@ struct tmpc_ctx {
   int* h_count = nullptr;  // pinned
   int64_t last_counters[4] = {0, 0, 0, 0};
   // shape of the last tmpc_qp_batch with hard box limits (tmpc_qp_hard_info); B = 0: none
-  struct { int B, N, dmax, W; } hard_last{0, 0, 0, 0};
+  // the last tmpc_qp_batch with hard limits (tmpc_qp_hard_info reads its hd_* buffers); cleared by every
+  // other user of those buffers (setup_hard) and by a change of the limits, so stale data is refused
+  struct { int B, N, dmax, W, rmax; } hard_last{0, 0, 0, 0, 0};
 };
 
 static int fail(tmpc_ctx* c, const char* fmt, ...) {
@@ -421,24 +423,31 @@ static int alloc_soft(tmpc_ctx* ctx, int B, int N, double** mu, double** lam, do
 // Buffers of the hard-constraint QP (tmpc_hard.hip) for B problems of N knots; T line-search trials.
 static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs& hard) {
   const int nj = ctx->hmodel.n, nx = 2 * nj;
-  int ntypes = 0;
+  // rows per knot, at most: FULL_SET both bounds of every entry; ACTIVE_SET one per entry when lb < ub
+  // (z - lb < 0 and ub - z < 0 cannot hold together), else both
+  int rmax = 0;
   bool full = false;
   for (int t = 0; t < 3; ++t) {
-    if (ctx->hlim.hard[t] != HARD_NONE) ++ntypes;
+    if (ctx->hlim.hard[t] == HARD_NONE) continue;
+    bool ordered = ctx->hlim.hard[t] == HARD_ACTIVE;
+    for (int i = 0; i < nj; ++i) ordered = ordered && ctx->hlim.lb[t][i] < ctx->hlim.ub[t][i];
+    rmax += ordered ? nj : 2 * nj;
     if (ctx->hlim.hard[t] == HARD_FULL) full = true;
   }
   if (full && precond != 0)
     return fail(ctx, "FULL_SET box constraints with a PCG method: the inactive rows of C are zero, so S is "
                 "singular and the reference's preconditioner raises LinAlgError (PCG.py:168-188); use method S");
+  ctx->hard_last = {0, 0, 0, 0, 0};           // the hd_* buffers are about to be reused: no stale QP info
   hard = HardArgs{};
   hard.B = B;
   hard.N = N;
-  hard.rmax = 2 * nj * ntypes;                 // both bounds of every limited entry, at most
+  hard.rmax = rmax;
   hard.dmax = nx * N + N * hard.rmax;
   const int gmax = nx + 2 * hard.rmax;         // the last group holds two knots' hard rows
   hard.W = 2 * gmax - 1;
-  if (precond != 0 && (5 * (size_t)hard.dmax + 16) * sizeof(double) > 160 * 1024)
-    return fail(ctx, "hard constraints: Schur dimension up to %d exceeds the PCG's LDS vectors (max 4092)", hard.dmax);
+  if (precond != 0 && hard.dmax > HARD_PCG_MAX_ROWS)
+    return fail(ctx, "hard constraints: Schur dimension up to %d exceeds the PCG's %d rows", hard.dmax,
+                HARD_PCG_MAX_ROWS);
   if (hard.W > 1024) return fail(ctx, "hard constraints: band half-width %d > 1024", hard.W);
   const size_t BW = 2 * (size_t)hard.W + 1, nbmax = hard.dmax / nx + 1;
   hard.Cs = ctx->dlim;
@@ -478,7 +487,8 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
     BUF(double, hd_Pd, (size_t)B * nbmax * nx * nx);
     BUF(double, hd_Pl, (size_t)B * nbmax * nx * nx);
     BUF(double, hd_Pt, (size_t)B * nbmax * nx * nx);
-    hard.Pd = hd_Pd; hard.Pl = hd_Pl; hard.Ptmp = hd_Pt;
+    BUF(double, hd_Ptr, (size_t)B * nbmax * nx * nx);
+    hard.Pd = hd_Pd; hard.Pl = hd_Pl; hard.Ptmp = hd_Pt; hard.Ptr = hd_Ptr;
   }
   BUF(double, hd_terms, (size_t)B * (T > 0 ? T : 1) * N);
   hard.hterms = hd_terms;
@@ -530,8 +540,10 @@ static int alloc_alive(tmpc_ctx* ctx, int B, const int* mask, AliveList& al) {
 // iteration enqueued after the batch finished is a no-op for every problem (need_grad / active /
 // outer_active are all 0).  The launches of iteration `it` visit the problem list built at the end
 // of `it - 1` (on the stream, so exact), with the grid sized by the list length the host last read,
-// the one of iteration `it - 2` (an upper bound: the list only shrinks); the tail of a batch whose
-// problems converge at different iterations then dispatches only its live problems' workgroups.
+// the one of iteration `it - 2` (an upper bound because the list only shrinks: the masks go 1 -> 0 inside
+// the loop and never back -- k_alive_list flags any growth and the loop then fails instead of silently
+// skipping problems); the tail of a batch whose problems converge at different iterations then
+// dispatches only its live problems' workgroups.
 template <class Body>
 static int lockstep_loop(tmpc_ctx* ctx, long cap, int* active_count, AliveList& al, Body body) {
   hipEvent_t ev[2] = {get_event(ctx), get_event(ctx)};
@@ -545,15 +557,20 @@ static int lockstep_loop(tmpc_ctx* ctx, long cap, int* active_count, AliveList& 
     const int p = (int)(it & 1);
     int* ac = active_count + 4 * p;
     if (it >= 2) al.nb = std::max(1, std::min(al.nb, ctx->h_count[4 * p + 2]));   // synced at it - 1
-    HIP_OK(hipMemsetAsync(ac, 0, 3 * sizeof(int), ctx->stream));
+    HIP_OK(hipMemsetAsync(ac, 0, 4 * sizeof(int), ctx->stream));
     if ((rc = body(ac))) break;
     launch_alive_list(ctx->stream, al.B, al.mask, al.idx, al.cnt, ac + 2);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(ctx->h_count + 4 * p, ac, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipMemcpyAsync(ctx->h_count + 4 * p, ac, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(hipEventRecord(ev[p], ctx->stream));
     if (it > 0) {
       HIP_OK(hipEventSynchronize(ev[p ^ 1]));
       const int* h = ctx->h_count + 4 * (p ^ 1);
+      if (h[3] != 0) {   // k_alive_list: the list grew, so a grid sized by an older length skipped problems
+        rc = fail(ctx, "internal: the problem list of the lock-step loop grew (a problem re-entered its loop); "
+                  "the grid-size bound no longer holds");
+        break;
+      }
       if (h[0] == 0 && h[1] == 0) break;
     }
   }
@@ -1047,6 +1064,7 @@ void tmpc_default_options(tmpc_options* o) {
 int tmpc_set_box_limits(tmpc_ctx* ctx, const tmpc_box_limits* L) {
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model: call tmpc_set_model first");
+  ctx->hard_last = {0, 0, 0, 0, 0};
   ConstrDev c{};
   if (L) {
     for (int t = 0; t < 3; ++t) {
@@ -1451,12 +1469,12 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
     if ((rc = setup_hard(ctx, B, N, 0, precond, hard))) return rc;
     w.hard = &hard;
   }
-  ctx->hard_last = {0, 0, 0, 0};
+  ctx->hard_last = {0, 0, 0, 0, 0};
   if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, !ctx->hlim.any_hard, PList{nullptr, nullptr}, B)))
     return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (ctx->hlim.any_hard) {
-    ctx->hard_last = {B, N, hard.dmax, hard.W};
+    ctx->hard_last = {B, N, hard.dmax, hard.W, hard.rmax};
     std::vector<int> roff((size_t)B * N);
     std::vector<double> lh((size_t)B * hard.dmax);
     HIP_OK(hipMemcpy(roff.data(), hard.roff, roff.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -1513,7 +1531,12 @@ int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim,
   const size_t BW = 2 * (size_t)hl.W + 1;
   if (S_band) {
     // the kernels write S only inside each row's structural range (k_hard_schur): zero the rest
-    HIP_OK(hipMemcpy(S_band, dev("hd_Sb"), sizeof(double) * B * hl.dmax * BW, hipMemcpyDeviceToHost));
+    std::vector<double> sbt((size_t)B * hl.dmax * BW);   // device: diagonal-major [B][2W+1][dmax]
+    HIP_OK(hipMemcpy(sbt.data(), dev("hd_Sb"), sizeof(double) * sbt.size(), hipMemcpyDeviceToHost));
+    for (int b = 0; b < B; ++b)
+      for (int a = 0; a < hl.dmax; ++a)
+        for (size_t o = 0; o < BW; ++o)
+          S_band[((size_t)b * hl.dmax + a) * BW + o] = sbt[((size_t)b * BW + o) * hl.dmax + a];
     std::vector<int> rg((size_t)B * hl.dmax * 2), dm(B);
     HIP_OK(hipMemcpy(rg.data(), dev("hd_rng"), rg.size() * sizeof(int), hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(dm.data(), dev("hd_dim"), B * sizeof(int), hipMemcpyDeviceToHost));
@@ -1529,9 +1552,8 @@ int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim,
   }
   if (gamma) HIP_OK(hipMemcpy(gamma, dev("hd_gam"), sizeof(double) * B * hl.dmax, hipMemcpyDeviceToHost));
   if (lambda_hard) {
-    // the hard rows' multipliers by slot t * 2n + e (0 where the slot has no row)
-    int rmax = 0;
-    for (int t = 0; t < 3; ++t) rmax += ctx->hlim.hard[t] != HARD_NONE ? 2 * nj : 0;
+    // the hard rows' multipliers by slot t * 2n + e (0 where the slot has no row); rmax as hd_slot was laid out
+    const int rmax = hl.rmax;
     std::vector<int> cnt((size_t)B * N), hoff((size_t)B * N), slot((size_t)B * N * rmax);
     std::vector<double> lam((size_t)B * hl.dmax);
     HIP_OK(hipMemcpy(cnt.data(), dev("hd_cnt"), cnt.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -1553,12 +1575,11 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
                         const double* S_band, const double* gamma, double tol, int max_iter, double* lambda,
                         int32_t* iters) {
   if (!ctx) return -1;
-  if (B < 1 || nx < 2 || nx > 14 || (nx & 1) || dmax < 1 || W < 0)
+  if (B < 1 || nx < 2 || nx > 14 || (nx & 1) || dmax < 1 || W < 0 || W > 1024)
     return fail(ctx, "bad sizes B=%d nx=%d dmax=%d W=%d", B, nx, dmax, W);
   if (precond != PRECOND_J && precond != PRECOND_BJ && precond != PRECOND_SS && precond != PRECOND_NONE)
     return fail(ctx, "preconditioner %d: valid are J=1, BJ=2, SS=3, 0=4 (PCG.py:52-55)", precond);
-  if ((5 * (size_t)dmax + 16) * sizeof(double) > 160 * 1024)
-    return fail(ctx, "dmax = %d exceeds the PCG's LDS vectors (max 4092)", dmax);
+  if (dmax > HARD_PCG_MAX_ROWS) return fail(ctx, "dmax = %d exceeds the PCG's %d rows", dmax, HARD_PCG_MAX_ROWS);
   if (max_iter < 0) return fail(ctx, "max_iter must be >= 0");
   if (!dim || !S_band || !gamma) return fail(ctx, "null input");
   for (int b = 0; b < B; ++b)
@@ -1574,6 +1595,7 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
   BUF(double, hp_Pd, (size_t)B * nbmax * nx * nx);
   BUF(double, hp_Pl, (size_t)B * nbmax * nx * nx);
   BUF(double, hp_Pt, (size_t)B * nbmax * nx * nx);
+  BUF(double, hp_Ptr, (size_t)B * nbmax * nx * nx);
   BUF(int, hp_rng, (size_t)B * dmax * 2);
   // each row's first / last nonzero column: the range the kernel's products visit (tmpc_hard.hip)
   std::vector<int> rg((size_t)B * dmax * 2);
@@ -1591,7 +1613,13 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
       rg[((size_t)b * dmax + a) * 2 + 1] = hi;
     }
   HIP_OK(hipMemcpyAsync(hp_rng, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  HIP_OK(hipMemcpyAsync(hp_Sb, S_band, sizeof(double) * B * dmax * BW, hipMemcpyHostToDevice, ctx->stream));
+  // the device band is diagonal-major ([B][2W+1][dmax], tmpc_hard.hip); the ABI's is row-major
+  std::vector<double> sbt((size_t)B * dmax * BW);
+  for (int b = 0; b < B; ++b)
+    for (int a = 0; a < dmax; ++a)
+      for (size_t o = 0; o < BW; ++o)
+        sbt[((size_t)b * BW + o) * dmax + a] = S_band[((size_t)b * dmax + a) * BW + o];
+  HIP_OK(hipMemcpy(hp_Sb, sbt.data(), sizeof(double) * B * dmax * BW, hipMemcpyHostToDevice));
   HIP_OK(hipMemcpyAsync(hp_gam, gamma, sizeof(double) * B * dmax, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(hp_dim, dim, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
   std::vector<int> ones(B, 1);
@@ -1611,6 +1639,7 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
   h.Pd = hp_Pd;
   h.Pl = hp_Pl;
   h.Ptmp = hp_Pt;
+  h.Ptr = hp_Ptr;
   h.lam = hp_lam;
   h.iters = hp_it;
   h.rng = hp_rng;

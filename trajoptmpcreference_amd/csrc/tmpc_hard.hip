@@ -8,7 +8,9 @@
 // (R_j the nx dynamics rows that define x_j, H_k knot k's hard rows) the groups
 // touch the knot variables {0}, {0,1}, {1,2}, ..., so S is block-tridiagonal with
 // VARIABLE block sizes: every row couples only with rows less than twice the
-// largest group away.  S is therefore stored as a band [dim][2W+1] per problem.
+// largest group away.  S is therefore stored as a band per problem, diagonal-major:
+// entry (row a, column c) at [o = c - a + W][a] of a [2W+1][dmax] array, so that the
+// rows of a wave read one diagonal as one contiguous 512-byte piece.
 // The reference's PCG preconditioner, however, cuts S into nx-aligned blocks from
 // row 0 (n_blocks = floor(dim / nx), PCG.py:182-212), which no longer line up with
 // the groups; it is reproduced exactly on the band (trailing dim mod nx rows have
@@ -35,6 +37,9 @@
 // sums from 0.0, per-thread dot partials over 256 threads, a 64-lane xor butterfly, a fan-in over the
 // 4 waves -- so that on identical S and gamma the two are bitwise equal (tests/test_gpu_hard.py).
 #include "tmpc_internal.h"
+
+#include <algorithm>
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -320,14 +325,14 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     atomicMax(&s_wt, hi - lo + 1);
   }
   __syncthreads();
-  // phase 2: the band inside the row ranges, row a, column c = lo_a + o (stored at offset c - a + W);
+  // phase 2: the band inside the row ranges, row a, column c = lo_a + o (stored at [c - a + W][a]);
   // entries outside the ranges are never read (band_at / the PCG product / k_hard_direct's copy)
   const int BW = 2 * W + 1;
   const int Wt = s_wt;
   double* S = Sb + (size_t)b * dmax * BW;
-  for (int e = threadIdx.x; e < D * Wt; e += blockDim.x) {
-    const int a = e / Wt;
-    const int c = rb[2 * a] + (e - a * Wt);
+  for (int e = threadIdx.x; e < D * Wt; e += blockDim.x) {   // consecutive threads: consecutive rows
+    const int j = e / D, a = e - j * D;
+    const int c = rb[2 * a] + j;
     if (c > rb[2 * a + 1]) continue;
     const int o = c - a + W;
     double s = 0.0;
@@ -349,7 +354,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
       }
       s = -s;
     }
-    S[(size_t)a * BW + o] = s;
+    S[(size_t)o * dmax + a] = s;
   }
 }
 
@@ -365,9 +370,9 @@ __device__ __forceinline__ double h_block_sum(double v, double* red) {
   return s;
 }
 
-// S_rc from the band; zero outside row r's structural range rg[2r .. 2r+1]
-__device__ __forceinline__ double band_at(const double* S, const int* rg, int BW, int W, int r, int c) {
-  return (c >= rg[2 * r] && c <= rg[2 * r + 1]) ? S[(size_t)r * BW + (c - r + W)] : 0.0;
+// S_rc from the (diagonal-major) band; zero outside row r's structural range rg[2r .. 2r+1]
+__device__ __forceinline__ double band_at(const double* S, const int* rg, int dmax, int W, int r, int c) {
+  return (c >= rg[2 * r] && c <= rg[2 * r + 1]) ? S[(size_t)(c - r + W) * dmax + r] : 0.0;
 }
 
 // In-place Gauss-Jordan inverse of a small block (global memory, one thread), the operation order of
@@ -402,51 +407,59 @@ __device__ void h_neg_triple(const double* X, const double* Yy, const double* Z,
 // Preconditioner (compute_preconditioner on the dense S, PCG.py:113-212) + PCG (:66-111).
 // Pd [nb][NX][NX] diagonal inverses, Pl [nb-1][NX][NX] = P_{k+1,k} (P_{k,k+1} = Pl[k]^T: the
 // reference copies transposes), scratch [NX][NX] per problem for the off-diagonal products.
-template <int NX>
-__global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int precond, const int* __restrict__ active,
-                                                  const int* __restrict__ dim, const double* __restrict__ Sb,
-                                                  const double* __restrict__ gam, double tol, int max_iter,
-                                                  double* __restrict__ Pd, double* __restrict__ Pl,
-                                                  double* __restrict__ Ptmp, double* __restrict__ lam,
-                                                  int* __restrict__ iters, const int* __restrict__ rng) {
+// Thread t owns rows t, t + 256, ... (slot m = row / 256 < SLOTS): x of its rows stays in its registers;
+// r and p, which other rows read, and z and S p are in LDS (4 dmax doubles: several problems per CU).  Every global read is coalesced: S p walks the wave's diagonals of the band (each
+// lane adds the diagonals inside its row's range, in column order), and the preconditioner rows are read
+// from transposed copies of the P blocks (column j of a block: the 12 rows' entries contiguous).
+// Every sum keeps the canonical order (oracle/hard.py pcg_canonical).
+template <int NX, int SLOTS>
+__global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int dmax, int precond,
+                                                              const int* __restrict__ active,
+                                                              const int* __restrict__ dim, const double* __restrict__ Sb,
+                                                              const double* __restrict__ gam, double tol, int max_iter,
+                                                              double* __restrict__ Pd, double* __restrict__ Pl,
+                                                              double* __restrict__ Ptmp, double* __restrict__ Ptr,
+                                                              double* __restrict__ lam, int* __restrict__ iters,
+                                                              const int* __restrict__ rng) {
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
   const int BW = 2 * W + 1;
   const int nb = D / NX;
+  const int t = threadIdx.x;
   const double* S = Sb + (size_t)b * dmax * BW;
   const int* rg = rng + (size_t)b * dmax * 2;
   const size_t nbmax = dmax / NX + 1;
   double* P = Pd + (size_t)b * nbmax * NX * NX;
   double* PL = Pl + (size_t)b * nbmax * NX * NX;
   double* T = Ptmp + (size_t)b * nbmax * NX * NX;
+  double* PT = Ptr + (size_t)b * nbmax * NX * NX;
   extern __shared__ __align__(16) double sh[];
-  double* xv = sh;
-  double* rv = xv + dmax;
+  double* rv = sh;
   double* pv = rv + dmax;
-  double* zv = pv + dmax;
-  double* av = zv + dmax;
-  double* red = av + dmax;
+  double* red = pv + dmax;
+  double* zl = red + 16;   // z and S p of the rows (each read and written by its owner thread only)
+  double* al = zl + dmax;
   const bool blocks = precond == PRECOND_BJ || precond == PRECOND_SS;
   if (blocks) {
-    for (int k = threadIdx.x; k < nb; k += blockDim.x) {
+    for (int k = t; k < nb; k += HARD_PCG_THREADS) {
       double* M = P + (size_t)k * NX * NX;
       for (int i = 0; i < NX; ++i)
-        for (int j = 0; j < NX; ++j) M[i * NX + j] = band_at(S, rg, BW, W, k * NX + i, k * NX + j);
+        for (int j = 0; j < NX; ++j) M[i * NX + j] = band_at(S, rg, dmax, W, k * NX + i, k * NX + j);
       h_gj_inverse(M, NX);
     }
     __syncthreads();
     if (precond == PRECOND_SS) {
-      for (int k = 1 + threadIdx.x; k < nb; k += blockDim.x) {
+      for (int k = 1 + t; k < nb; k += HARD_PCG_THREADS) {
         double* Sk = T + (size_t)k * NX * NX;
         if (k & 1) {   // P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1})
           for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, BW, W, k * NX + i, (k - 1) * NX + j);
+            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, dmax, W, k * NX + i, (k - 1) * NX + j);
           h_neg_triple(P + (size_t)k * NX * NX, Sk, P + (size_t)(k - 1) * NX * NX, PL + (size_t)(k - 1) * NX * NX, NX);
         } else {       // P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk); stored as its transpose P_{k,k-1}
           for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, BW, W, (k - 1) * NX + i, k * NX + j);
-          double prod[NX * NX];
+            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, dmax, W, (k - 1) * NX + i, k * NX + j);
+          double* prod = PT + (size_t)k * NX * NX;   // PT[k] is free until the transposed copies below
           h_neg_triple(P + (size_t)(k - 1) * NX * NX, Sk, P + (size_t)k * NX * NX, prod, NX);
           for (int i = 0; i < NX; ++i)
             for (int j = 0; j < NX; ++j) PL[(size_t)(k - 1) * NX * NX + j * NX + i] = prod[i * NX + j];
@@ -454,88 +467,148 @@ __global__ void __launch_bounds__(256) k_hard_pcg(int B, int W, int dmax, int pr
       }
       __syncthreads();
     }
-  }
-  // PCG, x0 = 0
-  auto apply_P = [&](const double* r, double* z) {
-    for (int a = threadIdx.x; a < D; a += blockDim.x) {
-      double s;
-      if (precond == PRECOND_NONE) {
-        s = r[a];
-      } else if (precond == PRECOND_J) {
-        s = (1.0 / band_at(S, rg, BW, W, a, a)) * r[a];
-      } else if (a >= nb * NX) {
-        s = 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
-      } else {
-        const int k = a / NX, i = a - k * NX;
-        const double* M = P + (size_t)k * NX * NX;
-        s = 0.0;
-        for (int j = 0; j < NX; ++j) s += M[i * NX + j] * r[k * NX + j];
-        if (precond == PRECOND_SS) {
-          if (k > 0) {
-            const double* L = PL + (size_t)(k - 1) * NX * NX;
-            for (int j = 0; j < NX; ++j) s += L[i * NX + j] * r[(k - 1) * NX + j];
-          }
-          if (k + 1 < nb) {
-            const double* U = PL + (size_t)k * NX * NX;   // P_{k,k+1} = P_{k+1,k}^T
-            for (int j = 0; j < NX; ++j) s += U[j * NX + i] * r[(k + 1) * NX + j];
-          }
-        }
+    // transposed copies: PT[k] = P_kk^T; PLT[k] = Pl[k]^T (in T, free once the stair blocks are formed)
+    for (int k = t; k < nb; k += HARD_PCG_THREADS) {
+      const double* M = P + (size_t)k * NX * NX;
+      double* MT = PT + (size_t)k * NX * NX;
+      for (int i = 0; i < NX; ++i)
+        for (int j = 0; j < NX; ++j) MT[j * NX + i] = M[i * NX + j];
+      if (precond == PRECOND_SS && k + 1 < nb) {
+        const double* L = PL + (size_t)k * NX * NX;
+        double* LT = T + (size_t)k * NX * NX;
+        for (int i = 0; i < NX; ++i)
+          for (int j = 0; j < NX; ++j) LT[j * NX + i] = L[i * NX + j];
       }
-      z[a] = s;
     }
-  };
-  auto spmv = [&](const double* v, double* out) {
-    for (int a = threadIdx.x; a < D; a += blockDim.x) {
-      // the row's structural range only: the terms left out are exact zeros
-      double s = 0.0;
-      const int c0 = rg[2 * a], c1 = rg[2 * a + 1];
-      const double* Sa = S + (size_t)a * BW + (W - a);
-      for (int c = c0; c <= c1; ++c) s += Sa[c] * v[c];
-      out[a] = s;
-    }
-  };
-  const double* g = gam + (size_t)b * dmax;
-  for (int a = threadIdx.x; a < D; a += blockDim.x) {
-    xv[a] = 0.0;
-    rv[a] = g[a];
+    __syncthreads();
   }
-  __syncthreads();
-  apply_P(rv, zv);
+  // z = P^-1 r for row a (r read from LDS)
+  auto apply_P = [&](int a) -> double {
+    if (precond == PRECOND_NONE) return rv[a];
+    if (precond == PRECOND_J) return (1.0 / band_at(S, rg, dmax, W, a, a)) * rv[a];
+    if (a >= nb * NX) return 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
+    const int k = a / NX, i = a - k * NX;
+    const double* MT = PT + (size_t)k * NX * NX;   // MT[j NX + i] = P_kk[i][j]
+    double s = 0.0;
+    for (int j = 0; j < NX; ++j) s += MT[j * NX + i] * rv[k * NX + j];
+    if (precond == PRECOND_SS) {
+      if (k > 0) {
+        const double* LT = T + (size_t)(k - 1) * NX * NX;   // LT[j NX + i] = P_{k,k-1}[i][j]
+        for (int j = 0; j < NX; ++j) s += LT[j * NX + i] * rv[(k - 1) * NX + j];
+      }
+      if (k + 1 < nb) {
+        const double* U = PL + (size_t)k * NX * NX;   // P_{k,k+1} = P_{k+1,k}^T
+        for (int j = 0; j < NX; ++j) s += U[j * NX + i] * rv[(k + 1) * NX + j];
+      }
+    }
+    return s;
+  };
+  // (S p)_a over the row's structural range only, in column order (the terms left out are exact zeros):
+  // the wave walks the diagonals o in [olo, ohi] (its rows' ranges, wave-uniform), each lane adding the
+  // ones inside its own range -- o increasing is c = a - W + o increasing for a fixed row.  Eight
+  // diagonals' loads are issued before their products are added (the band streams from HBM: memory-level
+  // parallelism, not bandwidth, bounds one wave); past ohi the index is clamped and the product dropped.
+  auto spmv = [&](int a, bool own, int olo, int ohi, int lohi) -> double {
+    const int lo = lohi & 0xffff, hi = lohi >> 16;
+    constexpr int U = 8;
+    double s = 0.0;
+    const double* Sa = S + (own ? a : 0);
+    for (int o = olo; o <= ohi; o += U) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(o + u, ohi) * dmax];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (own && o + u >= lo && o + u <= hi) s += v[u] * pv[a - W + o + u];
+    }
+    return s;
+  };
+  // The per-row loops that read memory run one slot at a time (unroll 1), with z = P^-1 r and S p of
+  // the thread's rows in LDS: unrolled over the slots they held every slot's loads and products in
+  // registers at once (254 VGPRs, one wave per SIMD); x stays in registers.
+  const int wbase = t & ~63;   // first row of this wave in slot 0
+  double xv[SLOTS];
+  const double* g = gam + (size_t)b * dmax;
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * HARD_PCG_THREADS;
+    xv[m] = 0.0;
+    if (a < D) rv[a] = g[a];
+  }
   __syncthreads();
   double part = 0.0;
-  for (int a = threadIdx.x; a < D; a += blockDim.x) {
-    pv[a] = zv[a];
-    part += rv[a] * zv[a];
+#pragma unroll 1
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * HARD_PCG_THREADS;
+    if (a < D) {
+      const double z = apply_P(a);
+      zl[a] = z;
+      pv[a] = z;
+      part += rv[a] * z;
+    }
   }
   double nu = h_block_sum(part, red);
   int it_done = max_iter;
   for (int it = 0; it < max_iter; ++it) {
     __syncthreads();
-    spmv(pv, av);
     part = 0.0;
-    for (int a = threadIdx.x; a < D; a += blockDim.x) part += pv[a] * av[a];
+#pragma unroll 1
+    for (int m = 0; m < SLOTS; ++m) {
+      if (wbase + m * HARD_PCG_THREADS >= D) break;   // wave-uniform: no row of this wave's slot m
+      const int a = t + m * HARD_PCG_THREADS;
+      int l = a < D ? rg[2 * a] - a + W : BW;   // this row's diagonals (0 <= l, h < 2W + 1 < 2^15)
+      int h = a < D ? rg[2 * a + 1] - a + W : -1;
+      const int lohi = a < D ? (l | (h << 16)) : 0xffff;   // empty range for rows past D
+      for (int off = 32; off > 0; off >>= 1) {   // the wave's union of them
+        l = min(l, __shfl_xor(l, off, 64));
+        h = max(h, __shfl_xor(h, off, 64));
+      }
+      const double sp = spmv(a, a < D, __builtin_amdgcn_readfirstlane(l), __builtin_amdgcn_readfirstlane(h), lohi);
+      if (a < D) {
+        al[a] = sp;
+        part += pv[a] * sp;
+      }
+    }
     const double alpha = nu / h_block_sum(part, red);
-    for (int a = threadIdx.x; a < D; a += blockDim.x) {
-      rv[a] = rv[a] - av[a] * alpha;
-      xv[a] = xv[a] + pv[a] * alpha;
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m) {
+      const int a = t + m * HARD_PCG_THREADS;
+      if (a < D) {
+        rv[a] = rv[a] - al[a] * alpha;
+        xv[m] = xv[m] + pv[a] * alpha;
+      }
     }
     __syncthreads();
-    apply_P(rv, zv);
-    __syncthreads();
     part = 0.0;
-    for (int a = threadIdx.x; a < D; a += blockDim.x) part += rv[a] * zv[a];
+#pragma unroll 1
+    for (int m = 0; m < SLOTS; ++m) {
+      const int a = t + m * HARD_PCG_THREADS;
+      if (a < D) {
+        const double z = apply_P(a);
+        zl[a] = z;
+        part += rv[a] * z;
+      }
+    }
     const double nup = h_block_sum(part, red);
     if (fabs(nup) < tol) {
       it_done = it + 1;
       break;
     }
     const double beta = nup / nu;
-    for (int a = threadIdx.x; a < D; a += blockDim.x) pv[a] = zv[a] + pv[a] * beta;
+    // p is rewritten only after every thread's S p and P^-1 r reads of this iteration (h_block_sum's barriers)
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m) {
+      const int a = t + m * HARD_PCG_THREADS;
+      if (a < D) pv[a] = zl[a] + pv[a] * beta;
+    }
     nu = nup;
   }
-  __syncthreads();
-  for (int a = threadIdx.x; a < D; a += blockDim.x) lam[(size_t)b * dmax + a] = xv[a];
-  if (threadIdx.x == 0) iters[b] = it_done;
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * HARD_PCG_THREADS;
+    if (a < D) lam[(size_t)b * dmax + a] = xv[m];
+  }
+  if (t == 0) iters[b] = it_done;
 }
 
 // Method S (and N): S lambda = gamma by banded elimination (S is negative definite: no pivoting).
@@ -575,8 +648,8 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int N, int NX, int W
   // M = S inside the row ranges, zero elsewhere; Wr = the half-bandwidth of those ranges, which the
   // elimination's fill-in never leaves (no pivoting)
   for (int e = threadIdx.x; e < D * BW; e += blockDim.x) {
-    const int a = e / BW, c = a - W + (e - a * BW);
-    Mb[e] = (c >= rg[2 * a] && c <= rg[2 * a + 1]) ? S[e] : 0.0;
+    const int a = e / BW, o = e - a * BW, c = a - W + o;
+    Mb[e] = (c >= rg[2 * a] && c <= rg[2 * a + 1]) ? S[(size_t)o * dmax + a] : 0.0;
   }
   for (int a = threadIdx.x; a < D; a += blockDim.x) atomicMax(&s_wr, max(a - rg[2 * a], rg[2 * a + 1] - a));
   for (int a = threadIdx.x; a < D; a += blockDim.x) y[a] = gam[(size_t)b * dmax + a];
@@ -783,9 +856,17 @@ struct LaunchHard {
                            h.hoff, h.cnt, h.hcol, h.hsgn, h.Sb, h.gam, h.M, h.rhs, h.lam, h.sing,
                            h.rng);
       } else {
-        const size_t lds = ((size_t)5 * h.dmax + 16) * sizeof(double);
-        hipLaunchKernelGGL((k_hard_pcg<NX>), dim3(B), dim3(256), lds, s, B, h.W, h.dmax, h.precond, h.active, h.dim,
-                           h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, h.Ptmp, h.lam, h.iters, h.rng);
+        size_t lds = ((size_t)4 * h.dmax + 16) * sizeof(double);
+        if (const char* e = getenv("TMPC_HARD_PCG_LDS_KB")) lds = std::max(lds, (size_t)atoi(e) * 1024);   // dev: residency sweep
+        const int slots = (h.dmax + HARD_PCG_THREADS - 1) / HARD_PCG_THREADS;
+#define HPCG(SL) hipLaunchKernelGGL((k_hard_pcg<NX, SL>), dim3(B), dim3(HARD_PCG_THREADS), lds, s, B, h.W, h.dmax, \
+                                    h.precond, h.active, h.dim, h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, h.Ptmp, \
+                                    h.Ptr, h.lam, h.iters, h.rng)
+        if (slots <= 4) HPCG(4);
+        else if (slots <= 8) HPCG(8);
+        else if (slots <= 12) HPCG(12);
+        else HPCG(16);
+#undef HPCG
       }
     } else if (h.phase == 2) {
       hipLaunchKernelGGL((k_hard_dxu<NJ>), HGRID(B * N, 64), 0, s, h.C, B, N, h.dmax, h.rmax, h.active, h.Ghat,
@@ -815,9 +896,12 @@ int launch_hard(hipStream_t s, int nj, const HardArgs& h) {
 int hard_set_max_lds() {
   const int bytes = 160 * 1024;
   int err = 0;
-#define SETH(V) err |= (int)hipFuncSetAttribute((const void*)k_hard_pcg<V>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#define SETH1(V, SL) err |= (int)hipFuncSetAttribute((const void*)k_hard_pcg<V, SL>, \
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#define SETH(V) SETH1(V, 4) SETH1(V, 8) SETH1(V, 12) SETH1(V, 16)
   SETH(2) SETH(4) SETH(6) SETH(8) SETH(10) SETH(12) SETH(14)
 #undef SETH
+#undef SETH1
   return err;
 }
 

@@ -1811,8 +1811,13 @@ __global__ void __launch_bounds__(1024) k_alive_list(int B, const int* __restric
   for (int b = lo; b < hi; ++b)
     if (alive[b]) idx[o++] = b;
   if (t == nt - 1) {
+    // the lock-step loop sizes its grids by an earlier length (tmpc_api.cpp lockstep_loop): valid only
+    // while the list never grows -- host_slot[1] flags a violation, which the host turns into an error
+    if (host_slot) {
+      host_slot[0] = part[t];
+      if (part[t] > *cnt) host_slot[1] = 1;
+    }
     *cnt = part[t];
-    if (host_slot) *host_slot = part[t];
   }
 }
 
