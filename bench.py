@@ -267,6 +267,32 @@ def ilqr_backward_flops_per_knot(nx, nu):
     return 2 * (2 * nx ** 3 + 2 * nx * nx * nu + nu * nu * nx + nx * nx * nu) + 2 * (nx + 1) * nu * nu
 
 
+def hard_limits(preset):
+    """the preset has ACTIVE_SET / FULL_SET (hard) rows"""
+    return any(v["mode"] in ("ACTIVE_SET", "FULL_SET") for v in LIMIT_PRESETS[preset].values())
+
+
+def hard_roofline(a, kernels, hard_bytes):
+    """Roofline of k_hard_pcg, the hard-limit path's dominant kernel: the banded Schur complement and the
+    preconditioner blocks stream from HBM every PCG iteration (too large for LDS: ~0.4 MB per problem), so
+    it is HBM-bound.  `achieved` = the algorithmic bytes the kernel itself counts (tmpc_kernel_bytes,
+    DESIGN.md 4f: the band's structural entries and the preconditioner entries each iteration reads, gamma
+    in, lambda out, the setup blocks) / the average launch time."""
+    hp = kernels["hard_pcg"]
+    per_launch = hard_bytes / hp["launches"]
+    avg_s = hp["avg_ms"] / 1e3
+    ach = per_launch / avg_s / 1e9
+    traffic, src = measured_traffic("void tmpc::k_hard_pcg<", workload_key(a))
+    out = {"kernel": "k_hard_pcg", "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "avg_launch_ms": hp["avg_ms"],
+           "algorithmic_bytes_per_launch": per_launch,
+           "bytes_basis": "counted by the kernel per problem: 8 B x (2 D + iterations x band entries + "
+                          "(iterations + 1) x preconditioner entries + setup blocks), DESIGN.md 4f"}
+    if traffic:
+        out.update(hbm_GBps=traffic / avg_s / 1e9, traffic_source=src)
+    return out
+
+
 def sqp_roofline(a, N, nx, nu, kernels, counters):
     """Roofline of the dominant kernel k_qp (Schur + PCG + dxu fused, one workgroup per problem).
     frac uses SURVEY §8(d)'s algorithmic flops (f_pcg per PCG iteration); the kernel keeps S and
@@ -486,6 +512,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = comm.max(t1 - t0)
     ctx.set_options(profile=0)
+    hard_bytes = ctx.kernel_bytes("hard_pcg") if limits and a.method != "S" and hard_limits(a.limits) else None
 
     kernels = {}
     for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "schur", "btsolve", "dxu", "ls_terms", "ls_decide",
@@ -531,8 +558,7 @@ def main():
     headline = a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and not limits and \
         a.cost == "quadratic" and N == 64 and a.precision == "fp64"
     if a.limits != "none":
-        hard = any(v["mode"] in ("ACTIVE_SET", "FULL_SET") for v in LIMIT_PRESETS[a.limits].values())
-        name += f", {'hard' if hard else 'soft'} box constraints {a.limits}"
+        name += f", {'hard' if hard_limits(a.limits) else 'soft'} box constraints {a.limits}"
     if a.cost == "ee":
         name += ", UrdfCost end-effector cost (twolinks.py goal)"
     if a.mpc_steps > 0:
@@ -561,6 +587,8 @@ def main():
     elif a.solver == "sqp" and a.method.startswith("PCG") and a.mpc_steps > 0 and "qp" in kernels and N * nx > 1024:
         # config 5 with SQP horizon solves: the GM QP kernel streams S / P^-1 rows (HBM roofline)
         roofline = sqp_roofline(a, N, nx, nu, kernels, counters)
+    elif hard_bytes and "hard_pcg" in kernels:
+        roofline = hard_roofline(a, kernels, hard_bytes)
     elif a.solver == "ilqr" and "ilqr_backward" in kernels:
         bw = kernels["ilqr_backward"]
         per_launch = int(counters[0]) / max(1, bw["launches"])

@@ -313,6 +313,11 @@ int tmpc_synchronize(tmpc_ctx* ctx);
  * "btsolve", "dxu", "ls_terms", "ls_decide", "hard_schur", "hard_pcg", "hard_direct", "ilqr_backward",
  * "ilqr_forward", "ilqr_decide", "mpc_shift", "pcg" (tmpc_pcg_batch / tmpc_hard_pcg_batch). */
 int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
+/* Algorithmic HBM bytes moved by a kernel that counts them, summed over its launches since the last
+ * tmpc_reset_stats (any options.profile): "hard_pcg" (the hard-limit PCG of tmpc_sqp_solve_batch* /
+ * tmpc_qp_batch: per launch and problem 8 B x (2 D + iterations x band entries + (iterations + 1) x
+ * preconditioner entries + setup blocks)).  Other names fail. */
+int tmpc_kernel_bytes(tmpc_ctx* ctx, const char* name, double* bytes);
 int tmpc_reset_stats(tmpc_ctx* ctx);
 
 /* Work counters of the last solve call on this context: [0] problem-QPs solved (iLQR: problem-

@@ -390,11 +390,31 @@ def test_hard_pcg_on_oracle_S_is_exact(name, N, ptype, seed):
         gb[i, :len(gm)] = gm
     ctx = _native.default_context(0)
     ctx.set_model(m)
+    ctx.reset_stats()
     lam, it = ctx.hard_pcg_batch(Sb, gb, dims, nx, ptype)
     for i, (S, gm) in enumerate(zip(Ss, gs)):
         lam_c, it_c = ohard.pcg_canonical(S, gm, nx, ptype, 1e-6, 100)
         assert int(it[i]) == it_c, (i, int(it[i]), it_c)
         assert np.array_equal(lam[i, :len(gm)], lam_c), i
+    # the kernel's own algorithmic-byte count (the hard bench line's roofline), exactly
+    assert ctx.kernel_bytes("hard_pcg") == _hard_pcg_bytes(Ss, it, nx, ptype)
+
+
+def _hard_pcg_bytes(Ss, iters, nx, ptype):
+    """8 B x (2 D + it x band entries + (it + 1) x preconditioner entries + setup blocks) per problem; band
+    entries: each row's first..last nonzero column (with the diagonal), the range the kernel visits."""
+    tot = 0.0
+    for S, it in zip(Ss, iters):
+        D = S.shape[0]
+        nnz = 0
+        for a in range(D):
+            nzc = np.nonzero(S[a])[0]
+            nnz += max(a, int(nzc.max(initial=a))) - min(a, int(nzc.min(initial=a))) + 1
+        nb, b2 = D // nx, nx * nx
+        pnnz, setup = {"0": (0, 0), "J": (D, 0), "BJ": (nb * b2, 2 * nb * b2),
+                       "SS": ((3 * nb - 2) * b2, (4 * nb - 2) * b2) if nb else (0, 0)}[ptype]
+        tot += 8.0 * (2.0 * D + int(it) * nnz + (int(it) + 1.0) * pnnz + setup)
+    return tot
 
 
 def test_hard_singular_duplicate_rows():

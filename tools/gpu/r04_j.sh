@@ -1,4 +1,4 @@
-# round 4 (j): hard PCG slot loops one slot at a time, z and S p in LDS (131 VGPRs, 3 waves per SIMD)
+# round 4 (j): hard PCG slot loops one slot at a time, z and S p in LDS; kernel-counted algorithmic bytes (hard roofline)
 # hard tests (bitwise canonical parity), the hard bench line, FETCH_SIZE of hard_pcg
 set -o pipefail
 cd /root/repo

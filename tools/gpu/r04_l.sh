@@ -1,0 +1,8 @@
+# round 4 (l): k_hard_pcg setup element-parallel in LDS; k_hard_schur rows in registers, diagonal walk, no scratch: hard tests, probe, hard bench
+set -o pipefail
+cd /root/repo
+O=/root/repo/gpurun_out/r04l; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_hard.py > $O/hard_tests.log 2>&1; echo "tests rc=$?" >> $O/rc.txt
+timeout -k 10 300 python tools/debug/r04_hardpcg_probe.py 352 1024 > $O/probe.json 2> $O/probe.err; echo "probe rc=$?" >> $O/rc.txt
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 --batch 1024 --limits torque-velocity-as --no-cpu-baseline > $O/hard.json 2> $O/hard.err; echo "bench rc=$?" >> $O/rc.txt
+exit 0

@@ -111,6 +111,7 @@ SIGNATURES = {
     "tmpc_kernel_stats": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.POINTER(C.c_double)]),
     "tmpc_reset_stats": (C.c_int, [C.c_void_p]),
     "tmpc_solve_counters": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+    "tmpc_kernel_bytes": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_double)]),
     "tmpc_comm_get_unique_id": (C.c_int, [C.c_void_p]),
     "tmpc_comm_create": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]),
     "tmpc_comm_destroy": (None, [C.c_void_p]),
@@ -497,6 +498,12 @@ class Context:
         ms = C.c_double(0.0)
         self._check(self.lib.tmpc_kernel_stats(self.h, name.encode(), C.byref(n), C.byref(ms)), "tmpc_kernel_stats")
         return int(n.value), float(ms.value)
+
+    def kernel_bytes(self, name):
+        """Algorithmic HBM bytes a counting kernel ("hard_pcg") moved since reset_stats (tmpc_kernel_bytes)."""
+        v = C.c_double(0.0)
+        self._check(self.lib.tmpc_kernel_bytes(self.h, name.encode(), C.byref(v)), "tmpc_kernel_bytes")
+        return float(v.value)
 
     def solve_counters(self):
         """[problem-QPs, PCG iterations, gradient recomputations, line-search trials per QP] of the last solve."""

@@ -66,6 +66,7 @@ struct tmpc_ctx {
   // the last tmpc_qp_batch with hard limits (tmpc_qp_hard_info reads its hd_* buffers); cleared by every
   // other user of those buffers (setup_hard) and by a change of the limits, so stale data is refused
   struct { int B, N, dmax, W, rmax; } hard_last{0, 0, 0, 0, 0};
+  std::map<std::string, double> kbytes;   // algorithmic HBM bytes of counting kernels since tmpc_reset_stats
 };
 
 static int fail(tmpc_ctx* c, const char* fmt, ...) {
@@ -492,6 +493,23 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
   }
   BUF(double, hd_terms, (size_t)B * (T > 0 ? T : 1) * N);
   hard.hterms = hd_terms;
+  if (precond != 0) {
+    BUF(double, hd_work, (size_t)B);
+    HIP_OK(hipMemsetAsync(hd_work, 0, (size_t)B * sizeof(double), ctx->stream));
+    hard.work = hd_work;
+  }
+  return 0;
+}
+
+// add the per-problem algorithmic bytes k_hard_pcg counted in this solve to ctx->kbytes["hard_pcg"]
+static int collect_hard_work(tmpc_ctx* ctx, const HardArgs& hard) {
+  if (!hard.work) return 0;
+  std::vector<double> w(hard.B);
+  HIP_OK(hipMemcpyAsync(w.data(), hard.work, sizeof(double) * hard.B, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  double sum = 0.0;
+  for (double v : w) sum += v;
+  ctx->kbytes["hard_pcg"] += sum;
   return 0;
 }
 
@@ -738,6 +756,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   ctx->last_counters[1] = (int64_t)hc[1];
   ctx->last_counters[2] = (int64_t)hc[2];
   ctx->last_counters[3] = (int64_t)T;
+  if (w.hard && (rc = collect_hard_work(ctx, hard))) return rc;
   resolve_timings(ctx);
   if (tr_out) *tr_out = tr;
   return 0;
@@ -1474,6 +1493,7 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
     return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (ctx->hlim.any_hard) {
+    if ((rc = collect_hard_work(ctx, hard))) return rc;
     ctx->hard_last = {B, N, hard.dmax, hard.W, hard.rmax};
     std::vector<int> roff((size_t)B * N);
     std::vector<double> lh((size_t)B * hard.dmax);
@@ -1643,11 +1663,15 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
   h.lam = hp_lam;
   h.iters = hp_it;
   h.rng = hp_rng;
+  int rc;
+  BUF(double, hp_work, (size_t)B);
+  HIP_OK(hipMemsetAsync(hp_work, 0, sizeof(double) * B, ctx->stream));
+  h.work = hp_work;
   {
     Timed t(ctx, "hard_pcg");
     LAUNCH_OK(launch_hard(ctx->stream, nx / 2, h));
   }
-  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if ((rc = collect_hard_work(ctx, h))) return rc;
   resolve_timings(ctx);
   if (lambda) HIP_OK(hipMemcpy(lambda, hp_lam, sizeof(double) * B * dmax, hipMemcpyDeviceToHost));
   if (iters) HIP_OK(hipMemcpy(iters, hp_it, sizeof(int) * B, hipMemcpyDeviceToHost));
@@ -1756,6 +1780,14 @@ int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double
   return 0;
 }
 
+int tmpc_kernel_bytes(tmpc_ctx* ctx, const char* name, double* bytes) {
+  if (!ctx || !name || !bytes) return -1;
+  if (std::string(name) != "hard_pcg") return fail(ctx, "kernel '%s' does not count its bytes (counting: hard_pcg)", name);
+  auto it = ctx->kbytes.find(name);
+  *bytes = it == ctx->kbytes.end() ? 0.0 : it->second;
+  return 0;
+}
+
 int tmpc_solve_counters(tmpc_ctx* ctx, int64_t* counters) {
   if (!ctx || !counters) return -1;
   for (int i = 0; i < 4; ++i) counters[i] = ctx->last_counters[i];
@@ -1766,6 +1798,7 @@ int tmpc_reset_stats(tmpc_ctx* ctx) {
   if (!ctx) return -1;
   resolve_timings(ctx);
   ctx->stats.clear();
+  ctx->kbytes.clear();
   return 0;
 }
 

@@ -194,45 +194,24 @@ __device__ __forceinline__ int row_piece(int kind, int knot, int idx, int p, con
                                          const double* __restrict__ Bm, const int* hcol, const double* hsgn,
                                          double (&cf)[3 * NJ]) {
   constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
-  for (int m = 0; m < NXU; ++m) cf[m] = 0.0;
+  // unit vectors by compare-select over the (unrolled) entries: no dynamic index into cf (no scratch)
   if (kind == 1) {
-    if (p) return -1;
-    cf[hcol[idx]] = hsgn[idx];
-    return knot;
+    const int col = hcol[idx];
+    const double sg = hsgn[idx];
+#pragma unroll
+    for (int m = 0; m < NXU; ++m) cf[m] = m == col ? sg : 0.0;
+    return p ? -1 : knot;
   }
   if (knot == 0 || p == 1) {
-    if (knot == 0 && p == 1) return -1;
-    cf[idx] = 1.0;
-    return knot;
+#pragma unroll
+    for (int m = 0; m < NXU; ++m) cf[m] = m == idx ? 1.0 : 0.0;
+    return (knot == 0 && p == 1) ? -1 : knot;
   }
   const double* Ak = A + (size_t)(knot - 1) * NX * NX;
   const double* Bk = Bm + (size_t)(knot - 1) * NX * NU;
   for (int m = 0; m < NX; ++m) cf[m] = -Ak[idx * NX + m];
   for (int m = 0; m < NU; ++m) cf[NX + m] = -Bk[idx * NU + m];
   return knot - 1;
-}
-
-// y = Ghat_k cf over [x; u] (terminal knot: x block only)
-template <int NJ>
-__device__ __forceinline__ void ghat_apply(const CostDev* C, const HGhat<NJ>& Gh, int k, int N,
-                                           const double (&cf)[3 * NJ], double (&y)[3 * NJ]) {
-  constexpr int NX = 2 * NJ, NU = NJ;
-  const double* Gx = Gh.x(C, k, N);
-  for (int r = 0; r < NX; ++r) {
-    double acc = 0.0;
-    for (int c = 0; c < NX; ++c) acc += Gx[r * NX + c] * cf[c];
-    y[r] = acc;
-  }
-  if (k < N - 1) {
-    const double* Gu = Gh.u(k);
-    for (int r = 0; r < NU; ++r) {
-      double acc = 0.0;
-      for (int c = 0; c < NU; ++c) acc += Gu[r * NU + c] * cf[NX + c];
-      y[NX + r] = acc;
-    }
-  } else {
-    for (int r = 0; r < NU; ++r) y[NX + r] = 0.0;
-  }
 }
 
 // S band and gamma.  Phase 1: per row and piece, Y = Ghat cf (global scratch [dmax][2][NXU] per
@@ -252,8 +231,8 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
                                                     double* __restrict__ Sb, double* __restrict__ gam,
                                                     int* __restrict__ rng) {
   constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
-  extern __shared__ int s_piece[];   // [N] first row, [N] last row touching each knot piece
-  __shared__ int s_wt;
+  extern __shared__ double s_grad[];   // [N][NXU] cost gradient per knot, then s_piece
+  int* s_piece = reinterpret_cast<int*>(s_grad + N * NXU);   // [N] first row, [N] last row touching each knot piece
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int K = N - 1;
@@ -270,6 +249,12 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
   double* Yb = Y + (size_t)b * dmax * 2 * NXU;
   int* PKb = PK + (size_t)b * dmax * 2;
   const size_t hb = (size_t)b * N * rmax;
+  // phase 0: the cost gradient of every knot (0 for the terminal knot's u part)
+  for (int e = threadIdx.x; e < N * NXU; e += blockDim.x) {
+    const int k = e / NXU, m = e - k * NXU;
+    s_grad[e] = (m < NX || k < K) ? hard_grad<NJ>(C, xb, ub, js, N, k, m) : 0.0;
+  }
+  __syncthreads();
   // phase 1
   for (int a = threadIdx.x; a < D; a += blockDim.x) {
     const int kind = rk[a], knot = rn[a], idx = ri[a];
@@ -277,14 +262,35 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     const double* hs = hsgn + hb + (size_t)knot * rmax;
     double g_dot = 0.0;
     for (int p = 0; p < 2; ++p) {
-      double cf[3 * NJ], y[3 * NJ];
+      double cf[3 * NJ];
       const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
       PKb[a * 2 + p] = kp;
       if (kp < 0) continue;
-      ghat_apply<NJ>(C, Gh, kp, N, cf, y);
-      for (int m = 0; m < NXU; ++m) Yb[((size_t)a * 2 + p) * NXU + m] = y[m];
+      // y = Ghat_kp cf (terminal knot: x block only), written out row by row, and s = y . g in the
+      // same order; the row loops stay rolled so one Ghat row's loads are live at a time
+      double* yo = Yb + ((size_t)a * 2 + p) * NXU;
+      const double* gk = s_grad + kp * NXU;
+      const double* Gx = Gh.x(C, kp, N);
       double s = 0.0;
-      for (int m = 0; m < NXU; ++m) s += y[m] * (m < NX || kp < K ? hard_grad<NJ>(C, xb, ub, js, N, kp, m) : 0.0);
+#pragma unroll 1
+      for (int r = 0; r < NX; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < NX; ++c) acc += Gx[r * NX + c] * cf[c];
+        yo[r] = acc;
+        s += acc * gk[r];
+      }
+      const double* Gu = Gh.u(kp);
+#pragma unroll 1
+      for (int r = 0; r < NU; ++r) {
+        double acc = 0.0;
+        if (kp < K) {
+#pragma unroll
+          for (int c = 0; c < NU; ++c) acc += Gu[r * NU + c] * cf[NX + c];
+        }
+        yo[NX + r] = acc;
+        s += acc * gk[NX + r];
+      }
       g_dot += s;
     }
     double ca;
@@ -299,7 +305,6 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     s_piece[k] = D;
     s_piece[N + k] = -1;
   }
-  if (threadIdx.x == 0) s_wt = 1;
   __syncthreads();
   for (int a = threadIdx.x; a < D; a += blockDim.x)
     for (int p = 0; p < 2; ++p) {
@@ -322,40 +327,63 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     hi = min(hi, min(D - 1, a + W));
     rb[2 * a] = lo;
     rb[2 * a + 1] = hi;
-    atomicMax(&s_wt, hi - lo + 1);
   }
   __syncthreads();
-  // phase 2: the band inside the row ranges, row a, column c = lo_a + o (stored at [c - a + W][a]);
-  // entries outside the ranges are never read (band_at / the PCG product / k_hard_direct's copy)
+  // phase 2: the band inside the row ranges, row a, column c (stored at [c - a + W][a]); entries outside
+  // the ranges are never read (band_at / the PCG product / k_hard_direct's copy).  Each thread keeps its
+  // row's two coefficient vectors in registers and the wave walks the diagonals of its rows (the stores
+  // of one diagonal are contiguous); S_ac = -(sum over pieces p of a, q of c on one knot of cf_ap . Y_cq)
   const int BW = 2 * W + 1;
-  const int Wt = s_wt;
   double* S = Sb + (size_t)b * dmax * BW;
-  for (int e = threadIdx.x; e < D * Wt; e += blockDim.x) {   // consecutive threads: consecutive rows
-    const int j = e / D, a = e - j * D;
-    const int c = rb[2 * a] + j;
-    if (c > rb[2 * a + 1]) continue;
-    const int o = c - a + W;
-    double s = 0.0;
-    {
+  for (int a0 = threadIdx.x & ~63; a0 < D; a0 += blockDim.x) {   // wave-uniform: the wave's first row
+    const int a = a0 + (threadIdx.x & 63);
+    const bool own = a < D;
+    double cf0[3 * NJ], cf1[3 * NJ];
+    int kp0 = -1, kp1 = -1, ol = BW, oh = -1;
+    if (own) {
       const int kind = rk[a], knot = rn[a], idx = ri[a];
       const int* hc = hcol + hb + (size_t)knot * rmax;
       const double* hs = hsgn + hb + (size_t)knot * rmax;
-      for (int p = 0; p < 2; ++p) {
-        double cf[3 * NJ];
-        const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
-        if (kp < 0) continue;
+      kp0 = row_piece<NJ>(kind, knot, idx, 0, A, Bm, hc, hs, cf0);
+      kp1 = row_piece<NJ>(kind, knot, idx, 1, A, Bm, hc, hs, cf1);
+      ol = rb[2 * a] - a + W;
+      oh = rb[2 * a + 1] - a + W;
+    }
+    int l = ol, h = oh;
+    for (int off = 32; off > 0; off >>= 1) {
+      l = min(l, __shfl_xor(l, off, 64));
+      h = max(h, __shfl_xor(h, off, 64));
+    }
+    l = __builtin_amdgcn_readfirstlane(l);
+    h = __builtin_amdgcn_readfirstlane(h);
+    for (int o = l; o <= h; ++o) {
+      if (o < ol || o > oh) continue;
+      const int c = a - W + o;
+      const int pc0 = PKb[c * 2], pc1 = PKb[c * 2 + 1];
+      double sum = 0.0;
+      auto piece = [&](const double(&cf)[3 * NJ], int kp) {   // pieces q of column c on row a's knot kp
+        if (kp < 0) return;
+#pragma unroll 1
         for (int q = 0; q < 2; ++q) {
-          if (PKb[c * 2 + q] != kp) continue;
+          if ((q ? pc1 : pc0) != kp) continue;   // (q loop rolled: one Y vector's loads live at a time)
           const double* y = Yb + ((size_t)c * 2 + q) * NXU;
           double d = 0.0;
+#pragma unroll
           for (int m = 0; m < NXU; ++m) d += cf[m] * y[m];
-          s += d;
+          sum += d;
         }
-      }
-      s = -s;
+      };
+      piece(cf0, kp0);
+      piece(cf1, kp1);
+      S[(size_t)o * dmax + a] = -sum;
     }
-    S[(size_t)o * dmax + a] = s;
   }
+}
+
+// doubles of LDS k_hard_pcg uses before its reduction slots: r, p, z, S p of dmax rows, and at least
+// four nx x nx blocks (with their pivot rows / columns) for the preconditioner setup
+__host__ __device__ constexpr int hard_pcg_scratch(int dmax, int nx) {
+  return 4 * dmax > 4 * (nx * nx + 2 * nx) ? 4 * dmax : 4 * (nx * nx + 2 * nx);
 }
 
 // ---- workgroup sum (deterministic): wave DPP butterfly via shuffles + fixed-order fan-in
@@ -375,43 +403,15 @@ __device__ __forceinline__ double band_at(const double* S, const int* rg, int dm
   return (c >= rg[2 * r] && c <= rg[2 * r + 1]) ? S[(size_t)(c - r + W) * dmax + r] : 0.0;
 }
 
-// In-place Gauss-Jordan inverse of a small block (global memory, one thread), the operation order of
-// the augmented [M | I] elimination (no pivoting: principal blocks of the negative definite S).
-__device__ void h_gj_inverse(double* M, int n) {
-  for (int p = 0; p < n; ++p) {
-    const double d = M[p * n + p];
-    for (int j = 0; j < n; ++j) M[p * n + j] = (j == p) ? 1.0 / d : M[p * n + j] / d;
-    for (int r = 0; r < n; ++r) {
-      if (r == p) continue;
-      const double f = M[r * n + p];
-      M[r * n + p] = 0.0;
-      for (int j = 0; j < n; ++j) M[r * n + j] -= f * M[p * n + j];
-    }
-  }
-}
-
-// out = -(X (Y Z)) for n x n blocks (row-major), one thread
-__device__ void h_neg_triple(const double* X, const double* Yy, const double* Z, double* out, int n) {
-  for (int r = 0; r < n; ++r)
-    for (int c = 0; c < n; ++c) {
-      double acc = 0.0;
-      for (int m = 0; m < n; ++m) {
-        double yz = 0.0;
-        for (int l = 0; l < n; ++l) yz += Yy[m * n + l] * Z[l * n + c];
-        acc += X[r * n + m] * yz;
-      }
-      out[r * n + c] = -acc;
-    }
-}
-
 // Preconditioner (compute_preconditioner on the dense S, PCG.py:113-212) + PCG (:66-111).
 // Pd [nb][NX][NX] diagonal inverses, Pl [nb-1][NX][NX] = P_{k+1,k} (P_{k,k+1} = Pl[k]^T: the
-// reference copies transposes), scratch [NX][NX] per problem for the off-diagonal products.
+// reference copies transposes); Ptr and Ptmp hold their transposes (column j of a block contiguous),
+// the layout P^-1 r reads.
 // Thread t owns rows t, t + 256, ... (slot m = row / 256 < SLOTS): x of its rows stays in its registers;
-// r and p, which other rows read, and z and S p are in LDS (4 dmax doubles: several problems per CU).  Every global read is coalesced: S p walks the wave's diagonals of the band (each
+// r and p, which other rows read, and z and S p are in LDS (4 dmax doubles: several problems per CU).
+// Every global read of the iterations is coalesced: S p walks the wave's diagonals of the band (each
 // lane adds the diagonals inside its row's range, in column order), and the preconditioner rows are read
-// from transposed copies of the P blocks (column j of a block: the 12 rows' entries contiguous).
-// Every sum keeps the canonical order (oracle/hard.py pcg_canonical).
+// from the transposed blocks.  Every sum keeps the canonical order (oracle/hard.py pcg_canonical).
 template <int NX, int SLOTS>
 __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int dmax, int precond,
                                                               const int* __restrict__ active,
@@ -420,7 +420,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
                                                               double* __restrict__ Pd, double* __restrict__ Pl,
                                                               double* __restrict__ Ptmp, double* __restrict__ Ptr,
                                                               double* __restrict__ lam, int* __restrict__ iters,
-                                                              const int* __restrict__ rng) {
+                                                              const int* __restrict__ rng, double* __restrict__ work) {
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
@@ -435,49 +435,89 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   double* T = Ptmp + (size_t)b * nbmax * NX * NX;
   double* PT = Ptr + (size_t)b * nbmax * NX * NX;
   extern __shared__ __align__(16) double sh[];
-  double* rv = sh;
+  double* rv = sh;                 // r, p, z and S p of the rows (z, S p: read and written by the owner only)
   double* pv = rv + dmax;
-  double* red = pv + dmax;
-  double* zl = red + 16;   // z and S p of the rows (each read and written by its owner thread only)
+  double* zl = pv + dmax;
   double* al = zl + dmax;
+  double* red = sh + hard_pcg_scratch(dmax, NX);
   const bool blocks = precond == PRECOND_BJ || precond == PRECOND_SS;
   if (blocks) {
-    for (int k = t; k < nb; k += HARD_PCG_THREADS) {
-      double* M = P + (size_t)k * NX * NX;
-      for (int i = 0; i < NX; ++i)
-        for (int j = 0; j < NX; ++j) M[i * NX + j] = band_at(S, rg, dmax, W, k * NX + i, k * NX + j);
-      h_gj_inverse(M, NX);
-    }
-    __syncthreads();
-    if (precond == PRECOND_SS) {
-      for (int k = 1 + t; k < nb; k += HARD_PCG_THREADS) {
-        double* Sk = T + (size_t)k * NX * NX;
-        if (k & 1) {   // P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1})
-          for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, dmax, W, k * NX + i, (k - 1) * NX + j);
-          h_neg_triple(P + (size_t)k * NX * NX, Sk, P + (size_t)(k - 1) * NX * NX, PL + (size_t)(k - 1) * NX * NX, NX);
-        } else {       // P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk); stored as its transpose P_{k,k-1}
-          for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) Sk[i * NX + j] = band_at(S, rg, dmax, W, (k - 1) * NX + i, k * NX + j);
-          double* prod = PT + (size_t)k * NX * NX;   // PT[k] is free until the transposed copies below
-          h_neg_triple(P + (size_t)(k - 1) * NX * NX, Sk, P + (size_t)k * NX * NX, prod, NX);
-          for (int i = 0; i < NX; ++i)
-            for (int j = 0; j < NX; ++j) PL[(size_t)(k - 1) * NX * NX + j * NX + i] = prod[i * NX + j];
+    // The setup runs on the whole workgroup, element-parallel, staged in the LDS that r, p, z, S p use
+    // later: each element of a block keeps the canonical (oracle/hard.py) operation sequence, so the
+    // blocks equal the oracle's bit for bit.
+    constexpr int B2 = NX * NX;
+    // (1) diagonal blocks: Gauss-Jordan on the augmented [M | I] without pivoting (oracle/hard.py _gj_inverse), `cap` blocks
+    //     at a time; per pivot p the new pivot row and the old column p are snapshotted first
+    const int cap = hard_pcg_scratch(dmax, NX) / (B2 + 2 * NX);
+    double* prow = sh + (size_t)cap * B2;
+    double* fcol = prow + (size_t)cap * NX;
+    for (int k0 = 0; k0 < nb; k0 += cap) {
+      const int kc = min(cap, nb - k0);
+      __syncthreads();
+      for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
+        const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
+        sh[e] = band_at(S, rg, dmax, W, (k0 + kk) * NX + i, (k0 + kk) * NX + j);
+      }
+      for (int p = 0; p < NX; ++p) {
+        __syncthreads();
+        for (int e = t; e < kc * NX; e += HARD_PCG_THREADS) {
+          const int kk = e / NX, j = e - kk * NX;
+          const double* M = sh + (size_t)kk * B2;
+          const double d = M[p * NX + p];
+          prow[e] = (j == p) ? 1.0 / d : M[p * NX + j] / d;
+          fcol[e] = M[j * NX + p];
+        }
+        __syncthreads();
+        for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
+          const int kk = e / B2, r = (e - kk * B2) / NX, j = e - kk * B2 - r * NX;
+          if (r == p) {
+            sh[e] = prow[kk * NX + j];
+          } else {
+            const double f = fcol[kk * NX + r];
+            const double m0 = (j == p) ? 0.0 : sh[e];
+            sh[e] = m0 - f * prow[kk * NX + j];
+          }
         }
       }
       __syncthreads();
+      for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {   // P_kk and its transpose
+        const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
+        P[(size_t)(k0 + kk) * B2 + i * NX + j] = sh[e];
+        PT[(size_t)(k0 + kk) * B2 + j * NX + i] = sh[e];
+      }
     }
-    // transposed copies: PT[k] = P_kk^T; PLT[k] = Pl[k]^T (in T, free once the stair blocks are formed)
-    for (int k = t; k < nb; k += HARD_PCG_THREADS) {
-      const double* M = P + (size_t)k * NX * NX;
-      double* MT = PT + (size_t)k * NX * NX;
-      for (int i = 0; i < NX; ++i)
-        for (int j = 0; j < NX; ++j) MT[j * NX + i] = M[i * NX + j];
-      if (precond == PRECOND_SS && k + 1 < nb) {
-        const double* L = PL + (size_t)k * NX * NX;
-        double* LT = T + (size_t)k * NX * NX;
-        for (int i = 0; i < NX; ++i)
-          for (int j = 0; j < NX; ++j) LT[j * NX + i] = L[i * NX + j];
+    // (2) SS stair blocks (oracle/hard.py _neg_triple, both products summed in index order): odd k: P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1});
+    //     even k: P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk), stored transposed.  Pl[k-1] = P_{k,k-1}
+    //     row-major and T[k-1] = its transpose.  yz = Y Z staged in LDS, `cap2` stairs at a time.
+    if (precond == PRECOND_SS && nb > 1) {
+      const int cap2 = hard_pcg_scratch(dmax, NX) / B2;
+      for (int k0 = 1; k0 < nb; k0 += cap2) {
+        const int kc = min(cap2, nb - k0);
+        __syncthreads();   // P written (global, this workgroup) / the previous chunk's yz read
+        for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
+          const int kk = e / B2, r = (e - kk * B2) / NX, c = e - kk * B2 - r * NX;
+          const int k = k0 + kk;
+          const bool odd = k & 1;
+          const int yr = odd ? k : k - 1, yc = odd ? k - 1 : k;        // Y = S_{yr, yc}
+          const double* Z = P + (size_t)(odd ? k - 1 : k) * B2;
+          double yz = 0.0;
+          for (int l = 0; l < NX; ++l) yz += band_at(S, rg, dmax, W, yr * NX + r, yc * NX + l) * Z[l * NX + c];
+          sh[e] = yz;
+        }
+        __syncthreads();
+        for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
+          const int kk = e / B2, r = (e - kk * B2) / NX, c = e - kk * B2 - r * NX;
+          const int k = k0 + kk;
+          const bool odd = k & 1;
+          const double* X = P + (size_t)(odd ? k : k - 1) * B2;
+          const double* yz = sh + (size_t)kk * B2;
+          double acc = 0.0;
+          for (int m = 0; m < NX; ++m) acc += X[r * NX + m] * yz[m * NX + c];
+          const double v = -acc;
+          const int pr = odd ? r : c, pc = odd ? c : r;                 // element of P_{k,k-1}
+          PL[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
+          T[(size_t)(k - 1) * B2 + pc * NX + pr] = v;
+        }
       }
     }
     __syncthreads();
@@ -527,6 +567,15 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   // the thread's rows in LDS: unrolled over the slots they held every slot's loads and products in
   // registers at once (254 VGPRs, one wave per SIMD); x stays in registers.
   const int wbase = t & ~63;   // first row of this wave in slot 0
+  double nnz = 0.0;            // structural entries of the band (work accounting)
+  if (work) {
+#pragma unroll 1
+    for (int m = 0; m < SLOTS; ++m) {
+      const int a = t + m * HARD_PCG_THREADS;
+      if (a < D) nnz += rg[2 * a + 1] - rg[2 * a] + 1;
+    }
+    nnz = h_block_sum(nnz, red);
+  }
   double xv[SLOTS];
   const double* g = gam + (size_t)b * dmax;
 #pragma unroll
@@ -609,6 +658,17 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     if (a < D) lam[(size_t)b * dmax + a] = xv[m];
   }
   if (t == 0) iters[b] = it_done;
+  if (work && t == 0) {
+    // algorithmic HBM bytes of this launch: gamma in, lambda out; per iteration the
+    // band's structural entries (S p) and the preconditioner entries one P^-1 r reads, it_done + 1 of
+    // those; the setup reads the band's diagonal (and for SS sub-diagonal) blocks and writes P (and Pl)
+    const double b2 = (double)NX * NX;
+    double pnnz = 0.0, setup = 0.0;
+    if (precond == PRECOND_J) pnnz = D;
+    if (precond == PRECOND_BJ) { pnnz = nb * b2; setup = 2.0 * nb * b2; }
+    if (precond == PRECOND_SS && nb > 0) { pnnz = (3.0 * nb - 2.0) * b2; setup = (4.0 * nb - 2.0) * b2; }
+    work[b] += 8.0 * (2.0 * D + it_done * nnz + (it_done + 1.0) * pnnz + setup);
+  }
 }
 
 // Method S (and N): S lambda = gamma by banded elimination (S is negative definite: no pivoting).
@@ -847,7 +907,7 @@ struct LaunchHard {
                          h.hcol, h.hsgn, h.hval, h.hslot, h.amask, h.iter, h.Wtr, h.tr_active);
       hipLaunchKernelGGL(k_hard_layout, dim3(B), dim3(64), 0, s, B, N, NX, h.rmax, h.active, h.cnt, h.roff, h.hoff,
                          h.dim, h.rkind, h.rknot, h.ridx, h.dmax);
-      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), 2 * N * sizeof(int), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
+      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), N * (3 * NJ * sizeof(double) + 2 * sizeof(int)), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
                          h.per_knot, h.A, h.Bm, h.cvec, h.x, h.u, h.jsoft, h.dim, h.rkind, h.rknot, h.ridx, h.hoff,
                          h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam, h.rng);
     } else if (h.phase == 1) {
@@ -856,12 +916,12 @@ struct LaunchHard {
                            h.hoff, h.cnt, h.hcol, h.hsgn, h.Sb, h.gam, h.M, h.rhs, h.lam, h.sing,
                            h.rng);
       } else {
-        size_t lds = ((size_t)4 * h.dmax + 16) * sizeof(double);
+        size_t lds = ((size_t)hard_pcg_scratch(h.dmax, NX) + 16) * sizeof(double);
         if (const char* e = getenv("TMPC_HARD_PCG_LDS_KB")) lds = std::max(lds, (size_t)atoi(e) * 1024);   // dev: residency sweep
         const int slots = (h.dmax + HARD_PCG_THREADS - 1) / HARD_PCG_THREADS;
 #define HPCG(SL) hipLaunchKernelGGL((k_hard_pcg<NX, SL>), dim3(B), dim3(HARD_PCG_THREADS), lds, s, B, h.W, h.dmax, \
                                     h.precond, h.active, h.dim, h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, h.Ptmp, \
-                                    h.Ptr, h.lam, h.iters, h.rng)
+                                    h.Ptr, h.lam, h.iters, h.rng, h.work)
         if (slots <= 4) HPCG(4);
         else if (slots <= 8) HPCG(8);
         else if (slots <= 12) HPCG(12);

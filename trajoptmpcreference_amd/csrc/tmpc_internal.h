@@ -184,6 +184,7 @@ struct HardArgs {
   const int* iter;                // per-problem SQP iteration (trace row iter + 1)
   int Wtr;                        // trace row stride (max_iter_SQP_DDP + 1)
   unsigned long long* tr_active;  // [B][Wtr][N] trace copy of amask (nullable)
+  double* work;                   // [B] algorithmic HBM bytes of k_hard_pcg, accumulated per problem (nullable)
 };
 // k_hard_pcg: 256 threads per problem, row a on thread a % 256 (row slot a / 256, at most 16 slots)
 constexpr int HARD_PCG_THREADS = 256, HARD_PCG_MAX_SLOTS = 16;
