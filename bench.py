@@ -287,7 +287,7 @@ def hard_roofline(a, kernels, hard_bytes):
            "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "avg_launch_ms": hp["avg_ms"],
            "algorithmic_bytes_per_launch": per_launch,
            "bytes_basis": "counted by the kernel per problem: 8 B x (2 D + iterations x band entries + "
-                          "(iterations + 1) x preconditioner entries + setup blocks), DESIGN.md 4f"}
+                          "(iterations + 1) x distinct preconditioner entries + setup blocks), DESIGN.md 4f"}
     if traffic:
         out.update(hbm_GBps=traffic / avg_s / 1e9, traffic_source=src)
     return out

@@ -316,7 +316,7 @@ int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double
 /* Algorithmic HBM bytes moved by a kernel that counts them, summed over its launches since the last
  * tmpc_reset_stats (any options.profile): "hard_pcg" (the hard-limit PCG of tmpc_sqp_solve_batch* /
  * tmpc_qp_batch: per launch and problem 8 B x (2 D + iterations x band entries + (iterations + 1) x
- * preconditioner entries + setup blocks)).  Other names fail. */
+ * distinct preconditioner entries + setup blocks)).  Other names fail. */
 int tmpc_kernel_bytes(tmpc_ctx* ctx, const char* name, double* bytes);
 int tmpc_reset_stats(tmpc_ctx* ctx);
 

@@ -183,8 +183,8 @@ def preconditioner_dense(S, nx, ptype):
 # order (pcg_dense with preconditioner_dense, CPU-dependent) and a plain sequential order
 # stop up to 5 iterations apart on the arm3 cases of tests/test_gpu_hard.py.  So the oracle fixes
 # ONE order -- every sum sequential from 0.0 in index order, every product and sum rounded on its
-# own (no fused multiply-add), dot products as per-thread partials over 256 threads (row a on thread
-# a mod 256) reduced by a 64-lane xor butterfly and a fan-in over the 4 waves -- and the GPU's
+# own (no fused multiply-add), dot products as per-thread partials over PCG_THREADS = 1024 threads
+# (row a on thread a mod 1024) reduced by a 64-lane xor butterfly and a fan-in over the 16 waves -- and the GPU's
 # k_hard_pcg follows it operation for operation (tmpc_hard.hip, fp contraction off), so the two are
 # bitwise equal on identical S and gamma.  The reference's own fixtures pin both orders on their
 # integers except where a count is decided by the order itself: the pendulum ACTIVE_SET PCG-SS run's
@@ -223,22 +223,26 @@ def _neg_triple(X, Y, Z):
     return -acc
 
 
+PCG_THREADS = 1024   # k_hard_pcg's workgroup (tmpc_internal.h HARD_PCG_THREADS)
+
+
 def _dot(a, b):
-    """sum(a * b): per-thread partials (thread t sums rows t, t + 256, ... in order), a 64-lane xor
-    butterfly per wave, then the 4 wave totals in order."""
+    """sum(a * b): per-thread partials (thread t sums rows t, t + 1024, ... in order), a 64-lane xor
+    butterfly per wave, then the 16 wave totals in order."""
+    T = PCG_THREADS
     prod = a * b
     D = len(prod)
-    J = (D + 255) // 256
-    pad = np.zeros(J * 256)
+    J = (D + T - 1) // T
+    pad = np.zeros(J * T)
     pad[:D] = prod
-    part = np.zeros(256)
+    part = np.zeros(T)
     for j in range(J):
-        part = part + pad[j * 256:(j + 1) * 256]
-    idx = np.arange(256)
+        part = part + pad[j * T:(j + 1) * T]
+    idx = np.arange(T)
     for off in (32, 16, 8, 4, 2, 1):
         part = part + part[idx ^ off]
     s = 0.0
-    for w in range(4):
+    for w in range(T // 64):
         s = s + part[w * 64]
     return s
 

@@ -397,12 +397,52 @@ def test_hard_pcg_on_oracle_S_is_exact(name, N, ptype, seed):
         assert int(it[i]) == it_c, (i, int(it[i]), it_c)
         assert np.array_equal(lam[i, :len(gm)], lam_c), i
     # the kernel's own algorithmic-byte count (the hard bench line's roofline), exactly
-    assert ctx.kernel_bytes("hard_pcg") == _hard_pcg_bytes(Ss, it, nx, ptype)
+    assert ctx.kernel_bytes("hard_pcg") == _hard_pcg_bytes(Ss, it, nx, ptype, dmax)
 
 
-def _hard_pcg_bytes(Ss, iters, nx, ptype):
-    """8 B x (2 D + it x band entries + (it + 1) x preconditioner entries + setup blocks) per problem; band
-    entries: each row's first..last nonzero column (with the diagonal), the range the kernel visits."""
+@pytest.mark.parametrize("ptype", ["SS", "BJ", "J"])
+def test_hard_pcg_large_banded_is_exact(ptype):
+    """Schur dimensions past one 1024-row slot and past the LDS block cache (D = 1530: 94 of 127 diagonal
+    blocks fit, the rest stream from HBM; D = 1100 and 700 alongside, all cached), a trailing partial block
+    (1530 mod 12 = 6 unpreconditioned rows): counts and lambda bit for bit against pcg_canonical, and the
+    kernel's byte count exactly."""
+    from oracle import hard as ohard
+    from trajoptmpcreference_amd import _native
+    nx, W = 12, 30
+    rng = np.random.default_rng(7)
+    Ss, gs = [], []
+    for D in (1530, 1100, 700):
+        M = np.zeros((D, D))
+        for o in range(-W // 2, W // 2 + 1):
+            M += np.diag(rng.uniform(-1.0, 1.0, D - abs(o)), o)
+        Ss.append(-(M @ M.T + 2.0 * np.eye(D)))
+        gs.append(rng.uniform(-1.0, 1.0, D))
+    dims = [len(g) for g in gs]
+    dmax = max(dims)
+    Sb = np.zeros((len(Ss), dmax, 2 * W + 1))
+    gb = np.zeros((len(Ss), dmax))
+    for i, (S, gm) in enumerate(zip(Ss, gs)):
+        Sb[i, :len(gm)] = _band(S, W)
+        gb[i, :len(gm)] = gm
+    ctx = _native.default_context(0)
+    ctx.set_model(arm_model("arm6"))
+    ctx.reset_stats()
+    lam, it = ctx.hard_pcg_batch(Sb, gb, dims, nx, ptype, tol=1e-10, max_iter=200)
+    for i, (S, gm) in enumerate(zip(Ss, gs)):
+        lam_c, it_c = ohard.pcg_canonical(S, gm, nx, ptype, 1e-10, 200)
+        assert 5 < it_c < 200, it_c
+        assert int(it[i]) == it_c, (i, int(it[i]), it_c)
+        assert np.array_equal(lam[i, :len(gm)], lam_c), i
+    assert ctx.kernel_bytes("hard_pcg") == _hard_pcg_bytes(Ss, it, nx, ptype, dmax)
+
+
+def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
+    """8 B x (2 D + it x band entries + (it + 1) x streamed preconditioner entries + setup blocks) per
+    problem; band entries: each row's first..last nonzero column (with the diagonal), the range the kernel
+    visits; streamed preconditioner entries: the distinct blocks one P^-1 r needs (SS: nb diagonal + nb - 1
+    stair) less those the kernel keeps in LDS -- as many as fit in the 160 KB after its vectors, diagonal
+    blocks first (tmpc_hard.hip hard_pcg_cache_offset)."""
+    slots = -(-dmax // 1024)
     tot = 0.0
     for S, it in zip(Ss, iters):
         D = S.shape[0]
@@ -411,8 +451,12 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype):
             nzc = np.nonzero(S[a])[0]
             nnz += max(a, int(nzc.max(initial=a))) - min(a, int(nzc.min(initial=a))) + 1
         nb, b2 = D // nx, nx * nx
-        pnnz, setup = {"0": (0, 0), "J": (D, 0), "BJ": (nb * b2, 2 * nb * b2),
-                       "SS": ((3 * nb - 2) * b2, (4 * nb - 2) * b2) if nb else (0, 0)}[ptype]
+        offset = max(4 * D, 4 * (b2 + 2 * nx)) + 16 + (D + 2 * slots * 16 + 1) // 2
+        ncap = max(0, 160 * 1024 // 8 - offset) // b2
+        ncd = min(nb, ncap) if ptype in ("BJ", "SS") else 0
+        ncl = min(nb - 1, ncap - ncd) if ptype == "SS" and nb > 1 else 0
+        pnnz, setup = {"0": (0, 0), "J": (D, 0), "BJ": ((nb - ncd) * b2, 2 * nb * b2),
+                       "SS": ((2 * nb - 1 - ncd - ncl) * b2, (4 * nb - 2) * b2) if nb else (0, 0)}[ptype]
         tot += 8.0 * (2.0 * D + int(it) * nnz + (int(it) + 1.0) * pnnz + setup)
     return tot
 

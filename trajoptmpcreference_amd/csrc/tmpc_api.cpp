@@ -487,9 +487,8 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
   } else {
     BUF(double, hd_Pd, (size_t)B * nbmax * nx * nx);
     BUF(double, hd_Pl, (size_t)B * nbmax * nx * nx);
-    BUF(double, hd_Pt, (size_t)B * nbmax * nx * nx);
     BUF(double, hd_Ptr, (size_t)B * nbmax * nx * nx);
-    hard.Pd = hd_Pd; hard.Pl = hd_Pl; hard.Ptmp = hd_Pt; hard.Ptr = hd_Ptr;
+    hard.Pd = hd_Pd; hard.Pl = hd_Pl; hard.Ptr = hd_Ptr;
   }
   BUF(double, hd_terms, (size_t)B * (T > 0 ? T : 1) * N);
   hard.hterms = hd_terms;
@@ -1614,7 +1613,6 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
   BUF(int, hp_it, (size_t)B);
   BUF(double, hp_Pd, (size_t)B * nbmax * nx * nx);
   BUF(double, hp_Pl, (size_t)B * nbmax * nx * nx);
-  BUF(double, hp_Pt, (size_t)B * nbmax * nx * nx);
   BUF(double, hp_Ptr, (size_t)B * nbmax * nx * nx);
   BUF(int, hp_rng, (size_t)B * dmax * 2);
   // each row's first / last nonzero column: the range the kernel's products visit (tmpc_hard.hip)
@@ -1658,7 +1656,6 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
   h.gam = hp_gam;
   h.Pd = hp_Pd;
   h.Pl = hp_Pl;
-  h.Ptmp = hp_Pt;
   h.Ptr = hp_Ptr;
   h.lam = hp_lam;
   h.iters = hp_it;

@@ -34,8 +34,8 @@
 // have no preconditioner rows): two valid orders stop up to 5 iterations apart on the same S.  Every
 // kernel of this file therefore rounds each product and sum on its own (fp contraction off below) and
 // k_hard_pcg sums in the canonical order that oracle/hard.py pcg_canonical restates -- sequential
-// sums from 0.0, per-thread dot partials over 256 threads, a 64-lane xor butterfly, a fan-in over the
-// 4 waves -- so that on identical S and gamma the two are bitwise equal (tests/test_gpu_hard.py).
+// sums from 0.0, per-thread dot partials over 1024 threads, a 64-lane xor butterfly, a fan-in over the
+// 16 waves -- so that on identical S and gamma the two are bitwise equal (tests/test_gpu_hard.py).
 #include "tmpc_internal.h"
 
 #include <algorithm>
@@ -385,6 +385,11 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
 __host__ __device__ constexpr int hard_pcg_scratch(int dmax, int nx) {
   return 4 * dmax > 4 * (nx * nx + 2 * nx) ? 4 * dmax : 4 * (nx * nx + 2 * nx);
 }
+// doubles before k_hard_pcg's preconditioner-block cache: the scratch, 16 reduction slots, the rows'
+// and the wave-slots' diagonal ranges (ints)
+__host__ __device__ constexpr int hard_pcg_cache_offset(int D, int nx, int slots) {
+  return hard_pcg_scratch(D, nx) + 16 + (D + 2 * slots * (HARD_PCG_THREADS / 64) + 1) / 2;
+}
 
 // ---- workgroup sum (deterministic): wave DPP butterfly via shuffles + fixed-order fan-in
 __device__ __forceinline__ double h_block_sum(double v, double* red) {
@@ -405,10 +410,14 @@ __device__ __forceinline__ double band_at(const double* S, const int* rg, int dm
 
 // Preconditioner (compute_preconditioner on the dense S, PCG.py:113-212) + PCG (:66-111).
 // Pd [nb][NX][NX] diagonal inverses, Pl [nb-1][NX][NX] = P_{k+1,k} (P_{k,k+1} = Pl[k]^T: the
-// reference copies transposes); Ptr and Ptmp hold their transposes (column j of a block contiguous),
-// the layout P^-1 r reads.
-// Thread t owns rows t, t + 256, ... (slot m = row / 256 < SLOTS): x of its rows stays in its registers;
-// r and p, which other rows read, and z and S p are in LDS (4 dmax doubles: several problems per CU).
+// reference copies transposes); Ptr holds the transposed diagonal blocks (column j contiguous).  P^-1 r
+// reads P_kk from Ptr and P_{k,k+1} = Pl[k]^T column-wise (both coalesced) and P_{k,k-1} = Pl[k-1]
+// row-wise: the lines of Pl[k-1] are the ones block row k-1 reads in the same pass, so they come from
+// cache, and Pl streams from HBM once per iteration instead of twice.
+// Thread t owns rows t, t + 1024, ... (slot m = row / 1024 < SLOTS; one 16-wave workgroup per problem,
+// so one problem's product has a whole CU's loads in flight): x of its rows stays in its registers;
+// r and p, which other rows read, and z and S p are in LDS (4 D doubles), and the rest of the CU's LDS
+// holds as many preconditioner blocks as fit.
 // Every global read of the iterations is coalesced: S p walks the wave's diagonals of the band (each
 // lane adds the diagonals inside its row's range, in column order), and the preconditioner rows are read
 // from the transposed blocks.  Every sum keeps the canonical order (oracle/hard.py pcg_canonical).
@@ -418,9 +427,10 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
                                                               const int* __restrict__ dim, const double* __restrict__ Sb,
                                                               const double* __restrict__ gam, double tol, int max_iter,
                                                               double* __restrict__ Pd, double* __restrict__ Pl,
-                                                              double* __restrict__ Ptmp, double* __restrict__ Ptr,
+                                                              double* __restrict__ Ptr,
                                                               double* __restrict__ lam, int* __restrict__ iters,
-                                                              const int* __restrict__ rng, double* __restrict__ work) {
+                                                              const int* __restrict__ rng, double* __restrict__ work,
+                                                              int lds_bytes) {
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
@@ -432,23 +442,35 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   const size_t nbmax = dmax / NX + 1;
   double* P = Pd + (size_t)b * nbmax * NX * NX;
   double* PL = Pl + (size_t)b * nbmax * NX * NX;
-  double* T = Ptmp + (size_t)b * nbmax * NX * NX;
   double* PT = Ptr + (size_t)b * nbmax * NX * NX;
+  // LDS (the whole allotment, lds_bytes; one workgroup per CU), laid out for this problem's D:
+  //   r, p, z, S p of the rows [4][D] (z, S p: read and written by the owner only) -- the setup's
+  //   staging area before; 16 reduction slots; each row's diagonal range; each wave-slot's union;
+  //   then as many preconditioner blocks as fit, transposed diagonal blocks first (ncd of them), then
+  //   stair blocks Pl (ncl): those never stream from HBM during the iterations
+  constexpr int B2 = NX * NX;
   extern __shared__ __align__(16) double sh[];
-  double* rv = sh;                 // r, p, z and S p of the rows (z, S p: read and written by the owner only)
-  double* pv = rv + dmax;
-  double* zl = pv + dmax;
-  double* al = zl + dmax;
-  double* red = sh + hard_pcg_scratch(dmax, NX);
+  double* rv = sh;
+  double* pv = rv + D;
+  double* zl = pv + D;
+  double* al = zl + D;
+  double* red = sh + hard_pcg_scratch(D, NX);
+  int* rlh = reinterpret_cast<int*>(red + 16);   // [D] each row's diagonal range lo | hi << 16
+  int* wlh = rlh + D;                            // [SLOTS][16 waves][2] each wave-slot's union of them
+  double* pcache = sh + hard_pcg_cache_offset(D, NX, SLOTS);
   const bool blocks = precond == PRECOND_BJ || precond == PRECOND_SS;
+  const int ncap = max(0, (int)(lds_bytes / sizeof(double)) - hard_pcg_cache_offset(D, NX, SLOTS)) / B2;
+  const int ncd = blocks ? min(nb, ncap) : 0;
+  const int ncl = precond == PRECOND_SS && nb > 1 ? min(nb - 1, ncap - ncd) : 0;
+  double* pcd = pcache;                    // [ncd][NX][NX] = PT blocks
+  double* pcl = pcache + (size_t)ncd * B2; // [ncl][NX][NX] = Pl blocks
   if (blocks) {
     // The setup runs on the whole workgroup, element-parallel, staged in the LDS that r, p, z, S p use
     // later: each element of a block keeps the canonical (oracle/hard.py) operation sequence, so the
     // blocks equal the oracle's bit for bit.
-    constexpr int B2 = NX * NX;
     // (1) diagonal blocks: Gauss-Jordan on the augmented [M | I] without pivoting (oracle/hard.py _gj_inverse), `cap` blocks
     //     at a time; per pivot p the new pivot row and the old column p are snapshotted first
-    const int cap = hard_pcg_scratch(dmax, NX) / (B2 + 2 * NX);
+    const int cap = hard_pcg_scratch(D, NX) / (B2 + 2 * NX);
     double* prow = sh + (size_t)cap * B2;
     double* fcol = prow + (size_t)cap * NX;
     for (int k0 = 0; k0 < nb; k0 += cap) {
@@ -483,14 +505,16 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {   // P_kk and its transpose
         const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
         P[(size_t)(k0 + kk) * B2 + i * NX + j] = sh[e];
-        PT[(size_t)(k0 + kk) * B2 + j * NX + i] = sh[e];
+        if (k0 + kk < ncd) pcd[(size_t)(k0 + kk) * B2 + j * NX + i] = sh[e];
+        else PT[(size_t)(k0 + kk) * B2 + j * NX + i] = sh[e];
       }
     }
-    // (2) SS stair blocks (oracle/hard.py _neg_triple, both products summed in index order): odd k: P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1});
-    //     even k: P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk), stored transposed.  Pl[k-1] = P_{k,k-1}
-    //     row-major and T[k-1] = its transpose.  yz = Y Z staged in LDS, `cap2` stairs at a time.
+    // (2) SS stair blocks (oracle/hard.py _neg_triple, both products summed in index order):
+    //     odd k: P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1}); even k: P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k}
+    //     P_kk), stored transposed.  Pl[k-1] = P_{k,k-1} row-major.  yz = Y Z staged in LDS, `cap2`
+    //     stairs at a time.
     if (precond == PRECOND_SS && nb > 1) {
-      const int cap2 = hard_pcg_scratch(dmax, NX) / B2;
+      const int cap2 = hard_pcg_scratch(D, NX) / B2;
       for (int k0 = 1; k0 < nb; k0 += cap2) {
         const int kc = min(cap2, nb - k0);
         __syncthreads();   // P written (global, this workgroup) / the previous chunk's yz read
@@ -516,7 +540,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
           const double v = -acc;
           const int pr = odd ? r : c, pc = odd ? c : r;                 // element of P_{k,k-1}
           PL[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
-          T[(size_t)(k - 1) * B2 + pc * NX + pr] = v;
+          if (k - 1 < ncl) pcl[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
         }
       }
     }
@@ -528,16 +552,17 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     if (precond == PRECOND_J) return (1.0 / band_at(S, rg, dmax, W, a, a)) * rv[a];
     if (a >= nb * NX) return 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
     const int k = a / NX, i = a - k * NX;
-    const double* MT = PT + (size_t)k * NX * NX;   // MT[j NX + i] = P_kk[i][j]
+    // MT[j NX + i] = P_kk[i][j]; L = P_{k,k-1}; U = P_{k+1,k} (U^T = P_{k,k+1}): LDS copies where cached
+    const double* MT = k < ncd ? pcd + (size_t)k * B2 : PT + (size_t)k * B2;
     double s = 0.0;
     for (int j = 0; j < NX; ++j) s += MT[j * NX + i] * rv[k * NX + j];
     if (precond == PRECOND_SS) {
       if (k > 0) {
-        const double* LT = T + (size_t)(k - 1) * NX * NX;   // LT[j NX + i] = P_{k,k-1}[i][j]
-        for (int j = 0; j < NX; ++j) s += LT[j * NX + i] * rv[(k - 1) * NX + j];
+        const double* L = k - 1 < ncl ? pcl + (size_t)(k - 1) * B2 : PL + (size_t)(k - 1) * B2;
+        for (int j = 0; j < NX; ++j) s += L[i * NX + j] * rv[(k - 1) * NX + j];
       }
       if (k + 1 < nb) {
-        const double* U = PL + (size_t)k * NX * NX;   // P_{k,k+1} = P_{k+1,k}^T
+        const double* U = k < ncl ? pcl + (size_t)k * B2 : PL + (size_t)k * B2;
         for (int j = 0; j < NX; ++j) s += U[j * NX + i] * rv[(k + 1) * NX + j];
       }
     }
@@ -545,12 +570,12 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   };
   // (S p)_a over the row's structural range only, in column order (the terms left out are exact zeros):
   // the wave walks the diagonals o in [olo, ohi] (its rows' ranges, wave-uniform), each lane adding the
-  // ones inside its own range -- o increasing is c = a - W + o increasing for a fixed row.  Eight
+  // ones inside its own range -- o increasing is c = a - W + o increasing for a fixed row.  Sixteen
   // diagonals' loads are issued before their products are added (the band streams from HBM: memory-level
   // parallelism, not bandwidth, bounds one wave); past ohi the index is clamped and the product dropped.
   auto spmv = [&](int a, bool own, int olo, int ohi, int lohi) -> double {
     const int lo = lohi & 0xffff, hi = lohi >> 16;
-    constexpr int U = 8;
+    constexpr int U = 16;
     double s = 0.0;
     const double* Sa = S + (own ? a : 0);
     for (int o = olo; o <= ohi; o += U) {
@@ -575,6 +600,22 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       if (a < D) nnz += rg[2 * a + 1] - rg[2 * a] + 1;
     }
     nnz = h_block_sum(nnz, red);
+  }
+  // the diagonal ranges, once: row a's [lo, hi] (0 <= lo, hi < 2W + 1 < 2^15) and each wave-slot's union
+#pragma unroll 1
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * HARD_PCG_THREADS;
+    int l = a < D ? rg[2 * a] - a + W : BW;
+    int h = a < D ? rg[2 * a + 1] - a + W : -1;
+    if (a < D) rlh[a] = l | (h << 16);
+    for (int off = 32; off > 0; off >>= 1) {
+      l = min(l, __shfl_xor(l, off, 64));
+      h = max(h, __shfl_xor(h, off, 64));
+    }
+    if ((t & 63) == 0) {
+      wlh[2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6))] = l;
+      wlh[2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6)) + 1] = h;
+    }
   }
   double xv[SLOTS];
   const double* g = gam + (size_t)b * dmax;
@@ -605,14 +646,10 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     for (int m = 0; m < SLOTS; ++m) {
       if (wbase + m * HARD_PCG_THREADS >= D) break;   // wave-uniform: no row of this wave's slot m
       const int a = t + m * HARD_PCG_THREADS;
-      int l = a < D ? rg[2 * a] - a + W : BW;   // this row's diagonals (0 <= l, h < 2W + 1 < 2^15)
-      int h = a < D ? rg[2 * a + 1] - a + W : -1;
-      const int lohi = a < D ? (l | (h << 16)) : 0xffff;   // empty range for rows past D
-      for (int off = 32; off > 0; off >>= 1) {   // the wave's union of them
-        l = min(l, __shfl_xor(l, off, 64));
-        h = max(h, __shfl_xor(h, off, 64));
-      }
-      const double sp = spmv(a, a < D, __builtin_amdgcn_readfirstlane(l), __builtin_amdgcn_readfirstlane(h), lohi);
+      const int lohi = a < D ? rlh[a] : 0xffff;   // empty range for rows past D
+      const int* w2 = wlh + 2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6));
+      const double sp = spmv(a, a < D, __builtin_amdgcn_readfirstlane(w2[0]), __builtin_amdgcn_readfirstlane(w2[1]),
+                             lohi);
       if (a < D) {
         al[a] = sp;
         part += pv[a] * sp;
@@ -660,13 +697,15 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   if (t == 0) iters[b] = it_done;
   if (work && t == 0) {
     // algorithmic HBM bytes of this launch: gamma in, lambda out; per iteration the
-    // band's structural entries (S p) and the preconditioner entries one P^-1 r reads, it_done + 1 of
-    // those; the setup reads the band's diagonal (and for SS sub-diagonal) blocks and writes P (and Pl)
+    // band's structural entries (S p) and the distinct preconditioner entries one P^-1 r needs that are
+    // not resident in LDS (SS: of the nb diagonal and nb - 1 stair blocks, each once, all but the ncd +
+    // ncl cached ones), it_done + 1 of those; the setup reads the band's diagonal (and for SS
+    // sub-diagonal) blocks and writes P (and Pl)
     const double b2 = (double)NX * NX;
     double pnnz = 0.0, setup = 0.0;
     if (precond == PRECOND_J) pnnz = D;
-    if (precond == PRECOND_BJ) { pnnz = nb * b2; setup = 2.0 * nb * b2; }
-    if (precond == PRECOND_SS && nb > 0) { pnnz = (3.0 * nb - 2.0) * b2; setup = (4.0 * nb - 2.0) * b2; }
+    if (precond == PRECOND_BJ) { pnnz = (double)(nb - ncd) * b2; setup = 2.0 * nb * b2; }
+    if (precond == PRECOND_SS && nb > 0) { pnnz = (double)(2 * nb - 1 - ncd - ncl) * b2; setup = (4.0 * nb - 2.0) * b2; }
     work[b] += 8.0 * (2.0 * D + it_done * nnz + (it_done + 1.0) * pnnz + setup);
   }
 }
@@ -916,16 +955,19 @@ struct LaunchHard {
                            h.hoff, h.cnt, h.hcol, h.hsgn, h.Sb, h.gam, h.M, h.rhs, h.lam, h.sing,
                            h.rng);
       } else {
-        size_t lds = ((size_t)hard_pcg_scratch(h.dmax, NX) + 16) * sizeof(double);
-        if (const char* e = getenv("TMPC_HARD_PCG_LDS_KB")) lds = std::max(lds, (size_t)atoi(e) * 1024);   // dev: residency sweep
+        // the whole LDS: one 16-wave workgroup per CU, the rest of it caches preconditioner blocks
+        size_t lds = HARD_PCG_LDS_BYTES;
+        if (const char* e = getenv("TMPC_HARD_PCG_LDS_KB"))   // dev: a smaller block cache (measurement)
+          lds = std::min(lds, std::max((size_t)atoi(e) * 1024,
+                                       (size_t)hard_pcg_cache_offset(h.dmax, NX, HARD_PCG_MAX_SLOTS) * sizeof(double)));
         const int slots = (h.dmax + HARD_PCG_THREADS - 1) / HARD_PCG_THREADS;
 #define HPCG(SL) hipLaunchKernelGGL((k_hard_pcg<NX, SL>), dim3(B), dim3(HARD_PCG_THREADS), lds, s, B, h.W, h.dmax, \
-                                    h.precond, h.active, h.dim, h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, h.Ptmp, \
-                                    h.Ptr, h.lam, h.iters, h.rng, h.work)
-        if (slots <= 4) HPCG(4);
-        else if (slots <= 8) HPCG(8);
-        else if (slots <= 12) HPCG(12);
-        else HPCG(16);
+                                    h.precond, h.active, h.dim, h.Sb, h.gam, h.tol, h.max_iter, h.Pd, h.Pl, \
+                                    h.Ptr, h.lam, h.iters, h.rng, h.work, (int)lds)
+        if (slots <= 1) HPCG(1);
+        else if (slots <= 2) HPCG(2);
+        else if (slots <= 3) HPCG(3);
+        else HPCG(4);
 #undef HPCG
       }
     } else if (h.phase == 2) {
@@ -954,11 +996,11 @@ int launch_hard(hipStream_t s, int nj, const HardArgs& h) {
 }
 
 int hard_set_max_lds() {
-  const int bytes = 160 * 1024;
+  const int bytes = HARD_PCG_LDS_BYTES;
   int err = 0;
 #define SETH1(V, SL) err |= (int)hipFuncSetAttribute((const void*)k_hard_pcg<V, SL>, \
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-#define SETH(V) SETH1(V, 4) SETH1(V, 8) SETH1(V, 12) SETH1(V, 16)
+#define SETH(V) SETH1(V, 1) SETH1(V, 2) SETH1(V, 3) SETH1(V, 4)
   SETH(2) SETH(4) SETH(6) SETH(8) SETH(10) SETH(12) SETH(14)
 #undef SETH
 #undef SETH1

@@ -176,7 +176,7 @@ struct HardArgs {
   const double *x, *u, *Ghat, *A, *Bm, *cvec, *jsoft, *alphas;
   const int* active;
   int *cnt, *hcol, *roff, *hoff, *dim, *rkind, *rknot, *ridx, *PK, *iters;
-  double *hsgn, *hval, *Y, *Sb, *gam, *Pd, *Pl, *Ptmp, *Ptr, *M, *rhs, *lam, *dx, *du, *hterms;
+  double *hsgn, *hval, *Y, *Sb, *gam, *Pd, *Pl, *Ptr, *M, *rhs, *lam, *dx, *du, *hterms;
   int* hslot;                     // [B][N][rmax] t * 2n + e of each row
   unsigned long long* amask;      // [B][N] active-set bitmask per knot (bit t * 2n + e)
   int* sing;                      // [B] the direct solve took the least-squares answer (singular S)
@@ -186,9 +186,10 @@ struct HardArgs {
   unsigned long long* tr_active;  // [B][Wtr][N] trace copy of amask (nullable)
   double* work;                   // [B] algorithmic HBM bytes of k_hard_pcg, accumulated per problem (nullable)
 };
-// k_hard_pcg: 256 threads per problem, row a on thread a % 256 (row slot a / 256, at most 16 slots)
-constexpr int HARD_PCG_THREADS = 256, HARD_PCG_MAX_SLOTS = 16;
+// k_hard_pcg: 1024 threads per problem, row a on thread a % 1024 (row slot a / 1024, at most 4 slots)
+constexpr int HARD_PCG_THREADS = 1024, HARD_PCG_MAX_SLOTS = 4;
 constexpr int HARD_PCG_MAX_ROWS = HARD_PCG_THREADS * HARD_PCG_MAX_SLOTS;
+constexpr int HARD_PCG_LDS_BYTES = 160 * 1024;   // all of a CU's LDS: vectors + preconditioner-block cache
 int launch_hard(hipStream_t s, int nj, const HardArgs& h);
 int hard_set_max_lds();
 

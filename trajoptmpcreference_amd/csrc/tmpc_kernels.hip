@@ -418,12 +418,17 @@ struct PcgRow {
 // N = 128: 1536 rows x 48 doubles = 74k doubles > the CU's 64k-double VGPR
 // file), so the GM kernels keep S and P^-1 in HBM (L2 / MALL resident while a
 // problem is solved) and the lane reads its rows there every product.  Layout
-// per problem element-major [4][NX][rows] (sd, sl, su, pr): for a fixed entry
-// j the lanes of a wave read consecutive rows.  Same interface as PcgRow.
+// per problem entry-pair-major [4][NX / 2][rows][2] (sd, sl, su, pr), rows in
+// lane order: a lane reads entries j, j + 1 of its row as one 16-byte load, and
+// for a fixed pair the lanes of a wave read 1 KB of consecutive slots.  Same
+// interface as PcgRow.
 struct GRowRef {
-  const double* __restrict__ p;
-  int stride;
-  __device__ __forceinline__ double operator[](int j) const { return p[(size_t)j * stride]; }
+  const double* __restrict__ p;   // this row's first pair
+  int stride;                     // doubles from one pair of the row to the next (2 rows)
+  __device__ __forceinline__ double operator[](int j) const {
+    const double2 v = *reinterpret_cast<const double2*>(p + (size_t)(j >> 1) * stride);
+    return (j & 1) ? v.y : v.x;
+  }
 };
 template <int NX>
 struct PcgRowG {
@@ -1116,7 +1121,7 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
 //       QP_MODE_SCHUR prologue only: S blocks and gamma to Sd_out / Sl_out / gam_out
 //                     (method S: the direct solve k_btsolve runs next);
 //       QP_MODE_DXU   epilogue only, lambda read from lam_out (method S, after k_btsolve).
-//       GM: more than 1024 rows -- S and P^-1 rows in HBM (Sg, [B][4][NX][rows], PcgRowG), two rows
+//       GM: more than 1024 rows -- S and P^-1 rows in HBM (Sg, [B][4][NX/2][rows][2], PcgRowG), two rows
 //           per lane, LDS vectors of QP_MAX_ROWS rows.
 template <int NJ, int RPL, int MAXT, bool PK, int MODE, bool GM = false>
 __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PList P, int B, int N, int precond,
@@ -1175,9 +1180,14 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
   } else {
   PcgRow<NX> R[RPL];
   double bv[RPL];
-  // GM: this lane's rows of S / P^-1 in HBM (invalid lanes point at row m L and never use it)
+  // GM: this lane's rows of S / P^-1 in HBM (invalid lanes point at slot m N L and never use it)
   double* const Sgb = GM ? Sg + (size_t)b * 4 * NX * rows : nullptr;
-  auto g_at = [&](int q, int m) { return Sgb + (size_t)q * NX * rows + ln.row(m); };
+  // storage slot of this lane's row m: lane-major (m N L + lane), so that one wave instruction reads
+  // 64 consecutive 16-byte pairs (1 KB, whole lines) whatever the rows' order inside a block
+  auto g_at = [&](int q, int m) {
+    return Sgb + (size_t)q * NX * rows + 2 * ((size_t)m * N * (NX / RPL) + (size_t)ln.k * (NX / RPL) + ln.i);
+  };
+  auto g_put = [&](int q, int m, int j, double v) { g_at(q, m)[(size_t)(j >> 1) * 2 * rows + (j & 1)] = v; };
 #pragma unroll
   for (int m = 0; m < RPL; ++m) {
 #pragma unroll
@@ -1199,9 +1209,9 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
       // off-diagonal rows to HBM now; the diagonal row stays for the preconditioner
 #pragma unroll
       for (int j = 0; j < NX; ++j) {
-        g_at(0, m)[(size_t)j * rows] = R[m].sd[j];
-        g_at(1, m)[(size_t)j * rows] = R[m].sl[j];
-        g_at(2, m)[(size_t)j * rows] = R[m].su[j];
+        g_put(0, m, j, R[m].sd[j]);
+        g_put(1, m, j, R[m].sl[j]);
+        g_put(2, m, j, R[m].su[j]);
         R[m].sl[j] = R[m].su[j] = 0.0;
       }
     }
@@ -1222,12 +1232,12 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
     for (int m = 0; m < RPL; ++m) {
       if (ln.valid) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) g_at(3, m)[(size_t)j * rows] = R[m].pr[j];
+        for (int j = 0; j < NX; ++j) g_put(3, m, j, R[m].pr[j]);
       }
-      RG[m].sd = GRowRef{g_at(0, m), rows};
-      RG[m].sl = GRowRef{g_at(1, m), rows};
-      RG[m].su = GRowRef{g_at(2, m), rows};
-      RG[m].pr = GRowRef{g_at(3, m), rows};
+      RG[m].sd = GRowRef{g_at(0, m), 2 * rows};
+      RG[m].sl = GRowRef{g_at(1, m), 2 * rows};
+      RG[m].su = GRowRef{g_at(2, m), 2 * rows};
+      RG[m].pr = GRowRef{g_at(3, m), 2 * rows};
     }
     pcg_dispatch<NX, RPL>(precond, RG, ln, N, L, bv, guess ? guess + (size_t)b * rows : nullptr, tol, max_iter,
                           nullptr, nullptr, &it_done, xv);
