@@ -547,6 +547,62 @@ def gen_soft_hooks(N=8, seed=2024):
     print(f"[golden] soft hooks: {len(out)} arrays")
 
 
+def gen_soft_hooks_multi(N=8, seed=2025):
+    """The reference's hooks with three soft kinds at once (joint QUADRATIC_PENALTY, velocity and torque
+    AUGMENTED_LAGRANGIAN), 1-link arm: value_soft_constraints (the kinds' sum; BoxConstraint reads
+    xk[:1], i.e. q, for the velocity kind too), jacobian_soft_constraints (the kinds' columns vstacked),
+    max_soft_constraint_value, and update_soft_constraint_constants (`flag and update(...)`: once a
+    kind returns False the later kinds are not updated) -- for TrajoptConstraint.reference_hooks.
+    Joint limits are sized N - 1 knots by the reference, so the trajectories keep knot N - 1 inside."""
+    _setup_reference()
+    from TrajoptConstraint import TrajoptConstraint
+    rng = np.random.default_rng(seed)
+    con = TrajoptConstraint(1, 1, 1, N)
+    con.overloading = False
+    con.set_joint_limits([0.5], [-0.5], "QUADRATIC_PENALTY", {"overloading": False})
+    con.set_velocity_limits([0.4], [-0.4], "AUGMENTED_LAGRANGIAN", {"overloading": False})
+    con.set_torque_limits([0.3], [-0.3], "AUGMENTED_LAGRANGIAN", {"overloading": False})
+    out = {"N": N}
+    for kind in ("joint", "velocity", "torque"):
+        box = getattr(con, f"{kind}_limits")
+        T = box.num_timesteps
+        box.quadratic_penalty_mu[:] = 10.0 ** rng.uniform(-2, 2, (2, T))
+        box.augmented_lagrangian_lambda[:] = rng.uniform(-1, 1, (2, T))
+        box.augmented_lagrangian_phi[:] = 10.0 ** rng.uniform(-3, 0, (2, T))
+        out[f"{kind}_mu0"] = box.quadratic_penalty_mu.copy()
+        out[f"{kind}_lam0"] = box.augmented_lagrangian_lambda.copy()
+        out[f"{kind}_phi0"] = box.augmented_lagrangian_phi.copy()
+    P = 24
+    xs = rng.uniform(-1.2, 1.2, (P, 2))
+    us = rng.uniform(-1.2, 1.2, (P, 1))
+    ks = rng.integers(0, N - 1, P)
+    vals, jacs = [], []
+    for i in range(P):
+        vals.append(float(np.asarray(con.value_soft_constraints(xs[i], us[i], int(ks[i]))).reshape(-1)[0]))
+        jacs.append(np.asarray(con.jacobian_soft_constraints(xs[i], us[i], int(ks[i])), dtype=float))
+    out["xk"], out["uk"], out["k"] = xs, us, ks.astype(np.int32)
+    out["value"], out["jac"] = np.array(vals), np.array(jacs)
+    res = {f"upd_{kind}_{a}": [] for kind in ("joint", "velocity", "torque") for a in ("mu", "lam", "phi")}
+    flags, maxv, Xs, Us = [], [], [], []
+    for r in range(4):
+        X = rng.uniform(-0.9, 0.9, (2, N))
+        X[:, N - 1] = rng.uniform(-0.3, 0.3, 2)
+        U = rng.uniform(-0.9, 0.9, (1, N - 1))
+        maxv.append(float(con.max_soft_constraint_value(X, U)))
+        flags.append(bool(con.update_soft_constraint_constants(X, U)))
+        for kind in ("joint", "velocity", "torque"):
+            box = getattr(con, f"{kind}_limits")
+            res[f"upd_{kind}_mu"].append(box.quadratic_penalty_mu.copy())
+            res[f"upd_{kind}_lam"].append(box.augmented_lagrangian_lambda.copy())
+            res[f"upd_{kind}_phi"].append(box.augmented_lagrangian_phi.copy())
+        Xs.append(X)
+        Us.append(U)
+    out["upd_x"], out["upd_u"], out["upd_flag"], out["max_value"] = np.array(Xs), np.array(Us), np.array(flags), np.array(maxv)
+    out.update({k: np.array(v) for k, v in res.items()})
+    np.savez_compressed(os.path.join(OUT, "hooks_soft_multi_arm1.npz"), **out)
+    print(f"[golden] soft hooks, three kinds: flags {flags}")
+
+
 def run_pendulum(args):
     """The pendulum of examples/pendulum.py on the reference's own URDFPlant / RBDReference: the
     reference imports a PendulumPlant it never defines, so the build's PendulumPlant is a
@@ -675,6 +731,8 @@ def main():
                 print(msg, flush=True)
     if a.only in (None, "hooks"):
         gen_soft_hooks()
+    if a.only in (None, "hooks_multi"):
+        gen_soft_hooks_multi()
     if a.only in (None, "sqpN"):
         # method N (dense KKT, solveKKTSystem :313-359), the reference's default SQP method
         jobs = [("arm2", 8, 0, "N", 0.1), ("arm3", 8, 1, "N", 0.1), ("arm3", 32, 0, "N", 0.1)]

@@ -425,7 +425,7 @@ def test_hard_pcg_large_banded_is_exact(ptype):
         Sb[i, :len(gm)] = _band(S, W)
         gb[i, :len(gm)] = gm
     ctx = _native.default_context(0)
-    ctx.set_model(arm_model("arm6"))
+    ctx.set_model(arm_model("arm6fix"))
     ctx.reset_stats()
     lam, it = ctx.hard_pcg_batch(Sb, gb, dims, nx, ptype, tol=1e-10, max_iter=200)
     for i, (S, gm) in enumerate(zip(Ss, gs)):

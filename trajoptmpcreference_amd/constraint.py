@@ -177,9 +177,19 @@ class BoxConstraint:
 
 
 class TrajoptConstraint:
-    """Joint / velocity / torque limits (TrajoptConstraint.py:178-387)."""
+    """Joint / velocity / torque limits (TrajoptConstraint.py:178-387).
+
+    The host hooks have two semantics.  By default (``reference_hooks = False``) they are the device's:
+    velocity limits act on the qd slice of x, several soft kinds sum their jacobian columns, and
+    update_soft_constraint_constants updates every kind (oracle/soft.py, what the GPU solve computes).
+    With ``reference_hooks = True`` they are the reference's, for callers that swap these hooks in for
+    its own: every state kind reads x[:constraint_size] (q, also for velocity limits), the kinds'
+    jacobian columns are vstacked, and the update is ``flag = flag and update(...)``, so once a kind
+    returns False the later kinds are left as they are (TrajoptConstraint.py:295-378; pinned bit for
+    bit to the reference's own evaluation, tests/test_plugin_hooks.py)."""
 
     KINDS = ("joint_limits", "velocity_limits", "torque_limits")
+    reference_hooks = False
 
     def __init__(self, nq: int = 0, nv: int = 0, nu: int = 0, num_timesteps: int = 0):
         self.nq, self.nv, self.nu, self.num_timesteps = nq, nv, nu, num_timesteps
@@ -298,7 +308,7 @@ class TrajoptConstraint:
                 if t >= T - 1 or uk is None:
                     continue
                 z = np.asarray(uk, dtype=np.float64).reshape(-1)
-            elif kind == "joint_limits":
+            elif kind == "joint_limits" or self.reference_hooks:
                 z = np.asarray(xk, dtype=np.float64).reshape(-1)[:self.nq]
             else:
                 z = np.asarray(xk, dtype=np.float64).reshape(-1)[self.nq:self.nq + self.nv]
@@ -324,7 +334,7 @@ class TrajoptConstraint:
         jac = None
         for _, c, z, t in self._soft_slices(xk, uk, timestep):
             j = c.jacobian(z, t)
-            jac = j if jac is None else jac + j
+            jac = j if jac is None else (np.vstack((jac, j)) if self.reference_hooks else jac + j)
         return jac
 
     def update_soft_constraint_constants(self, x, u):
@@ -335,14 +345,17 @@ class TrajoptConstraint:
         x = np.asarray(x, dtype=np.float64)
         flag = True
         for kind, c in self.limits():
-            if kind == "joint_limits":
+            if kind == "joint_limits" or (kind == "velocity_limits" and self.reference_hooks):
                 z = x[:self.nq]
             elif kind == "velocity_limits":
                 z = x[self.nq:self.nq + self.nv]
             else:
                 z = np.asarray(u, dtype=np.float64)
-            f = c.update_soft_constraint_constants(z)
-            flag = flag and f
+            if self.reference_hooks:
+                flag = flag and c.update_soft_constraint_constants(z)   # the reference's short circuit
+            else:
+                f = c.update_soft_constraint_constants(z)
+                flag = flag and f
         return flag
 
     def max_soft_constraint_value(self, x, u):
@@ -353,7 +366,8 @@ class TrajoptConstraint:
             if kind == "joint_limits":
                 m = max(m, c.max_soft_constraint_value(np.asarray(x)[:self.nq]))
             elif kind == "velocity_limits":
-                m = max(m, c.max_soft_constraint_value(np.asarray(x)[self.nq:self.nq + self.nv]))
+                lo = 0 if self.reference_hooks else self.nq
+                m = max(m, c.max_soft_constraint_value(np.asarray(x)[lo:lo + self.nv]))
             else:
                 m = max(m, c.max_soft_constraint_value(np.asarray(u)))
         return m
