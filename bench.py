@@ -174,17 +174,21 @@ def workload_key(a):
     return key.replace("/", "-")
 
 
-def measured_traffic(kernel_prefix, key):
+def measured_traffic(kernel_prefix, key, raw=False):
     """HBM bytes per launch of a kernel from THIS workload's rocprofv3 PMC summary (tools/pmc_summary.py
-    writes profiles/pmc/<workload key>.json from separate FETCH_SIZE and WRITE_SIZE passes), or None."""
+    writes profiles/pmc/<workload key>.json from separate FETCH_SIZE and WRITE_SIZE passes), or None.
+    raw=True also returns the uncorrected FETCH_SIZE + WRITE_SIZE bytes."""
     path = os.path.join(ROOT, "profiles", "pmc", key + ".json")
     if not os.path.exists(path):
-        return None, None
+        return (None, None, None) if raw else (None, None)
     d = json.load(open(path))
     for k, v in d["kernels"].items():
         if k.startswith(kernel_prefix):
-            return v["hbm_bytes_per_launch"], d.get("source", os.path.relpath(path, ROOT))
-    return None, None
+            src = d.get("source", os.path.relpath(path, ROOT))
+            if raw:
+                return v["hbm_bytes_per_launch"], src, (v["fetch_size_kib_raw"] + v["write_size_kib"]) * 1024
+            return v["hbm_bytes_per_launch"], src
+    return (None, None, None) if raw else (None, None)
 
 
 # ------------------------------------------------------------------ CPU baseline (oracle = restatement)
@@ -308,7 +312,8 @@ def sqp_roofline(a, N, nx, nu, kernels, counters):
     lds_bytes = per_launch_iters * pcg_lds_bytes_per_iter(N, nx, a.method)
     traffic, src = measured_traffic(f"void tmpc::k_qp<{nx // 2}, ", workload_key(a))
     if N * nx > 1024:
-        return gm_roofline(a, N, nx, qp, per_launch_iters, per_launch_qps, traffic, src)
+        traffic, src, raw = measured_traffic(f"void tmpc::k_qp<{nx // 2}, ", workload_key(a), raw=True)
+        return gm_roofline(a, N, nx, qp, per_launch_iters, per_launch_qps, traffic, src, raw)
     out = {"kernel": "k_qp (Schur + PCG + dxu, fused)", "bound": "fp64-valu", "achieved": ach,
            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": traffic,
            "avg_launch_ms": qp["avg_ms"], "pcg_iters_per_launch": per_launch_iters,
@@ -333,24 +338,43 @@ def sqp_roofline(a, N, nx, nu, kernels, counters):
     return out
 
 
-def gm_roofline(a, N, nx, qp, per_launch_iters, per_launch_qps, traffic, src):
+def gm_request_doubles_per_row(method):
+    """doubles of S rows the GM kernel requests per row and PCG iteration (the P_kk^-1 row stays in
+    registers): S p reads S_{k,k-1}, S_kk, S_{k,k+1} (3 nx); SS reads S_{k,k+/-1} again for
+    t = r - S_off w: 5 nx; BJ / J / 0: 3 nx."""
+    return {"PCG-SS": 5}.get(method, 3)
+
+
+def gm_roofline(a, N, nx, qp, per_launch_iters, per_launch_qps, traffic, src, raw=None):
     """k_qp<..., GM> (N nx > 1024 rows, BASELINE config 5): the rows of S and P^-1 no longer fit a CU's
     registers and are re-read from HBM scratch (through L2 / MALL) every PCG iteration -- the design
     SURVEY 8(d)'s byte model prices, so the HBM roofline applies: achieved = b_pcg x PCG iterations per
-    launch / launch time, against 8 TB/s; traffic = the PMC bytes of this workload."""
+    launch / launch time, against 8 TB/s; traffic = the PMC bytes of this workload (FETCH_SIZE doubled
+    per the guide's gfx950 correction for 16-B/lane coalesced streams, which the rows are read as; the
+    raw figure beside it).  FETCH_SIZE counts every L2 miss, Infinity-Cache (MALL) hits included, so it
+    is an upper bound on HBM bytes; the kernel requests more than b_pcg (it re-reads S_off and P_kk
+    inside an SS iteration: l2_request_model), and the difference is served by L2 / MALL."""
     avg_s = qp["avg_ms"] / 1000.0
     alg = per_launch_iters * b_pcg_survey(N, nx)
     ach = alg / avg_s / 1e9
+    req = per_launch_iters * 8.0 * N * nx * nx * gm_request_doubles_per_row(a.method)
     out = {"kernel": "k_qp<GM> (Schur + PCG + dxu, S / P^-1 rows in HBM)", "bound": "hbm", "achieved": ach,
            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
            "avg_launch_ms": qp["avg_ms"], "pcg_iters_per_launch": per_launch_iters,
            "problem_qps_per_launch": per_launch_qps,
            "bytes_basis": f"SURVEY 8(d) b_pcg = 8 (2 (2N-1) nx^2 + 10 N nx) = {b_pcg_survey(N, nx)} B per PCG "
                           f"iteration at N={N}, nx={nx}, x PCG iterations per launch",
-           "algorithmic_bytes_per_launch": alg}
+           "algorithmic_bytes_per_launch": alg,
+           "l2_request_model": {"bytes_per_launch": req, "GBps": req / avg_s / 1e9,
+                                "basis": f"{gm_request_doubles_per_row(a.method)} nx doubles of S / P^-1 rows "
+                                         "requested per row and PCG iteration (bench.py gm_request_doubles_per_row)"}}
     if traffic:
         out.update(hbm_GBps=traffic / avg_s / 1e9, hbm_frac=traffic / avg_s / 1e9 / HBM_PEAK_GBS,
-                   traffic_source=src)
+                   traffic_source=src,
+                   traffic_note="2 x FETCH_SIZE + WRITE_SIZE; FETCH_SIZE includes Infinity-Cache (MALL) hits, so "
+                                "this bounds HBM bytes from above")
+    if raw:
+        out.update(traffic_raw=raw, traffic_raw_GBps=raw / avg_s / 1e9)
     return out
 
 

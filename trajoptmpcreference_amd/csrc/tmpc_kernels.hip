@@ -418,8 +418,8 @@ struct PcgRow {
 // N = 128: 1536 rows x 48 doubles = 74k doubles > the CU's 64k-double VGPR
 // file), so the GM kernels keep S and P^-1 in HBM (L2 / MALL resident while a
 // problem is solved) and the lane reads its rows there every product.  Layout
-// per problem entry-pair-major [4][NX / 2][rows][2] (sd, sl, su, pr), rows in
-// lane order: a lane reads entries j, j + 1 of its row as one 16-byte load, and
+// per problem entry-pair-major [4][NX / 2][rows][2] (sd, sl, su; the P_kk^-1
+// row pr stays in registers, slot 3 is unused), rows in lane order: a lane reads entries j, j + 1 of its row as one 16-byte load, and
 // for a fixed pair the lanes of a wave read 1 KB of consecutive slots.  Same
 // interface as PcgRow.
 struct GRowRef {
@@ -432,7 +432,8 @@ struct GRowRef {
 };
 template <int NX>
 struct PcgRowG {
-  GRowRef sd, sl, su, pr;
+  GRowRef sd, sl, su;
+  double pr[NX];   // the P_kk^-1 row stays in registers: an SS iteration reads it twice (w, z)
 };
 // HBM rows: bound the loads in flight (the compiler would hoist all of a product's row loads, 2-4
 // dozen doubles per row, past the 168-VGPR budget of the GM kernel's 3 waves per SIMD)
@@ -1230,14 +1231,11 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
     PcgRowG<NX> RG[RPL];
 #pragma unroll
     for (int m = 0; m < RPL; ++m) {
-      if (ln.valid) {
 #pragma unroll
-        for (int j = 0; j < NX; ++j) g_put(3, m, j, R[m].pr[j]);
-      }
+      for (int j = 0; j < NX; ++j) RG[m].pr[j] = R[m].pr[j];
       RG[m].sd = GRowRef{g_at(0, m), 2 * rows};
       RG[m].sl = GRowRef{g_at(1, m), 2 * rows};
       RG[m].su = GRowRef{g_at(2, m), 2 * rows};
-      RG[m].pr = GRowRef{g_at(3, m), 2 * rows};
     }
     pcg_dispatch<NX, RPL>(precond, RG, ln, N, L, bv, guess ? guess + (size_t)b * rows : nullptr, tol, max_iter,
                           nullptr, nullptr, &it_done, xv);
