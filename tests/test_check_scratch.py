@@ -41,3 +41,11 @@ def test_scratch_in_hot_fp32_kernel_fails():
 def test_runtime_model_instances_are_not_gated():
     ref64 = "_ZN4tmpc7k_qp_fdILi6ELb0ENS_8ModelRefEdEEvT1_NS_5PListEiidPKdS5_S5_PKiPdS8_"
     assert _run(_remarks(ref64, 256, 2176)).returncode == 0
+
+
+def test_model_independent_hot_kernels_are_gated():
+    ginv6 = "_ZN4tmpc11k_ginv_softILi6EEEvPKNS_7CostDevEPKNS_9ConstrDevENS_5PListEiiPKdPKiS9_S9_S9_S9_PdSB_"
+    assert _run(_remarks(ginv6, 256, 1168)).returncode == 1
+    assert _run(_remarks(ginv6, 120, 0)).returncode == 0
+    pcg = "_ZN4tmpc10k_hard_pcgILi12ELi2EEEviiiiPKiS2_PKdS4_diPdS5_S5_S5_PiS2_S5_i"
+    assert _run(_remarks(pcg, 128, 96)).returncode == 1

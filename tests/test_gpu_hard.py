@@ -443,13 +443,27 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
     stair) less those the kernel keeps in LDS -- as many as fit in the 160 KB after its vectors, diagonal
     blocks first (tmpc_hard.hip hard_pcg_cache_offset)."""
     slots = -(-dmax // 1024)
+    REG = 24   # tmpc_internal.h HARD_PCG_REG_DIAG: slot 0's first diagonals of each wave held in registers
     tot = 0.0
+    W = max(int(np.max(np.abs(np.subtract(*np.nonzero(S2))))) for S2 in Ss)   # the batch's band half-width
     for S, it in zip(Ss, iters):
         D = S.shape[0]
-        nnz = 0
+        lo = np.empty(D, dtype=int)
+        hi = np.empty(D, dtype=int)
         for a in range(D):
             nzc = np.nonzero(S[a])[0]
-            nnz += max(a, int(nzc.max(initial=a))) - min(a, int(nzc.min(initial=a))) + 1
+            lo[a] = min(a, int(nzc.min(initial=a))) - a + W
+            hi[a] = max(a, int(nzc.max(initial=a))) - a + W
+        nnz, nnz_reg = 0, 0
+        for a in range(D):
+            if a < 1024:
+                w0 = a - a % 64
+                olo = int(lo[w0:min(w0 + 64, D)].min())
+                streamed = max(0, hi[a] - max(lo[a], olo + REG) + 1)
+                nnz += streamed
+                nnz_reg += hi[a] - lo[a] + 1 - streamed
+            else:
+                nnz += hi[a] - lo[a] + 1
         nb, b2 = D // nx, nx * nx
         offset = max(4 * D, 4 * (b2 + 2 * nx)) + 16 + (D + 2 * slots * 16 + 1) // 2
         ncap = max(0, 160 * 1024 // 8 - offset) // b2
@@ -457,7 +471,7 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
         ncl = min(nb - 1, ncap - ncd) if ptype == "SS" and nb > 1 else 0
         pnnz, setup = {"0": (0, 0), "J": (D, 0), "BJ": ((nb - ncd) * b2, 2 * nb * b2),
                        "SS": ((2 * nb - 1 - ncd - ncl) * b2, (4 * nb - 2) * b2) if nb else (0, 0)}[ptype]
-        tot += 8.0 * (2.0 * D + int(it) * nnz + (int(it) + 1.0) * pnnz + setup)
+        tot += 8.0 * (2.0 * D + int(it) * nnz + (int(it) + 1.0) * pnnz + setup + nnz_reg)
     return tot
 
 

@@ -32,6 +32,9 @@ def main():
         # fp64 / fp32 instances on a compiled model (...Arm6Ed... / ...Arm6Ef...), and the Riccati sweep
         # (...ILi6Ed... / ...ILi6Ef...)
         hot = any(h in k for h in HOT) and (re.search(r"Arm\d+E[df]", k) or re.search(r"k_ilqr_backwardILi\d+E[df]", k))
+        # model-independent hot kernels: the soft-limit (G + rho I)^-1 of config 4 (its 2-link-only UrdfCost
+        # branch once spilled the other instances) and the hard-limit PCG
+        hot = hot or re.search(r"k_ginv_softILi\d+E|k_hard_pcgILi", k)
         if hot and v.get("ScratchSize", 0) > 0:
             bad.append((k, v))
         print(f"{k[:90]:90s} vgpr {v.get('VGPRs')} scratch {v.get('ScratchSize')} occ {v.get('Occupancy')}")

@@ -380,6 +380,10 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
   }
 }
 
+// band diagonals of slot 0 (each wave's first, from its rows' union) k_hard_pcg holds in registers for
+// the whole solve (48 VGPRs of its 128)
+constexpr int HARD_PCG_REG_DIAG = 24;
+
 // doubles of LDS k_hard_pcg uses before its reduction slots: r, p, z, S p of dmax rows, and at least
 // four nx x nx blocks (with their pivot rows / columns) for the preconditioner setup
 __host__ __device__ constexpr int hard_pcg_scratch(int dmax, int nx) {
@@ -570,15 +574,24 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   };
   // (S p)_a over the row's structural range only, in column order (the terms left out are exact zeros):
   // the wave walks the diagonals o in [olo, ohi] (its rows' ranges, wave-uniform), each lane adding the
-  // ones inside its own range -- o increasing is c = a - W + o increasing for a fixed row.  Sixteen
-  // diagonals' loads are issued before their products are added (the band streams from HBM: memory-level
-  // parallelism, not bandwidth, bounds one wave); past ohi the index is clamped and the product dropped.
-  auto spmv = [&](int a, bool own, int olo, int ohi, int lohi) -> double {
+  // ones inside its own range -- o increasing is c = a - W + o increasing for a fixed row.  S does not
+  // change during the solve: for the rows of slot 0 the wave's first HARD_PCG_REG_DIAG diagonals were
+  // loaded into registers once (vc) and only the rest stream from HBM, eight diagonals' loads in flight
+  // before their products are added; past ohi the index is clamped and the product dropped.
+  auto spmv = [&](int a, bool own, int olo, int ohi, int lohi, bool cached, const double (&vc)[HARD_PCG_REG_DIAG])
+      -> double {
     const int lo = lohi & 0xffff, hi = lohi >> 16;
-    constexpr int U = 16;
+    constexpr int U = 8;
     double s = 0.0;
     const double* Sa = S + (own ? a : 0);
-    for (int o = olo; o <= ohi; o += U) {
+    int o0 = olo;
+    if (cached) {
+#pragma unroll
+      for (int u = 0; u < HARD_PCG_REG_DIAG; ++u)
+        if (own && olo + u >= lo && olo + u <= hi) s += vc[u] * pv[a - W + olo + u];
+      o0 = olo + HARD_PCG_REG_DIAG;
+    }
+    for (int o = o0; o <= ohi; o += U) {
       double v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(o + u, ohi) * dmax];
@@ -592,22 +605,18 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   // the thread's rows in LDS: unrolled over the slots they held every slot's loads and products in
   // registers at once (254 VGPRs, one wave per SIMD); x stays in registers.
   const int wbase = t & ~63;   // first row of this wave in slot 0
-  double nnz = 0.0;            // structural entries of the band (work accounting)
-  if (work) {
-#pragma unroll 1
-    for (int m = 0; m < SLOTS; ++m) {
-      const int a = t + m * HARD_PCG_THREADS;
-      if (a < D) nnz += rg[2 * a + 1] - rg[2 * a] + 1;
-    }
-    nnz = h_block_sum(nnz, red);
-  }
-  // the diagonal ranges, once: row a's [lo, hi] (0 <= lo, hi < 2W + 1 < 2^15) and each wave-slot's union
+  // the diagonal ranges, once: row a's [lo, hi] (0 <= lo, hi < 2W + 1 < 2^15) and each wave-slot's
+  // union; slot 0's first HARD_PCG_REG_DIAG diagonals of the union into registers; the band entries
+  // that stream from HBM every iteration (work accounting: the rest of slot 0's, all of the others')
+  double vc[HARD_PCG_REG_DIAG];
+  double nnz = 0.0, nnz_reg = 0.0;
 #pragma unroll 1
   for (int m = 0; m < SLOTS; ++m) {
     const int a = t + m * HARD_PCG_THREADS;
     int l = a < D ? rg[2 * a] - a + W : BW;
     int h = a < D ? rg[2 * a + 1] - a + W : -1;
     if (a < D) rlh[a] = l | (h << 16);
+    const int lo = l, hi = h;
     for (int off = 32; off > 0; off >>= 1) {
       l = min(l, __shfl_xor(l, off, 64));
       h = max(h, __shfl_xor(h, off, 64));
@@ -616,6 +625,23 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       wlh[2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6))] = l;
       wlh[2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6)) + 1] = h;
     }
+    if (m == 0) {
+      const double* Sa = S + (a < D ? a : 0);
+      const int ol = __builtin_amdgcn_readfirstlane(l);
+#pragma unroll
+      for (int u = 0; u < HARD_PCG_REG_DIAG; ++u) vc[u] = Sa[(size_t)min(ol + u, BW - 1) * dmax];
+      if (a < D) {
+        const int streamed = max(0, hi - max(lo, ol + HARD_PCG_REG_DIAG) + 1);
+        nnz += streamed;
+        nnz_reg += hi - lo + 1 - streamed;
+      }
+    } else if (a < D) {
+      nnz += hi - lo + 1;
+    }
+  }
+  if (work) {
+    nnz = h_block_sum(nnz, red);
+    nnz_reg = h_block_sum(nnz_reg, red);
   }
   double xv[SLOTS];
   const double* g = gam + (size_t)b * dmax;
@@ -649,7 +675,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       const int lohi = a < D ? rlh[a] : 0xffff;   // empty range for rows past D
       const int* w2 = wlh + 2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6));
       const double sp = spmv(a, a < D, __builtin_amdgcn_readfirstlane(w2[0]), __builtin_amdgcn_readfirstlane(w2[1]),
-                             lohi);
+                             lohi, m == 0, vc);
       if (a < D) {
         al[a] = sp;
         part += pv[a] * sp;
@@ -697,16 +723,17 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   if (t == 0) iters[b] = it_done;
   if (work && t == 0) {
     // algorithmic HBM bytes of this launch: gamma in, lambda out; per iteration the
-    // band's structural entries (S p) and the distinct preconditioner entries one P^-1 r needs that are
-    // not resident in LDS (SS: of the nb diagonal and nb - 1 stair blocks, each once, all but the ncd +
-    // ncl cached ones), it_done + 1 of those; the setup reads the band's diagonal (and for SS
-    // sub-diagonal) blocks and writes P (and Pl)
+    // band's structural entries (S p) not held in registers, and the distinct preconditioner entries
+    // one P^-1 r needs that are not resident in LDS (SS: of the nb diagonal and nb - 1 stair blocks,
+    // each once, all but the ncd + ncl cached ones), it_done + 1 of those; once: the register-held band
+    // entries, and the setup's reads of the band's diagonal (and for SS sub-diagonal) blocks and writes
+    // of P (and Pl)
     const double b2 = (double)NX * NX;
     double pnnz = 0.0, setup = 0.0;
     if (precond == PRECOND_J) pnnz = D;
     if (precond == PRECOND_BJ) { pnnz = (double)(nb - ncd) * b2; setup = 2.0 * nb * b2; }
     if (precond == PRECOND_SS && nb > 0) { pnnz = (double)(2 * nb - 1 - ncd - ncl) * b2; setup = (4.0 * nb - 2.0) * b2; }
-    work[b] += 8.0 * (2.0 * D + it_done * nnz + (it_done + 1.0) * pnnz + setup);
+    work[b] += 8.0 * (2.0 * D + it_done * nnz + (it_done + 1.0) * pnnz + setup + nnz_reg);
   }
 }
 

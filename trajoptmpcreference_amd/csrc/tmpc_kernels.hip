@@ -270,11 +270,13 @@ __global__ void __launch_bounds__(64) k_ginv_soft(const CostDev* __restrict__ C,
   const double rh = act ? rho[b] : 0.0;
   // UrdfCost: state-dependent x block (Q Jt)^T Jt (hess_mode 0, TrajoptCost.py:490-492)
   // and its gradient (y^T Q) Jt (:449) joins the soft jacobian in jsoft
-  const bool ee = C->kind == COST_EE && which == 0;
+  // (2-link only, tmpc_set_cost_ee: compiled out of the other instances, whose registers it would
+  // otherwise spill -- k_ginv_soft<6> carried 1168 B/lane of scratch for it)
+  const bool ee = NJ == 2 && C->kind == COST_EE && which == 0;
   double eg[NX], hrow[NX];
 #pragma unroll
   for (int c = 0; c < NX; ++c) eg[c] = hrow[c] = 0.0;
-  if (ee) {
+  if constexpr (NJ == 2) if (ee) {
     double Jt[NX * NX], qj[NX];
     ee_eval<NJ>(C, src, z, eg, Jt);
 #pragma unroll
