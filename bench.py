@@ -290,8 +290,12 @@ def hard_roofline(a, kernels, hard_bytes):
     out = {"kernel": "k_hard_pcg", "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "avg_launch_ms": hp["avg_ms"],
            "algorithmic_bytes_per_launch": per_launch,
-           "bytes_basis": "counted by the kernel per problem: 8 B x (2 D + iterations x band entries + "
-                          "(iterations + 1) x distinct preconditioner entries + setup blocks), DESIGN.md 4f"}
+           "bytes_basis": "counted by the kernel per problem: 8 B x (2 D + iterations x streamed band entries + "
+                          "(iterations + 1) x streamed distinct preconditioner entries + once: register-held band "
+                          "entries, setup blocks), DESIGN.md 4f",
+           "note": "each row's first band entries stay in registers and the preconditioner blocks in LDS for "
+                   "the whole solve, so HBM is no longer what binds: one 16-wave workgroup per problem, the "
+                   "PCG iteration's barrier-separated phases (DESIGN.md 4f)"}
     if traffic:
         out.update(hbm_GBps=traffic / avg_s / 1e9, traffic_source=src)
     return out

@@ -443,27 +443,17 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
     stair) less those the kernel keeps in LDS -- as many as fit in the 160 KB after its vectors, diagonal
     blocks first (tmpc_hard.hip hard_pcg_cache_offset)."""
     slots = -(-dmax // 1024)
-    REG = 24   # tmpc_internal.h HARD_PCG_REG_DIAG: slot 0's first diagonals of each wave held in registers
+    REG = 16 if nx <= 4 else (20 if nx >= 14 else 24)   # tmpc_hard.hip hard_pcg_reg_diag (slot 0, in registers)
     tot = 0.0
-    W = max(int(np.max(np.abs(np.subtract(*np.nonzero(S2))))) for S2 in Ss)   # the batch's band half-width
     for S, it in zip(Ss, iters):
         D = S.shape[0]
-        lo = np.empty(D, dtype=int)
-        hi = np.empty(D, dtype=int)
-        for a in range(D):
-            nzc = np.nonzero(S[a])[0]
-            lo[a] = min(a, int(nzc.min(initial=a))) - a + W
-            hi[a] = max(a, int(nzc.max(initial=a))) - a + W
         nnz, nnz_reg = 0, 0
         for a in range(D):
-            if a < 1024:
-                w0 = a - a % 64
-                olo = int(lo[w0:min(w0 + 64, D)].min())
-                streamed = max(0, hi[a] - max(lo[a], olo + REG) + 1)
-                nnz += streamed
-                nnz_reg += hi[a] - lo[a] + 1 - streamed
-            else:
-                nnz += hi[a] - lo[a] + 1
+            nzc = np.nonzero(S[a])[0]
+            width = max(a, int(nzc.max(initial=a))) - min(a, int(nzc.min(initial=a))) + 1
+            streamed = max(0, width - REG) if a < 1024 else width
+            nnz += streamed
+            nnz_reg += width - streamed
         nb, b2 = D // nx, nx * nx
         offset = max(4 * D, 4 * (b2 + 2 * nx)) + 16 + (D + 2 * slots * 16 + 1) // 2
         ncap = max(0, 160 * 1024 // 8 - offset) // b2

@@ -1549,13 +1549,11 @@ int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim,
   if (singular) HIP_OK(hipMemcpy(singular, dev("hd_sing"), sizeof(int) * B, hipMemcpyDeviceToHost));
   const size_t BW = 2 * (size_t)hl.W + 1;
   if (S_band) {
-    // the kernels write S only inside each row's structural range (k_hard_schur): zero the rest
-    std::vector<double> sbt((size_t)B * hl.dmax * BW);   // device: diagonal-major [B][2W+1][dmax]
+    // device: row-start-relative [B][2W+1][dmax] (entry j of row a = column rng_a + j, tmpc_hard.hip),
+    // written only inside each row's structural range (k_hard_schur); the ABI's band is row-major
+    // [B][dmax][2W+1] (column c at a - W + o), zero outside the ranges
+    std::vector<double> sbt((size_t)B * hl.dmax * BW);
     HIP_OK(hipMemcpy(sbt.data(), dev("hd_Sb"), sizeof(double) * sbt.size(), hipMemcpyDeviceToHost));
-    for (int b = 0; b < B; ++b)
-      for (int a = 0; a < hl.dmax; ++a)
-        for (size_t o = 0; o < BW; ++o)
-          S_band[((size_t)b * hl.dmax + a) * BW + o] = sbt[((size_t)b * BW + o) * hl.dmax + a];
     std::vector<int> rg((size_t)B * hl.dmax * 2), dm(B);
     HIP_OK(hipMemcpy(rg.data(), dev("hd_rng"), rg.size() * sizeof(int), hipMemcpyDeviceToHost));
     HIP_OK(hipMemcpy(dm.data(), dev("hd_dim"), B * sizeof(int), hipMemcpyDeviceToHost));
@@ -1565,7 +1563,7 @@ int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim,
         const int* r = rg.data() + ((size_t)b * hl.dmax + a) * 2;
         for (size_t o = 0; o < BW; ++o) {
           const int c = a - hl.W + (int)o;
-          if (a >= dm[b] || c < r[0] || c > r[1]) row[o] = 0.0;
+          row[o] = (a >= dm[b] || c < r[0] || c > r[1]) ? 0.0 : sbt[((size_t)b * BW + (c - r[0])) * hl.dmax + a];
         }
       }
   }
@@ -1631,12 +1629,15 @@ int tmpc_hard_pcg_batch(tmpc_ctx* ctx, int B, int nx, int dmax, int W, const int
       rg[((size_t)b * dmax + a) * 2 + 1] = hi;
     }
   HIP_OK(hipMemcpyAsync(hp_rng, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-  // the device band is diagonal-major ([B][2W+1][dmax], tmpc_hard.hip); the ABI's is row-major
-  std::vector<double> sbt((size_t)B * dmax * BW);
+  // the device band is row-start-relative ([B][2W+1][dmax], entry j of row a = column rg_a + j,
+  // tmpc_hard.hip); the ABI's is row-major [B][dmax][2W+1]
+  std::vector<double> sbt((size_t)B * dmax * BW, 0.0);
   for (int b = 0; b < B; ++b)
-    for (int a = 0; a < dmax; ++a)
-      for (size_t o = 0; o < BW; ++o)
-        sbt[((size_t)b * BW + o) * dmax + a] = S_band[((size_t)b * dmax + a) * BW + o];
+    for (int a = 0; a < dmax; ++a) {
+      const int lo = rg[((size_t)b * dmax + a) * 2], hi = rg[((size_t)b * dmax + a) * 2 + 1];
+      for (int c = lo; c <= hi; ++c)
+        sbt[((size_t)b * BW + (c - lo)) * dmax + a] = S_band[((size_t)b * dmax + a) * BW + (c - a + W)];
+    }
   HIP_OK(hipMemcpy(hp_Sb, sbt.data(), sizeof(double) * B * dmax * BW, hipMemcpyHostToDevice));
   HIP_OK(hipMemcpyAsync(hp_gam, gamma, sizeof(double) * B * dmax, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(hp_dim, dim, sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));

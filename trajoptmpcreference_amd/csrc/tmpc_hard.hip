@@ -8,9 +8,10 @@
 // (R_j the nx dynamics rows that define x_j, H_k knot k's hard rows) the groups
 // touch the knot variables {0}, {0,1}, {1,2}, ..., so S is block-tridiagonal with
 // VARIABLE block sizes: every row couples only with rows less than twice the
-// largest group away.  S is therefore stored as a band per problem, diagonal-major:
-// entry (row a, column c) at [o = c - a + W][a] of a [2W+1][dmax] array, so that the
-// rows of a wave read one diagonal as one contiguous 512-byte piece.
+// largest group away.  S is therefore stored per problem in a row-start-relative band
+// (ELL): row a's structurally nonzero columns c in [lo_a, hi_a] (rng) at [c - lo_a][a] of
+// a [2W+1][dmax] array, so that the rows of a wave read their j-th entries as one
+// contiguous 512-byte piece, and a wave walks only its longest row's entries.
 // The reference's PCG preconditioner, however, cuts S into nx-aligned blocks from
 // row 0 (n_blocks = floor(dim / nx), PCG.py:182-212), which no longer line up with
 // the groups; it is reproduced exactly on the band (trailing dim mod nx rows have
@@ -329,10 +330,10 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     rb[2 * a + 1] = hi;
   }
   __syncthreads();
-  // phase 2: the band inside the row ranges, row a, column c (stored at [c - a + W][a]); entries outside
-  // the ranges are never read (band_at / the PCG product / k_hard_direct's copy).  Each thread keeps its
-  // row's two coefficient vectors in registers and the wave walks the diagonals of its rows (the stores
-  // of one diagonal are contiguous); S_ac = -(sum over pieces p of a, q of c on one knot of cf_ap . Y_cq)
+  // phase 2: the band inside the row ranges, row a, column c = lo_a + j (stored at [j][a]); entries
+  // outside the ranges are never read (band_at / the PCG product / k_hard_direct's copy).  Each thread
+  // keeps its row's two coefficient vectors in registers and the wave walks j up to its longest row (the
+  // stores of one j are contiguous); S_ac = -(sum over pieces p of a, q of c on one knot of cf_ap . Y_cq)
   const int BW = 2 * W + 1;
   double* S = Sb + (size_t)b * dmax * BW;
   for (int a0 = threadIdx.x & ~63; a0 < D; a0 += blockDim.x) {   // wave-uniform: the wave's first row
@@ -346,8 +347,8 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
       const double* hs = hsgn + hb + (size_t)knot * rmax;
       kp0 = row_piece<NJ>(kind, knot, idx, 0, A, Bm, hc, hs, cf0);
       kp1 = row_piece<NJ>(kind, knot, idx, 1, A, Bm, hc, hs, cf1);
-      ol = rb[2 * a] - a + W;
-      oh = rb[2 * a + 1] - a + W;
+      ol = 0;
+      oh = rb[2 * a + 1] - rb[2 * a];
     }
     int l = ol, h = oh;
     for (int off = 32; off > 0; off >>= 1) {
@@ -358,7 +359,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     h = __builtin_amdgcn_readfirstlane(h);
     for (int o = l; o <= h; ++o) {
       if (o < ol || o > oh) continue;
-      const int c = a - W + o;
+      const int c = rb[2 * a] + o;
       const int pc0 = PKb[c * 2], pc1 = PKb[c * 2 + 1];
       double sum = 0.0;
       auto piece = [&](const double(&cf)[3 * NJ], int kp) {   // pieces q of column c on row a's knot kp
@@ -380,9 +381,9 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
   }
 }
 
-// band diagonals of slot 0 (each wave's first, from its rows' union) k_hard_pcg holds in registers for
-// the whole solve (48 VGPRs of its 128)
-constexpr int HARD_PCG_REG_DIAG = 24;
+// band entries of each slot-0 row (its first ones) k_hard_pcg holds in registers for the whole solve:
+// 24 (48 VGPRs of its 128); fewer where that spills (nx = 14: 20; nx = 2, 4: 16)
+__host__ __device__ constexpr int hard_pcg_reg_diag(int nx) { return nx <= 4 ? 16 : (nx >= 14 ? 20 : 24); }
 
 // doubles of LDS k_hard_pcg uses before its reduction slots: r, p, z, S p of dmax rows, and at least
 // four nx x nx blocks (with their pivot rows / columns) for the preconditioner setup
@@ -407,9 +408,9 @@ __device__ __forceinline__ double h_block_sum(double v, double* red) {
   return s;
 }
 
-// S_rc from the (diagonal-major) band; zero outside row r's structural range rg[2r .. 2r+1]
-__device__ __forceinline__ double band_at(const double* S, const int* rg, int dmax, int W, int r, int c) {
-  return (c >= rg[2 * r] && c <= rg[2 * r + 1]) ? S[(size_t)(c - r + W) * dmax + r] : 0.0;
+// S_rc from the (row-start-relative) band; zero outside row r's structural range rg[2r .. 2r+1]
+__device__ __forceinline__ double band_at(const double* S, const int* rg, int dmax, int r, int c) {
+  return (c >= rg[2 * r] && c <= rg[2 * r + 1]) ? S[(size_t)(c - rg[2 * r]) * dmax + r] : 0.0;
 }
 
 // Preconditioner (compute_preconditioner on the dense S, PCG.py:113-212) + PCG (:66-111).
@@ -435,6 +436,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
                                                               double* __restrict__ lam, int* __restrict__ iters,
                                                               const int* __restrict__ rng, double* __restrict__ work,
                                                               int lds_bytes) {
+  constexpr int REG = hard_pcg_reg_diag(NX);
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
@@ -459,8 +461,8 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   double* zl = pv + D;
   double* al = zl + D;
   double* red = sh + hard_pcg_scratch(D, NX);
-  int* rlh = reinterpret_cast<int*>(red + 16);   // [D] each row's diagonal range lo | hi << 16
-  int* wlh = rlh + D;                            // [SLOTS][16 waves][2] each wave-slot's union of them
+  int* rlh = reinterpret_cast<int*>(red + 16);   // [D] each row's last entry | first column << 16
+  int* wlh = rlh + D;                            // [SLOTS][16 waves] each wave-slot's longest row (last entry)
   double* pcache = sh + hard_pcg_cache_offset(D, NX, SLOTS);
   const bool blocks = precond == PRECOND_BJ || precond == PRECOND_SS;
   const int ncap = max(0, (int)(lds_bytes / sizeof(double)) - hard_pcg_cache_offset(D, NX, SLOTS)) / B2;
@@ -482,7 +484,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       __syncthreads();
       for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
         const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
-        sh[e] = band_at(S, rg, dmax, W, (k0 + kk) * NX + i, (k0 + kk) * NX + j);
+        sh[e] = band_at(S, rg, dmax, (k0 + kk) * NX + i, (k0 + kk) * NX + j);
       }
       for (int p = 0; p < NX; ++p) {
         __syncthreads();
@@ -529,7 +531,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
           const int yr = odd ? k : k - 1, yc = odd ? k - 1 : k;        // Y = S_{yr, yc}
           const double* Z = P + (size_t)(odd ? k - 1 : k) * B2;
           double yz = 0.0;
-          for (int l = 0; l < NX; ++l) yz += band_at(S, rg, dmax, W, yr * NX + r, yc * NX + l) * Z[l * NX + c];
+          for (int l = 0; l < NX; ++l) yz += band_at(S, rg, dmax, yr * NX + r, yc * NX + l) * Z[l * NX + c];
           sh[e] = yz;
         }
         __syncthreads();
@@ -553,7 +555,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   // z = P^-1 r for row a (r read from LDS)
   auto apply_P = [&](int a) -> double {
     if (precond == PRECOND_NONE) return rv[a];
-    if (precond == PRECOND_J) return (1.0 / band_at(S, rg, dmax, W, a, a)) * rv[a];
+    if (precond == PRECOND_J) return (1.0 / band_at(S, rg, dmax, a, a)) * rv[a];
     if (a >= nb * NX) return 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
     const int k = a / NX, i = a - k * NX;
     // MT[j NX + i] = P_kk[i][j]; L = P_{k,k-1}; U = P_{k+1,k} (U^T = P_{k,k+1}): LDS copies where cached
@@ -573,31 +575,31 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     return s;
   };
   // (S p)_a over the row's structural range only, in column order (the terms left out are exact zeros):
-  // the wave walks the diagonals o in [olo, ohi] (its rows' ranges, wave-uniform), each lane adding the
-  // ones inside its own range -- o increasing is c = a - W + o increasing for a fixed row.  S does not
-  // change during the solve: for the rows of slot 0 the wave's first HARD_PCG_REG_DIAG diagonals were
-  // loaded into registers once (vc) and only the rest stream from HBM, eight diagonals' loads in flight
-  // before their products are added; past ohi the index is clamped and the product dropped.
-  auto spmv = [&](int a, bool own, int olo, int ohi, int lohi, bool cached, const double (&vc)[HARD_PCG_REG_DIAG])
+  // the wave walks j = 0 .. its longest row's width - 1 (wave-uniform), each lane adding its row's
+  // entries j <= hi (column c = lo_a + j, increasing with j).  S does not change during the solve: for
+  // the rows of slot 0 the first REG entries were loaded into registers once (vc) and only
+  // the rest stream from HBM, eight entries' loads in flight before their products are added; past the
+  // wave's longest row the index is clamped and the product dropped.
+  auto spmv = [&](int a, bool own, int jmax, int c0hi, bool cached, const double (&vc)[REG])
       -> double {
-    const int lo = lohi & 0xffff, hi = lohi >> 16;
+    const int hi = c0hi & 0xffff, c0 = c0hi >> 16;
     constexpr int U = 8;
     double s = 0.0;
     const double* Sa = S + (own ? a : 0);
-    int o0 = olo;
+    int j0 = 0;
     if (cached) {
 #pragma unroll
-      for (int u = 0; u < HARD_PCG_REG_DIAG; ++u)
-        if (own && olo + u >= lo && olo + u <= hi) s += vc[u] * pv[a - W + olo + u];
-      o0 = olo + HARD_PCG_REG_DIAG;
+      for (int u = 0; u < REG; ++u)
+        if (own && u <= hi) s += vc[u] * pv[c0 + u];
+      j0 = REG;
     }
-    for (int o = o0; o <= ohi; o += U) {
+    for (int j = j0; j <= jmax; j += U) {
       double v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(o + u, ohi) * dmax];
+      for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(j + u, jmax) * dmax];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (own && o + u >= lo && o + u <= hi) s += v[u] * pv[a - W + o + u];
+        if (own && j + u <= hi) s += v[u] * pv[c0 + j + u];
     }
     return s;
   };
@@ -605,38 +607,30 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   // the thread's rows in LDS: unrolled over the slots they held every slot's loads and products in
   // registers at once (254 VGPRs, one wave per SIMD); x stays in registers.
   const int wbase = t & ~63;   // first row of this wave in slot 0
-  // the diagonal ranges, once: row a's [lo, hi] (0 <= lo, hi < 2W + 1 < 2^15) and each wave-slot's
-  // union; slot 0's first HARD_PCG_REG_DIAG diagonals of the union into registers; the band entries
+  // the row ranges, once: row a's first column lo_a and last entry hi_a = width - 1 (both < 2^15), each
+  // wave-slot's longest row; slot 0's first REG entries into registers; the band entries
   // that stream from HBM every iteration (work accounting: the rest of slot 0's, all of the others')
-  double vc[HARD_PCG_REG_DIAG];
+  double vc[REG];
   double nnz = 0.0, nnz_reg = 0.0;
 #pragma unroll 1
   for (int m = 0; m < SLOTS; ++m) {
     const int a = t + m * HARD_PCG_THREADS;
-    int l = a < D ? rg[2 * a] - a + W : BW;
-    int h = a < D ? rg[2 * a + 1] - a + W : -1;
-    if (a < D) rlh[a] = l | (h << 16);
-    const int lo = l, hi = h;
-    for (int off = 32; off > 0; off >>= 1) {
-      l = min(l, __shfl_xor(l, off, 64));
-      h = max(h, __shfl_xor(h, off, 64));
-    }
-    if ((t & 63) == 0) {
-      wlh[2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6))] = l;
-      wlh[2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6)) + 1] = h;
-    }
+    const int hi = a < D ? rg[2 * a + 1] - rg[2 * a] : -1;
+    if (a < D) rlh[a] = hi | (rg[2 * a] << 16);
+    int h = hi;
+    for (int off = 32; off > 0; off >>= 1) h = max(h, __shfl_xor(h, off, 64));
+    if ((t & 63) == 0) wlh[m * (HARD_PCG_THREADS / 64) + (t >> 6)] = h;
     if (m == 0) {
       const double* Sa = S + (a < D ? a : 0);
-      const int ol = __builtin_amdgcn_readfirstlane(l);
 #pragma unroll
-      for (int u = 0; u < HARD_PCG_REG_DIAG; ++u) vc[u] = Sa[(size_t)min(ol + u, BW - 1) * dmax];
+      for (int u = 0; u < REG; ++u) vc[u] = Sa[(size_t)min(u, BW - 1) * dmax];
       if (a < D) {
-        const int streamed = max(0, hi - max(lo, ol + HARD_PCG_REG_DIAG) + 1);
+        const int streamed = max(0, hi + 1 - REG);
         nnz += streamed;
-        nnz_reg += hi - lo + 1 - streamed;
+        nnz_reg += hi + 1 - streamed;
       }
     } else if (a < D) {
-      nnz += hi - lo + 1;
+      nnz += hi + 1;
     }
   }
   if (work) {
@@ -672,10 +666,9 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     for (int m = 0; m < SLOTS; ++m) {
       if (wbase + m * HARD_PCG_THREADS >= D) break;   // wave-uniform: no row of this wave's slot m
       const int a = t + m * HARD_PCG_THREADS;
-      const int lohi = a < D ? rlh[a] : 0xffff;   // empty range for rows past D
-      const int* w2 = wlh + 2 * (m * (HARD_PCG_THREADS / 64) + (t >> 6));
-      const double sp = spmv(a, a < D, __builtin_amdgcn_readfirstlane(w2[0]), __builtin_amdgcn_readfirstlane(w2[1]),
-                             lohi, m == 0, vc);
+      const int c0hi = a < D ? rlh[a] : 0;   // (rows past D: own = false, nothing added)
+      const int jmax = __builtin_amdgcn_readfirstlane(wlh[m * (HARD_PCG_THREADS / 64) + (t >> 6)]);
+      const double sp = spmv(a, a < D, jmax, c0hi, m == 0, vc);
       if (a < D) {
         al[a] = sp;
         part += pv[a] * sp;
@@ -775,7 +768,7 @@ __global__ void __launch_bounds__(256) k_hard_direct(int B, int N, int NX, int W
   // elimination's fill-in never leaves (no pivoting)
   for (int e = threadIdx.x; e < D * BW; e += blockDim.x) {
     const int a = e / BW, o = e - a * BW, c = a - W + o;
-    Mb[e] = (c >= rg[2 * a] && c <= rg[2 * a + 1]) ? S[(size_t)o * dmax + a] : 0.0;
+    Mb[e] = (c >= rg[2 * a] && c <= rg[2 * a + 1]) ? S[(size_t)(c - rg[2 * a]) * dmax + a] : 0.0;
   }
   for (int a = threadIdx.x; a < D; a += blockDim.x) atomicMax(&s_wr, max(a - rg[2 * a], rg[2 * a + 1] - a));
   for (int a = threadIdx.x; a < D; a += blockDim.x) y[a] = gam[(size_t)b * dmax + a];
