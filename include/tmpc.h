@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 6
+#define TMPC_ABI_VERSION 7   /* 7: tmpc_kernel_bytes */
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
