@@ -455,7 +455,7 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
             nnz += streamed
             nnz_reg += width - streamed
         nb, b2 = D // nx, nx * nx
-        offset = max(4 * D, 4 * (b2 + 2 * nx)) + 16 + (D + 2 * slots * 16 + 1) // 2
+        offset = max(4 * D, 4 * (b2 + 2 * nx)) + 32 + (D + 2 * slots * 16 + 1) // 2
         ncap = max(0, 160 * 1024 // 8 - offset) // b2
         ncd = min(nb, ncap) if ptype in ("BJ", "SS") else 0
         ncl = min(nb - 1, ncap - ncd) if ptype == "SS" and nb > 1 else 0

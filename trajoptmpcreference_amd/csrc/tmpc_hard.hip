@@ -390,13 +390,27 @@ __host__ __device__ constexpr int hard_pcg_reg_diag(int nx) { return nx <= 4 ? 1
 __host__ __device__ constexpr int hard_pcg_scratch(int dmax, int nx) {
   return 4 * dmax > 4 * (nx * nx + 2 * nx) ? 4 * dmax : 4 * (nx * nx + 2 * nx);
 }
-// doubles before k_hard_pcg's preconditioner-block cache: the scratch, 16 reduction slots, the rows'
+// doubles before k_hard_pcg's preconditioner-block cache: the scratch, 2 x 16 reduction slots, the rows'
 // and the wave-slots' diagonal ranges (ints)
 __host__ __device__ constexpr int hard_pcg_cache_offset(int D, int nx, int slots) {
-  return hard_pcg_scratch(D, nx) + 16 + (D + 2 * slots * (HARD_PCG_THREADS / 64) + 1) / 2;
+  return hard_pcg_scratch(D, nx) + 32 + (D + 2 * slots * (HARD_PCG_THREADS / 64) + 1) / 2;
 }
 
 // ---- workgroup sum (deterministic): wave DPP butterfly via shuffles + fixed-order fan-in
+// Double-buffered form for a sequence of sums (k_hard_pcg): sum number k uses slots red[16 (k & 1) ..],
+// so the barrier that protects a slot set from being overwritten while a slow wave still reads it is
+// the NEXT sum's own barrier -- one barrier per sum instead of two.
+__device__ __forceinline__ double h_block_sum_db(double v, double* red, int& k) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  double* rs = red + 16 * (k & 1);
+  ++k;
+  if ((threadIdx.x & 63) == 0) rs[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < nw; ++i) s += rs[i];
+  return s;
+}
 __device__ __forceinline__ double h_block_sum(double v, double* red) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
@@ -461,7 +475,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   double* zl = pv + D;
   double* al = zl + D;
   double* red = sh + hard_pcg_scratch(D, NX);
-  int* rlh = reinterpret_cast<int*>(red + 16);   // [D] each row's last entry | first column << 16
+  int* rlh = reinterpret_cast<int*>(red + 32);   // [D] each row's last entry | first column << 16
   int* wlh = rlh + D;                            // [SLOTS][16 waves] each wave-slot's longest row (last entry)
   double* pcache = sh + hard_pcg_cache_offset(D, NX, SLOTS);
   const bool blocks = precond == PRECOND_BJ || precond == PRECOND_SS;
@@ -612,6 +626,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   // that stream from HBM every iteration (work accounting: the rest of slot 0's, all of the others')
   double vc[REG];
   double nnz = 0.0, nnz_reg = 0.0;
+  int nsum = 0;   // workgroup sums so far (h_block_sum_db's slot parity)
 #pragma unroll 1
   for (int m = 0; m < SLOTS; ++m) {
     const int a = t + m * HARD_PCG_THREADS;
@@ -634,8 +649,8 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     }
   }
   if (work) {
-    nnz = h_block_sum(nnz, red);
-    nnz_reg = h_block_sum(nnz_reg, red);
+    nnz = h_block_sum_db(nnz, red, nsum);
+    nnz_reg = h_block_sum_db(nnz_reg, red, nsum);
   }
   double xv[SLOTS];
   const double* g = gam + (size_t)b * dmax;
@@ -657,7 +672,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       part += rv[a] * z;
     }
   }
-  double nu = h_block_sum(part, red);
+  double nu = h_block_sum_db(part, red, nsum);
   int it_done = max_iter;
   for (int it = 0; it < max_iter; ++it) {
     __syncthreads();
@@ -674,7 +689,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
         part += pv[a] * sp;
       }
     }
-    const double alpha = nu / h_block_sum(part, red);
+    const double alpha = nu / h_block_sum_db(part, red, nsum);
 #pragma unroll
     for (int m = 0; m < SLOTS; ++m) {
       const int a = t + m * HARD_PCG_THREADS;
@@ -694,7 +709,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
         part += rv[a] * z;
       }
     }
-    const double nup = h_block_sum(part, red);
+    const double nup = h_block_sum_db(part, red, nsum);
     if (fabs(nup) < tol) {
       it_done = it + 1;
       break;
