@@ -9,7 +9,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
-ARM_N = {"arm2": 2, "arm3": 3, "arm6fix": 6}
+ARM_N = {"arm2": 2, "arm3": 3, "arm6fix": 6, "arm7": 7}
 
 
 def pytest_configure(config):

@@ -400,18 +400,24 @@ def test_hard_pcg_on_oracle_S_is_exact(name, N, ptype, seed):
     assert ctx.kernel_bytes("hard_pcg") == _hard_pcg_bytes(Ss, it, nx, ptype, dmax)
 
 
-@pytest.mark.parametrize("ptype", ["SS", "BJ", "J"])
-def test_hard_pcg_large_banded_is_exact(ptype):
+LARGE_CASES = [(ptype, 12, (1530, 1100, 700), "arm6fix") for ptype in ("SS", "BJ", "J")] + \
+    [("SS", 14, (3000, 2100), "arm7")]
+
+
+@pytest.mark.parametrize("ptype,nx,dims_,model", LARGE_CASES,
+                         ids=[f"{c[0]}-nx{c[1]}-D{c[2][0]}" for c in LARGE_CASES])
+def test_hard_pcg_large_banded_is_exact(ptype, nx, dims_, model):
     """Schur dimensions past one 1024-row slot and past the LDS block cache (D = 1530: 94 of 127 diagonal
-    blocks fit, the rest stream from HBM; D = 1100 and 700 alongside, all cached), a trailing partial block
-    (1530 mod 12 = 6 unpreconditioned rows): counts and lambda bit for bit against pcg_canonical, and the
+    blocks fit, the rest stream from HBM; D = 1100 and 700 alongside, all cached; D = 3000 at nx = 14:
+    three row slots, 35 of 214 diagonal blocks cached), trailing partial blocks (1530 mod 12 = 6,
+    3000 mod 14 = 4 unpreconditioned rows): counts and lambda bit for bit against pcg_canonical, and the
     kernel's byte count exactly."""
     from oracle import hard as ohard
     from trajoptmpcreference_amd import _native
-    nx, W = 12, 30
+    W = 30
     rng = np.random.default_rng(7)
     Ss, gs = [], []
-    for D in (1530, 1100, 700):
+    for D in dims_:
         M = np.zeros((D, D))
         for o in range(-W // 2, W // 2 + 1):
             M += np.diag(rng.uniform(-1.0, 1.0, D - abs(o)), o)
@@ -425,7 +431,7 @@ def test_hard_pcg_large_banded_is_exact(ptype):
         Sb[i, :len(gm)] = _band(S, W)
         gb[i, :len(gm)] = gm
     ctx = _native.default_context(0)
-    ctx.set_model(arm_model("arm6fix"))
+    ctx.set_model(arm_model(model))
     ctx.reset_stats()
     lam, it = ctx.hard_pcg_batch(Sb, gb, dims, nx, ptype, tol=1e-10, max_iter=200)
     for i, (S, gm) in enumerate(zip(Ss, gs)):
