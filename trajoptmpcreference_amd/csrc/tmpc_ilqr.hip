@@ -1077,6 +1077,8 @@ struct LaunchIlqr {
   }
 };
 
+// (Unlike tmpc_fd.hip / tmpc_kernels.hip, a runtime chain model keeps the CHAIN instance here: the rollout
+// measured 2.1 ms per launch on it against 3.2 ms on the general-topology one, arm6 B = 4096.)
 #define TMPC_DISPATCH_ILQR(nj, chain, CALL)                                                              \
   switch (mid) {                                                                                       \
     TMPC_STATIC_MODEL_CASES(LaunchIlqr, CALL)                                                            \

@@ -2023,6 +2023,9 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
                      phi);
 }
 
+// A runtime model (ModelRef: every coefficient a load) always takes the general-topology instance: with
+// runtime coefficients the CHAIN specialisation's fully unrolled recursion spills about 9x more
+// (k_ls_terms<6, chain, ModelRef, double> 19 kB per lane against 2.2 kB).
 // dispatch tables over the joint count and the chain specialisation
 #ifdef TMPC_DEV_NJ
 #define TMPC_DISPATCH_NJ(nj, chain, CALL)                                          \
@@ -2037,13 +2040,13 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
     default: break;                                                                                    \
   }                                                                                                    \
   switch (nj) {                                                                                        \
-    case 1: if (chain) Launch<1, true, ModelRef>::CALL; else Launch<1, false, ModelRef>::CALL; break;  \
-    case 2: if (chain) Launch<2, true, ModelRef>::CALL; else Launch<2, false, ModelRef>::CALL; break;  \
-    case 3: if (chain) Launch<3, true, ModelRef>::CALL; else Launch<3, false, ModelRef>::CALL; break;  \
-    case 4: if (chain) Launch<4, true, ModelRef>::CALL; else Launch<4, false, ModelRef>::CALL; break;  \
-    case 5: if (chain) Launch<5, true, ModelRef>::CALL; else Launch<5, false, ModelRef>::CALL; break;  \
-    case 6: if (chain) Launch<6, true, ModelRef>::CALL; else Launch<6, false, ModelRef>::CALL; break;  \
-    case 7: if (chain) Launch<7, true, ModelRef>::CALL; else Launch<7, false, ModelRef>::CALL; break;  \
+    case 1: (void)chain; Launch<1, false, ModelRef>::CALL; break;  \
+    case 2: (void)chain; Launch<2, false, ModelRef>::CALL; break;  \
+    case 3: (void)chain; Launch<3, false, ModelRef>::CALL; break;  \
+    case 4: (void)chain; Launch<4, false, ModelRef>::CALL; break;  \
+    case 5: (void)chain; Launch<5, false, ModelRef>::CALL; break;  \
+    case 6: (void)chain; Launch<6, false, ModelRef>::CALL; break;  \
+    case 7: (void)chain; Launch<7, false, ModelRef>::CALL; break;  \
     default: return -2;                                                                                \
   }                                                                                                    \
   return 0;
