@@ -310,8 +310,8 @@ int tmpc_synchronize(tmpc_ctx* ctx);
 
 /* Kernel timing collected with HIP events on the context stream when options.profile = 1.
  * name: "qp_fd", "qp_minv", "qp_grad", "ginv", "qp" (the fused Schur + PCG + dxu kernel), "schur",
- * "btsolve", "dxu", "ls_terms", "ls_decide", "hard_schur", "hard_pcg", "hard_direct", "ilqr_backward",
- * "ilqr_forward", "ilqr_decide", "mpc_shift", "pcg" (tmpc_pcg_batch / tmpc_hard_pcg_batch). */
+ * "btsolve", "dxu", "ls_terms", "ls_decide", "hard_schur", "hard_pcg" (also tmpc_hard_pcg_batch),
+ * "hard_direct", "ilqr_backward", "ilqr_forward", "ilqr_decide", "mpc_shift", "pcg" (tmpc_pcg_batch). */
 int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
 /* Algorithmic HBM bytes moved by a kernel that counts them, summed over its launches since the last
  * tmpc_reset_stats (any options.profile): "hard_pcg" (the hard-limit PCG of tmpc_sqp_solve_batch* /
