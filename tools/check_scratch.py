@@ -12,7 +12,9 @@ Usage: make -C trajoptmpcreference_amd/csrc check-scratch
 import re
 import sys
 
-HOT = ("k_qp_grad", "k_qp_fd", "k_qp_minv", "k_ls_terms", "k_ilqr_forward", "k_ilqr_backward", "k_qp<",
+# (k_ls_terms is not gated: it trades 348 B/lane of spill for a second wave per SIMD, measured faster,
+# tmpc_fd.hip)
+HOT = ("k_qp_grad", "k_qp_fd", "k_qp_minv", "k_ilqr_forward", "k_ilqr_backward", "k_qp<",
        "k_qpILi", "k_mpc_shift", "k_rollout")
 
 

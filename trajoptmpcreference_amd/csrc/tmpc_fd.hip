@@ -70,8 +70,11 @@ __global__ void __launch_bounds__(256) k_qp_fd(MT M, PList P, int B, int N, doub
 // |x_0 - xs| violation term.  SOFT: soft-limit value (slot 3, summed after
 // the cost terms as totalCost does, :303-307) and jacobian . dxu added to D
 // (:633-646).  terms: [B][T][N][4] = cost, violation, D, soft value.
+// Two waves per SIMD (amdgpu_waves_per_eu(2)): left to itself the compiler took 256 VGPRs + 76 AGPRs, one
+// wave per SIMD, with nothing to hide the dynamics' latencies; at two it spills 348 B/lane and the headline
+// launch takes 0.142 ms instead of 0.195 (profiles/r04/ls_terms).
 template <int NJ, bool CHAIN, bool SOFT, class MT, class R>
-__global__ void __launch_bounds__(256) k_ls_terms(MT M, const CostDev* __restrict__ C,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_ls_terms(MT M, const CostDev* __restrict__ C,
                                                   const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
                                                   const double* __restrict__ lam,
                                                   PList P, int B, int N, int T, double dt, const double* __restrict__ alphas,
