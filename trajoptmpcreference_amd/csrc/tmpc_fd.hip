@@ -359,12 +359,17 @@ struct LaunchFD {
       hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), P, B, N, dt, x, u,
                          xs, need, qdd, cvec);
   }
+  // a runtime model (ModelRef) takes the general-topology line-search instance even for a chain: with
+  // runtime coefficients the chain specialisation's unrolled recursion spills 9x more (k_ls_terms<6,
+  // chain, ModelRef, double> 19 kB per lane against 2.2 kB; 11.2 -> 1.9 ms per headline launch, DESIGN.md
+  // 4a); the other FD kernels keep the chain instance, which measured faster for them
+  static constexpr bool LCHAIN = MT::STATIC ? CHAIN : false;
   static void ls_terms(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
                        const double* lam, PList P, int B, int N, int T, double dt, const double* alphas, const double* x,
                        const double* u, const double* xs, const double* dx, const double* du, const int* active,
                        double* terms) {
 #define TMPC_LS(SOFTV, RV)                                                                                        \
-    hipLaunchKernelGGL((k_ls_terms<NJ, CHAIN, SOFTV, MT, RV>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, \
+    hipLaunchKernelGGL((k_ls_terms<NJ, LCHAIN, SOFTV, MT, RV>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, \
                        lam, P, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms);
     if (mu) { if (f32) { TMPC_LS(true, float) } else { TMPC_LS(true, double) } }
     else { if (f32) { TMPC_LS(false, float) } else { TMPC_LS(false, double) } }
@@ -390,9 +395,6 @@ struct LaunchFD {
   }
 };
 
-// A runtime model (ModelRef: every coefficient a load) always takes the general-topology instance: with
-// runtime coefficients the CHAIN specialisation's fully unrolled recursion spills about 9x more
-// (k_ls_terms<6, chain, ModelRef, double> 19 kB per lane against 2.2 kB).
 // dispatch tables over the joint count and the chain specialisation
 #define TMPC_DISPATCH_NJ(nj, chain, CALL)                                                              \
   switch (mid) {                                                                                       \
@@ -400,13 +402,13 @@ struct LaunchFD {
     default: break;                                                                                    \
   }                                                                                                    \
   switch (nj) {                                                                                        \
-    case 1: (void)chain; LaunchFD<1, false, ModelRef>::CALL; break;  \
-    case 2: (void)chain; LaunchFD<2, false, ModelRef>::CALL; break;  \
-    case 3: (void)chain; LaunchFD<3, false, ModelRef>::CALL; break;  \
-    case 4: (void)chain; LaunchFD<4, false, ModelRef>::CALL; break;  \
-    case 5: (void)chain; LaunchFD<5, false, ModelRef>::CALL; break;  \
-    case 6: (void)chain; LaunchFD<6, false, ModelRef>::CALL; break;  \
-    case 7: (void)chain; LaunchFD<7, false, ModelRef>::CALL; break;  \
+    case 1: if (chain) LaunchFD<1, true, ModelRef>::CALL; else LaunchFD<1, false, ModelRef>::CALL; break;  \
+    case 2: if (chain) LaunchFD<2, true, ModelRef>::CALL; else LaunchFD<2, false, ModelRef>::CALL; break;  \
+    case 3: if (chain) LaunchFD<3, true, ModelRef>::CALL; else LaunchFD<3, false, ModelRef>::CALL; break;  \
+    case 4: if (chain) LaunchFD<4, true, ModelRef>::CALL; else LaunchFD<4, false, ModelRef>::CALL; break;  \
+    case 5: if (chain) LaunchFD<5, true, ModelRef>::CALL; else LaunchFD<5, false, ModelRef>::CALL; break;  \
+    case 6: if (chain) LaunchFD<6, true, ModelRef>::CALL; else LaunchFD<6, false, ModelRef>::CALL; break;  \
+    case 7: if (chain) LaunchFD<7, true, ModelRef>::CALL; else LaunchFD<7, false, ModelRef>::CALL; break;  \
     default: return -2;                                                                                \
   }                                                                                                    \
   return 0;

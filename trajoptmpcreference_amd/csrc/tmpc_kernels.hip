@@ -1651,13 +1651,17 @@ struct Launch {
       hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), P, B, N,
                          x, need, minv);
   }
+  // a runtime model (ModelRef) takes the general-topology gradient instance even for a chain: with runtime
+  // coefficients the chain specialisation's unrolled recursion spills 2.5x more (k_qp_grad<6, chain,
+  // ModelRef, double> 4.4 kB per lane against 1.7 kB; 2.7 -> 1.3 ms per headline launch)
+  static constexpr bool GCHAIN = MT::STATIC ? CHAIN : false;
   static void qp_grad(bool f32, hipStream_t s, const ModelDev* M, PList P, int B, int N, double dt, const double* x,
                       const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
     if (f32)
-      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P, B,
+      hipLaunchKernelGGL((k_qp_grad<NJ, GCHAIN, MT, float>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P, B,
                          N, dt, x, need, qdd, minv, A, Bm);
     else
-      hipLaunchKernelGGL((k_qp_grad<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P,
+      hipLaunchKernelGGL((k_qp_grad<NJ, GCHAIN, MT, double>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P,
                          B, N, dt, x, need, qdd, minv, A, Bm);
   }
   static void unit_minv(bool f32, hipStream_t s, const ModelDev* M, int K, const double* x, double* minv) {
@@ -1669,10 +1673,10 @@ struct Launch {
   static void unit_grad(bool f32, hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* qdd,
                         const double* minv, double* A, double* Bm, double* dqdd) {
     if (f32)
-      hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN, MT, float>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
+      hipLaunchKernelGGL((k_unit_grad<NJ, GCHAIN, MT, float>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
                          minv, A, Bm, dqdd);
     else
-      hipLaunchKernelGGL((k_unit_grad<NJ, CHAIN, MT, double>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
+      hipLaunchKernelGGL((k_unit_grad<NJ, GCHAIN, MT, double>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
                          minv, A, Bm, dqdd);
   }
 };
@@ -2023,9 +2027,6 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
                      phi);
 }
 
-// A runtime model (ModelRef: every coefficient a load) always takes the general-topology instance: with
-// runtime coefficients the CHAIN specialisation's fully unrolled recursion spills about 9x more
-// (k_ls_terms<6, chain, ModelRef, double> 19 kB per lane against 2.2 kB).
 // dispatch tables over the joint count and the chain specialisation
 #ifdef TMPC_DEV_NJ
 #define TMPC_DISPATCH_NJ(nj, chain, CALL)                                          \
@@ -2040,13 +2041,13 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
     default: break;                                                                                    \
   }                                                                                                    \
   switch (nj) {                                                                                        \
-    case 1: (void)chain; Launch<1, false, ModelRef>::CALL; break;  \
-    case 2: (void)chain; Launch<2, false, ModelRef>::CALL; break;  \
-    case 3: (void)chain; Launch<3, false, ModelRef>::CALL; break;  \
-    case 4: (void)chain; Launch<4, false, ModelRef>::CALL; break;  \
-    case 5: (void)chain; Launch<5, false, ModelRef>::CALL; break;  \
-    case 6: (void)chain; Launch<6, false, ModelRef>::CALL; break;  \
-    case 7: (void)chain; Launch<7, false, ModelRef>::CALL; break;  \
+    case 1: if (chain) Launch<1, true, ModelRef>::CALL; else Launch<1, false, ModelRef>::CALL; break;  \
+    case 2: if (chain) Launch<2, true, ModelRef>::CALL; else Launch<2, false, ModelRef>::CALL; break;  \
+    case 3: if (chain) Launch<3, true, ModelRef>::CALL; else Launch<3, false, ModelRef>::CALL; break;  \
+    case 4: if (chain) Launch<4, true, ModelRef>::CALL; else Launch<4, false, ModelRef>::CALL; break;  \
+    case 5: if (chain) Launch<5, true, ModelRef>::CALL; else Launch<5, false, ModelRef>::CALL; break;  \
+    case 6: if (chain) Launch<6, true, ModelRef>::CALL; else Launch<6, false, ModelRef>::CALL; break;  \
+    case 7: if (chain) Launch<7, true, ModelRef>::CALL; else Launch<7, false, ModelRef>::CALL; break;  \
     default: return -2;                                                                                \
   }                                                                                                    \
   return 0;
