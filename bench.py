@@ -277,11 +277,13 @@ def hard_limits(preset):
 
 
 def hard_roofline(a, kernels, hard_bytes):
-    """Roofline of k_hard_pcg, the hard-limit path's dominant kernel: the banded Schur complement and the
-    preconditioner blocks stream from HBM every PCG iteration (too large for LDS: ~0.4 MB per problem), so
-    it is HBM-bound.  `achieved` = the algorithmic bytes the kernel itself counts (tmpc_kernel_bytes,
-    DESIGN.md 4f: the band's structural entries and the preconditioner entries each iteration reads, gamma
-    in, lambda out, the setup blocks) / the average launch time."""
+    """Roofline of k_hard_pcg, the hard-limit path's dominant kernel.  `achieved` = the bytes the kernel
+    itself counts (tmpc_kernel_bytes): everything it reads and writes beyond its registers and
+    LDS -- per iteration the band entries not held in registers and the preconditioner blocks not held in
+    LDS, gamma in, lambda out, the setup blocks -- / the average launch time, against the HBM peak.  After
+    the first iteration those re-reads are L2 hits (a problem's streamed part is ~85 kB; 32 problems per
+    XCD fit its 4 MB L2): `traffic`, the PMC bytes, is what reaches the fabric, and hbm_GBps / hbm_frac
+    show how little HBM the kernel uses.  It is bound by one problem's iteration latency, not by memory."""
     hp = kernels["hard_pcg"]
     per_launch = hard_bytes / hp["launches"]
     avg_s = hp["avg_ms"] / 1e3
@@ -290,14 +292,17 @@ def hard_roofline(a, kernels, hard_bytes):
     out = {"kernel": "k_hard_pcg", "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "avg_launch_ms": hp["avg_ms"],
            "algorithmic_bytes_per_launch": per_launch,
-           "bytes_basis": "counted by the kernel per problem: 8 B x (2 D + iterations x streamed band entries + "
-                          "(iterations + 1) x streamed distinct preconditioner entries + once: register-held band "
-                          "entries, setup blocks), DESIGN.md 4f",
+           "bytes_basis": "counted by the kernel per problem: 8 B x (2 D + iterations x band entries not in "
+                          "registers + (iterations + 1) x distinct preconditioner entries not in LDS + once: "
+                          "register-held band entries, setup blocks), DESIGN.md 4f; served by L2 after the first "
+                          "iteration",
            "note": "each row's first band entries stay in registers and the preconditioner blocks in LDS for "
-                   "the whole solve, so HBM is no longer what binds: one 16-wave workgroup per problem, the "
-                   "PCG iteration's barrier-separated phases (DESIGN.md 4f)"}
+                   "the whole solve, so memory is not what binds: one 16-wave workgroup per problem, the PCG "
+                   "iteration's barrier-separated phases (DESIGN.md 4f)"}
     if traffic:
-        out.update(hbm_GBps=traffic / avg_s / 1e9, traffic_source=src)
+        out.update(hbm_GBps=traffic / avg_s / 1e9, hbm_frac=traffic / avg_s / 1e9 / HBM_PEAK_GBS,
+                   traffic_source=src,
+                   traffic_note="2 x FETCH_SIZE + WRITE_SIZE per launch; FETCH_SIZE includes Infinity-Cache hits")
     return out
 
 

@@ -313,7 +313,8 @@ int tmpc_synchronize(tmpc_ctx* ctx);
  * "btsolve", "dxu", "ls_terms", "ls_decide", "hard_schur", "hard_pcg" (also tmpc_hard_pcg_batch),
  * "hard_direct", "ilqr_backward", "ilqr_forward", "ilqr_decide", "mpc_shift", "pcg" (tmpc_pcg_batch). */
 int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
-/* Algorithmic HBM bytes moved by a kernel that counts them, summed over its launches since the last
+/* Bytes a counting kernel reads and writes beyond its registers and LDS (its algorithmic memory traffic,
+ * served by L2 / Infinity Cache / HBM), summed over its launches since the last
  * tmpc_reset_stats (any options.profile): "hard_pcg" (the hard-limit PCG of tmpc_sqp_solve_batch* /
  * tmpc_qp_batch: per launch and problem 8 B x (2 D + iterations x band entries + (iterations + 1) x
  * distinct preconditioner entries + setup blocks)).  Other names fail. */

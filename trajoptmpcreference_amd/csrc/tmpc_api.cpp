@@ -66,7 +66,7 @@ struct tmpc_ctx {
   // the last tmpc_qp_batch with hard limits (tmpc_qp_hard_info reads its hd_* buffers); cleared by every
   // other user of those buffers (setup_hard) and by a change of the limits, so stale data is refused
   struct { int B, N, dmax, W, rmax; } hard_last{0, 0, 0, 0, 0};
-  std::map<std::string, double> kbytes;   // algorithmic HBM bytes of counting kernels since tmpc_reset_stats
+  std::map<std::string, double> kbytes;   // bytes beyond registers / LDS of counting kernels since tmpc_reset_stats
 };
 
 static int fail(tmpc_ctx* c, const char* fmt, ...) {

@@ -730,7 +730,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   }
   if (t == 0) iters[b] = it_done;
   if (work && t == 0) {
-    // algorithmic HBM bytes of this launch: gamma in, lambda out; per iteration the
+    // bytes of this launch beyond registers and LDS: gamma in, lambda out; per iteration the
     // band's structural entries (S p) not held in registers, and the distinct preconditioner entries
     // one P^-1 r needs that are not resident in LDS (SS: of the nb diagonal and nb - 1 stair blocks,
     // each once, all but the ncd + ncl cached ones), it_done + 1 of those; once: the register-held band
