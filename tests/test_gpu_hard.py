@@ -135,12 +135,13 @@ def test_hard_batch_matches_oracle(name, N, B, method, spec):
         _replay_pcg_counts(solver, r, np.array(xs), np.array(us), N, method, hard, n)
 
 
-def _replay_pcg_counts(solver, r, x0s, u0s, N, method, hard, n):
+def _replay_pcg_counts(solver, r, x0s, u0s, N, method, hard, n, base_opts=None):
     from oracle import hard as ohard
     nx = 2 * n
     B = x0s.shape[0]
     nqs = [int(r["sqp_iter"][i]) + (1 if int(r["exit_sqp"][i]) == 3 else 0) for i in range(B)]
-    opts = {}
+    base_opts = dict(base_opts or {})
+    opts = dict(base_opts)
     solver.set_default_options(opts)
     ctx = solver._context(opts)
     # rho of each QP: the trace row holds rho before check_for_exit_or_error's increase on a failed line
@@ -162,7 +163,7 @@ def _replay_pcg_counts(solver, r, x0s, u0s, N, method, hard, n):
         if j == 0:
             xj, uj = x0s[live], u0s[live]
         else:   # the GPU's own iterate j: the same solve, stopped after j iterations
-            rj = solver.SQP_batch(x0s, u0s, N, 0.1, method, {"max_iter_SQP_DDP": j})
+            rj = solver.SQP_batch(x0s, u0s, N, 0.1, method, dict(base_opts, max_iter_SQP_DDP=j))
             xj, uj = rj["x"][live], rj["u"][live]
         rho = np.array([rho_seq[i][j] for i in live])
         ctx = solver._context(dict(opts))

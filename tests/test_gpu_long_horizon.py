@@ -18,7 +18,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, arm_model, golden, quad_cost_arrays
+from conftest import GOLDEN, arm_model, golden, quad_cost_arrays, replay_qp_counts
 
 pytestmark = pytest.mark.gpu
 
@@ -54,6 +54,28 @@ def test_sqp_pcgss_arm6_n128_matches_oracle():
         assert list(r["trace"]["alpha"][i, 1:len(al) + 1]) == al, i
         assert _rel(r["x"][i], d["x"][i]) < 1e-6, i
         assert _rel(r["u"][i], d["u"][i]) < 1e-6, i
+    # integer parity on identical inputs: the GM instance against its canonical-order restatement
+    solver = _solver(6)
+    for i in range(2):
+        nq = int(r["sqp_iter"][i]) + (1 if int(r["exit_sqp"][i]) == 3 else 0)
+        counts = [int(v) for v in r["trace"]["pcg_iters"][i, 1:nq + 1]]
+        ok = [bool(v) for v in r["trace"]["succeeded_line_search"][i, 1:nq + 1]]
+        replay_qp_counts(solver, x[i:i + 1], u[i:i + 1], N, 0.1, "PCG-SS", counts, ok)
+
+
+def test_sqp_pcgss_arm6_n128_warm_start_replay():
+    """Config 5's QP path: the GM instance with the PCG warm start (each QP from the previous QP's
+    lambda), every QP replayed exactly against the canonical order started from the same guess."""
+    N = 128
+    x, u = _problems(N, [975])
+    solver = _solver(6)
+    opts = {"pcg_warm_start": True}
+    r = solver.SQP_batch(x, u, N, 0.1, "PCG-SS", dict(opts))
+    nq = int(r["sqp_iter"][0]) + (1 if int(r["exit_sqp"][0]) == 3 else 0)
+    assert nq >= 3
+    counts = [int(v) for v in r["trace"]["pcg_iters"][0, 1:nq + 1]]
+    ok = [bool(v) for v in r["trace"]["succeeded_line_search"][0, 1:nq + 1]]
+    replay_qp_counts(solver, x, u, N, 0.1, "PCG-SS", counts, ok, opts=opts, warm=True)
 
 
 def test_sqp_method_s_arm6_n128_matches_oracle():
@@ -82,6 +104,13 @@ def test_config5_mpc_loop_sqp_pcgss_arm6_n128():
         assert np.allclose(r["u_exec"][i], d["u_exec"][i], rtol=1e-6, atol=1e-8), i
 
 
+# the GM instance's PCG-J counts where they differ from the reference's recorded ones (test_gpu_sqp.py
+# PCGJ_ORDER_DECIDED): fixture -> {QP index: (the GPU's count, the reference's)}
+PCGJ_ORDER_DECIDED_GM = {
+    "sqp_arm3_N8_s2_PCG-J.npz": {1: (58, 59), 2: (58, 59)},
+}
+
+
 @pytest.mark.parametrize("f", sorted(glob.glob(os.path.join(GOLDEN, "sqp_arm*_N*_s*_PCG-*.npz"))),
                          ids=lambda f: os.path.basename(f))
 def test_gm_instance_matches_reference_fixtures(f, monkeypatch):
@@ -98,11 +127,14 @@ def test_gm_instance_matches_reference_fixtures(f, monkeypatch):
     tr = solver.trace
     assert [t["alpha"] for t in tr] == list(d["tr_alpha"])
     ours = [t["inner_iters"] for t in tr[1:]]
-    if method == "PCG-J":   # test_gpu_sqp.py: Jacobi CG may stop one iteration apart after QP 0
+    if method == "PCG-J":   # test_gpu_sqp.py: the QPs whose Jacobi CG count the rounding of S decides
+        from test_gpu_sqp import pcgj_diffs
         assert ours[0] == int(d["pcg_iters"][0])
-        assert all(abs(a - int(v)) <= 1 for a, v in zip(ours, d["pcg_iters"]))
+        assert pcgj_diffs(ours, d["pcg_iters"]) == PCGJ_ORDER_DECIDED_GM.get(os.path.basename(f), {})
     else:
         assert ours == list(d["pcg_iters"])
+    replay_qp_counts(solver, d["x0"][None], d["u0"][None], N, float(d["dt"]), method, ours,
+                     [t["succeeded_line_search"] for t in tr[1:]], gm_min_rows=1)
     rtol = 1e-4 if method == "PCG-J" else 1e-7
     assert _rel(x, d["x"]) < rtol
     assert _rel(u, d["u"]) < rtol

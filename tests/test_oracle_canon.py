@@ -24,11 +24,14 @@ def canon():
     return c
 
 
+@pytest.mark.parametrize("rpl", [1, 2])
 @pytest.mark.parametrize("name", ["qp_arm2_N8", "qp_arm3_N32", "qp_arm6fix_N64"])
 @pytest.mark.parametrize("ptype", ["J", "BJ", "SS", "0"])
-def test_canonical_pcg_counts_match_reference(canon, name, ptype):
+def test_canonical_pcg_counts_match_reference(canon, name, ptype, rpl):
+    """Both lane layouts of the kernel (one row of S per lane; two -- the register instance past 768
+    rows and the HBM-row GM instance) take the reference's counts on its own S."""
     d = golden(f"{name}.npz")
-    lam, it, tn = canon.pcg(d["S_diag"], d["S_lo"], d["gamma"], ptype)
+    lam, it, tn = canon.pcg(d["S_diag"], d["S_lo"], d["gamma"], ptype, rpl=rpl)
     assert it == int(d[f"iters_{ptype}"])
     ref = d[f"lam_{ptype}"]
     # unpreconditioned CG ('0') on cond(S) ~ 1e6 amplifies the order's rounding in its truncated iterate
@@ -46,3 +49,23 @@ def test_canonical_block_inverse(canon, name):
     P = canon.block_inverse(d["S_diag"])
     ref = d["P_BJ_diag"]
     assert float(np.max(np.abs(P - ref))) <= 1e-12 * float(np.max(np.abs(ref)))
+
+
+def test_canonical_layouts_and_warm_start(canon):
+    """The two layouts are different operation orders (their lambdas differ in the last bits), the
+    warm start from the solution itself exits at once, and sizes past the layout's 1024 lanes raise."""
+    d = golden("qp_arm6fix_N64.npz")
+    l1, i1, _ = canon.pcg(d["S_diag"], d["S_lo"], d["gamma"], "SS", rpl=1)
+    l2, i2, _ = canon.pcg(d["S_diag"], d["S_lo"], d["gamma"], "SS", rpl=2)
+    assert i1 == i2 and not np.array_equal(l1, l2)
+    assert float(np.max(np.abs(l1 - l2))) < 1e-8 * float(np.max(np.abs(l1)))
+    l3, i3, _ = canon.pcg(d["S_diag"], d["S_lo"], d["gamma"], "SS", rpl=2, guess=l2, tol=1e-3)
+    assert i3 <= 2
+    assert canon.qp_rpl(64, 12) == 1 and canon.qp_rpl(80, 12) == 2 and canon.qp_rpl(128, 12) == 2
+    assert canon.qp_rpl(8, 6, gm_min_rows=1) == 2
+    N, nx = 86, 12   # 1032 rows, 516 lanes at rpl 2; 1032 > 1024 lanes at rpl 1
+    Sd = np.tile(-np.eye(nx), (N, 1, 1))
+    with pytest.raises(ValueError):
+        canon.pcg(Sd, np.zeros((N - 1, nx, nx)), np.ones(N * nx), "SS", rpl=1)
+    lam, it, _ = canon.pcg(Sd, np.zeros((N - 1, nx, nx)), np.ones(N * nx), "SS", rpl=2)
+    assert it == 1 and np.array_equal(lam, -np.ones(N * nx))

@@ -312,7 +312,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   if (precond == 0) {   // method S: Schur blocks -> direct solve -> dxu
     {
       Timed t(ctx, "schur");
-      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, G,
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, dt, PRECOND_SS, QP_MODE_SCHUR, d_x, d_u, st.active, G,
                           w.A, w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, nullptr, w.Sd, w.Sl, w.gam, nullptr,
                           w.jsoft, nullptr, nullptr));
     }
@@ -322,7 +322,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
     }
     {
       Timed t(ctx, "dxu");
-      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, G, w.A,
+      LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, dt, PRECOND_SS, QP_MODE_DXU, d_x, d_u, st.active, G, w.A,
                           w.Bm, w.cvec, 0.0, 0, w.iters, w.dx, w.du, w.lam, nullptr, nullptr, nullptr, nullptr,
                           w.jsoft, nullptr, nullptr));
     }
@@ -330,7 +330,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   }
   {
     Timed t(ctx, "qp");
-    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, precond, QP_MODE_PCG, d_x, d_u, st.active, G, w.A,
+    LAUNCH_OK(launch_qp(ctx->stream, nj, ctx->dcost, P, nb, N, dt, precond, QP_MODE_PCG, d_x, d_u, st.active, G, w.A,
                         w.Bm, w.cvec, ctx->opts.exit_tolerance_linSys, ctx->opts.max_iter_linSys, w.iters, w.dx,
                         w.du, keep_blocks ? w.lam : w.lam_keep, keep_blocks ? w.Sd : nullptr,
                         keep_blocks ? w.Sl : nullptr, keep_blocks ? w.gam : nullptr, keep_blocks ? w.Pd : nullptr,

@@ -104,8 +104,9 @@ int launch_unit_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const
 int launch_rollout(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
                    const double* u);
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, PList P, int B, const double* rho, const int* active, double* G);
-int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, int precond, int mode, const double* x,
-              const double* u,
+// dt: the Euler step of A_k / B_k (their structural rows are not read, tmpc_kernels.hip qp_schur_row)
+int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, double dt, int precond, int mode,
+              const double* x, const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
               double* Pd, const double* jsoft, const double* guess, double* Sg);

@@ -1051,10 +1051,16 @@ struct GhatSrc {
   }
 };
 
+// A_k, B_k of the Euler integrator (TrajoptPlant.py:92-108) as k_qp_grad writes them:
+//   A_k = [[I, dt I], [dt dqdd_q, I + dt dqdd_qd]],   B_k = [[0], [dt M^-1]].
+// Their first NJ rows are structural -- exactly 1, dt and 0 -- so the fused QP kernel reads only the
+// bottom NJ rows: a product's chain keeps its order term by term, a structural 1 or dt
+// is the same fma, a structural zero term is dropped (fma(0, g, acc) == acc for finite g, up to the
+// sign of a zero).  Half of A_k / B_k never leaves HBM for the QP, prologue and epilogue alike.
 template <int NJ, bool PK>
 __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, const QpStage& S,
                                                const GhatSrc<NJ, PK>& Gh, const double* __restrict__ g_lds,
-                                               double c_ki, int k, int i, int N, PcgRow<2 * NJ>& R) {
+                                               double c_ki, int k, int i, int N, double dt, PcgRow<2 * NJ>& R) {
   constexpr int NX = 2 * NJ, NU = NJ;
   const int K = N - 1;
   const double* Gxk = Gh.x(C, k, N);
@@ -1076,28 +1082,44 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
     const double* gm = g_lds + km * (NX + NU);
     const double* A = S.A + km * NX * NX;
     const double* Bm = S.B + km * NX * NU;
+    // R.sl = row i of A_{k-1} Ghat_{k-1}: a structural row i < NJ is e_i + dt e_{i+NJ}
+    if (i < NJ) {
 #pragma unroll
-    for (int j = 0; j < NX; ++j) {
-      double acc = 0.0;
+      for (int j = 0; j < NX; ++j) R.sl[j] = fma(dt, Gxm[(i + NJ) * NX + j], Gxm[i * NX + j] + 0.0);
+    } else {
 #pragma unroll
-      for (int m = 0; m < NX; ++m) acc += A[i * NX + m] * Gxm[m * NX + j];
-      R.sl[j] = acc;
+      for (int j = 0; j < NX; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NX; ++m) acc += A[i * NX + m] * Gxm[m * NX + j];
+        R.sl[j] = acc;
+      }
     }
+    // row i of B_{k-1} Ghat_u: zero for a structural row
     double BG[NU];
 #pragma unroll
-    for (int j = 0; j < NU; ++j) {
-      double acc = 0.0;
+    for (int j = 0; j < NU; ++j) BG[j] = 0.0;
+    if (i >= NJ) {
 #pragma unroll
-      for (int m = 0; m < NU; ++m) acc += Bm[i * NU + m] * Gu[m * NU + j];
-      BG[j] = acc;
+      for (int j = 0; j < NU; ++j) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < NU; ++m) acc += Bm[i * NU + m] * Gu[m * NU + j];
+        BG[j] = acc;
+      }
     }
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      double acc = 0.0;
+      double acc;
+      if (j < NJ) {   // structural row j of A_{k-1}; row j of B_{k-1} is zero
+        acc = fma(R.sl[j + NJ], dt, R.sl[j] + 0.0);
+      } else {
+        acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < NX; ++m) acc += R.sl[m] * A[j * NX + m];
+        for (int m = 0; m < NX; ++m) acc += R.sl[m] * A[j * NX + m];
 #pragma unroll
-      for (int m = 0; m < NU; ++m) acc += BG[m] * Bm[j * NU + m];
+        for (int m = 0; m < NU; ++m) acc += BG[m] * Bm[j * NU + m];
+      }
       R.sd[j] = -(acc + Gxk[i * NX + j]);
     }
     double s = 0.0;
@@ -1111,9 +1133,14 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
     const double* A = S.A + k * NX * NX;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      double acc = 0.0;
+      double acc;
+      if (j < NJ) {
+        acc = fma(dt, Gxk[(j + NJ) * NX + i], Gxk[j * NX + i] + 0.0);
+      } else {
+        acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < NX; ++m) acc += A[j * NX + m] * Gxk[m * NX + i];
+        for (int m = 0; m < NX; ++m) acc += A[j * NX + m] * Gxk[m * NX + i];
+      }
       R.su[j] = acc;
     }
   }
@@ -1127,7 +1154,7 @@ __device__ __forceinline__ double qp_schur_row(const CostDev* __restrict__ C, co
 //       GM: more than 1024 rows -- S and P^-1 rows in HBM (Sg, [B][4][NX/2][rows][2], PcgRowG), two rows
 //           per lane, LDS vectors of QP_MAX_ROWS rows.
 template <int NJ, int RPL, int MAXT, bool PK, int MODE, bool GM = false>
-__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PList P, int B, int N, int precond,
+__global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PList P, int B, int N, double dt, int precond,
                                              const double* __restrict__ x, const double* __restrict__ u,
                                              const int* __restrict__ active, const double* __restrict__ Ginv,
                                              const double* __restrict__ Aall, const double* __restrict__ Ball,
@@ -1198,7 +1225,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
     bv[m] = 0.0;
     if (!ln.valid) continue;
     const int i = ln.r(m);
-    bv[m] = qp_schur_row<NJ, PK>(C, S, Gh, g_lds, cvec[(size_t)b * N * NX + k * NX + i], k, i, N, R[m]);
+    bv[m] = qp_schur_row<NJ, PK>(C, S, Gh, g_lds, cvec[(size_t)b * N * NX + k * NX + i], k, i, N, dt, R[m]);
     if (Sd_out) {
 #pragma unroll
       for (int j = 0; j < NX; ++j) Sd_out[(((size_t)b * N + k) * NX + i) * NX + j] = R[m].sd[j];
@@ -1260,7 +1287,9 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
   }
   __syncthreads();
   // C^T lambda per knot: x part lambda_k - A_k^T lambda_{k+1} (terminal: lambda_{N-1}),
-  // u part -B_k^T lambda_{k+1}; stored in the (dead) x / u staging slots
+  // u part -B_k^T lambda_{k+1}; stored in the (dead) x / u staging slots.  The structural rows m < NJ
+  // of A_k (e_m + dt e_{m+NJ}) and B_k (0) are not read (qp_schur_row above): column j of A_k^T lambda
+  // starts from its one structural term, lambda_j (j < NJ) or dt lambda_{j-NJ}, as the full chain would.
   double* ctl_x = S.x;   // [N][NX]
   double* ctl_u = S.u;   // [K][NU]
   for (int e = threadIdx.x; e < N * NX + K * NU; e += blockDim.x) {
@@ -1270,8 +1299,9 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
       if (kk < K) {
         const double* A = S.A + kk * NX * NX;
         const double* l1 = lam_lds + (kk + 1) * NX;
+        atl = j < NJ ? l1[j] + 0.0 : fma(dt, l1[j - NJ], 0.0);
 #pragma unroll
-        for (int m = 0; m < NX; ++m) atl += A[m * NX + j] * l1[m];
+        for (int m = NJ; m < NX; ++m) atl += A[m * NX + j] * l1[m];
       }
       ctl_x[e] = lam_lds[e] - atl;
     } else {
@@ -1281,7 +1311,7 @@ __global__ void __launch_bounds__(MAXT) k_qp(const CostDev* __restrict__ C, PLis
       const double* l1 = lam_lds + (kk + 1) * NX;
       double btl = 0.0;
 #pragma unroll
-      for (int m = 0; m < NX; ++m) btl += Bm[m * NU + j] * l1[m];
+      for (int m = NJ; m < NX; ++m) btl += Bm[m * NU + j] * l1[m];
       ctl_u[f] = -btl;
     }
   }
@@ -1686,7 +1716,7 @@ struct LaunchNJ {
   static void ginv(hipStream_t s, const CostDev* C, PList P, int B, const double* rho, const int* active, double* G) {
     hipLaunchKernelGGL((k_ginv<NJ>), TMPC_GRID(B * 3 * 16, 64), 0, s, C, P, B, rho, active, G);
   }
-  static void qp(hipStream_t s, const CostDev* C, PList P, int B, int N, int precond, int mode, const double* x,
+  static void qp(hipStream_t s, const CostDev* C, PList P, int B, int N, double dt, int precond, int mode, const double* x,
                  const double* u,
                  const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
                  int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
@@ -1699,7 +1729,7 @@ struct LaunchNJ {
     const int rpl = gm ? 2 : pcg_rpl(N, NX);
     const int threads = ((rows / rpl + 63) / 64) * 64;
     const size_t lds = qp_lds_doubles(N, NX, NJ, gm ? QP_MAX_ROWS : 1024) * sizeof(double);
-#define TMPC_QP_ARGS s, C, P, B, N, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, \
+#define TMPC_QP_ARGS s, C, P, B, N, dt, precond, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam, Sd, \
                      Sl, gam, Pd, jsoft, guess, Sg
 #define TMPC_QP_LAUNCH(PKV, MODEV)                                                                        \
     if (gm)                                                                                                \
@@ -2095,8 +2125,8 @@ int launch_ginv(hipStream_t s, int nj, const CostDev* C, PList P, int B, const d
                 double* G) {
   TMPC_DISPATCH_NJ2(nj, ginv(s, C, P, B, rho, active, G))
 }
-int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, int precond, int mode, const double* x,
-              const double* u,
+int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, double dt, int precond, int mode,
+              const double* x, const double* u,
               const int* active, const double* G, const double* A, const double* Bm, const double* cvec, double tol,
               int max_iter, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl, double* gam,
               double* Pd, const double* jsoft, const double* guess, double* Sg) {
@@ -2105,7 +2135,7 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, in
   const bool gm = rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG);
   if (gm && mode == QP_MODE_PCG && !Sg) return -4;
   if (qp_lds_doubles(N, 2 * nj, nj, gm ? QP_MAX_ROWS : 1024) * sizeof(double) > 160 * 1024) return -3;
-  TMPC_DISPATCH_NJ2(nj, qp(s, C, P, B, N, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam,
+  TMPC_DISPATCH_NJ2(nj, qp(s, C, P, B, N, dt, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam,
                            Sd, Sl, gam, Pd, jsoft, guess, Sg))
 }
 int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N,
