@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 7   /* 7: tmpc_kernel_bytes */
+#define TMPC_ABI_VERSION 8   /* 8: tmpc_qp_blocks_batch; 7: tmpc_kernel_bytes */
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
@@ -270,6 +270,25 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
 int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
                   const double* u, const double* xs, const double* guess, double* dxul, int32_t* pcg_iters,
                   double* S_diag, double* S_lo, double* gamma, double* P_diag);
+
+/* solveKKTSystem / solveKKTSystem_Schur (TrajoptMPCReference.py:313-455) on the blocks of formKKTSystemBlocks
+ * (:118-271) as the caller's own plugin hooks formed them -- the QP of the drop-in's plugin-hook path, for
+ * TrajoptCost / TrajoptPlant subclasses whose hooks have no device implementation.  n = nx + nu with
+ * nx = 2 nu (1 <= nu <= 7), N nx <= 1024:
+ *   G [B][N][n][n]   cost Hessian per knot, soft-limit outer products included, WITHOUT rho (knot N-1:
+ *                    its nx x nx block in the top-left corner; the rest is ignored), x-u coupling allowed;
+ *   g [B][N][n]      cost gradient (+ soft-limit jacobian) per knot (knot N-1: the first nx entries);
+ *   A [B][N-1][nx][nx], Bm [B][N-1][nx][nu]   integrator Jacobians (C rows [-A_k -B_k I]);
+ *   c [B][N][nx]     c_0 = x_0 - xs, c_{k+1} = x_{k+1} - f(x_k, u_k);
+ *   rho [B]          the regularisation added to G in place (:419-420);
+ *   linsys           TMPC_LINSYS_N / _S (direct) or _PCG_J / _BJ / _SS / _0;
+ *   guess [B][N nx]  PCG initial iterate (nullable: zeros).
+ * Outputs dxul [B][n(N-1)+nx + nx N] ([x0,u0,...,x_{N-1}; lambda], the reference's order), pcg_iters [B]
+ * (0 for the direct methods), S_diag / S_lo / gamma (nullable).  (G_k + rho I)^-1 is formed without
+ * pivoting: a zero or non-finite pivot (np.linalg.inv's LinAlgError) is an error. */
+int tmpc_qp_blocks_batch(tmpc_ctx* ctx, int B, int N, int nx, int nu, int linsys, const double* G, const double* g,
+                         const double* A, const double* Bm, const double* c, const double* rho, const double* guess,
+                         double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma);
 
 /* Hard-limit detail of the last tmpc_qp_batch call with hard box limits (same B, N): sizes[2] = {dmax, W} of
  * the banded Schur complement (rows padded to dmax, half band W), dim [B] its dimension per problem

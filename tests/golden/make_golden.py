@@ -674,6 +674,88 @@ def run_pendulum(args):
            f"pcg={list(pcg_iters)} wall={wall:.1f}s"
 
 
+# ---------------------------------------------------------------- user plugins (the plugin-hook path)
+def run_plugins(args):
+    """The reference's SQP with two user plugins written against its own base classes
+    (tests/plugin_models.py): CoupledCost (a TrajoptCost with an x-u cross term, time-varying) on arm3, and
+    SpringPlant (a TrajoptPlant without URDF) with CoupledCost."""
+    which, N, seed, method, dt = args
+    _setup_reference()
+    sys.path.insert(0, os.path.dirname(OUT))
+    import plugin_models as pm
+    from TrajoptMPCReference import TrajoptMPCReference, SQPSolverMethods
+    from TrajoptCost import TrajoptCost
+    from TrajoptPlant import TrajoptPlant
+    from overloading import matrix_
+    matrix_.iteration = 0
+    matrix_.soft_constraint_iteration = 0
+    matrix_.line_search_iteration = 0
+
+    class CoupledCost(TrajoptCost):
+        def __init__(self, nx, nu):
+            self.arrs = pm.coupled_arrays(nx, nu)
+
+        def value(self, x, u=None, timestep=None, *a, **k):
+            return pm.coupled_value(x, u, timestep, self.arrs)
+
+        def gradient(self, x, u=None, timestep=None, *a, **k):
+            return pm.coupled_gradient(x, u, timestep, self.arrs)
+
+        def hessian(self, x, u=None, timestep=None, *a, **k):
+            return pm.coupled_hessian(x, u, timestep, self.arrs)
+
+    class _Shim:
+        overloading = False
+
+    class SpringPlant(TrajoptPlant):
+        def __init__(self):
+            super().__init__(0, {"overloading": False})
+            self.rbdReference = _Shim()
+
+        def forward_dynamics(self, x, u, *a, **k):
+            return pm.spring_qdd(np.asarray(x, dtype=float), np.asarray(u, dtype=float))
+
+        def forward_dynamics_gradient(self, x, u, *a, **k):
+            return pm.spring_dqdd(np.asarray(x, dtype=float), np.asarray(u, dtype=float))
+
+        def get_num_pos(self):
+            return pm.NQ
+
+        def get_num_vel(self):
+            return pm.NQ
+
+        def get_num_cntrl(self):
+            return pm.NQ
+
+    if which == "cost":
+        plant = make_plant("arm3")
+        x0, u0 = initial_problem(plant, N, dt, seed)
+    else:
+        plant = SpringPlant()
+        x0, u0 = pm.spring_initial(N, dt, seed)
+    n = plant.get_num_pos()
+    cost = CoupledCost(2 * n, n)
+    solver = TrajoptMPCReference(plant, cost)
+    m = {"S": SQPSolverMethods.S, "PCG-J": SQPSolverMethods.PCG_J, "PCG-BJ": SQPSolverMethods.PCG_BJ,
+         "PCG-SS": SQPSolverMethods.PCG_SS, "N": SQPSolverMethods.N}[method]
+    import io
+    import contextlib
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(copy.deepcopy(x0), copy.deepcopy(u0), N, dt, m, {})
+    tr = solver.trace
+    keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
+            "succeeded_line_search"]
+    rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(t[k]) for t in tr]) for k in keys}
+    pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
+    dxul = np.array([d["value"][:, 0] for d in solver.saved_dxul])
+    np.savez_compressed(os.path.join(OUT, f"plugin_{which}_N{N}_s{seed}_{method}.npz"),
+                        x0=x0, u0=u0, x=np.asarray(x), u=np.asarray(u), dt=dt, exit_sqp=exit_sqp,
+                        exit_soft=exit_soft, outer_iter=outer_iter, sqp_iter=sqp_iter, pcg_iters=pcg_iters,
+                        dxul=dxul, **rec)
+    return f"[golden] plugin {which} N={N} seed={seed} {method}: exit={exit_sqp} iters={sqp_iter} " \
+           f"pcg={list(pcg_iters)}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="skip the slow arm6 N=64 solves")
@@ -738,6 +820,12 @@ def main():
         jobs = [("arm2", 8, 0, "N", 0.1), ("arm3", 8, 1, "N", 0.1), ("arm3", 32, 0, "N", 0.1)]
         with mp.get_context("fork").Pool(len(jobs)) as pool:
             for msg in pool.imap_unordered(run_sqp, jobs):
+                print(msg, flush=True)
+    if a.only in (None, "plugins"):
+        jobs = [("cost", 10, 0, "PCG-SS", 0.1), ("cost", 10, 1, "N", 0.1), ("plant", 20, 0, "PCG-SS", 0.1),
+                ("plant", 20, 1, "N", 0.1), ("plant", 20, 2, "PCG-BJ", 0.1)]
+        with mp.get_context("fork").Pool(len(jobs)) as pool:
+            for msg in pool.imap_unordered(run_plugins, jobs):
                 print(msg, flush=True)
     if a.only in (None, "soft"):
         jobs = [("QUADRATIC_PENALTY", "PCG-SS", 8, 2.0, 0, 0.1), ("AUGMENTED_LAGRANGIAN", "PCG-SS", 8, 2.0, 0, 0.1),

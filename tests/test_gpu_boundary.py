@@ -167,3 +167,36 @@ def test_mpc_qp_n_method():
     rn = solver.MPC_batch(np.array(xs), np.array(us), 16, 0.1, MPCSolverMethods.QP_N, {}, mpc_steps=2)
     rs = solver.MPC_batch(np.array(xs), np.array(us), 16, 0.1, MPCSolverMethods.QP_S, {}, mpc_steps=2)
     assert np.array_equal(rn["x_exec"], rs["x_exec"]) and np.array_equal(rn["exit_codes"], rs["exit_codes"])
+
+
+@pytest.mark.parametrize("mode", ["QUADRATIC_PENALTY", "AUGMENTED_LAGRANGIAN"])
+def test_soft_limit_qp_solves_the_dense_kkt(mode):
+    """tmpc_qp_batch with soft limits (the jacobian terms of formKKTSystemBlocks :220-225, :255-259 formed on
+    the device at the constraint objects' mu / lambda): solveKKTSystem_Schur's dxul solves the dense KKT
+    system that formKKTSystemBlocks builds with the same hooks -- residual at rounding, for both soft modes,
+    two limit kinds, and mu / lambda away from their defaults (TrajoptConstraint.py:138-166)."""
+    from oracle import sqp as osqp
+    from conftest import arm_model
+    from trajoptmpcreference_amd import QuadraticCost, TrajoptConstraint, TrajoptMPCReference, URDFPlant, \
+        planar_arm_urdf
+    n, N, dt, rho = 3, 10, 0.1, 2e-3
+    plant = URDFPlant(options={"path_to_urdf": planar_arm_urdf(n)})
+    con = TrajoptConstraint(n, n, n, N)
+    con.set_torque_limits([0.2] * n, [-0.2] * n, mode)
+    con.set_joint_limits([0.5] * n, [-0.5] * n, mode)
+    rng = np.random.default_rng(11)
+    for box in (con.torque_limits, con.joint_limits):
+        box.quadratic_penalty_mu[:] = rng.uniform(0.5, 5.0, box.quadratic_penalty_mu.shape)
+        box.augmented_lagrangian_lambda[:] = rng.uniform(-0.3, 0.3, box.augmented_lagrangian_lambda.shape)
+    solver = TrajoptMPCReference(plant, QuadraticCost(*quad_cost_arrays(n)), con)
+    x, u = osqp.initial_problem(arm_model("arm3"), N, dt, 21)
+    u = u + rng.uniform(-0.6, 0.6, u.shape)   # torques outside +-0.2, joints outside +-0.5
+    xs = x[:, 0].copy()
+    G, g, C, c = solver.formKKTSystemBlocks(x, u, xs, N, dt)
+    assert np.any(G[np.triu_indices_from(G, 1)] != 0)   # the soft terms' outer products are present
+    Kk = np.block([[G + rho * np.eye(G.shape[0]), C.T], [C, np.zeros((C.shape[0], C.shape[0]))]])
+    rhs = np.vstack((g, c))
+    for dxul in (solver.solveKKTSystem_Schur(x, u, xs, N, dt, rho),
+                 solver.solveKKTSystem(x, u, xs, N, dt, rho)):
+        res = float(np.max(np.abs(Kk @ dxul - rhs)))
+        assert res < 1e-9 * max(1.0, float(np.max(np.abs(rhs)))), res

@@ -402,7 +402,7 @@ def test_hard_pcg_on_oracle_S_is_exact(name, N, ptype, seed):
 
 
 LARGE_CASES = [(ptype, 12, (1530, 1100, 700), "arm6fix") for ptype in ("SS", "BJ", "J")] + \
-    [("SS", 14, (3000, 2100), "arm7")]
+    [("SS", 14, (3000, 2100), "arm7"), ("SS", 14, (4000, 3100), "arm7"), ("BJ", 14, (4090,), "arm7")]
 
 
 @pytest.mark.parametrize("ptype,nx,dims_,model", LARGE_CASES,
@@ -410,9 +410,10 @@ LARGE_CASES = [(ptype, 12, (1530, 1100, 700), "arm6fix") for ptype in ("SS", "BJ
 def test_hard_pcg_large_banded_is_exact(ptype, nx, dims_, model):
     """Schur dimensions past one 1024-row slot and past the LDS block cache (D = 1530: 94 of 127 diagonal
     blocks fit, the rest stream from HBM; D = 1100 and 700 alongside, all cached; D = 3000 at nx = 14:
-    three row slots, 35 of 214 diagonal blocks cached), trailing partial blocks (1530 mod 12 = 6,
-    3000 mod 14 = 4 unpreconditioned rows): counts and lambda bit for bit against pcg_canonical, and the
-    kernel's byte count exactly."""
+    three row slots, 35 of 214 diagonal blocks cached; D = 4000 and 4090 at nx = 14: the four-slot instance
+    k_hard_pcg<14, 4> at the edge of the LDS budget, 9 blocks cached), trailing partial blocks
+    (1530 mod 12 = 6, 3000 mod 14 = 4, 4000 mod 14 = 10 unpreconditioned rows): counts and lambda bit for
+    bit against pcg_canonical, and the kernel's byte count exactly."""
     from oracle import hard as ohard
     from trajoptmpcreference_amd import _native
     W = 30

@@ -97,6 +97,8 @@ SIGNATURES = {
     "tmpc_fd_grad_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp]),
     "tmpc_qp_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _ip,
                                 _dp, _dp, _dp, _dp]),
+    "tmpc_qp_blocks_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp,
+                                       _dp, _dp, _dp, _dp, _ip, _dp, _dp, _dp]),
     "tmpc_qp_hard_info": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _up, _dp, _dp, _dp, _ip]),
     "tmpc_hard_pcg_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _ip, C.c_int, _dp, _dp,
                                       C.c_double, C.c_int, _dp, _ip]),
@@ -415,6 +417,30 @@ class Context:
                                            _ptr(Pd)),
                     "tmpc_qp_batch")
         return dict(dxul=dxul, pcg_iters=iters, S_diag=Sd, S_lo=Sl, gamma=g, P_diag=Pd)
+
+    def qp_blocks_batch(self, G, g, A, Bm, c, rho, method="PCG-SS", guess=None, want_blocks=False):
+        """solveKKTSystem(_Schur) on caller-formed blocks (tmpc_qp_blocks_batch, the plugin-hook QP):
+        G [B][N][n][n] (without rho; knot N-1 in the top-left nx x nx corner), g [B][N][n], A [B][N-1][nx][nx],
+        Bm [B][N-1][nx][nu], c [B][N][nx], rho [B] -> dict(dxul [B][n(N-1)+nx+nx N], pcg_iters [B], and with
+        want_blocks S_diag / S_lo / gamma)."""
+        G, g, A, Bm, c = _c64(G), _c64(g), _c64(A), _c64(Bm), _c64(c)
+        B, N, n, _ = G.shape
+        nx, nu = A.shape[2], Bm.shape[3]
+        if g.shape != (B, N, n) or A.shape != (B, N - 1, nx, nx) or Bm.shape != (B, N - 1, nx, nu) \
+                or c.shape != (B, N, nx) or n != nx + nu:
+            raise ValueError(f"inconsistent block shapes G {G.shape} g {g.shape} A {A.shape} B {Bm.shape} c {c.shape}")
+        rho = _c64(np.broadcast_to(np.asarray(rho, dtype=np.float64), (B,)))
+        if guess is not None:
+            guess = _c64(guess).reshape(B, N * nx)
+        dxul = np.zeros((B, n * (N - 1) + nx + nx * N))
+        iters = np.zeros(B, dtype=np.int32)
+        Sd = np.zeros((B, N, nx, nx)) if want_blocks else None
+        Sl = np.zeros((B, N - 1, nx, nx)) if want_blocks else None
+        gam = np.zeros((B, N * nx)) if want_blocks else None
+        self._check(self.lib.tmpc_qp_blocks_batch(self.h, B, N, nx, nu, LINSYS[method], _ptr(G), _ptr(g), _ptr(A),
+                                                  _ptr(Bm), _ptr(c), _ptr(rho), _ptr(guess), _ptr(dxul), _ptr(iters),
+                                                  _ptr(Sd), _ptr(Sl), _ptr(gam)), "tmpc_qp_blocks_batch")
+        return dict(dxul=dxul, pcg_iters=iters, S_diag=Sd, S_lo=Sl, gamma=gam)
 
     def qp_hard_info(self, B, N):
         """Hard-limit detail of the last qp_batch (tmpc_qp_hard_info): dict with dim [B], active [B][N]

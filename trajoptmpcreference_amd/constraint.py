@@ -337,6 +337,20 @@ class TrajoptConstraint:
             jac = j if jac is None else (np.vstack((jac, j)) if self.reference_hooks else jac + j)
         return jac
 
+    def soft_outer(self, xk, uk=None, timestep=None):
+        """The soft limits' term of the QP's Hessian block at `timestep`: formKKTSystemBlocks adds
+        outer(jac, jac) of the jacobian column (:220-225, :255-259); with several soft kinds (whose columns
+        the reference vstacks and cannot consume) it is the sum of the per-kind outer products,
+        the term the device QP and oracle/soft.py form.  None when no limit is soft."""
+        if self.reference_hooks:
+            raise NotImplementedError("soft_outer: with reference_hooks the jacobians are vstacked (the "
+                                      "reference's form, which no QP consumes)")
+        H = None
+        for _, c, z, t in self._soft_slices(xk, uk, timestep):
+            j = np.asarray(c.jacobian(z, t), dtype=np.float64).reshape(-1)
+            H = np.outer(j, j) if H is None else H + np.outer(j, j)
+        return H
+
     def update_soft_constraint_constants(self, x, u):
         """TrajoptConstraint.update_soft_constraint_constants (:369-378) for trajectories x
         (nq + nv) x N and u nu x (N - 1): the AL update of every limit; True when no constant changed.

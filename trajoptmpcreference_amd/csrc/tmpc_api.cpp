@@ -932,6 +932,7 @@ int tmpc_create(int device, tmpc_ctx** out) {
   }
   pcg_set_max_lds();
   hard_set_max_lds();
+  qp_blocks_set_max_lds();
   tmpc_default_options(&ctx->opts);
   *out = ctx;
   return 0;
@@ -1527,6 +1528,112 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   if (gamma) HIP_OK(hipMemcpy(gamma, w.gam, sizeof(double) * B * N * nx, hipMemcpyDeviceToHost));
   if (P_diag && precond != PRECOND_J && precond != 0)
     HIP_OK(hipMemcpy(P_diag, w.Pd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_qp_blocks_batch(tmpc_ctx* ctx, int B, int N, int nx, int nu, int linsys, const double* G, const double* g,
+                         const double* A, const double* Bm, const double* c, const double* rho, const double* guess,
+                         double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma) {
+  if (!ctx) return -1;
+  if (B < 1 || N < 2) return fail(ctx, "bad sizes B=%d N=%d (B >= 1, N >= 2)", B, N);
+  if (nu < 1 || nu > 7 || nx != 2 * nu)
+    return fail(ctx, "tmpc_qp_blocks_batch: nx = %d, nu = %d; the device QP takes nx = 2 nu, 1 <= nu <= 7", nx, nu);
+  if (N * nx > 1024) return fail(ctx, "tmpc_qp_blocks_batch: N * nx = %d exceeds 1024 rows", N * nx);
+  const int precond = precond_of(linsys);
+  if (precond < 0) return fail(ctx, "linear system method %d is not available on the GPU", linsys);
+  if (!G || !g || !A || !Bm || !c || !rho) return fail(ctx, "null input");
+  hipSetDevice(ctx->device);
+  const int n = nx + nu, K = N - 1;
+  BUF(double, hb_G, (size_t)B * N * n * n);
+  BUF(double, hb_Gh, (size_t)B * N * n * n);
+  BUF(double, hb_g, (size_t)B * N * n);
+  BUF(double, hb_A, (size_t)B * K * nx * nx);
+  BUF(double, hb_B, (size_t)B * K * nx * nu);
+  BUF(double, hb_c, (size_t)B * N * nx);
+  BUF(double, hb_rho, (size_t)B);
+  BUF(int, hb_err, (size_t)B);
+  BUF(int, hb_it, (size_t)B);
+  BUF(double, hb_dx, (size_t)B * N * nx);
+  BUF(double, hb_du, (size_t)B * K * nu);
+  BUF(double, hb_lam, (size_t)B * N * nx);
+  BUF(double, hb_Sd, (size_t)B * N * nx * nx);
+  BUF(double, hb_Sl, (size_t)B * K * nx * nx);
+  BUF(double, hb_gam, (size_t)B * N * nx);
+  double* hb_guess = nullptr;
+  if (guess && precond != 0) {
+    BUF(double, hb_x0, (size_t)B * N * nx);
+    HIP_OK(hipMemcpyAsync(hb_x0, guess, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
+    hb_guess = hb_x0;
+  }
+  HIP_OK(hipMemcpyAsync(hb_G, G, sizeof(double) * B * N * n * n, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_g, g, sizeof(double) * B * N * n, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_A, A, sizeof(double) * B * K * nx * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_B, Bm, sizeof(double) * B * K * nx * nu, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_c, c, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_rho, rho, sizeof(double) * B, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemsetAsync(hb_err, 0, sizeof(int) * B, ctx->stream));
+  {
+    Timed t(ctx, "ghat_full");
+    LAUNCH_OK(launch_ghat_full(ctx->stream, nu, B, N, hb_G, hb_rho, hb_Gh, hb_err));
+  }
+  const double tol = ctx->opts.exit_tolerance_linSys;
+  const int max_iter = ctx->opts.max_iter_linSys;
+  const bool keep = S_diag || S_lo || gamma;
+  if (precond == 0) {   // methods S / N: Schur blocks -> block-Thomas -> dxu
+    std::vector<int> act(B, 1);
+    BUF(int, hb_act, (size_t)B);
+    BUF(double, hb_U, (size_t)B * K * nx * nx);
+    BUF(double, hb_Y, (size_t)B * N * nx);
+    HIP_OK(hipMemcpyAsync(hb_act, act.data(), sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+    {
+      Timed t(ctx, "qp_blocks_schur");
+      LAUNCH_OK(launch_qp_blocks(ctx->stream, nu, B, N, PRECOND_SS, QP_MODE_SCHUR, hb_Gh, hb_g, hb_A, hb_B, hb_c,
+                                 hb_err, tol, max_iter, nullptr, hb_it, hb_dx, hb_du, hb_lam, hb_Sd, hb_Sl, hb_gam));
+    }
+    {
+      Timed t(ctx, "btsolve");
+      LAUNCH_OK(launch_btsolve(ctx->stream, nx, B, N, hb_act, hb_Sd, hb_Sl, hb_gam, hb_U, hb_Y, hb_lam));
+    }
+    {
+      Timed t(ctx, "qp_blocks_dxu");
+      LAUNCH_OK(launch_qp_blocks(ctx->stream, nu, B, N, PRECOND_SS, QP_MODE_DXU, hb_Gh, hb_g, hb_A, hb_B, hb_c,
+                                 hb_err, tol, max_iter, nullptr, hb_it, hb_dx, hb_du, hb_lam, nullptr, nullptr,
+                                 nullptr));
+    }
+  } else {
+    Timed t(ctx, "qp_blocks");
+    LAUNCH_OK(launch_qp_blocks(ctx->stream, nu, B, N, precond, QP_MODE_PCG, hb_Gh, hb_g, hb_A, hb_B, hb_c, hb_err,
+                               tol, max_iter, hb_guess, hb_it, hb_dx, hb_du, hb_lam, keep ? hb_Sd : nullptr,
+                               keep ? hb_Sl : nullptr, keep ? hb_gam : nullptr));
+  }
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  resolve_timings(ctx);
+  std::vector<int> err(B);
+  HIP_OK(hipMemcpy(err.data(), hb_err, sizeof(int) * B, hipMemcpyDeviceToHost));
+  for (int b = 0; b < B; ++b)
+    if (err[b])
+      return fail(ctx, "problem %d: G_k + rho I has a zero or non-finite pivot (singular matrix, the reference's "
+                  "np.linalg.inv raises LinAlgError)", b);
+  std::vector<double> dx((size_t)B * N * nx), du((size_t)B * K * nu), lam((size_t)B * N * nx);
+  HIP_OK(hipMemcpy(dx.data(), hb_dx, dx.size() * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(du.data(), hb_du, du.size() * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(lam.data(), hb_lam, lam.size() * sizeof(double), hipMemcpyDeviceToHost));
+  if (dxul) {
+    const size_t L = (size_t)n * K + nx + (size_t)nx * N;
+    for (int b = 0; b < B; ++b) {
+      double* o = dxul + b * L;
+      for (int k = 0; k < N; ++k) {
+        for (int i = 0; i < nx; ++i) o[(size_t)k * n + i] = dx[((size_t)b * N + k) * nx + i];
+        if (k < K)
+          for (int i = 0; i < nu; ++i) o[(size_t)k * n + nx + i] = du[((size_t)b * K + k) * nu + i];
+      }
+      memcpy(o + (size_t)n * K + nx, lam.data() + (size_t)b * N * nx, sizeof(double) * N * nx);
+    }
+  }
+  if (pcg_iters) HIP_OK(hipMemcpy(pcg_iters, hb_it, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (S_diag) HIP_OK(hipMemcpy(S_diag, hb_Sd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
+  if (S_lo) HIP_OK(hipMemcpy(S_lo, hb_Sl, sizeof(double) * B * K * nx * nx, hipMemcpyDeviceToHost));
+  if (gamma) HIP_OK(hipMemcpy(gamma, hb_gam, sizeof(double) * B * N * nx, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -128,6 +128,13 @@ int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* C
 int launch_pcg(hipStream_t s, int nx, int B, int N, int precond, const double* Sd, const double* Sl,
                const double* Su, const double* gam, const double* guess, double tol, int max_iter, double* lam,
                int* iters, double* tnu, double* tres, double* Pd);
+// plugin-hook QP on caller-formed blocks (tmpc_hooks.hip)
+int launch_ghat_full(hipStream_t s, int nj, int B, int N, const double* G, const double* rho, double* Gh, int* err);
+int launch_qp_blocks(hipStream_t s, int nj, int B, int N, int precond, int mode, const double* Gh, const double* g,
+                     const double* A, const double* Bm, const double* c, const int* err, double tol, int max_iter,
+                     const double* guess, int* iters, double* dx, double* du, double* lam, double* Sd, double* Sl,
+                     double* gam);
+int qp_blocks_set_max_lds();
 int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const double* Sd, const double* Sl,
                    const double* gam, double* U, double* Y, double* lam);
 int pcg_set_max_lds();

@@ -12,7 +12,7 @@ import enum
 
 import numpy as np
 
-from . import _native
+from . import _native, hooks
 from ._options import NO_OPTIONS, fresh
 from .constraint import TrajoptConstraint
 from .cost import QuadraticCost, TrajoptCost, UrdfCost
@@ -104,7 +104,8 @@ class TrajoptMPCReference:
         options.setdefault("max_iter_linSys", 100)
         options.setdefault("DEBUG_MODE_linSys", False)
         options.setdefault("RETURN_TRACE_linSys", False)
-        options.setdefault("overloading", self.plant.rbdReference.overloading)
+        # plant.rbdReference.overloading (:97); a plugin plant without an rbdReference does no tracing
+        options.setdefault("overloading", getattr(getattr(self.plant, "rbdReference", None), "overloading", False))
         options.setdefault("exit_tolerance_SQP_DDP", 1e-6)
         options.setdefault("max_iter_SQP_DDP", 100)
         options.setdefault("DEBUG_MODE_SQP_DDP", False)
@@ -129,12 +130,30 @@ class TrajoptMPCReference:
                 or u.shape[1:] != (nu, N - 1):
             raise ValueError(f"expected x [B][{nx}][{N}] and u [B][{nu}][{N - 1}], got {x.shape} and {u.shape}")
 
+    def _hooks(self):
+        """True when a plugin's hooks are the caller's own (a TrajoptCost / TrajoptPlant / TrajoptConstraint
+        subclass, or one overriding a built-in's hooks): SQP then runs the plugin-hook path (hooks.py), the
+        reference's loop over those hooks with every QP on the GPU.  The built-ins run wholly on the device."""
+        return hooks.needs_hooks(self.plant, self.cost, self.other_constraints)
+
+    def _hook_context(self, options):
+        """A context for the plugin-hook path: only the linear-system options matter (the blocks come from
+        the hooks)."""
+        ctx = _native.default_context(getattr(self.plant, "device", 0))
+        ctx.set_options(**{v: options[k] for k, v in _OPTION_MAP.items()})
+        return ctx
+
     def _context(self, options):
-        if not isinstance(self.plant, URDFPlant):
-            raise NotImplementedError("the GPU solver needs a URDFPlant (custom TrajoptPlant subclasses have no "
-                                      "device implementation)")
-        if not isinstance(self.cost, QuadraticCost):
-            raise NotImplementedError("the GPU solver supports QuadraticCost and UrdfCost")
+        if self._hooks():
+            which = [name for name, ok in (("cost", hooks.device_cost(self.cost) is not None),
+                                           ("plant", hooks.device_plant(self.plant)),
+                                           ("constraints", hooks.device_constraints(self.other_constraints)))
+                     if not ok]
+            raise NotImplementedError(
+                f"this entry point runs on device plugins only; the {' / '.join(which)} hooks here are the "
+                f"caller's own ({type(self.cost).__name__}, {type(self.plant).__name__}, "
+                f"{type(self.other_constraints).__name__}): SQP / SQP_batch / solveKKTSystem(_Schur) honour them "
+                f"(the plugin-hook path, hooks.py)")
         spec = self.other_constraints.gpu_spec()   # raises for ADMM_PROJECTION (the reference exits too)
         if options.get("overloading"):
             raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
@@ -169,6 +188,8 @@ class TrajoptMPCReference:
         # method N (solveKKTSystem, the dense KKT solve, :313-359) has the Schur complement's solution and
         # runs the direct Schur path with the same least-squares fallback (include/tmpc.h TMPC_LINSYS_N)
         method = _method_name(LINEAR_SYSTEM_SOLVER_METHOD)
+        if self._hooks():
+            return self._sqp_hooks_batch(x, u, N, dt, method, options, soft_state)
         ctx = self._context(options)
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
@@ -185,6 +206,41 @@ class TrajoptMPCReference:
         r = ctx.sqp_solve_batch(x, u, N, dt, method, hard_active=hard_active)
         if soft:
             r["soft_state"] = ctx.get_soft_state(B, N)
+        return r
+
+    def _sqp_hooks_batch(self, x, u, N, dt, method, options, soft_state):
+        """SQP_batch on the plugin-hook path (hooks.py).  With several problems and soft limits each
+        problem runs on its own copy of the constraint object (the device path's per-problem soft state);
+        the returned r["soft_state"] holds every problem's final constants."""
+        if options.get("overloading"):
+            raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
+        x = np.asarray(x, dtype=np.float64)
+        u = np.asarray(u, dtype=np.float64)
+        self._check_xu(x, u, N)
+        B = x.shape[0]
+        ctx = self._hook_context(options)
+        con = self.other_constraints
+        soft = con.has_any()
+        if soft and con.num_timesteps != N:
+            raise ValueError(f"TrajoptConstraint was built for {con.num_timesteps} knots, solving with N = {N}")
+        if B == 1 and soft_state is None:
+            return hooks.sqp_hooks_batch(self, ctx, x, u, N, dt, method, options)
+        outs, states = [], []
+        try:
+            for b in range(B):
+                self.other_constraints = copy.deepcopy(con)
+                if soft and soft_state is not None:
+                    self.other_constraints.unpack_state(*[np.asarray(a)[b] for a in soft_state])
+                outs.append(hooks.sqp_hooks_batch(self, ctx, x[b:b + 1], u[b:b + 1], N, dt, method, options))
+                if soft:
+                    states.append(self.other_constraints.pack_state(N))
+        finally:
+            self.other_constraints = con
+        r = {k: np.concatenate([o[k] for o in outs]) for k in ("exit_sqp", "exit_soft", "outer_iter", "sqp_iter",
+                                                                "x", "u")}
+        r["trace"] = {k: np.concatenate([o["trace"][k] for o in outs]) for k in outs[0]["trace"]}
+        if soft:
+            r["soft_state"] = tuple(np.array([st[i] for st in states]) for i in range(3))
         return r
 
     def SQP(self, x, u, N: int, dt: float, LINEAR_SYSTEM_SOLVER_METHOD=SQPSolverMethods.N, options=NO_OPTIONS):
@@ -339,11 +395,16 @@ class TrajoptMPCReference:
         nq, nv, nu = self.plant.get_num_pos(), self.plant.get_num_vel(), self.plant.get_num_cntrl()
         return nq + nv, nu
 
-    def _gpu_plant(self):
-        if not isinstance(self.plant, URDFPlant):
-            raise NotImplementedError("the GPU solver needs a URDFPlant (custom TrajoptPlant subclasses have no "
-                                      "device implementation)")
-        return self.plant
+    def _dynamics(self, x, u, N, dt, return_gradient=False):
+        """The integrator over knots 0..N-2 (TrajoptPlant.integrator, :83-108): one GPU launch for a plant
+        with device dynamics, else the plant's own hook knot by knot (the plugin-hook path)."""
+        X, U = x[:, :N - 1].T, u[:, :N - 1].T
+        if hooks.device_plant(self.plant):
+            return self.plant.integrator_batch(X, U, dt, return_gradient=return_gradient)
+        r = [self.plant.integrator(x[:, k], u[:, k], dt, return_gradient=return_gradient) for k in range(N - 1)]
+        if return_gradient:
+            return np.array([a for a, _ in r]), np.array([b for _, b in r])
+        return np.array(r)
 
     def formKKTSystemBlocks(self, x, u, xs, N: int, dt: float):
         """formKKTSystemBlocks (:118-271, the NumPy branch :200-271): dense G, g, C, c of the QP at (x, u).
@@ -351,15 +412,14 @@ class TrajoptMPCReference:
         the soft-limit jacobian terms (:220-225, :255-259) and the hard-limit rows appended after each
         knot's dynamics rows (:238-248, :262-270) are the plugins' own hooks, placed as the reference
         places them."""
-        plant = self._gpu_plant()
+        self._check_reference_hooks()
         nx, nu = self._dims()
         n = nx + nu
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
         xs = np.asarray(xs, dtype=np.float64).reshape(-1)
-        X, U = x[:, :N - 1].T, u[:, :N - 1].T
-        A, B = plant.integrator_batch(X, U, dt, return_gradient=True)
-        xkp1 = plant.integrator_batch(X, U, dt)
+        A, B = self._dynamics(x, u, N, dt, return_gradient=True)
+        xkp1 = self._dynamics(x, u, N, dt)
         con = self.other_constraints
         nz = n * (N - 1) + nx
         n_other = con.total_hard_constraints(x, u)
@@ -377,7 +437,7 @@ class TrajoptMPCReference:
             if con.total_soft_constraints(timestep=k) > 0:
                 gck = con.jacobian_soft_constraints(x[:, k], u[:, k], k)
                 g[si:si + n, :] = g[si:si + n, :] + gck
-                G[si:si + n, si:si + n] += np.outer(gck, gck)
+                G[si:si + n, si:si + n] += hooks.soft_hessian(con, x[:, k], u[:, k], k, np.ravel(gck))
             C[ci:ci + nx, si:si + n + nx] = np.hstack((-A[k], -B[k], np.eye(nx)))
             c[ci:ci + nx, 0] = x[:, k + 1] - xkp1[k]
             ci += nx
@@ -395,7 +455,8 @@ class TrajoptMPCReference:
         if con.total_soft_constraints(timestep=N - 1) > 0:
             gc = con.jacobian_soft_constraints(x[:, N - 1], timestep=N - 1)
             g[si:si + nx, :] = g[si:si + nx, :] + gc
-            G[si:si + nx, si:si + nx] = G[si:si + nx, si:si + nx] + np.outer(gc, gc)
+            G[si:si + nx, si:si + nx] = G[si:si + nx, si:si + nx] + hooks.soft_hessian(con, x[:, N - 1], None, N - 1,
+                                                                                       np.ravel(gc))
         if n_other > 0 and con.total_hard_constraints(x, u, N - 1):
             jac = con.jacobian_hard_constraints(x[:, N - 1], timestep=N - 1)
             val = con.value_hard_constraints(x[:, N - 1], timestep=N - 1)
@@ -409,12 +470,11 @@ class TrajoptMPCReference:
         """totalHardConstraintViolation (:273-294): |x_0 - xs|_1 + sum_k |x_{k+1} - f(x_k, u_k)|_1 (+ the hard
         limits' |values|), each term summed as the reference sums it; mode "MAX" takes max instead of sum.
         f of all knots is one GPU launch."""
-        plant = self._gpu_plant()
         mode_func = max if mode == "MAX" else sum
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
         xs = np.asarray(xs, dtype=np.float64).reshape(-1)
-        xkp1 = plant.integrator_batch(x[:, :N - 1].T, u[:, :N - 1].T, dt)
+        xkp1 = self._dynamics(x, u, N, dt)
         c = mode_func(list(map(abs, x[:, 0] - xs)))
         for k in range(N - 1):
             c = c + mode_func(list(map(abs, x[:, k + 1] - xkp1[k])))
@@ -445,19 +505,32 @@ class TrajoptMPCReference:
             J = J + con.value_soft_constraints(x[:, N - 1], timestep=N - 1)
         return J
 
+    def _check_reference_hooks(self):
+        """With reference_hooks the constraint hooks are the reference's (velocity limits on q, vstacked
+        jacobians): for soft velocity limits or several soft kinds they describe a QP that neither the
+        device nor the reference's own SQP can form, so the QP-level methods refuse them."""
+        con = self.other_constraints
+        if not getattr(con, "reference_hooks", False):
+            return
+        soft = [k for k, c in con.limits() if c.is_soft_constraint_mode()]
+        if "velocity_limits" in soft or len(soft) > 1:
+            raise NotImplementedError("reference_hooks with soft velocity limits or several soft limit kinds: "
+                                      "the reference's hooks read q for velocity limits and vstack the kinds' "
+                                      "jacobians, which no QP consumes (SURVEY F6); unset reference_hooks")
+
     def _qp(self, x, u, xs, N, dt, rho, method, options):
         """One QP on the GPU (tmpc_qp_batch) -> the reference's dxul column [dxu; lambda], lambda in the
         reference's row order (initial state, then per knot its dynamics rows and its active hard rows).
         options are the reference's linear-system options (solveKKTSystem_Schur passes PCG's keys:
         exit_tolerance, max_iter, preconditioner_type, guess -- PCG.py:19-25, :439-440); the caller's dict
         is not modified."""
+        self._check_reference_hooks()
         opts = dict(options)
         self.set_default_options(opts)
         if "exit_tolerance" in opts:
             opts["exit_tolerance_linSys"] = opts["exit_tolerance"]
         if "max_iter" in opts:
             opts["max_iter_linSys"] = opts["max_iter"]
-        ctx = self._context(opts)
         nx, nu = self._dims()
         x = np.asarray(x, dtype=np.float64)
         u = np.asarray(u, dtype=np.float64)
@@ -468,6 +541,15 @@ class TrajoptMPCReference:
             guess = np.asarray(guess, dtype=np.float64).reshape(1, -1)
             if guess.shape[1] != N * nx:
                 raise ValueError(f"options['guess'] must have N * nx = {N * nx} entries, got {guess.shape[1]}")
+        if self._hooks():   # the plugin-hook path: the hooks form the blocks, the GPU solves the QP
+            if any(c.is_hard_constraint_mode() for _, c in self.other_constraints.limits()):
+                raise NotImplementedError("hard box constraints with plugin-hook costs or plants (hooks.py)")
+            hs = hooks._HookSQP(self, self._hook_context(opts), N, dt, method, opts)
+            G, g, A, Bm, c = hs.blocks(x, u, xs[0])
+            r = hs.ctx.qp_blocks_batch(G[None], g[None], A[None], Bm[None], c[None], rho, method, guess=guess)
+            self.n_inner_iter = int(r["pcg_iters"][0])
+            return r["dxul"][0].reshape(-1, 1)
+        ctx = self._context(opts)
         con = self.other_constraints
         if any(c.is_soft_constraint_mode() for _, c in con.limits()):   # the objects' current mu / lambda
             ctx.set_soft_state(1, N, *[a[None] for a in con.pack_state(N)])
