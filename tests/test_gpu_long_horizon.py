@@ -107,7 +107,7 @@ def test_config5_mpc_loop_sqp_pcgss_arm6_n128():
 # the GM instance's PCG-J counts where they differ from the reference's recorded ones (test_gpu_sqp.py
 # PCGJ_ORDER_DECIDED): fixture -> {QP index: (the GPU's count, the reference's)}
 PCGJ_ORDER_DECIDED_GM = {
-    "sqp_arm3_N8_s2_PCG-J.npz": {1: (58, 59), 2: (58, 59)},
+    "sqp_arm3_N8_s2_PCG-J.npz": {1: (58, 59)},
 }
 
 

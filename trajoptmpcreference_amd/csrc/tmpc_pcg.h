@@ -133,6 +133,7 @@ template <int NX> struct RowInHbm<PcgRowG<NX>> { static constexpr bool value = t
 constexpr int PCG_NVEC = 7;
 struct PcgLds {
   double *pbuf, *rbuf[2], *abuf, *wbuf, *tbuf, *xbuf, *red, *piv;
+  int* flags;   // [2][16] per-wave epochs: p published (0..15), w published (16..31)
 };
 
 // Fixed stride (the VR-row maximum plus the pads) so that every buffer is a
@@ -141,7 +142,7 @@ struct PcgLds {
 // kernels, QP_MAX_ROWS for the global-row ones (GM, more than 1024 rows).
 __host__ __device__ constexpr size_t pcg_vec_doubles(int NX, int VR) { return (size_t)VR + 2 * NX; }
 __host__ __device__ inline size_t pcg_lds_doubles(int N, int NX, int VR) {
-  return PCG_NVEC * pcg_vec_doubles(NX, VR) + 48 + (size_t)2 * N * NX;
+  return PCG_NVEC * pcg_vec_doubles(NX, VR) + 64 + (size_t)2 * N * NX;
 }
 
 __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX, int VR) {
@@ -155,15 +156,16 @@ __device__ __forceinline__ PcgLds pcg_lds(double* lds, int N, int NX, int VR) {
   L.tbuf = L.wbuf + v;
   L.xbuf = L.tbuf + v;
   L.red = lds + PCG_NVEC * v;   // 3 x 16 reduction slots
-  L.piv = L.red + 48;           // 2 x N x NX
+  L.flags = reinterpret_cast<int*>(L.red + 48);   // 32 ints (16 doubles)
+  L.piv = L.red + 64;           // 2 x N x NX
   return L;
 }
 
-// zero the pads and the reduction slots (callers barrier before first use)
+// zero the pads, the reduction slots and the neighbour flags (callers barrier before first use)
 __device__ __forceinline__ void pcg_lds_clear(double* lds, int N, int NX, int VR) {
   const size_t v = pcg_vec_doubles(NX, VR);
   const int rows = N * NX;
-  for (int e = threadIdx.x; e < PCG_NVEC * 2 * NX + 48; e += blockDim.x) {
+  for (int e = threadIdx.x; e < PCG_NVEC * 2 * NX + 64; e += blockDim.x) {
     if (e < PCG_NVEC * 2 * NX) {
       const int buf = e / (2 * NX), o = e - buf * 2 * NX;
       lds[buf * v + (o < NX ? o : rows + o)] = 0.0;
@@ -328,6 +330,32 @@ __device__ __forceinline__ double red_total(const double* red) {
   return readlane_f64(dpp_row_sum(red[threadIdx.x & 15]), 0);
 }
 
+// Neighbour flags instead of two of the iteration's workgroup barriers.  The products S p and
+// S_{k,k+-1} w read block vectors of the lane's own block and of blocks k - 1, k + 1 only; the rows a
+// wave reads past its own lie in the waves just before and after it (a block is at most NX <= 16 rows,
+// a wave 64 lanes), so a wave needs the vector published by waves w - 1, w + 1 (its own writes precede
+// its reads in program order), not by the whole workgroup.  The writer's release fence drains the
+// wave's LDS writes (s_waitcnt lgkmcnt(0)) before lane 0 stores the epoch; the reader polls both
+// neighbours' epochs (wave-uniform ds_read, s_sleep between polls) and acquires.  Write-after-read
+// safety comes from the iteration's remaining full barriers (B2: alpha, B4: nu'), which lie between a
+// vector's last readers of one iteration and its writers of the next.
+__device__ __forceinline__ void nb_signal(int* flags, int epoch) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(flags + (threadIdx.x >> 6), epoch, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void nb_wait(const int* flags, int epoch) {
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  const int lo = w > 0 ? w - 1 : w, hi = w + 1 < nw ? w + 1 : w;
+  while (true) {
+    const int a = __hip_atomic_load(flags + lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int b = __hip_atomic_load(flags + hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__builtin_amdgcn_readfirstlane(a < b ? a : b) >= epoch) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // t = r - (S_{k,k-1} w_{k-1} + S_{k,k+1} w_{k+1}) for this lane's rows
 template <int NX, int RPL, class RT>
 __device__ __forceinline__ void pcg_off(const RT (&R)[RPL], const double* __restrict__ w, int kb,
@@ -463,6 +491,7 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
 #pragma unroll
   for (int m = 0; m < RPL; ++m) pv[m] = zv[m];
   put(L.pbuf, pv);
+  nb_signal(L.flags, 1);
   if (tn && t == 0) tn[0] = fabs(nu);
   if (tr) {
     const double rn = true_residual();
@@ -472,7 +501,7 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
   int cur = 0;
   for (int it = 0; it < max_iter; ++it) {
     PCG_STAMP(0);
-    __syncthreads();                                   // B1: p
+    nb_wait(L.flags, it + 1);                          // B1: p of the neighbour waves
     PCG_STAMP(1);
     pcg_spmv<NX, RPL>(R, L.pbuf, kb, av);
     double po[RPL];
@@ -526,8 +555,9 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
     double nup;
     if (PRE == PRECOND_SS) {
       put(L.wbuf, w);
+      nb_signal(L.flags + 16, it + 1);
       PCG_STAMP(4);
-      __syncthreads();                                 // B3: w
+      nb_wait(L.flags + 16, it + 1);                   // B3: w of the neighbour waves
       PCG_STAMP(5);
       double tv[RPL];
       pcg_off<NX, RPL>(R, L.wbuf, kb, rv, tv);
@@ -562,6 +592,7 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
 #pragma unroll
     for (int m = 0; m < RPL; ++m) pv[m] = __dadd_rn(zv[m], __dmul_rn(po[m], beta));
     put(L.pbuf, pv);
+    nb_signal(L.flags, it + 2);
     nu = nup;
     PCG_STAMP(9);
   }

@@ -151,9 +151,9 @@ class _HookSQP:
         G[N - 1, :nx, :nx] = cost.hessian(x[:, N - 1], timestep=N - 1, **kw)
         g[N - 1, :nx] = np.asarray(cost.gradient(x[:, N - 1], timestep=N - 1, **kw)).reshape(-1)
         if con.total_soft_constraints(timestep=N - 1) > 0:
-            gc = np.asarray(con.jacobian_soft_constraints(x[:, N - 1], timestep=N - 1)).reshape(-1)
+            gc = np.asarray(con.jacobian_soft_constraints(x[:, N - 1], timestep=N - 1)).reshape(-1)[:nx]
             g[N - 1, :nx] = g[N - 1, :nx] + gc
-            G[N - 1, :nx, :nx] = G[N - 1, :nx, :nx] + soft_hessian(con, x[:, N - 1], None, N - 1, gc)
+            G[N - 1, :nx, :nx] = G[N - 1, :nx, :nx] + soft_hessian(con, x[:, N - 1], None, N - 1, gc)[:nx, :nx]
         return G, g, A, Bm, c
 
     def directional(self, x_new, u_new, dxul):
@@ -170,7 +170,7 @@ class _HookSQP:
         D += float(np.asarray(cost.gradient(x_new[:, N - 1], timestep=N - 1, iter_1=self.it, iter_2=self.outer,
                                             iter_3=self.ls)) @ dxul[n * (N - 1):n * (N - 1) + nx, 0])
         if con.total_soft_constraints(timestep=N - 1) > 0:
-            D += float(np.asarray(con.jacobian_soft_constraints(x_new[:, N - 1], timestep=N - 1)).reshape(-1)
+            D += float(np.asarray(con.jacobian_soft_constraints(x_new[:, N - 1], timestep=N - 1)).reshape(-1)[:nx]
                        .dot(dxul[n * (N - 1):n * (N - 1) + nx, 0]))
         return D
 

@@ -453,10 +453,12 @@ class TrajoptMPCReference:
         G[si:si + nx, si:si + nx] = self.cost.hessian(x[:, N - 1], timestep=N - 1)
         g[si:si + nx, 0] = self.cost.gradient(x[:, N - 1], timestep=N - 1)
         if con.total_soft_constraints(timestep=N - 1) > 0:
-            gc = con.jacobian_soft_constraints(x[:, N - 1], timestep=N - 1)
-            g[si:si + nx, :] = g[si:si + nx, :] + gc
-            G[si:si + nx, si:si + nx] = G[si:si + nx, si:si + nx] + hooks.soft_hessian(con, x[:, N - 1], None, N - 1,
-                                                                                       np.ravel(gc))
+            # the terminal knot has only x: the state part of the column (oracle/soft.py; the reference adds
+            # an n_xu column to an nx slice there)
+            gc = np.ravel(con.jacobian_soft_constraints(x[:, N - 1], timestep=N - 1))[:nx]
+            g[si:si + nx, 0] = g[si:si + nx, 0] + gc
+            G[si:si + nx, si:si + nx] = G[si:si + nx, si:si + nx] + \
+                hooks.soft_hessian(con, x[:, N - 1], None, N - 1, gc)[:nx, :nx]
         if n_other > 0 and con.total_hard_constraints(x, u, N - 1):
             jac = con.jacobian_hard_constraints(x[:, N - 1], timestep=N - 1)
             val = con.value_hard_constraints(x[:, N - 1], timestep=N - 1)
