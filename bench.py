@@ -93,6 +93,10 @@ def parse(argv=None):
                     help="CPU-baseline processes (0: the cores this job may use -- the cgroup CPU quota when one "
                          "is set, else os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the config-4 line the default (headline) run adds after its own measurement")
+    ap.add_argument("--secondary-steps", type=int, default=3)
+    ap.add_argument("--secondary-parity", type=int, default=64, help="config-4 problems checked against the oracle")
     return ap.parse_args(argv)
 
 
@@ -213,6 +217,24 @@ def cpu_baseline(n, N, sample, procs, seed0):
         res = pool.map(_cpu_solve, jobs, chunksize=1)
     wall = time.perf_counter() - t0
     return sample / wall, wall, res
+
+
+def _cpu_solve_config4(args):
+    """the oracle's config-4 solve of one problem (tests/golden/make_oracle_fixtures.py job_config4)"""
+    seed, n, N = args
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import sqp as osqp
+    from oracle.soft import SoftConstraints, SoftLimit
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    m = parse_urdf(planar_arm_urdf(n))
+    x, u = osqp.initial_problem(m, N, 0.1, seed)
+    cost = osqp.QuadCost(np.eye(2 * n), 100 * np.eye(2 * n), 0.1 * np.eye(n), np.zeros(2 * n))
+    lim = LIMIT_PRESETS["torque-joint-al"]
+    lims = [SoftLimit(k, n, N, [v["lb"]] * n, [v["ub"]] * n, v["mode"]) for k, v in lim.items()]
+    with np.errstate(all="ignore"):
+        r = osqp.sqp(m, cost, x, u, N, 0.1, "PCG-SS", {}, SoftConstraints(lims))
+    return dict(exit_sqp=int(r["exit_sqp"]), sqp_iter=int(r["sqp_iter"]), exit_soft=int(r["exit_soft"]),
+                outer_iter=int(r["outer_iter"]), pcg_iters=list(r["pcg_iters"]), x=r["x"], u=r["u"])
 
 
 def parity_check(gpu, cpu):
@@ -582,14 +604,18 @@ def main():
                 "note": "tmpc_sqp_solve_batch with host x/u (H2D, solve, D2H of x, u and the status arrays), "
                         "one batch, this GPU; `value` above is the HBM-resident rate"}
     comm.barrier()
+    headline = a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and not limits and \
+        a.cost == "quadratic" and N == 64 and a.precision == "fp64"
+    # BASELINE config 4 beside the headline (after its measurement; every rank takes part)
+    secondary = None
+    if headline and not a.no_secondary and n == 6:
+        secondary = run_secondary(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0)
 
     if rank != 0:
         comm.close()
         return
 
     name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
-    headline = a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and not limits and \
-        a.cost == "quadratic" and N == 64 and a.precision == "fp64"
     if a.limits != "none":
         name += f", {'hard' if hard_limits(a.limits) else 'soft'} box constraints {a.limits}"
     if a.cost == "ee":
@@ -679,8 +705,90 @@ def main():
     out["iters_mean"] = float(np.mean(iters_all))
     out["iters_max"] = int(np.max(iters_all))
     out["problems_gathered"] = int(exit_all.size)
+    if secondary is not None:
+        out["secondary"] = secondary
     print(json.dumps(out))
     comm.close()
+
+
+def run_secondary(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0):
+    """BASELINE config 4 beside the headline, measured after it (the headline's timed region is untouched):
+    the same workload under soft torque + joint limits by augmented Lagrangian (LIMIT_PRESETS
+    "torque-joint-al", SQP PCG-SS), timed exactly as the headline (barrier + synchronize around
+    --secondary-steps solves, max over ranks), with its own kernel stats and k_qp roofline, and the GPU's
+    exit codes / iterations / outer passes / per-QP PCG counts against the oracle on the first
+    --secondary-parity problems (rank 0)."""
+    import copy
+    nx, nu = 2 * n, n
+    a4 = copy.copy(a)
+    a4.limits = "torque-joint-al"
+    limits = LIMIT_PRESETS[a4.limits]
+    ctx.set_box_limits(limits)
+    xb, ub = B * nx * N * 8, B * nu * (N - 1) * 8
+
+    def step():
+        ctx.d2d(d_x, d_x0, xb)
+        ctx.d2d(d_u, d_u0, ub)
+        ctx.set_soft_state(B, N)
+        ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method)
+
+    step()
+    ctx.synchronize()
+    ctx.set_options(profile=1)
+    ctx.reset_stats()
+    counters = np.zeros(4, dtype=np.int64)
+    comm.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.secondary_steps):
+        step()
+        counters += np.array(ctx.solve_counters(), dtype=np.int64)
+    ctx.synchronize()
+    comm.barrier()
+    elapsed = comm.max(time.perf_counter() - t0)
+    ctx.set_options(profile=0)
+    kernels = {}
+    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "ls_terms", "ls_decide"]:
+        cnt, ms = ctx.kernel_stats(name)
+        if cnt:
+            kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
+    ctx.d2d(d_x, d_x0, xb)
+    ctx.d2d(d_u, d_u0, ub)
+    ctx.set_soft_state(B, N)
+    exit_codes, iters = ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=True)
+    from trajoptmpcreference_amd import dist
+    g = dist.gather_summaries(comm, exit_codes=exit_codes.astype(np.int32), iters=iters.astype(np.int32))
+    par = None
+    if rank == 0 and a.secondary_parity > 0:
+        S = min(B, a.secondary_parity)
+        share, _, _ = host_cores()
+        jobs = [(a.seed0 + i, n, N) for i in range(S)]
+        with mp.get_context("fork").Pool(min(share, S), initializer=os.environ.__setitem__,
+                                          initargs=("OMP_NUM_THREADS", "1")) as pool:
+            res = pool.map(_cpu_solve_config4, jobs, chunksize=1)
+        ctx.set_soft_state(S, N)
+        gr = ctx.sqp_solve_batch(x0_host(ctx, d_x0, B, nx, N)[:S], u0[:S], N, dt, a.method)
+        par = parity_check(gr, res)
+        soft_mism = [i for i, c in enumerate(res) if (int(gr["exit_soft"][i]), int(gr["outer_iter"][i]))
+                     != (c["exit_soft"], c["outer_iter"])]
+        par["mismatches"] += len([i for i in soft_mism if i not in par["mismatched_problems"]])
+        par["compared"] += "; exit_soft, outer_iter (exact)"
+    ctx.set_box_limits(None)
+    value = B * a.secondary_steps * world / elapsed
+    return {"metric": f"MPC solves/sec (arm{n}.urdf, N={N}, SQP {a.method}, soft torque + joint box limits by "
+                      "augmented Lagrangian) -- BASELINE config 4's per-GPU slice",
+            "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.secondary_steps, "warmup": 1,
+            "ms_per_step": 1000.0 * elapsed / a.secondary_steps, "higher_is_better": True, "scaling": "weak",
+            "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} SQP {a.method}, batch {B} per GPU, limits "
+                                   f"{a4.limits} (torque +-0.5, joint +-1, AUGMENTED_LAGRANGIAN)",
+                       "global_batch": B * world},
+            "roofline": sqp_roofline(a4, N, nx, nu, kernels, counters) if "qp" in kernels else None,
+            "kernels": kernels, "parity": par,
+            "lockstep": {"batch_iterations_per_solve": kernels["ls_decide"]["launches"] / a.secondary_steps,
+                         "problem_iterations_mean": int(counters[0]) / (B * a.secondary_steps)}
+            if "ls_decide" in kernels else None,
+            "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(g["exit_codes"], return_counts=True))},
+            "iters_mean": float(np.mean(g["iters"])), "iters_max": int(np.max(g["iters"]))}
 
 
 def x0_host(ctx, d_x0, B, nx, N):

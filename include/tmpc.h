@@ -266,7 +266,12 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
  * With hard box limits (ACTIVE_SET / FULL_SET) the knots' constraint rows join the QP
  * (TrajoptMPCReference.py:238-248): the lambda part of dxul then holds the multipliers of the
  * N nx dynamics / initial-state rows in knot order (the hard rows' multipliers are dropped), and
- * guess, S_diag, S_lo, gamma, P_diag must be NULL (S is banded with variable blocks). */
+ * guess, S_diag, S_lo, gamma, P_diag must be NULL (S is banded with variable blocks).
+ * With soft box limits the QP carries their jacobian terms (:220-225, :255-259) at the context's soft state
+ * (mu / lambda per knot, tmpc_set_soft_state).  That state is kept per (B, N): when the last
+ * tmpc_set_soft_state or solve was for a different B or N, it is first reset to the limits' initial
+ * constants -- so set it (tmpc_set_soft_state with this B, N) right before a tmpc_qp_batch that must see a
+ * particular mu / lambda (the Python drop-in's solveKKTSystem(_Schur) always does). */
 int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const double* rho, const double* x,
                   const double* u, const double* xs, const double* guess, double* dxul, int32_t* pcg_iters,
                   double* S_diag, double* S_lo, double* gamma, double* P_diag);

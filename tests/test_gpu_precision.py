@@ -66,6 +66,11 @@ def test_fp32_dynamics_match_reference(ctx, name):
 @pytest.mark.parametrize("name,n,N", [("arm3", 3, 32), ("arm6fix", 6, 64)])
 @pytest.mark.parametrize("prec", ["fp32", "mixed"])
 def test_reduced_precision_ilqr_tracks_fp64(name, n, N, prec):
+    """16 converged problems: the fp32 / mixed iLQR trajectories against the fp64 run's.  Bounds from the
+    measured maxima over the builds of rounds 3-4 (GPUTEST_r04: fp32 1.16e-3 on arm6, mixed 1.74e-4; the
+    round-3 binary's fp32 2.65e-3 -- a compiler change moves fp32 rounding by that much, the full-unroll
+    build of DESIGN.md 4e and the round-3 one differ in it) with a margin of about 2-5x: fp32 3e-3, mixed 1e-3."""
+    bound = 3e-3 if prec == "fp32" else 1e-3
     x, u = _problems(name, N, range(300, 316))
     s = _solver(n, N)
     r64 = s.iLQR_batch(x.copy(), u.copy(), N, 0.1, {})
@@ -73,8 +78,8 @@ def test_reduced_precision_ilqr_tracks_fp64(name, n, N, prec):
     r = s.iLQR_batch(x.copy(), u.copy(), N, 0.1, {"precision": prec})
     errs = [_rel(r["x"][i], r64["x"][i]) for i in range(len(x))]
     import warnings
-    warnings.warn(f"{prec} iLQR {name}: max state rel err vs fp64 {max(errs):.2e} (bound 5e-3)")
-    assert max(errs) < 5e-3, errs
+    warnings.warn(f"{prec} iLQR {name}: max state rel err vs fp64 {max(errs):.2e} (bound {bound:.0e})")
+    assert max(errs) < bound, errs
     erru = [_rel(r["u"][i], r64["u"][i]) for i in range(len(x))]
     assert max(erru) < 2e-2, erru
     assert not np.array_equal(r["x"], r64["x"])

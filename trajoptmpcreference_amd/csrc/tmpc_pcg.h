@@ -339,6 +339,14 @@ __device__ __forceinline__ double red_total(const double* red) {
 // neighbours' epochs (wave-uniform ds_read, s_sleep between polls) and acquires.  Write-after-read
 // safety comes from the iteration's remaining full barriers (B2: alpha, B4: nu'), which lie between a
 // vector's last readers of one iteration and its writers of the next.
+// TMPC_PCG_NB: which of B1 (bit 0) / B3 (bit 1) become neighbour waits; TMPC_PCG_NB_SLEEP: s_sleep 1
+// between polls (experiment builds)
+#ifndef TMPC_PCG_NB
+#define TMPC_PCG_NB 0
+#endif
+#ifndef TMPC_PCG_NB_SLEEP
+#define TMPC_PCG_NB_SLEEP 1
+#endif
 __device__ __forceinline__ void nb_signal(int* flags, int epoch) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(flags + (threadIdx.x >> 6), epoch, __ATOMIC_RELAXED,
@@ -351,7 +359,7 @@ __device__ __forceinline__ void nb_wait(const int* flags, int epoch) {
     const int a = __hip_atomic_load(flags + lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int b = __hip_atomic_load(flags + hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (__builtin_amdgcn_readfirstlane(a < b ? a : b) >= epoch) break;
-    __builtin_amdgcn_s_sleep(1);
+    if (TMPC_PCG_NB_SLEEP) __builtin_amdgcn_s_sleep(1);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
@@ -491,7 +499,7 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
 #pragma unroll
   for (int m = 0; m < RPL; ++m) pv[m] = zv[m];
   put(L.pbuf, pv);
-  nb_signal(L.flags, 1);
+  if (TMPC_PCG_NB & 1) nb_signal(L.flags, 1);
   if (tn && t == 0) tn[0] = fabs(nu);
   if (tr) {
     const double rn = true_residual();
@@ -501,7 +509,10 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
   int cur = 0;
   for (int it = 0; it < max_iter; ++it) {
     PCG_STAMP(0);
-    nb_wait(L.flags, it + 1);                          // B1: p of the neighbour waves
+    if (TMPC_PCG_NB & 1)
+      nb_wait(L.flags, it + 1);                        // B1: p of the neighbour waves
+    else
+      __syncthreads();                                 // B1: p
     PCG_STAMP(1);
     pcg_spmv<NX, RPL>(R, L.pbuf, kb, av);
     double po[RPL];
@@ -555,9 +566,12 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
     double nup;
     if (PRE == PRECOND_SS) {
       put(L.wbuf, w);
-      nb_signal(L.flags + 16, it + 1);
+      if (TMPC_PCG_NB & 2) nb_signal(L.flags + 16, it + 1);
       PCG_STAMP(4);
-      nb_wait(L.flags + 16, it + 1);                   // B3: w of the neighbour waves
+      if (TMPC_PCG_NB & 2)
+        nb_wait(L.flags + 16, it + 1);                 // B3: w of the neighbour waves
+      else
+        __syncthreads();                               // B3: w
       PCG_STAMP(5);
       double tv[RPL];
       pcg_off<NX, RPL>(R, L.wbuf, kb, rv, tv);
@@ -592,7 +606,7 @@ __device__ __forceinline__ void pcg_run(const RT (&R)[RPL], const PcgLane<NX, RP
 #pragma unroll
     for (int m = 0; m < RPL; ++m) pv[m] = __dadd_rn(zv[m], __dmul_rn(po[m], beta));
     put(L.pbuf, pv);
-    nb_signal(L.flags, it + 2);
+    if (TMPC_PCG_NB & 1) nb_signal(L.flags, it + 2);
     nu = nup;
     PCG_STAMP(9);
   }
