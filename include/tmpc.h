@@ -233,7 +233,10 @@ int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double*
  * x[:, 0] = the new state; QF_start -= 1 (floor 0) when set; soft-limit constants shifted.
  * Outputs: the executed states x_exec [B][nx][steps+1] and controls u_exec [B][nu][steps], per-step
  * exit codes and iteration counts [B][steps] (all nullable); x, u hold the final shifted horizon.
- * Horizons up to N * nx = 1536 for SQP (past 1024 rows the PCG keeps S in HBM); iLQR has no horizon limit. */
+ * SQP horizons: the fused QP up to N * nx = 1536 (past 1024 rows the PCG keeps S in HBM); past that the banded
+ * path of the hard-limit kernels with no constraint rows, PCG up to N * nx = 4096 and the direct methods (S, N)
+ * without a row limit (pcg_warm_start is refused there: the banded PCG takes no guess).  iLQR has no horizon
+ * limit. */
 #define TMPC_SOLVER_ILQR 16
 int tmpc_mpc_batch(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps, double* x, double* u,
                    double* x_exec, double* u_exec, int32_t* exit_codes, int32_t* iters);

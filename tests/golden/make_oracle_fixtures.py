@@ -125,6 +125,29 @@ def job_mpc128sqp(seed):
     return dict(seed=seed, exit_codes=o["exit_codes"], iters=o["iters"], x_exec=o["x_exec"], u_exec=o["u_exec"])
 
 
+# SQP past the fused QP's 1536 Schur rows (the banded path, csrc/tmpc_api.cpp qp_banded): arm7 at N = 128
+# (1792 rows) with PCG-SS, arm6 at N = 256 (3072 rows) with method S; the oracle's QP in the banded path's
+# canonical order (oracle/hard.py: the dense KKT with no constraint rows, pcg_canonical)
+CBIG = [(7, 128, 1000, "PCG-SS", {}), (7, 128, 1001, "PCG-SS", {}), (6, 256, 1010, "S", {}),
+        # PCG-SS at the reference's defaults saturates at max_iter 100 on these S; a looser exit
+        # tolerance makes every QP's count a decision the two runs must agree on
+        (7, 128, 1002, "PCG-SS", {"exit_tolerance_linSys": 1e-3})]
+
+
+def job_big(args):
+    n, N, seed, method, opts = args
+    from oracle import hard as ohard
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    m = parse_urdf(planar_arm_urdf(n))
+    x, u = osqp.initial_problem(m, N, 0.1, seed)
+    cost = osqp.QuadCost(np.eye(2 * n), 100 * np.eye(2 * n), 0.1 * np.eye(n), np.zeros(2 * n))
+    with np.errstate(all="ignore"):
+        o = osqp.sqp(m, cost, x, u, N, 0.1, method, dict(opts), hard=ohard.HardConstraints([]), order="canonical")
+    return dict(n=n, N=N, seed=seed, method=method, opts=opts, exit_sqp=o["exit_sqp"], sqp_iter=o["sqp_iter"], x=o["x"],
+                u=o["u"], pcg_iters=list(o["pcg_iters"]), alpha=[t["alpha"] for t in o["trace"][1:]])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
@@ -148,6 +171,18 @@ def main():
         np.savez_compressed(os.path.join(OUT, "oracle_config3_arm6_N64_ilqr_al.npz"), **rec)
         print(f"[oracle] config3: {time.time() - t:.0f} s; (exit, iter, soft, outer) "
               f"{list(zip(rec['exit_code'], rec['iter'], rec['exit_soft'], rec['outer_iter']))}", flush=True)
+    if a.only in (None, "big"):
+        t = time.time()
+        for r in pool.map(job_big, CBIG, chunksize=1):
+            tol = r["opts"].get("exit_tolerance_linSys")
+            np.savez_compressed(os.path.join(OUT, f"oracle_big_arm{r['n']}_N{r['N']}_s{r['seed']}_{r['method']}.npz"),
+                                seed=r["seed"], N=r["N"], exit_sqp=r["exit_sqp"], sqp_iter=r["sqp_iter"], x=r["x"],
+                                exit_tolerance_linSys=np.nan if tol is None else tol,
+                                u=r["u"], pcg_iters=np.array(r["pcg_iters"], dtype=np.int32),
+                                alpha=np.array(r["alpha"]))
+            print(f"[oracle] big arm{r['n']} N={r['N']} s{r['seed']} {r['method']}: exit {r['exit_sqp']} iters "
+                  f"{r['sqp_iter']} pcg {r['pcg_iters']}", flush=True)
+        print(f"[oracle] big: {time.time() - t:.0f} s", flush=True)
     if a.only in (None, "config4"):
         t = time.time()
         res = pool.map(job_config4, [C4["seed0"] + i for i in range(C4["B"])], chunksize=1)

@@ -176,7 +176,8 @@ def _replay_pcg_counts(solver, r, x0s, u0s, N, method, hard, n, base_opts=None):
             assert [int(v) for v in info["active"][a]] == [int(v) for v in r["trace"]["hard_active"][i, j + 1]]
             D = int(info["dim"][a])
             S_g = _unband(info["S_band"][a], W, D)
-            lam_c, it_c = ohard.pcg_canonical(S_g, info["gamma"][a, :D], nx, method[4:], 1e-6, 100)
+            lam_c, it_c = ohard.pcg_canonical(S_g, info["gamma"][a, :D], nx, method[4:],
+                                              opts["exit_tolerance_linSys"], opts["max_iter_linSys"])
             assert it_c == want, (i, j, it_c, want)
             dyn, hrows = _row_layout(hard, xj[a], uj[a], N, nx)
             nz = (nx + n) * (N - 1) + nx

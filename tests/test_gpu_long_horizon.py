@@ -138,3 +138,49 @@ def test_gm_instance_matches_reference_fixtures(f, monkeypatch):
     rtol = 1e-4 if method == "PCG-J" else 1e-7
     assert _rel(x, d["x"]) < rtol
     assert _rel(u, d["u"]) < rtol
+
+
+BIG = sorted(glob.glob(os.path.join(GOLDEN, "oracle_big_*.npz")))
+
+
+@pytest.mark.parametrize("f", BIG, ids=lambda f: os.path.basename(f))
+def test_sqp_past_the_fused_rows_matches_oracle(f):
+    """Past the fused QP's 1536 Schur rows the QP takes the banded path of the hard-limit kernels with no
+    constraint rows (csrc/tmpc_api.cpp qp_banded): a 7-joint chain at N = 128 (1792 rows, PCG-SS) and arm6 at
+    N = 256 (3072 rows, method S: the banded direct elimination), against the oracle in that path's canonical
+    order (tests/golden/oracle_big_*.npz, make_oracle_fixtures.py --only big): exit code, SQP iterations, the
+    alpha path and every PCG count identical, trajectories within 1e-6; and every QP of the GPU's own run
+    replayed at its own iterate -- the canonical-order PCG (oracle/hard.py pcg_canonical) on the QP's own
+    banded S takes the GPU's count and returns its lambda bit for bit (test_gpu_hard._replay_pcg_counts)."""
+    from oracle import hard as ohard
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    from test_gpu_hard import _replay_pcg_counts
+    d = np.load(f)
+    n = int(os.path.basename(f).split("_")[2][3:])
+    N, method = int(d["N"]), os.path.basename(f)[:-4].split("_")[-1]
+    m = parse_urdf(planar_arm_urdf(n))
+    x0, u0 = osqp.initial_problem(m, N, 0.1, int(d["seed"]))
+    x, u = x0[None], u0[None]
+    solver = _solver(n)
+    tol = float(d["exit_tolerance_linSys"]) if "exit_tolerance_linSys" in d else float("nan")
+    opts = {} if np.isnan(tol) else {"exit_tolerance_linSys": tol}
+    r = solver.SQP_batch(x, u, N, 0.1, method, dict(opts), hard_active=True)
+    got = (int(r["exit_sqp"][0]), int(r["sqp_iter"][0]))
+    assert got == (int(d["exit_sqp"]), int(d["sqp_iter"])), got
+    nq = got[1] + (1 if got[0] == 3 else 0)
+    assert list(r["trace"]["alpha"][0, 1:nq + 1]) == list(d["alpha"])
+    if method.startswith("PCG"):
+        assert [int(v) for v in r["trace"]["pcg_iters"][0, 1:nq + 1]] == [int(v) for v in d["pcg_iters"]]
+    assert _rel(r["x"][0], d["x"]) < 1e-6
+    assert _rel(r["u"][0], d["u"]) < 1e-6
+    if method.startswith("PCG"):
+        _replay_pcg_counts(solver, r, x, u, N, method, ohard.HardConstraints([]), n, base_opts=opts)
+
+
+def test_banded_path_refuses_warm_start():
+    """The banded PCG takes no guess: pcg_warm_start past the fused rows is an error, not ignored."""
+    from trajoptmpcreference_amd import _native
+    x, u = _problems(130, [5])
+    with pytest.raises(_native.NativeError, match="warm"):
+        _solver(6).SQP_batch(x, u, 130, 0.1, "PCG-SS", {"pcg_warm_start": True})

@@ -229,10 +229,17 @@ static int check_ready(tmpc_ctx* ctx, int B, int N, bool qp = true) {
                 ctx->hmodel.n);
   if (B < 1) return fail(ctx, "batch size must be >= 1 (got %d)", B);
   if (N < 2) return fail(ctx, "N must be >= 2 (got %d)", N);
-  if (qp && N * ctx->hcost.nx > QP_MAX_ROWS)
-    return fail(ctx, "N * nx = %d exceeds %d rows (one PCG workgroup per problem); larger horizons are not "
-                "supported", N * ctx->hcost.nx, QP_MAX_ROWS);
+  (void)qp;   // QPs past the fused kernel's QP_MAX_ROWS take the banded path (qp_banded)
   return 0;
+}
+
+// The QP takes the banded variable-block path of tmpc_hard.hip -- built for hard box constraints --
+// with hard limits, and also without them past the fused k_qp's QP_MAX_ROWS (1536) rows: there the
+// Schur complement is the same block-tridiagonal S with no constraint rows (every knot's row count 0),
+// which the banded kernels solve up to HARD_PCG_MAX_ROWS rows by PCG (and without a row limit by the
+// direct banded elimination), in their own canonical order (oracle/hard.py pcg_canonical).
+static bool qp_banded(const tmpc_ctx* ctx, int N) {
+  return ctx->hlim.any_hard || N * 2 * ctx->hmodel.n > QP_MAX_ROWS;
 }
 
 // ------------------------------------------------------------------ QP phase (shared by SQP and tmpc_qp_batch)
@@ -353,7 +360,7 @@ static int alloc_work(tmpc_ctx* ctx, int B, int N, Work& w, bool with_blocks) {
   BUF(int, iters, (size_t)B);
   w = Work{xs, qdd, minv, cvec, Amat, Bmat, Ginv, nullptr, nullptr, nullptr, nullptr, dx, du, nullptr, iters,
            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
-  if (N * nx >= qp_gm_min_rows()) {   // the GM QP kernel's rows of S / P^-1
+  if (N * nx >= qp_gm_min_rows() && !qp_banded(ctx, N)) {   // the GM QP kernel's rows of S / P^-1
     BUF(double, qp_gm, qp_gm_doubles(B, N, nx));
     w.Sg = qp_gm;
   }
@@ -447,16 +454,18 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
   const int gmax = nx + 2 * hard.rmax;         // the last group holds two knots' hard rows
   hard.W = 2 * gmax - 1;
   if (precond != 0 && hard.dmax > HARD_PCG_MAX_ROWS)
-    return fail(ctx, "hard constraints: Schur dimension up to %d exceeds the PCG's %d rows", hard.dmax,
-                HARD_PCG_MAX_ROWS);
+    return fail(ctx, "%s: Schur dimension up to %d exceeds the banded PCG's %d rows (methods S / N have no "
+                "row limit)", ctx->hlim.any_hard ? "hard constraints" : "N * nx past the fused QP's rows",
+                hard.dmax, HARD_PCG_MAX_ROWS);
   if (hard.W > 1024) return fail(ctx, "hard constraints: band half-width %d > 1024", hard.W);
   const size_t BW = 2 * (size_t)hard.W + 1, nbmax = hard.dmax / nx + 1;
   hard.Cs = ctx->dlim;
   hard.C = ctx->dcost;
+  const int rbuf = hard.rmax > 0 ? hard.rmax : 1;   // no hard limits (the banded path past QP_MAX_ROWS): rmax = 0
   BUF(int, hd_cnt, (size_t)B * N);
-  BUF(int, hd_col, (size_t)B * N * hard.rmax);
-  BUF(double, hd_sgn, (size_t)B * N * hard.rmax);
-  BUF(double, hd_val, (size_t)B * N * hard.rmax);
+  BUF(int, hd_col, (size_t)B * N * rbuf);
+  BUF(double, hd_sgn, (size_t)B * N * rbuf);
+  BUF(double, hd_val, (size_t)B * N * rbuf);
   BUF(int, hd_roff, (size_t)B * N);
   BUF(int, hd_hoff, (size_t)B * N);
   BUF(int, hd_dim, (size_t)B);
@@ -464,7 +473,7 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
   BUF(int, hd_rknot, (size_t)B * hard.dmax);
   BUF(int, hd_ridx, (size_t)B * hard.dmax);
   BUF(int, hd_pk, (size_t)B * hard.dmax * 2);
-  BUF(int, hd_slot, (size_t)B * N * hard.rmax);
+  BUF(int, hd_slot, (size_t)B * N * rbuf);
   BUF(unsigned long long, hd_amask, (size_t)B * N);
   BUF(int, hd_sing, (size_t)B);
   HIP_OK(hipMemsetAsync(hd_sing, 0, (size_t)B * sizeof(int), ctx->stream));
@@ -650,21 +659,24 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   // hard box constraints (ACTIVE_SET / FULL_SET): per-knot rows, a banded Schur complement per problem
   HardArgs hard{};
   double* hterms = nullptr;
-  if (ctx->hlim.any_hard) {
+  const bool banded = qp_banded(ctx, N);
+  if (banded) {
     if ((rc = setup_hard(ctx, B, N, T, precond, hard))) return rc;
-    hterms = hard.hterms;
+    if (ctx->hlim.any_hard) hterms = hard.hterms;   // the limits' violation terms of the line search
     w.hard = &hard;
     w.Wtr = W;
-    if (hard_trace) {   // per-QP active-set bitmasks in the trace (tmpc_trace.hard_active)
+    if (hard_trace && ctx->hlim.any_hard) {   // per-QP active-set bitmasks in the trace (tmpc_trace.hard_active)
       BUF(unsigned long long, tr_hard, (size_t)B * W * N);
       HIP_OK(hipMemsetAsync(tr_hard, 0, (size_t)B * W * N * sizeof(unsigned long long), ctx->stream));
       w.tr_active = tr_hard;
       tr.hard_active = tr_hard;
     }
   }
-  if (o.pcg_warm_start && precond != 0 && ctx->hlim.any_hard)
-    return fail(ctx, "pcg_warm_start with hard box constraints: the Schur dimension changes with the active set "
-                "from QP to QP, so a previous lambda is no PCG guess; unset pcg_warm_start");
+  if (o.pcg_warm_start && precond != 0 && banded)
+    return fail(ctx, ctx->hlim.any_hard
+                ? "pcg_warm_start with hard box constraints: the Schur dimension changes with the active set "
+                  "from QP to QP, so a previous lambda is no PCG guess; unset pcg_warm_start"
+                : "pcg_warm_start past the fused QP's rows: the banded PCG takes no guess; unset pcg_warm_start");
   if (o.pcg_warm_start && precond != 0) {
     // PCG warm start: each QP starts from the problem's previous lambda (in place: a workgroup reads
     // its guess before it writes its lambda)
@@ -1284,9 +1296,9 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "the MPC loop supports QuadraticCost only");
   if (steps < 1) return fail(ctx, "steps must be >= 1");
   if (!ilqr && precond_of(solver) < 0) return fail(ctx, "solver %d: use TMPC_LINSYS_* or TMPC_SOLVER_ILQR", solver);
-  if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0 && ctx->hlim.any_hard)
-    return fail(ctx, "pcg_warm_start with hard box constraints: the Schur dimension changes with the active set "
-                "from QP to QP, so a previous lambda is no PCG guess; unset pcg_warm_start");
+  if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0 && qp_banded(ctx, N))
+    return fail(ctx, "pcg_warm_start with hard box constraints or past the fused QP's rows: the banded PCG takes "
+                "no guess; unset pcg_warm_start");
   const int nj = ctx->hmodel.n, nx = 2 * nj;
   const bool chain = ctx->hmodel.chain != 0;
   // work counters of the whole loop: the sum over its horizon solves (tmpc_solve_counters)
@@ -1299,7 +1311,7 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
               : sqp_device(ctx, B, N, dt, solver, d_x, d_u, nullptr, /*keep_warm=*/s > 0);
     if (rc) return rc;
     for (int i = 0; i < 3; ++i) sum_counters[i] += ctx->last_counters[i];
-    if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0 && !ctx->hlim.any_hard) {
+    if (!ilqr && ctx->opts.pcg_warm_start && precond_of(solver) != 0 && !qp_banded(ctx, N)) {
       // the next step's first PCG starts from this step's last lambda shifted by one knot
       // (lambda_k <- lambda_{k+1}, last block kept), as x and u are shifted (oracle/mpc.py)
       double* lw = (double*)ctx->bufs["lam_warm"].ptr;
@@ -1433,10 +1445,13 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "tmpc_qp_batch supports QuadraticCost only");
-  if (ctx->hlim.any_hard && guess) return fail(ctx, "tmpc_qp_batch: no PCG guess with hard box constraints");
-  if (ctx->hlim.any_hard && (S_diag || S_lo || gamma || P_diag))
-    return fail(ctx, "tmpc_qp_batch: with hard box constraints S is banded with variable blocks; "
-                     "S_diag / S_lo / gamma / P_diag must be NULL");
+  const bool banded = qp_banded(ctx, N);
+  if (banded && guess)
+    return fail(ctx, "tmpc_qp_batch: no PCG guess on the banded path (hard box constraints, or N * nx past %d)",
+                QP_MAX_ROWS);
+  if (banded && (S_diag || S_lo || gamma || P_diag))
+    return fail(ctx, "tmpc_qp_batch: on the banded path (hard box constraints, or N * nx past %d) S is banded; "
+                     "S_diag / S_lo / gamma / P_diag must be NULL (tmpc_qp_hard_info has S_band)", QP_MAX_ROWS);
   const int precond = precond_of(linsys);
   if (precond < 0) return fail(ctx, "linear system method %d is not available on the GPU", linsys);
   if (!rho || !x || !u) return fail(ctx, "null input");
@@ -1484,15 +1499,15 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
   // hard box constraints: the QP with the knots' constraint rows (tmpc_hard.hip); the lambda part of
   // dxul then holds the multipliers of the N nx dynamics / initial-state rows, in knot order
   HardArgs hard{};
-  if (ctx->hlim.any_hard) {
+  if (banded) {
     if ((rc = setup_hard(ctx, B, N, 0, precond, hard))) return rc;
     w.hard = &hard;
   }
   ctx->hard_last = {0, 0, 0, 0, 0};
-  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, !ctx->hlim.any_hard, PList{nullptr, nullptr}, B)))
+  if ((rc = run_qp(ctx, B, N, dt, precond, io_x, io_u, st, w, !banded, PList{nullptr, nullptr}, B)))
     return rc;
   HIP_OK(hipStreamSynchronize(ctx->stream));
-  if (ctx->hlim.any_hard) {
+  if (banded) {
     if ((rc = collect_hard_work(ctx, hard))) return rc;
     ctx->hard_last = {B, N, hard.dmax, hard.W, hard.rmax};
     std::vector<int> roff((size_t)B * N);
@@ -1641,7 +1656,9 @@ int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim,
                       double* lambda_hard, double* S_band, double* gamma, int32_t* singular) {
   if (!ctx) return -1;
   const auto& hl = ctx->hard_last;
-  if (hl.B == 0) return fail(ctx, "tmpc_qp_hard_info: the last tmpc_qp_batch ran without hard box limits");
+  if (hl.B == 0)
+    return fail(ctx, "tmpc_qp_hard_info: the last tmpc_qp_batch did not take the banded path (hard box limits, or "
+                "N * nx past %d rows)", QP_MAX_ROWS);
   if (hl.B != B || hl.N != N)
     return fail(ctx, "tmpc_qp_hard_info: the last hard-limit QP was B=%d N=%d, asked for B=%d N=%d", hl.B, hl.N, B, N);
   hipSetDevice(ctx->device);

@@ -381,6 +381,13 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
   }
 }
 
+#ifndef TMPC_HX_NOSTREAM
+#define TMPC_HX_NOSTREAM 0
+#endif
+#ifndef TMPC_HX_NOPREC
+#define TMPC_HX_NOPREC 0
+#endif
+
 // band entries of each slot-0 row (its first ones) k_hard_pcg holds in registers for the whole solve:
 // 24 (48 VGPRs of its 128); fewer where that spills (nx = 14: 20; nx = 2, 4: 16)
 __host__ __device__ constexpr int hard_pcg_reg_diag(int nx) { return nx <= 4 ? 16 : (nx >= 14 ? 20 : 24); }
@@ -568,7 +575,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   }
   // z = P^-1 r for row a (r read from LDS)
   auto apply_P = [&](int a) -> double {
-    if (precond == PRECOND_NONE) return rv[a];
+    if (precond == PRECOND_NONE || TMPC_HX_NOPREC) return rv[a];
     if (precond == PRECOND_J) return (1.0 / band_at(S, rg, dmax, a, a)) * rv[a];
     if (a >= nb * NX) return 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
     const int k = a / NX, i = a - k * NX;
@@ -606,6 +613,9 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       for (int u = 0; u < REG; ++u)
         if (own && u <= hi) s += vc[u] * pv[c0 + u];
       j0 = REG;
+#if TMPC_HX_NOSTREAM   // timing experiment only (wrong answers): no streamed band entries
+      return s;
+#endif
     }
     for (int j = j0; j <= jmax; j += U) {
       double v[U];
