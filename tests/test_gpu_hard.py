@@ -452,7 +452,9 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
     stair) less those the kernel keeps in LDS -- as many as fit in the 160 KB after its vectors, diagonal
     blocks first (tmpc_hard.hip hard_pcg_cache_offset)."""
     slots = -(-dmax // 1024)
-    REG = 16 if nx <= 4 else (20 if nx >= 14 else 24)   # tmpc_hard.hip hard_pcg_reg_diag (slot 0, in registers)
+    # tmpc_hard.hip hard_pcg_reg_diag (slot 0, in registers; TMPC_HARD_REG, a build constant)
+    reg = int(os.environ.get("TMPC_TEST_HARD_REG", "24"))
+    REG = (16 if nx <= 4 else (reg - 4 if nx >= 14 else reg)) - (8 if slots >= 3 else 0)
     tot = 0.0
     for S, it in zip(Ss, iters):
         D = S.shape[0]
@@ -464,7 +466,8 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
             nnz += streamed
             nnz_reg += width - streamed
         nb, b2 = D // nx, nx * nx
-        offset = max(4 * D, 4 * (b2 + 2 * nx)) + 32 + (D + 2 * slots * 16 + 1) // 2
+        offset = max(2 * D + 2 * max(D - 1024, 0), 4 * (b2 + 2 * nx)) + 32 + (D + 2 * slots * 16 + 1) // 2
+        offset += offset & 1   # 16-byte aligned
         ncap = max(0, 160 * 1024 // 8 - offset) // b2
         ncd = min(nb, ncap) if ptype in ("BJ", "SS") else 0
         ncl = min(nb - 1, ncap - ncd) if ptype == "SS" and nb > 1 else 0

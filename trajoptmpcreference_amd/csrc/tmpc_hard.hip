@@ -38,6 +38,7 @@
 // sums from 0.0, per-thread dot partials over 1024 threads, a 64-lane xor butterfly, a fan-in over the
 // 16 waves -- so that on identical S and gamma the two are bitwise equal (tests/test_gpu_hard.py).
 #include "tmpc_internal.h"
+#include "tmpc_pcg.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -358,7 +359,11 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     l = __builtin_amdgcn_readfirstlane(l);
     h = __builtin_amdgcn_readfirstlane(h);
     for (int o = l; o <= h; ++o) {
-      if (o < ol || o > oh) continue;
+      if (!own) continue;
+      if (o > oh) {   // zero up to the wave's longest row: k_hard_pcg's products read it (exact zeros)
+        S[(size_t)o * dmax + a] = 0.0;
+        continue;
+      }
       const int c = rb[2 * a] + o;
       const int pc0 = PKb[c * 2], pc1 = PKb[c * 2 + 1];
       double sum = 0.0;
@@ -387,45 +392,149 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
 #ifndef TMPC_HX_NOPREC
 #define TMPC_HX_NOPREC 0
 #endif
+#ifndef TMPC_HX_STAMPS
+#define TMPC_HX_STAMPS 0
+#endif
 
 // band entries of each slot-0 row (its first ones) k_hard_pcg holds in registers for the whole solve:
-// 24 (48 VGPRs of its 128); fewer where that spills (nx = 14: 20; nx = 2, 4: 16)
-__host__ __device__ constexpr int hard_pcg_reg_diag(int nx) { return nx <= 4 ? 16 : (nx >= 14 ? 20 : 24); }
+// 24 (48 VGPRs of its 128); fewer where that spills (nx = 14: 20; nx = 2, 4: 16; 8 fewer in the three- and
+// four-slot instances, which hold x of three / four rows)
+#ifndef TMPC_HARD_REG
+#define TMPC_HARD_REG 24
+#endif
+__host__ __device__ constexpr int hard_pcg_reg_diag(int nx, int slots) {
+  return (nx <= 4 ? 16 : (nx >= 14 ? TMPC_HARD_REG - 4 : TMPC_HARD_REG)) - (slots >= 3 ? 8 : 0);
+}
 
-// doubles of LDS k_hard_pcg uses before its reduction slots: r, p, z, S p of dmax rows, and at least
-// four nx x nx blocks (with their pivot rows / columns) for the preconditioner setup
+// doubles of LDS k_hard_pcg uses before its reduction slots: r and p of dmax rows, z and S p of the rows
+// past slot 0 (slot 0's are registers), and at least four nx x nx blocks (with their pivot rows /
+// columns) for the preconditioner setup
+// (p is followed by HARD_PCG_GUARD zeros: the register-held band entries past a row read them)
+constexpr int HARD_PCG_GUARD = 24;
 __host__ __device__ constexpr int hard_pcg_scratch(int dmax, int nx) {
-  return 4 * dmax > 4 * (nx * nx + 2 * nx) ? 4 * dmax : 4 * (nx * nx + 2 * nx);
+  return 2 * dmax + HARD_PCG_GUARD + 2 * (dmax > HARD_PCG_THREADS ? dmax - HARD_PCG_THREADS : 0) >
+                 4 * (nx * nx + 2 * nx)
+             ? 2 * dmax + HARD_PCG_GUARD + 2 * (dmax > HARD_PCG_THREADS ? dmax - HARD_PCG_THREADS : 0)
+             : 4 * (nx * nx + 2 * nx);
 }
 // doubles before k_hard_pcg's preconditioner-block cache: the scratch, 2 x 16 reduction slots, the rows'
 // and the wave-slots' diagonal ranges (ints)
+// (rounded up to 16 bytes: the cached blocks are read as 16-byte pieces)
 __host__ __device__ constexpr int hard_pcg_cache_offset(int D, int nx, int slots) {
-  return hard_pcg_scratch(D, nx) + 32 + (D + 2 * slots * (HARD_PCG_THREADS / 64) + 1) / 2;
+  return (hard_pcg_scratch(D, nx) + 32 + (D + 2 * slots * (HARD_PCG_THREADS / 64) + 1) / 2 + 1) & ~1;
 }
 
 // ---- workgroup sum (deterministic): wave DPP butterfly via shuffles + fixed-order fan-in
 // Double-buffered form for a sequence of sums (k_hard_pcg): sum number k uses slots red[16 (k & 1) ..],
 // so the barrier that protects a slot set from being overwritten while a slow wave still reads it is
 // the NEXT sum's own barrier -- one barrier per sum instead of two.
-__device__ __forceinline__ double h_block_sum_db(double v, double* red, int& k) {
+// The 64-lane xor butterfly v += v[l ^ off] for off = 32, 16, 8, 4, 2, 1 (oracle/hard.py _dot) on the
+// VALU: permlane swaps (32, 16), DPP row_ror:8, row_shl:4 / row_shr:4 picked by lane bit 2, quad_perm
+// (2, 1).  Each step adds the same two values as the shuffle form (addition commutes), so the sums
+// are bitwise those of __shfl_xor, without its six ds_bpermute round trips through the LDS unit.
+#ifndef TMPC_HARD_DPP
+#define TMPC_HARD_DPP 1
+#endif
+__device__ __forceinline__ double h_wave_butterfly(double v) {
+#if TMPC_HARD_DPP
+  v = perm_pair_sum32(v);
+  v = perm_pair_sum16(v);
+  v += dpp_get<0x128, 0xf>(v);   // row_ror:8: lane l reads l ^ 8
+  {
+    const double up = dpp_get<0x104, 0xf>(v);   // row_shl:4: lane l reads l + 4 (lanes with bit 2 clear)
+    const double dn = dpp_get<0x114, 0xf>(v);   // row_shr:4: lane l reads l - 4 (bit 2 set)
+    v += (threadIdx.x & 4) ? dn : up;
+  }
+  v += dpp_get<0x4E, 0xf>(v);    // quad_perm [2,3,0,1]: l ^ 2
+  v += dpp_get<0xB1, 0xf>(v);    // quad_perm [1,0,3,2]: l ^ 1
+#else
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+#endif
+  return v;
+}
+
+// (k_hard_pcg's HARD_PCG_THREADS workgroup: the fan-in over its 16 waves unrolled)
+__device__ __forceinline__ double h_block_sum_db(double v, double* red, int& k) {
+  constexpr int NW = HARD_PCG_THREADS / 64;
+  v = h_wave_butterfly(v);
+  const int w = threadIdx.x >> 6;
   double* rs = red + 16 * (k & 1);
   ++k;
   if ((threadIdx.x & 63) == 0) rs[w] = v;
   __syncthreads();
   double s = 0.0;
-  for (int i = 0; i < nw; ++i) s += rs[i];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += rs[i];
   return s;
 }
 __device__ __forceinline__ double h_block_sum(double v, double* red) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  v = h_wave_butterfly(v);
   const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[w] = v;
   __syncthreads();
   double s = 0.0;
   for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+// A preconditioner block's row / column from the LDS cache or from HBM, through pointers typed with
+// their address space: a plain pointer that may point to either (or two branches the compiler merges)
+// makes every read a flat load, issued one at a time here.  s += M_ij r_j in j order (canonical).
+typedef __attribute__((address_space(3))) const double lds_cdouble;
+typedef __attribute__((address_space(1))) const double glb_cdouble;
+__device__ __forceinline__ lds_cdouble* lds_ptr(const double* p) { return (lds_cdouble*)p; }
+__device__ __forceinline__ glb_cdouble* glb_ptr(const double* p) { return (glb_cdouble*)p; }
+// The LDS copies of the preconditioner blocks are row-major with each row's 16-byte pieces swizzled:
+// piece c of row i of block k sits at c ^ sw, sw = bit 3 of the global row k NX + i (NX a multiple of 4,
+// so that c ^ 1 stays in the row).  A wave reads its rows' pieces with ds_read_b128: the 16 lanes of a
+// lane group hold 16 consecutive global rows mod 16, which the swizzle spreads over all 64 banks
+// (unswizzled, rows r and r + 8 share banks: two LDS cycles per piece instead of one).
+template <int NX>
+__device__ __forceinline__ int hp_swz(int k, int i) {
+  return NX % 4 == 0 ? ((k * NX + i) >> 3) & 1 : 0;
+}
+// offset of element (i, j) of block k in the swizzled layout
+template <int NX>
+__device__ __forceinline__ int hp_off(int k, int i, int j) {
+  return k * NX * NX + i * NX + ((((j >> 1) ^ hp_swz<NX>(k, i)) << 1) | (j & 1));
+}
+// s += P_ij r_j over row i of block k of the swizzled LDS copy (16-byte pieces, j in order)
+template <int NX>
+__device__ __forceinline__ double hp_row_lds(const double* base, int k, int i, const double* r, double s) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) const d2v lds_cd2v;
+  lds_cd2v* row = (lds_cd2v*)(base + (size_t)k * NX * NX + i * NX);
+  const int sw = hp_swz<NX>(k, i);
+#pragma unroll
+  for (int c = 0; c < NX / 2; ++c) {
+    const d2v m = row[c ^ sw];
+    s += m.x * r[2 * c];
+    s += m.y * r[2 * c + 1];
+  }
+  return s;
+}
+// s += P_ji r_j over column i of block k of the swizzled LDS copy
+template <int NX>
+__device__ __forceinline__ double hp_col_lds(const double* base, int k, int i, const double* r, double s) {
+  lds_cdouble* blk = lds_ptr(base);
+#pragma unroll
+  for (int j = 0; j < NX; ++j) s += blk[hp_off<NX>(k, j, i)] * r[j];
+  return s;
+}
+
+// column i of M (row-major M, i.e. M_ji for j = 0 ..): the transposed blocks
+template <int NX, class P>
+__device__ __forceinline__ double hp_col(P M, int i, const double* r, double s) {
+#pragma unroll
+  for (int j = 0; j < NX; ++j) s += M[j * NX + i] * r[j];
+  return s;
+}
+// row i of M
+template <int NX, class P>
+__device__ __forceinline__ double hp_row(P M, int i, const double* r, double s) {
+#pragma unroll
+  for (int j = 0; j < NX; ++j) s += M[i * NX + j] * r[j];
   return s;
 }
 
@@ -457,7 +566,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
                                                               double* __restrict__ lam, int* __restrict__ iters,
                                                               const int* __restrict__ rng, double* __restrict__ work,
                                                               int lds_bytes) {
-  constexpr int REG = hard_pcg_reg_diag(NX);
+  constexpr int REG = hard_pcg_reg_diag(NX, SLOTS);
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int D = dim[b];
@@ -471,16 +580,17 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   double* PL = Pl + (size_t)b * nbmax * NX * NX;
   double* PT = Ptr + (size_t)b * nbmax * NX * NX;
   // LDS (the whole allotment, lds_bytes; one workgroup per CU), laid out for this problem's D:
-  //   r, p, z, S p of the rows [4][D] (z, S p: read and written by the owner only) -- the setup's
-  //   staging area before; 16 reduction slots; each row's diagonal range; each wave-slot's union;
+  //   r, p of the rows [2][D], z, S p of the rows past slot 0 [2][D - 1024] (read and written by the
+  //   owner only; slot 0's live in registers) -- the setup's staging area before; 16 reduction slots; each row's diagonal range; each wave-slot's union;
   //   then as many preconditioner blocks as fit, transposed diagonal blocks first (ncd of them), then
   //   stair blocks Pl (ncl): those never stream from HBM during the iterations
   constexpr int B2 = NX * NX;
   extern __shared__ __align__(16) double sh[];
   double* rv = sh;
   double* pv = rv + D;
-  double* zl = pv + D;
-  double* al = zl + D;
+  const int ext = D > HARD_PCG_THREADS ? D - HARD_PCG_THREADS : 0;
+  double* zl = pv + D + HARD_PCG_GUARD - HARD_PCG_THREADS;   // zl[a], al[a] for a >= 1024 only
+  double* al = zl + ext;
   double* red = sh + hard_pcg_scratch(D, NX);
   int* rlh = reinterpret_cast<int*>(red + 32);   // [D] each row's last entry | first column << 16
   int* wlh = rlh + D;                            // [SLOTS][16 waves] each wave-slot's longest row (last entry)
@@ -497,21 +607,26 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     // blocks equal the oracle's bit for bit.
     // (1) diagonal blocks: Gauss-Jordan on the augmented [M | I] without pivoting (oracle/hard.py _gj_inverse), `cap` blocks
     //     at a time; per pivot p the new pivot row and the old column p are snapshotted first
-    const int cap = hard_pcg_scratch(D, NX) / (B2 + 2 * NX);
-    double* prow = sh + (size_t)cap * B2;
+    //     Staged in the scratch or, where larger, in the cache's tail past the diagonal blocks (the stair
+    //     blocks' place, written only in (2))
+    const int tail = (int)(lds_bytes / sizeof(double)) - hard_pcg_cache_offset(D, NX, SLOTS) - ncd * B2;
+    const bool in_tail = tail > hard_pcg_scratch(D, NX);
+    double* stg = in_tail ? pcache + (size_t)ncd * B2 : sh;
+    const int cap = (in_tail ? tail : hard_pcg_scratch(D, NX)) / (B2 + 2 * NX);
+    double* prow = stg + (size_t)cap * B2;
     double* fcol = prow + (size_t)cap * NX;
     for (int k0 = 0; k0 < nb; k0 += cap) {
       const int kc = min(cap, nb - k0);
       __syncthreads();
       for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
         const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
-        sh[e] = band_at(S, rg, dmax, (k0 + kk) * NX + i, (k0 + kk) * NX + j);
+        stg[e] = band_at(S, rg, dmax, (k0 + kk) * NX + i, (k0 + kk) * NX + j);
       }
       for (int p = 0; p < NX; ++p) {
         __syncthreads();
         for (int e = t; e < kc * NX; e += HARD_PCG_THREADS) {
           const int kk = e / NX, j = e - kk * NX;
-          const double* M = sh + (size_t)kk * B2;
+          const double* M = stg + (size_t)kk * B2;
           const double d = M[p * NX + p];
           prow[e] = (j == p) ? 1.0 / d : M[p * NX + j] / d;
           fcol[e] = M[j * NX + p];
@@ -520,20 +635,20 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
         for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
           const int kk = e / B2, r = (e - kk * B2) / NX, j = e - kk * B2 - r * NX;
           if (r == p) {
-            sh[e] = prow[kk * NX + j];
+            stg[e] = prow[kk * NX + j];
           } else {
             const double f = fcol[kk * NX + r];
-            const double m0 = (j == p) ? 0.0 : sh[e];
-            sh[e] = m0 - f * prow[kk * NX + j];
+            const double m0 = (j == p) ? 0.0 : stg[e];
+            stg[e] = m0 - f * prow[kk * NX + j];
           }
         }
       }
       __syncthreads();
       for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {   // P_kk and its transpose
         const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
-        P[(size_t)(k0 + kk) * B2 + i * NX + j] = sh[e];
-        if (k0 + kk < ncd) pcd[(size_t)(k0 + kk) * B2 + j * NX + i] = sh[e];
-        else PT[(size_t)(k0 + kk) * B2 + j * NX + i] = sh[e];
+        P[(size_t)(k0 + kk) * B2 + i * NX + j] = stg[e];
+        if (k0 + kk < ncd) pcd[hp_off<NX>(k0 + kk, i, j)] = stg[e];
+        else PT[(size_t)(k0 + kk) * B2 + j * NX + i] = stg[e];
       }
     }
     // (2) SS stair blocks (oracle/hard.py _neg_triple, both products summed in index order):
@@ -567,7 +682,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
           const double v = -acc;
           const int pr = odd ? r : c, pc = odd ? c : r;                 // element of P_{k,k-1}
           PL[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
-          if (k - 1 < ncl) pcl[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
+          if (k - 1 < ncl) pcl[hp_off<NX>(k - 1, pr, pc)] = v;
         }
       }
     }
@@ -579,18 +694,22 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     if (precond == PRECOND_J) return (1.0 / band_at(S, rg, dmax, a, a)) * rv[a];
     if (a >= nb * NX) return 0.0;   // rows past the last full block: not preconditioned (PCG.py:182)
     const int k = a / NX, i = a - k * NX;
-    // MT[j NX + i] = P_kk[i][j]; L = P_{k,k-1}; U = P_{k+1,k} (U^T = P_{k,k+1}): LDS copies where cached
-    const double* MT = k < ncd ? pcd + (size_t)k * B2 : PT + (size_t)k * B2;
+    // MT[j NX + i] = P_kk[i][j]; L = P_{k,k-1}; U = P_{k+1,k} (U^T = P_{k,k+1}).  The LDS copy where
+    // cached, else HBM -- in separate branches, so that each read is a ds_read or a global load: one
+    // pointer that may point to either makes every read of the three blocks a flat load
+    const double* rk = rv + k * NX;
     double s = 0.0;
-    for (int j = 0; j < NX; ++j) s += MT[j * NX + i] * rv[k * NX + j];
+    // (LDS copies: P_kk and P_{k+1,k} row-major swizzled, hp_off; HBM: P_kk transposed, Pl row-major)
+    if (k < ncd) s = hp_row_lds<NX>(pcd, k, i, rk, s);
+    else s = hp_col<NX>(glb_ptr(PT + (size_t)k * B2), i, rk, s);
     if (precond == PRECOND_SS) {
       if (k > 0) {
-        const double* L = k - 1 < ncl ? pcl + (size_t)(k - 1) * B2 : PL + (size_t)(k - 1) * B2;
-        for (int j = 0; j < NX; ++j) s += L[i * NX + j] * rv[(k - 1) * NX + j];
+        if (k - 1 < ncl) s = hp_row_lds<NX>(pcl, k - 1, i, rk - NX, s);
+        else s = hp_row<NX>(glb_ptr(PL + (size_t)(k - 1) * B2), i, rk - NX, s);
       }
       if (k + 1 < nb) {
-        const double* U = k < ncl ? pcl + (size_t)k * B2 : PL + (size_t)k * B2;
-        for (int j = 0; j < NX; ++j) s += U[j * NX + i] * rv[(k + 1) * NX + j];
+        if (k < ncl) s = hp_col_lds<NX>(pcl, k, i, rk + NX, s);
+        else s = hp_col<NX>(glb_ptr(PL + (size_t)k * B2), i, rk + NX, s);
       }
     }
     return s;
@@ -603,27 +722,32 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   // wave's longest row the index is clamped and the product dropped.
   auto spmv = [&](int a, bool own, int jmax, int c0hi, bool cached, const double (&vc)[REG])
       -> double {
-    const int hi = c0hi & 0xffff, c0 = c0hi >> 16;
+    const int c0 = c0hi >> 16;
     constexpr int U = 8;
     double s = 0.0;
     const double* Sa = S + (own ? a : 0);
     int j0 = 0;
     if (cached) {
+      // Branch-free, no select: vc is zero past the row (set once), p is finite and the zero guard after
+      // p covers c0 + u past D, so those products are exact zeros, and s + 0 = s bitwise (s starts at +0
+      // and a sum of nonzero terms is never -0 in round-to-nearest): the row's own terms in column order.
+      // (A branch per entry kept one LDS read in flight per wave.)
 #pragma unroll
-      for (int u = 0; u < REG; ++u)
-        if (own && u <= hi) s += vc[u] * pv[c0 + u];
+      for (int u = 0; u < REG; ++u) s = s + vc[u] * pv[c0 + u];
       j0 = REG;
 #if TMPC_HX_NOSTREAM   // timing experiment only (wrong answers): no streamed band entries
       return s;
 #endif
     }
+    // the streamed entries up to the wave's longest row: the band is zero past each row (k_hard_schur
+    // fills it up to that row; tmpc_hard_pcg_batch's host copy is zero there), p clamped into range
     for (int j = j0; j <= jmax; j += U) {
       double v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(j + u, jmax) * dmax];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (own && j + u <= hi) s += v[u] * pv[c0 + j + u];
+        if (j + u <= jmax) s = s + v[u] * pv[min(c0 + j + u, D - 1)];   // wave-uniform test
     }
     return s;
   };
@@ -648,7 +772,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     if (m == 0) {
       const double* Sa = S + (a < D ? a : 0);
 #pragma unroll
-      for (int u = 0; u < REG; ++u) vc[u] = Sa[(size_t)min(u, BW - 1) * dmax];
+      for (int u = 0; u < REG; ++u) vc[u] = (a < D && u <= hi) ? Sa[(size_t)min(u, BW - 1) * dmax] : 0.0;
       if (a < D) {
         const int streamed = max(0, hi + 1 - REG);
         nnz += streamed;
@@ -662,6 +786,8 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     nnz = h_block_sum_db(nnz, red, nsum);
     nnz_reg = h_block_sum_db(nnz_reg, red, nsum);
   }
+  static_assert(hard_pcg_reg_diag(NX, SLOTS) <= HARD_PCG_GUARD, "the guard covers the register entries");
+  for (int e = t; e < HARD_PCG_GUARD; e += HARD_PCG_THREADS) pv[D + e] = 0.0;   // (after the setup's staging)
   double xv[SLOTS];
   const double* g = gam + (size_t)b * dmax;
 #pragma unroll
@@ -672,20 +798,29 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   }
   __syncthreads();
   double part = 0.0;
+  double z0 = 0.0, sp0 = 0.0;   // z and S p of the slot-0 row (the other slots': zl, al in LDS)
 #pragma unroll 1
   for (int m = 0; m < SLOTS; ++m) {
     const int a = t + m * HARD_PCG_THREADS;
     if (a < D) {
       const double z = apply_P(a);
-      zl[a] = z;
+      if (m == 0) z0 = z;
+      else zl[a] = z;
       pv[a] = z;
       part += rv[a] * z;
     }
   }
   double nu = h_block_sum_db(part, red, nsum);
   int it_done = max_iter;
+#if TMPC_HX_STAMPS   // timing experiment: per-phase shader-clock sums of every wave of problem 0
+  unsigned long long hs_[8] = {}, hs_prev_ = __builtin_amdgcn_s_memtime();
+#define HX_STAMP(i_) { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); hs_[i_] += n_ - hs_prev_; hs_prev_ = n_; }
+#else
+#define HX_STAMP(i_)
+#endif
   for (int it = 0; it < max_iter; ++it) {
     __syncthreads();
+    HX_STAMP(0);
     part = 0.0;
 #pragma unroll 1
     for (int m = 0; m < SLOTS; ++m) {
@@ -695,31 +830,39 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       const int jmax = __builtin_amdgcn_readfirstlane(wlh[m * (HARD_PCG_THREADS / 64) + (t >> 6)]);
       const double sp = spmv(a, a < D, jmax, c0hi, m == 0, vc);
       if (a < D) {
-        al[a] = sp;
+        if (m == 0) sp0 = sp;
+        else al[a] = sp;
         part += pv[a] * sp;
       }
     }
+    HX_STAMP(1);
     const double alpha = nu / h_block_sum_db(part, red, nsum);
+    HX_STAMP(2);
 #pragma unroll
     for (int m = 0; m < SLOTS; ++m) {
       const int a = t + m * HARD_PCG_THREADS;
       if (a < D) {
-        rv[a] = rv[a] - al[a] * alpha;
+        rv[a] = rv[a] - (m == 0 ? sp0 : al[a]) * alpha;
         xv[m] = xv[m] + pv[a] * alpha;
       }
     }
+    HX_STAMP(3);
     __syncthreads();
+    HX_STAMP(4);
     part = 0.0;
 #pragma unroll 1
     for (int m = 0; m < SLOTS; ++m) {
       const int a = t + m * HARD_PCG_THREADS;
       if (a < D) {
         const double z = apply_P(a);
-        zl[a] = z;
+        if (m == 0) z0 = z;
+        else zl[a] = z;
         part += rv[a] * z;
       }
     }
+    HX_STAMP(5);
     const double nup = h_block_sum_db(part, red, nsum);
+    HX_STAMP(6);
     if (fabs(nup) < tol) {
       it_done = it + 1;
       break;
@@ -729,10 +872,17 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
 #pragma unroll
     for (int m = 0; m < SLOTS; ++m) {
       const int a = t + m * HARD_PCG_THREADS;
-      if (a < D) pv[a] = zl[a] + pv[a] * beta;
+      if (a < D) pv[a] = (m == 0 ? z0 : zl[a]) + pv[a] * beta;
     }
     nu = nup;
+    HX_STAMP(7);
   }
+#if TMPC_HX_STAMPS
+  if (b == 0 && (t & 63) == 0 && t < D)
+    printf("hx_stamps wave %d it %d D %d: top %llu spmv %llu sum_a %llu upd %llu bar %llu precond %llu sum_nu %llu pupd %llu\n",
+           t >> 6, it_done, D, hs_[0], hs_[1], hs_[2], hs_[3], hs_[4], hs_[5], hs_[6], hs_[7]);
+#endif
+#undef HX_STAMP
 #pragma unroll
   for (int m = 0; m < SLOTS; ++m) {
     const int a = t + m * HARD_PCG_THREADS;
