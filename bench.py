@@ -99,6 +99,10 @@ def parse(argv=None):
                     help="skip the config-4 line the default (headline) run adds after its own measurement")
     ap.add_argument("--secondary-steps", type=int, default=3)
     ap.add_argument("--secondary-parity", type=int, default=64, help="config-4 problems checked against the oracle")
+    ap.add_argument("--no-hard-line", action="store_true",
+                    help="skip the hard-limit line (ACTIVE_SET torque + velocity) after the headline")
+    ap.add_argument("--hard-steps", type=int, default=3)
+    ap.add_argument("--hard-parity", type=int, default=16, help="hard-limit problems checked against the oracle")
     return ap.parse_args(argv)
 
 
@@ -237,6 +241,24 @@ def _cpu_solve_config4(args):
         r = osqp.sqp(m, cost, x, u, N, 0.1, "PCG-SS", {}, SoftConstraints(lims))
     return dict(exit_sqp=int(r["exit_sqp"]), sqp_iter=int(r["sqp_iter"]), exit_soft=int(r["exit_soft"]),
                 outer_iter=int(r["outer_iter"]), pcg_iters=list(r["pcg_iters"]), x=r["x"], u=r["u"])
+
+
+def _cpu_solve_hard(args):
+    """the oracle's solve of one problem under the hard preset torque-velocity-as, in the banded PCG's
+    canonical summation order (oracle/hard.py pcg_canonical; tests/test_gpu_hard.py)"""
+    seed, n, N = args
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import hard as ohard
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    m = parse_urdf(planar_arm_urdf(n))
+    x, u = osqp.initial_problem(m, N, 0.1, seed)
+    cost = osqp.QuadCost(np.eye(2 * n), 100 * np.eye(2 * n), 0.1 * np.eye(n), np.zeros(2 * n))
+    lims = [ohard.HardLimit(k, n, v["lb"], v["ub"], v["mode"]) for k, v in LIMIT_PRESETS["torque-velocity-as"].items()]
+    with np.errstate(all="ignore"):
+        r = osqp.sqp(m, cost, x, u, N, 0.1, "PCG-SS", {}, hard=ohard.HardConstraints(lims), order="canonical")
+    return dict(exit_sqp=int(r["exit_sqp"]), sqp_iter=int(r["sqp_iter"]), pcg_iters=list(r["pcg_iters"]),
+                x=r["x"], u=r["u"])
 
 
 def parity_check(gpu, cpu):
@@ -622,6 +644,9 @@ def main():
     secondary = None
     if headline and not a.no_secondary and n == 6:
         secondary = run_secondary(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0)
+    hard_line = None
+    if headline and not a.no_hard_line and n == 6:
+        hard_line = run_hard_line(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0)
 
     if rank != 0:
         comm.close()
@@ -719,8 +744,80 @@ def main():
     out["problems_gathered"] = int(exit_all.size)
     if secondary is not None:
         out["secondary"] = secondary
+    if hard_line is not None:
+        out["hard_limits"] = hard_line
     print(json.dumps(out))
     comm.close()
+
+
+def run_hard_line(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0):
+    """The headline workload under hard ACTIVE_SET torque + velocity limits (LIMIT_PRESETS
+    "torque-velocity-as": constraint rows in C, the banded Schur path, TrajoptMPCReference.py:238-248),
+    measured after the headline and the secondary, timed as the headline (barrier + synchronize around
+    --hard-steps solves, max over ranks), with k_hard_pcg's roofline and the GPU's exit codes /
+    iterations / per-QP PCG counts against the oracle (canonical order) on the first --hard-parity
+    problems (rank 0)."""
+    import copy
+    nx, nu = 2 * n, n
+    ah = copy.copy(a)
+    ah.limits = "torque-velocity-as"
+    ctx.set_box_limits(LIMIT_PRESETS[ah.limits])
+    xb, ub = B * nx * N * 8, B * nu * (N - 1) * 8
+
+    def step():
+        ctx.d2d(d_x, d_x0, xb)
+        ctx.d2d(d_u, d_u0, ub)
+        ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method)
+
+    step()
+    ctx.synchronize()
+    ctx.set_options(profile=1)
+    ctx.reset_stats()
+    comm.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.hard_steps):
+        step()
+    ctx.synchronize()
+    comm.barrier()
+    elapsed = comm.max(time.perf_counter() - t0)
+    ctx.set_options(profile=0)
+    hard_bytes = ctx.kernel_bytes("hard_pcg")
+    kernels = {}
+    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "hard_schur", "hard_pcg", "dxu", "ls_terms", "ls_decide"]:
+        cnt, ms = ctx.kernel_stats(name)
+        if cnt:
+            kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
+    ctx.d2d(d_x, d_x0, xb)
+    ctx.d2d(d_u, d_u0, ub)
+    exit_codes, iters = ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=True)
+    from trajoptmpcreference_amd import dist
+    dist.gather_summaries(comm, exit_codes=exit_codes.astype(np.int32), iters=iters.astype(np.int32))
+    par = None
+    if rank == 0 and a.hard_parity > 0:
+        S = min(B, a.hard_parity)
+        share, _, _ = host_cores()
+        jobs = [(a.seed0 + i, n, N) for i in range(S)]
+        with mp.get_context("fork").Pool(min(share, S), initializer=os.environ.__setitem__,
+                                          initargs=("OMP_NUM_THREADS", "1")) as pool:
+            res = pool.map(_cpu_solve_hard, jobs, chunksize=1)
+        gr = ctx.sqp_solve_batch(x0_host(ctx, d_x0, B, nx, N)[:S], u0[:S], N, dt, a.method)
+        par = parity_check(gr, res)
+        par["note"] = ("oracle/sqp.py with oracle/hard.py's rows and pcg_canonical, the banded PCG's summation "
+                       "order; the QP-by-QP replay on the GPU's own S is tests/test_gpu_hard.py")
+    ctx.set_box_limits(None)
+    value = B * a.hard_steps * world / elapsed
+    return {"metric": f"MPC solves/sec (arm{n}.urdf, N={N}, SQP {a.method}, hard ACTIVE_SET torque + velocity "
+                      "box limits)",
+            "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.hard_steps, "warmup": 1,
+            "ms_per_step": 1000.0 * elapsed / a.hard_steps, "higher_is_better": True, "scaling": "weak",
+            "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} SQP {a.method}, batch {B} per GPU, limits "
+                                   f"{ah.limits} (torque +-0.5, velocity +-1, ACTIVE_SET)",
+                       "global_batch": B * world},
+            "roofline": hard_roofline(ah, kernels, hard_bytes) if "hard_pcg" in kernels and hard_bytes else None,
+            "kernels": kernels, "parity": par,
+            "lockstep": {"batch_iterations_per_solve": kernels["ls_decide"]["launches"] / a.hard_steps}
+            if "ls_decide" in kernels else None}
 
 
 def run_secondary(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0):

@@ -147,6 +147,16 @@ def test_bench_cpu_baseline_runs_the_oracle_on_a_bounded_sample():
     assert bench.parity_check(gpu, res)["mismatches"] == 1
 
 
+def test_bench_hard_line_oracle_solve():
+    """bench.py's hard-limit line checks the GPU against the oracle's solve under the same preset
+    (ACTIVE_SET torque + velocity rows, canonical-order PCG): a small instance runs and returns the
+    integers parity_check compares."""
+    import bench
+    r = bench._cpu_solve_hard((0, 2, 8))
+    assert r["exit_sqp"] in (1, 2, 3, 4) and len(r["pcg_iters"]) >= r["sqp_iter"]
+    assert r["x"].shape == (4, 8) and r["u"].shape == (2, 7)
+
+
 def test_bench_byte_and_flop_models():
     """b_pcg = 8 (2 (2N-1) nx^2 + 10 N nx) = 354,048 B/iteration and
     f_pcg = 2*3*nx^2*N*2 + 10*N*nx = 118,272 flop/iteration for arm6 N=64."""

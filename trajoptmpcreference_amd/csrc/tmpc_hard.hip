@@ -402,6 +402,10 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
 #ifndef TMPC_HARD_REG
 #define TMPC_HARD_REG 24
 #endif
+// streamed band entries per batch of loads in k_hard_pcg's product
+#ifndef TMPC_HARD_U
+#define TMPC_HARD_U 8
+#endif
 __host__ __device__ constexpr int hard_pcg_reg_diag(int nx, int slots) {
   return (nx <= 4 ? 16 : (nx >= 14 ? TMPC_HARD_REG - 4 : TMPC_HARD_REG)) - (slots >= 3 ? 8 : 0);
 }
@@ -723,10 +727,18 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   auto spmv = [&](int a, bool own, int jmax, int c0hi, bool cached, const double (&vc)[REG])
       -> double {
     const int c0 = c0hi >> 16;
-    constexpr int U = 8;
+    constexpr int U = TMPC_HARD_U;
     double s = 0.0;
     const double* Sa = S + (own ? a : 0);
-    int j0 = 0;
+    // The streamed entries (past the register-held ones, up to the wave's longest row; the band is zero
+    // past each row: k_hard_schur fills it up to that row, tmpc_hard_pcg_batch's host copy is zero there)
+    // in batches of U; the first batch's loads are in flight while the register-held entries are added.  p is clamped into range (a zero entry times a finite p).
+    int j = cached ? REG : 0;
+    double v[U];
+    if (j <= jmax) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(j + u, jmax) * dmax];
+    }
     if (cached) {
       // Branch-free, no select: vc is zero past the row (set once), p is finite and the zero guard after
       // p covers c0 + u past D, so those products are exact zeros, and s + 0 = s bitwise (s starts at +0
@@ -734,20 +746,19 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       // (A branch per entry kept one LDS read in flight per wave.)
 #pragma unroll
       for (int u = 0; u < REG; ++u) s = s + vc[u] * pv[c0 + u];
-      j0 = REG;
 #if TMPC_HX_NOSTREAM   // timing experiment only (wrong answers): no streamed band entries
       return s;
 #endif
     }
-    // the streamed entries up to the wave's longest row: the band is zero past each row (k_hard_schur
-    // fills it up to that row; tmpc_hard_pcg_batch's host copy is zero there), p clamped into range
-    for (int j = j0; j <= jmax; j += U) {
-      double v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(j + u, jmax) * dmax];
+    while (j <= jmax) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (j + u <= jmax) s = s + v[u] * pv[min(c0 + j + u, D - 1)];   // wave-uniform test
+      j += U;
+      if (j <= jmax) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = Sa[(size_t)min(j + u, jmax) * dmax];
+      }
     }
     return s;
   };
