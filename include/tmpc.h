@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 8   /* 8: tmpc_qp_blocks_batch; 7: tmpc_kernel_bytes */
+#define TMPC_ABI_VERSION 9   /* 9: tmpc_pcg_dense_batch; 8: tmpc_qp_blocks_batch; 7: tmpc_kernel_bytes */
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
@@ -327,6 +327,21 @@ int tmpc_pcg_batch(tmpc_ctx* ctx, int B, int N, int nx, int precond, const doubl
                    const double* S_up, const double* gamma, const double* guess, double tol, int max_iter,
                    double* lambda, int32_t* iters, double* trace_nu, double* trace_res, double* P_diag);
 
+/* PCG.pcg(A, b, Pinv, guess, options) (GBD-PCG-Python/PCG.py:66-111) on B dense systems with ANY
+ * preconditioner matrix: A [B][D][D], b [B][D], Pinv [B][D][D] (row-major; replaces the reference's
+ * dense Pinv argument).  Pinv = NULL: PCG.solve's own preconditioner (compute_preconditioner,
+ * PCG.py:113-212) is built on the device from A -- precond TMPC_PRECOND_* with block size nx (1..16;
+ * the floor(D / nx) nx-aligned blocks from row 0, rows past the last full block unpreconditioned).
+ * guess [B][D] the initial iterate (nullable = zeros).  Outputs: x [B][D], iters [B], trace_nu /
+ * trace_res [B][max_iter+1] (|nu| and ||b - A x|| per iteration as PCG.py:82-95, nullable: without
+ * trace_res the explicit residual's extra product is skipped), Pinv_out [B][D][D] (nullable: the
+ * preconditioner matrix the solve used).  1 <= D <= 4096: no block-tridiagonal structure is assumed,
+ * the arbitrary-Pinv and the past-1024-row forms of the reference's PCG class.  Summation order:
+ * oracle/dense.py (bitwise reproducible on the CPU). */
+int tmpc_pcg_dense_batch(tmpc_ctx* ctx, int B, int D, const double* A, const double* b, const double* Pinv,
+                         int precond, int nx, const double* guess, double tol, int max_iter, double* x,
+                         int32_t* iters, double* trace_nu, double* trace_res, double* Pinv_out);
+
 /* ---- device memory / timing helpers (the bench keeps inputs resident in HBM) ---- */
 int tmpc_device_alloc(tmpc_ctx* ctx, size_t bytes, void** ptr);
 int tmpc_device_free(tmpc_ctx* ctx, void* ptr);
@@ -338,7 +353,8 @@ int tmpc_synchronize(tmpc_ctx* ctx);
 /* Kernel timing collected with HIP events on the context stream when options.profile = 1.
  * name: "qp_fd", "qp_minv", "qp_grad", "ginv", "qp" (the fused Schur + PCG + dxu kernel), "schur",
  * "btsolve", "dxu", "ls_terms", "ls_decide", "hard_schur", "hard_pcg" (also tmpc_hard_pcg_batch),
- * "hard_direct", "ilqr_backward", "ilqr_forward", "ilqr_decide", "mpc_shift", "pcg" (tmpc_pcg_batch). */
+ * "hard_direct", "ilqr_backward", "ilqr_forward", "ilqr_decide", "mpc_shift", "pcg" (tmpc_pcg_batch),
+ * "pcg_dense" (tmpc_pcg_dense_batch: transposes, preconditioner build and PCG). */
 int tmpc_kernel_stats(tmpc_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
 /* Bytes a counting kernel reads and writes beyond its registers and LDS (its algorithmic memory traffic,
  * served by L2 / Infinity Cache / HBM), summed over its launches since the last

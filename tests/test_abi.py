@@ -37,7 +37,7 @@ def test_binding_matches_header():
     from trajoptmpcreference_amd import _native
     assert sorted(_native.SIGNATURES) == header_functions()
     lib = _native.load_library()
-    assert lib.tmpc_abi_version() == 8
+    assert lib.tmpc_abi_version() == 9
 
 
 def test_options_struct_layout_and_defaults():

@@ -104,6 +104,8 @@ SIGNATURES = {
                                       C.c_double, C.c_int, _dp, _ip]),
     "tmpc_pcg_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, C.c_double,
                                  C.c_int, _dp, _ip, _dp, _dp, _dp]),
+    "tmpc_pcg_dense_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _dp, _dp, _dp, C.c_int, C.c_int, _dp,
+                                       C.c_double, C.c_int, _dp, _ip, _dp, _dp, _dp]),
     "tmpc_device_alloc": (C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     "tmpc_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "tmpc_memcpy_h2d": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
@@ -486,6 +488,30 @@ class Context:
                                             _ptr(gamma), _ptr(guess), float(tol), int(max_iter), _ptr(lam), _ptr(it),
                                             _ptr(tn), _ptr(tr), _ptr(Pd)), "tmpc_pcg_batch")
         return lam, it, tn, tr, Pd
+
+    def pcg_dense_batch(self, A, b, Pinv=None, precond="SS", nx=1, guess=None, tol=1e-6, max_iter=100, trace=True,
+                        want_pinv=False):
+        """tmpc_pcg_dense_batch: PCG.pcg on dense systems A [B][D][D], b [B][D] with the preconditioner matrix
+        Pinv [B][D][D] (None: PCG.solve's block preconditioner `precond` of block size nx, built on the
+        device).  Returns x [B][D], iters [B], trace_nu, trace_res ([B][max_iter+1] or None) and the
+        preconditioner matrix used (want_pinv, else None)."""
+        A, b = _c64(A), _c64(b)
+        B, D = b.shape
+        if A.shape != (B, D, D):
+            raise ValueError(f"A must be [B][D][D] = {(B, D, D)}, got {A.shape}")
+        Pinv = _c64(Pinv) if Pinv is not None else None
+        if Pinv is not None and Pinv.shape != (B, D, D):
+            raise ValueError(f"Pinv must be [B][D][D] = {(B, D, D)}, got {Pinv.shape}")
+        guess = _c64(guess) if guess is not None else None
+        x = np.zeros((B, D))
+        it = np.zeros(B, dtype=np.int32)
+        tn = np.full((B, max_iter + 1), np.nan) if trace else None
+        tr = np.full((B, max_iter + 1), np.nan) if trace else None
+        Po = np.zeros((B, D, D)) if want_pinv else None
+        self._check(self.lib.tmpc_pcg_dense_batch(self.h, B, D, _ptr(A), _ptr(b), _ptr(Pinv), PRECOND[precond],
+                                                  int(nx), _ptr(guess), float(tol), int(max_iter), _ptr(x), _ptr(it),
+                                                  _ptr(tn), _ptr(tr), _ptr(Po)), "tmpc_pcg_dense_batch")
+        return x, it, tn, tr, Po
 
     # ---------------------------------------------------------------- device memory (bench)
     def alloc(self, nbytes):

@@ -944,6 +944,7 @@ int tmpc_create(int device, tmpc_ctx** out) {
   }
   pcg_set_max_lds();
   hard_set_max_lds();
+  dense_set_max_lds();
   qp_blocks_set_max_lds();
   tmpc_default_options(&ctx->opts);
   *out = ctx;
@@ -1844,6 +1845,79 @@ int tmpc_pcg_batch(tmpc_ctx* ctx, int B, int N, int nx, int precond, const doubl
   if (trace_res) HIP_OK(hipMemcpy(trace_res, p_tr, sizeof(double) * B * (max_iter + 1), hipMemcpyDeviceToHost));
   if (P_diag && precond != PRECOND_J)
     HIP_OK(hipMemcpy(P_diag, p_Pd, sizeof(double) * B * N * nx * nx, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tmpc_pcg_dense_batch(tmpc_ctx* ctx, int B, int D, const double* A, const double* b, const double* Pinv,
+                         int precond, int nx, const double* guess, double tol, int max_iter, double* x,
+                         int32_t* iters, double* trace_nu, double* trace_res, double* Pinv_out) {
+  if (!ctx) return -1;
+  if (B < 1 || D < 1 || D > HARD_PCG_MAX_ROWS)
+    return fail(ctx, "bad sizes B=%d D=%d (the dense PCG takes 1 <= D <= %d)", B, D, HARD_PCG_MAX_ROWS);
+  if (!A || !b) return fail(ctx, "null input");
+  if (max_iter < 0) return fail(ctx, "max_iter must be >= 0");
+  if (!Pinv) {
+    if (precond != PRECOND_J && precond != PRECOND_BJ && precond != PRECOND_SS && precond != PRECOND_NONE)
+      return fail(ctx, "preconditioner %d: valid are J=1, BJ=2, SS=3, 0=4 (PCG.py:52-55)", precond);
+    if ((precond == PRECOND_BJ || precond == PRECOND_SS) && (nx < 1 || nx > 16))
+      return fail(ctx, "block size %d: the device preconditioner takes 1..16", nx);
+  }
+  hipSetDevice(ctx->device);
+  const size_t DD = (size_t)B * D * D;
+  BUF(double, dn_stage, DD);
+  BUF(double, dn_AT, DD);
+  BUF(double, dn_PT, DD);
+  BUF(double, dn_b, (size_t)B * D);
+  BUF(double, dn_x0, (size_t)B * D);
+  BUF(double, dn_x, (size_t)B * D);
+  BUF(int, dn_it, (size_t)B);
+  BUF(double, dn_tn, (size_t)B * (max_iter + 1));
+  BUF(double, dn_tr, (size_t)B * (max_iter + 1));
+  const int nbk = (!Pinv && (precond == PRECOND_BJ || precond == PRECOND_SS)) ? D / nx : 0;
+  BUF(double, dn_Pd, (size_t)B * (nbk + 1) * (nx > 0 ? nx * nx : 1));
+  DenseArgs a{};
+  a.B = B;
+  a.D = D;
+  a.nx = nx;
+  a.precond = precond;
+  a.max_iter = max_iter;
+  a.tol = tol;
+  a.A = dn_stage;
+  a.b = dn_b;
+  a.guess = guess ? dn_x0 : nullptr;
+  a.AT = dn_AT;
+  a.PT = dn_PT;
+  a.Pd = dn_Pd;
+  a.x = dn_x;
+  a.iters = dn_it;
+  a.trace_nu = trace_nu ? dn_tn : nullptr;
+  a.trace_res = trace_res ? dn_tr : nullptr;
+  HIP_OK(hipMemcpyAsync(dn_stage, A, sizeof(double) * DD, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(dn_b, b, sizeof(double) * B * D, hipMemcpyHostToDevice, ctx->stream));
+  if (guess) HIP_OK(hipMemcpyAsync(dn_x0, guess, sizeof(double) * B * D, hipMemcpyHostToDevice, ctx->stream));
+  {
+    Timed t(ctx, "pcg_dense");
+    LAUNCH_OK(launch_dense_transpose(ctx->stream, B, D, dn_stage, dn_AT));
+    if (Pinv) {
+      HIP_OK(hipMemcpyAsync(dn_stage, Pinv, sizeof(double) * DD, hipMemcpyHostToDevice, ctx->stream));
+      LAUNCH_OK(launch_dense_transpose(ctx->stream, B, D, dn_stage, dn_PT));
+    } else {
+      HIP_OK(hipMemsetAsync(dn_PT, 0, sizeof(double) * DD, ctx->stream));
+      LAUNCH_OK(launch_dense_precond(ctx->stream, a));   // reads A row-major from the stage
+    }
+    LAUNCH_OK(launch_pcg_dense(ctx->stream, a));
+  }
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  resolve_timings(ctx);
+  if (x) HIP_OK(hipMemcpy(x, dn_x, sizeof(double) * B * D, hipMemcpyDeviceToHost));
+  if (iters) HIP_OK(hipMemcpy(iters, dn_it, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (trace_nu) HIP_OK(hipMemcpy(trace_nu, dn_tn, sizeof(double) * B * (max_iter + 1), hipMemcpyDeviceToHost));
+  if (trace_res) HIP_OK(hipMemcpy(trace_res, dn_tr, sizeof(double) * B * (max_iter + 1), hipMemcpyDeviceToHost));
+  if (Pinv_out) {   // Pinv = PT^T: back through the transpose, into the stage
+    LAUNCH_OK(launch_dense_transpose(ctx->stream, B, D, dn_PT, dn_stage));
+    HIP_OK(hipMemcpyAsync(Pinv_out, dn_stage, sizeof(double) * DD, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+  }
   return 0;
 }
 

@@ -1214,3 +1214,294 @@ int hard_set_max_lds() {
 }
 
 }  // namespace tmpc
+
+// ============================================================== dense PCG (tmpc_pcg_dense_batch)
+// PCG.pcg(A, b, Pinv, guess, options) (GBD-PCG-Python/PCG.py:66-111) with any dense A and preconditioner
+// matrix Pinv -- the caller's, or PCG.solve's block preconditioner (compute_preconditioner, PCG.py:113-212)
+// built here from A -- for dimensions up to HARD_PCG_MAX_ROWS.  Operation order: oracle/dense.py (every
+// matrix-vector product sequential over the columns, the dot products of k_hard_pcg).
+namespace tmpc {
+
+// out[b][c][r] = in[b][r][c] (D x D per system): the PCG reads column c of A and Pinv as one coalesced row
+__global__ void __launch_bounds__(256) k_dense_transpose(int D, const double* __restrict__ in, double* __restrict__ out) {
+  __shared__ double tile[32][33];
+  const size_t off = (size_t)blockIdx.z * D * D;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + threadIdx.x;
+    if (r < D && c < D) tile[i][threadIdx.x] = in[off + (size_t)r * D + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + threadIdx.x;
+    if (r < D && c < D) out[off + (size_t)c * D + r] = tile[threadIdx.x][i];
+  }
+}
+
+// '0' / J: the diagonal of Pinv (PT is zero-filled before)
+__global__ void __launch_bounds__(256) k_dense_diag(int D, int precond, const double* __restrict__ A, double* __restrict__ PT) {
+  const size_t off = (size_t)blockIdx.x * D * D;
+  for (int a = threadIdx.x; a < D; a += blockDim.x)
+    PT[off + (size_t)a * D + a] = precond == PRECOND_J ? 1.0 / A[off + (size_t)a * D + a] : 1.0;
+}
+
+// BJ / SS diagonal blocks: Gauss-Jordan on the augmented [A_kk | I] without pivoting, the operation
+// sequence of k_hard_pcg's setup (oracle/hard.py _gj_inverse); one 64-thread workgroup per (block, system).
+// Pd [B][nb][NX][NX] row-major; PT[(k NX + j) D + k NX + i] = (P_kk)_ij.
+template <int NX>
+__global__ void __launch_bounds__(64) k_dense_gj(int D, int nb, const double* __restrict__ A, double* __restrict__ Pd,
+                                                 double* __restrict__ PT) {
+  constexpr int B2 = NX * NX;
+  __shared__ double M[B2], prow[NX], fcol[NX];
+  const int k = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const size_t off = (size_t)b * D * D;
+  for (int e = t; e < B2; e += 64) M[e] = A[off + (size_t)(k * NX + e / NX) * D + k * NX + e % NX];
+  for (int p = 0; p < NX; ++p) {
+    __syncthreads();
+    for (int j = t; j < NX; j += 64) {
+      const double d = M[p * NX + p];
+      prow[j] = (j == p) ? 1.0 / d : M[p * NX + j] / d;
+      fcol[j] = M[j * NX + p];
+    }
+    __syncthreads();
+    for (int e = t; e < B2; e += 64) {
+      const int r = e / NX, j = e - r * NX;
+      if (r == p) {
+        M[e] = prow[j];
+      } else {
+        const double f = fcol[r];
+        const double m0 = (j == p) ? 0.0 : M[e];
+        M[e] = m0 - f * prow[j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < B2; e += 64) {
+    const int i = e / NX, j = e - i * NX;
+    Pd[((size_t)b * nb + k) * B2 + e] = M[e];
+    PT[off + (size_t)(k * NX + j) * D + k * NX + i] = M[e];
+  }
+}
+
+// SS stair blocks (k_hard_pcg's setup (2), oracle/hard.py _neg_triple): odd k: P_{k,k-1} = -P_kk (S_{k,k-1}
+// P_{k-1,k-1}); even k: P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k} P_kk); each mirrored by its transpose.  One
+// workgroup per (k - 1, system).
+template <int NX>
+__global__ void __launch_bounds__(256) k_dense_stair(int D, int nb, const double* __restrict__ A,
+                                                     const double* __restrict__ Pd, double* __restrict__ PT) {
+  constexpr int B2 = NX * NX;
+  __shared__ double yz[B2];
+  const int k = blockIdx.x + 1, b = blockIdx.y, t = threadIdx.x;
+  const size_t off = (size_t)b * D * D;
+  const bool odd = k & 1;
+  const int yr = odd ? k : k - 1, yc = odd ? k - 1 : k;   // Y = S_{yr, yc}
+  const double* Z = Pd + ((size_t)b * nb + (odd ? k - 1 : k)) * B2;
+  const double* X = Pd + ((size_t)b * nb + (odd ? k : k - 1)) * B2;
+  for (int e = t; e < B2; e += blockDim.x) {
+    const int r = e / NX, c = e - r * NX;
+    double s = 0.0;
+    for (int l = 0; l < NX; ++l) s += A[off + (size_t)(yr * NX + r) * D + yc * NX + l] * Z[l * NX + c];
+    yz[e] = s;
+  }
+  __syncthreads();
+  for (int e = t; e < B2; e += blockDim.x) {
+    const int r = e / NX, c = e - r * NX;
+    double acc = 0.0;
+    for (int m = 0; m < NX; ++m) acc += X[r * NX + m] * yz[m * NX + c];
+    const double v = -acc;
+    const int pr = odd ? r : c, pc = odd ? c : r;   // element (pr, pc) of P_{k,k-1}
+    PT[off + (size_t)((k - 1) * NX + pc) * D + k * NX + pr] = v;   // Pinv[k NX + pr][(k-1) NX + pc]
+    PT[off + (size_t)(k * NX + pr) * D + (k - 1) * NX + pc] = v;   // its mirror P_{k-1,k}
+  }
+}
+
+// The PCG: one 1024-thread workgroup per system, row a on thread a mod 1024 (slot a / 1024); p, r, x of
+// every row in LDS (the products read them all), each thread's own rows' r, x, p, z, A p in registers.
+// Column c of A / Pinv (AT / PT rows) is one coalesced read per wave, p / r / x[c] an LDS broadcast.
+template <int SLOTS>
+__global__ void __launch_bounds__(HARD_PCG_THREADS) k_pcg_dense(int D, const double* __restrict__ AT,
+                                                               const double* __restrict__ PT,
+                                                               const double* __restrict__ bv,
+                                                               const double* __restrict__ guess, double tol,
+                                                               int max_iter, double* __restrict__ xo,
+                                                               int* __restrict__ iters, double* __restrict__ tnu,
+                                                               double* __restrict__ tres) {
+  constexpr int T = HARD_PCG_THREADS;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const size_t DD = (size_t)D * D;
+  const double* A = AT + b * DD;
+  const double* P = PT + b * DD;
+  const double* bb = bv + (size_t)b * D;
+  extern __shared__ __align__(16) double sh[];
+  double* pv = sh;
+  double* rv = pv + D;
+  double* xl = rv + D;
+  double* red = xl + D;   // 2 x 16 reduction slots
+  int nsum = 0;
+  const int W = max_iter + 1;
+  // y = M v for this thread's rows, sequential over the columns (rows past D read a clamped, in-range
+  // entry and are never used)
+  auto mv = [&](const double* M, const double* v, double (&y)[SLOTS]) {
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m) y[m] = 0.0;
+    constexpr int UNR = SLOTS >= 3 ? 2 : 4;   // (4 x 4 slots of loads in flight spilled)
+#pragma unroll UNR
+    for (int c = 0; c < D; ++c) {
+      const double vc = v[c];
+      const double* col = M + (size_t)c * D;
+#pragma unroll
+      for (int m = 0; m < SLOTS; ++m) y[m] = y[m] + col[min(t + m * T, D - 1)] * vc;
+    }
+  };
+  double xr[SLOTS], rr[SLOTS], pr[SLOTS], y[SLOTS];
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * T;
+    xr[m] = (guess && a < D) ? guess[(size_t)b * D + a] : 0.0;
+    if (a < D) xl[a] = xr[m];
+  }
+  __syncthreads();
+  mv(A, xl, y);
+  double part = 0.0;
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * T;
+    rr[m] = a < D ? bb[a] - y[m] : 0.0;
+    if (a < D) {
+      rv[a] = rr[m];
+      part = part + rr[m] * rr[m];
+    }
+  }
+  const double res0 = h_block_sum_db(part, red, nsum);   // (its barrier also publishes r)
+  if (t == 0 && tres) tres[(size_t)b * W] = sqrt(res0);
+  mv(P, rv, y);
+  part = 0.0;
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * T;
+    pr[m] = y[m];
+    if (a < D) {
+      pv[a] = pr[m];
+      part = part + rr[m] * y[m];
+    }
+  }
+  double nu = h_block_sum_db(part, red, nsum);
+  if (t == 0 && tnu) tnu[(size_t)b * W] = fabs(nu);
+  int it_done = max_iter;
+  for (int it = 0; it < max_iter; ++it) {
+    __syncthreads();   // p published
+    mv(A, pv, y);      // A p
+    part = 0.0;
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m)
+      if (t + m * T < D) part = part + pr[m] * y[m];
+    const double alpha = nu / h_block_sum_db(part, red, nsum);
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m) {
+      const int a = t + m * T;
+      rr[m] = rr[m] - y[m] * alpha;
+      xr[m] = xr[m] + pr[m] * alpha;
+      if (a < D) {
+        rv[a] = rr[m];
+        xl[a] = xr[m];
+      }
+    }
+    __syncthreads();   // r, x published
+    mv(P, rv, y);      // z = Pinv r
+    part = 0.0;
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m)
+      if (t + m * T < D) part = part + rr[m] * y[m];
+    const double nup = h_block_sum_db(part, red, nsum);
+    if (tres) {        // ||b - A x|| of the explicit residual (PCG.py:95)
+      double q[SLOTS];
+      mv(A, xl, q);
+      double pq = 0.0;
+#pragma unroll
+      for (int m = 0; m < SLOTS; ++m) {
+        const int a = t + m * T;
+        if (a < D) {
+          const double e = bb[a] - q[m];
+          pq = pq + e * e;
+        }
+      }
+      const double rs = h_block_sum_db(pq, red, nsum);
+      if (t == 0) tres[(size_t)b * W + it + 1] = sqrt(rs);
+    }
+    if (t == 0 && tnu) tnu[(size_t)b * W + it + 1] = fabs(nup);
+    if (fabs(nup) < tol) {
+      it_done = it + 1;
+      break;
+    }
+    const double beta = nup / nu;
+#pragma unroll
+    for (int m = 0; m < SLOTS; ++m) {
+      const int a = t + m * T;
+      pr[m] = y[m] + pr[m] * beta;
+      if (a < D) pv[a] = pr[m];
+    }
+    nu = nup;
+  }
+#pragma unroll
+  for (int m = 0; m < SLOTS; ++m) {
+    const int a = t + m * T;
+    if (a < D) xo[(size_t)b * D + a] = xr[m];
+  }
+  if (t == 0) iters[b] = it_done;
+}
+
+static size_t pcg_dense_lds(int D) { return ((size_t)3 * D + 32) * sizeof(double); }
+
+template <int NX>
+static void dense_blocks(hipStream_t s, const DenseArgs& a, int nb) {
+  hipLaunchKernelGGL((k_dense_gj<NX>), dim3(nb, a.B), dim3(64), 0, s, a.D, nb, a.A, a.Pd, a.PT);
+  if (a.precond == PRECOND_SS && nb > 1)
+    hipLaunchKernelGGL((k_dense_stair<NX>), dim3(nb - 1, a.B), dim3(256), 0, s, a.D, nb, a.A, a.Pd, a.PT);
+}
+
+int launch_dense_precond(hipStream_t s, const DenseArgs& a) {
+  if (a.precond == PRECOND_NONE || a.precond == PRECOND_J) {
+    hipLaunchKernelGGL(k_dense_diag, dim3(a.B), dim3(256), 0, s, a.D, a.precond, a.A, a.PT);
+    return 0;
+  }
+  const int nb = a.D / a.nx;
+  if (nb < 1) return 0;   // no full block: no row is preconditioned (PCG.py:182)
+  switch (a.nx) {
+#define DB(V) case V: dense_blocks<V>(s, a, nb); break;
+    DB(1) DB(2) DB(3) DB(4) DB(5) DB(6) DB(7) DB(8) DB(9) DB(10) DB(11) DB(12) DB(13) DB(14) DB(15) DB(16)
+#undef DB
+    default: return -2;
+  }
+  return 0;
+}
+
+int launch_dense_transpose(hipStream_t s, int B, int D, const double* in, double* out) {
+  hipLaunchKernelGGL(k_dense_transpose, dim3((D + 31) / 32, (D + 31) / 32, B), dim3(32, 8), 0, s, D, in, out);
+  return 0;
+}
+
+int launch_pcg_dense(hipStream_t s, const DenseArgs& a) {
+  const int slots = (a.D + HARD_PCG_THREADS - 1) / HARD_PCG_THREADS;
+  const size_t lds = pcg_dense_lds(a.D);
+#define PD(SL) hipLaunchKernelGGL((k_pcg_dense<SL>), dim3(a.B), dim3(HARD_PCG_THREADS), lds, s, a.D, a.AT, a.PT, a.b, \
+                                  a.guess, a.tol, a.max_iter, a.x, a.iters, a.trace_nu, a.trace_res)
+  if (slots <= 1) PD(1);
+  else if (slots <= 2) PD(2);
+  else if (slots <= 3) PD(3);
+  else if (slots <= 4) PD(4);
+  else return -2;
+#undef PD
+  return 0;
+}
+
+int dense_set_max_lds() {
+  const int bytes = (int)pcg_dense_lds(HARD_PCG_MAX_ROWS);
+  int err = 0;
+  err |= (int)hipFuncSetAttribute((const void*)k_pcg_dense<1>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  err |= (int)hipFuncSetAttribute((const void*)k_pcg_dense<2>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  err |= (int)hipFuncSetAttribute((const void*)k_pcg_dense<3>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  err |= (int)hipFuncSetAttribute((const void*)k_pcg_dense<4>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  return err;
+}
+
+}  // namespace tmpc

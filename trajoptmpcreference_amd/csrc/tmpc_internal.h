@@ -201,4 +201,19 @@ constexpr int HARD_PCG_LDS_BYTES = 160 * 1024;   // all of a CU's LDS: vectors +
 int launch_hard(hipStream_t s, int nj, const HardArgs& h);
 int hard_set_max_lds();
 
+// the dense PCG of tmpc_pcg_dense_batch (tmpc_hard.hip): PCG.pcg with any A / Pinv, D <= HARD_PCG_MAX_ROWS.
+// A row-major [B][D][D] (the preconditioner builders read it), AT / PT column-major (A^T, Pinv^T: the PCG
+// reads columns), Pd [B][D / nx][nx][nx] the builders' diagonal blocks
+struct DenseArgs {
+  int B, D, nx, precond, max_iter;
+  double tol;
+  const double *A, *b, *guess;
+  double *AT, *PT, *Pd, *x, *trace_nu, *trace_res;
+  int* iters;
+};
+int launch_dense_transpose(hipStream_t s, int B, int D, const double* in, double* out);
+int launch_dense_precond(hipStream_t s, const DenseArgs& a);
+int launch_pcg_dense(hipStream_t s, const DenseArgs& a);
+int dense_set_max_lds();
+
 }  // namespace tmpc

@@ -4,10 +4,12 @@ the GPU.
 Same constructor and ``solve()`` contract: ``PCG(A, b, block_size, Nblocks,
 guess=None, options={}).solve()`` returns ``(x, (trace_nu, trace_res))`` with
 x a column vector, trace_nu = |rho_k| per iteration (PCG.py:82,94,110) and
-trace_res = ||b - A x_k|| (:83,95).  A must be block-tridiagonal with blocks of
-``block_size`` (the Schur complement of the trajectory KKT system); the blocks
-are extracted at this boundary and the solve runs in libtmpc's one-workgroup-
-per-system kernel.  Invalid options raise ValueError instead of exit().
+trace_res = ||b - A x_k|| (:83,95).  A block-tridiagonal A of at most 1024 rows
+(the Schur complement of the trajectory KKT system) runs in libtmpc's fused
+one-workgroup-per-system kernel on its blocks; any other A, and
+``pcg(A, b, Pinv, guess, options)`` with any preconditioner matrix, run the
+dense device PCG (tmpc_pcg_dense_batch, up to 4096 rows).  Invalid options
+raise ValueError instead of exit().
 """
 import numpy as np
 
@@ -15,6 +17,8 @@ from . import _native
 from ._options import NO_OPTIONS, fresh
 
 VALID_PRECONDITIONERS = ("0", "J", "BJ", "SS")
+FUSED_MAX_ROWS = 1024   # tmpc_pcg_batch: one row of S per lane of one workgroup
+DENSE_MAX_ROWS = 4096   # tmpc_pcg_dense_batch (HARD_PCG_MAX_ROWS)
 
 
 def extract_blocks(A, block_size):
@@ -90,7 +94,17 @@ class PCG:
         self.options["RETURN_TRACE"] = mode
 
     def _run(self, A, b, guess, options):
-        Dg, Lo, Up = extract_blocks(A, self.block_size)
+        """PCG.solve: the fused block-tridiagonal kernel (tmpc_pcg_batch) where A is block-tridiagonal with
+        at most 1024 rows, else the dense PCG with the block preconditioner built on the device
+        (tmpc_pcg_dense_batch, up to 4096 rows)."""
+        A = np.asarray(A, dtype=np.float64)
+        n = A.shape[0]
+        if n > FUSED_MAX_ROWS or A.shape != (n, n) or n % self.block_size:
+            return self._run_dense(A, b, None, guess, options)
+        try:
+            Dg, Lo, Up = extract_blocks(A, self.block_size)
+        except ValueError:
+            return self._run_dense(A, b, None, guess, options)
         b = np.asarray(b, dtype=np.float64).reshape(1, -1)
         if guess is not None:
             g = np.asarray(guess, dtype=np.float64).reshape(1, -1)
@@ -106,55 +120,67 @@ class PCG:
         trace2 = [float(v) for v in tr[0, :n_it + 1]]
         return lam[0].reshape(-1, 1), (trace, trace2), Pd[0]
 
+    def _run_dense(self, A, b, Pinv, guess, options):
+        """PCG.pcg on the dense A with the preconditioner matrix Pinv (None: options['preconditioner_type']
+        with this object's block size, built on the device) -- tmpc_pcg_dense_batch."""
+        A = np.asarray(A, dtype=np.float64)
+        n = A.shape[0]
+        if A.shape != (n, n):
+            raise ValueError(f"A must be square, got {A.shape}")
+        if n > DENSE_MAX_ROWS:
+            raise NotImplementedError(f"PCG: {n} rows exceed the device PCG's {DENSE_MAX_ROWS}")
+        b = np.asarray(b, dtype=np.float64).reshape(1, -1)
+        g = None
+        if guess is not None:
+            g = np.asarray(guess, dtype=np.float64).reshape(1, -1)
+            g = g if np.any(g != 0) else None
+        if Pinv is not None:
+            Pinv = np.asarray(Pinv, dtype=np.float64)
+            if Pinv.shape != (n, n):
+                raise ValueError(f"Pinv must be {(n, n)}, got {Pinv.shape}")
+            Pinv = Pinv[None]
+        max_iter = int(options["max_iter"])
+        ctx = _native.default_context(self.device)
+        x, it, tn, tr, _ = ctx.pcg_dense_batch(A[None], b, Pinv, precond=options["preconditioner_type"],
+                                               nx=self.block_size, guess=g, tol=float(options["exit_tolerance"]),
+                                               max_iter=max_iter)
+        n_it = int(it[0])
+        self.iterations = n_it
+        trace = [float(v) for v in tn[0, :n_it + 1]]
+        trace2 = [float(v) for v in tr[0, :n_it + 1]]
+        return x[0].reshape(-1, 1), (trace, trace2), None
+
     def solve(self):
         """PCG.solve (PCG.py:214-215): pcg(A, b, Pinv, guess, options) with this object's preconditioner."""
         x, traces, self._Pd = self._run(self.A, self.b, self.guess, self.options)
         return x, traces
 
     def pcg(self, A, b, Pinv, guess, options=NO_OPTIONS):
-        """PCG.pcg (PCG.py:66-111).  The GPU applies the preconditioner of options['preconditioner_type']
-        from A's blocks; Pinv must be that preconditioner (compute_preconditioner(A, block_size, type),
-        to 1e-10 relative) -- an arbitrary dense Pinv has no device path and raises."""
+        """PCG.pcg (PCG.py:66-111) with the caller's preconditioner matrix, whatever it is: z = Pinv r on
+        the device (tmpc_pcg_dense_batch, up to 4096 rows)."""
         options = fresh(options)
         self.set_default_options(options)
-        want = self.compute_preconditioner(A, self.block_size, options["preconditioner_type"])
-        Pinv = np.asarray(Pinv, dtype=np.float64)
-        if Pinv.shape != want.shape or not np.allclose(Pinv, want, rtol=1e-10, atol=1e-300):
-            raise NotImplementedError("PCG.pcg: Pinv is not the block preconditioner of type "
-                                      f"{options['preconditioner_type']!r} of A (the GPU builds it from A's blocks)")
-        x, traces, _ = self._run(A, b, guess, options)
+        x, traces, _ = self._run_dense(A, b, Pinv, guess, options)
         return x, traces
 
     def compute_preconditioner(self, A, block_size, preconditioner_type):
         """PCG.compute_preconditioner (PCG.py:113-212) as a dense matrix: '0' identity, J diag(A)^-1, BJ the
-        diagonal block inverses, SS the symmetric stair (odd block rows carry -P_k A_k,k+-1 P_k+-1, mirrored
-        to the even ones).  The block inverses come from the GPU's Gauss-Jordan (the solver's own P)."""
+        inverses of the floor(n / block_size) diagonal blocks, SS the symmetric stair (odd block rows carry
+        -P_k A_k,k+-1 P_k+-1, mirrored to the even ones) -- built on the device from A (the dense PCG's
+        builder, k_dense_gj / k_dense_stair), any A up to 4096 rows."""
         self.validate_precon_type(preconditioner_type)
         A = np.asarray(A, dtype=np.float64)
-        b = int(block_size)
+        n = A.shape[0]
         if preconditioner_type == "0":
-            return np.identity(A.shape[0])
-        if preconditioner_type == "J":
-            return np.diag(1.0 / np.diag(A))
-        Dg, Lo, Up = extract_blocks(A, b)
-        N = Dg.shape[0]
+            return np.identity(n)
+        if A.shape != (n, n):
+            raise ValueError(f"A must be square, got {A.shape}")
+        if n > DENSE_MAX_ROWS:
+            raise NotImplementedError(f"PCG: {n} rows exceed the device PCG's {DENSE_MAX_ROWS}")
         ctx = _native.default_context(self.device)
-        _, _, _, _, Pd = ctx.pcg_batch(Dg[None], Lo[None], np.zeros((1, N * b)), precond=preconditioner_type,
-                                       S_up=Up[None], tol=1.0, max_iter=0, trace=False)
-        Pd = Pd[0]
-        P = np.zeros((N * b, N * b))
-        for k in range(N):
-            P[k * b:(k + 1) * b, k * b:(k + 1) * b] = Pd[k]
-        if preconditioner_type == "SS":
-            for k in range(1, N, 2):
-                lo = -Pd[k] @ (Lo[k - 1] @ Pd[k - 1])
-                P[k * b:(k + 1) * b, (k - 1) * b:k * b] = lo
-                P[(k - 1) * b:k * b, k * b:(k + 1) * b] = lo.T
-                if k < N - 1:
-                    up = -Pd[k] @ (Up[k] @ Pd[k + 1])
-                    P[k * b:(k + 1) * b, (k + 1) * b:(k + 2) * b] = up
-                    P[(k + 1) * b:(k + 2) * b, k * b:(k + 1) * b] = up.T
-        return P
+        _, _, _, _, P = ctx.pcg_dense_batch(A[None], np.zeros((1, n)), None, precond=preconditioner_type,
+                                            nx=int(block_size), tol=1.0, max_iter=0, trace=False, want_pinv=True)
+        return P[0]
 
     @property
     def Pinv(self):
