@@ -261,6 +261,54 @@ def _cpu_solve_hard(args):
                 x=r["x"], u=r["u"])
 
 
+def hard_order_decided(ctx, x0, u0, N, dt, method, gr, i, ref):
+    """For a problem whose hard-limit run differs from the oracle's: at the first QP j where the two runs'
+    PCG counts differ, the GPU's own iterate j (the same solve stopped after j iterations) is re-solved on
+    the device (tmpc_qp_batch) and the oracle's canonical-order PCG (oracle/hard.py pcg_canonical) runs on
+    that QP's own S and gamma.  True when it takes the GPU's count: the runs part only because their S
+    differ in the last bits (the GPU's and the oracle's dynamics / Schur formation), on a count the
+    summation order decides -- the replay tests/test_gpu_hard.py applies to every QP."""
+    from oracle import hard as ohard
+    ex, it = int(gr["exit_sqp"][i]), int(gr["sqp_iter"][i])
+    g_counts = [int(v) for v in gr["trace"]["pcg_iters"][i, 1:it + (1 if ex == 3 else 0) + 1]]
+    o_counts = list(ref["pcg_iters"])
+    j = next((q for q in range(min(len(g_counts), len(o_counts))) if g_counts[q] != o_counts[q]), None)
+    if j is None:
+        return False
+    o = ctx.options
+    rho, drho = o.rho_init_SQP_DDP, 1.0
+    for q in range(j):   # the rho schedule up to QP j (check_for_exit_or_error, TrajoptMPCReference.py:457-481)
+        if gr["trace"]["succeeded_line_search"][i, q + 1]:
+            drho = min(drho / o.rho_factor_SQP_DDP, 1.0 / o.rho_factor_SQP_DDP)
+        else:
+            drho = max(drho * o.rho_factor_SQP_DDP, o.rho_factor_SQP_DDP)
+        rho = max(rho * drho, o.rho_min_SQP_DDP)
+    xi, ui = x0[i:i + 1], u0[i:i + 1]
+    if j > 0:
+        keep = o.max_iter_SQP_DDP
+        ctx.set_options(max_iter_SQP_DDP=j)
+        try:
+            rj = ctx.sqp_solve_batch(xi, ui, N, dt, method, with_trace=False)
+        finally:
+            ctx.set_options(max_iter_SQP_DDP=keep)
+        xi, ui = rj["x"], rj["u"]
+    q = ctx.qp_batch(xi, ui, N, dt, np.array([rho]), method, want_blocks=False, xs=x0[i:i + 1, :, 0])
+    if int(q["pcg_iters"][0]) != g_counts[j]:
+        return False
+    info = ctx.qp_hard_info(1, N)
+    D, W = int(info["dim"][0]), int(info["W"])
+    S = np.zeros((D, D))
+    for off in range(2 * W + 1):
+        a = np.arange(D)
+        c = a - W + off
+        ok = (c >= 0) & (c < D)
+        S[a[ok], c[ok]] = info["S_band"][0][a[ok], off]
+    nx = x0.shape[1]
+    _, it_c = ohard.pcg_canonical(S, info["gamma"][0, :D], nx, method[4:], o.exit_tolerance_linSys,
+                                  o.max_iter_linSys)
+    return it_c == g_counts[j]
+
+
 def parity_check(gpu, cpu):
     """GPU vs oracle on the same problems: exit code, SQP iterations and the per-QP PCG counts must be
     identical (integer parity); trajectories are compared relative to their magnitude."""
@@ -801,10 +849,17 @@ def run_hard_line(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, 
         with mp.get_context("fork").Pool(min(share, S), initializer=os.environ.__setitem__,
                                           initargs=("OMP_NUM_THREADS", "1")) as pool:
             res = pool.map(_cpu_solve_hard, jobs, chunksize=1)
-        gr = ctx.sqp_solve_batch(x0_host(ctx, d_x0, B, nx, N)[:S], u0[:S], N, dt, a.method)
+        xh = x0_host(ctx, d_x0, B, nx, N)[:S]
+        gr = ctx.sqp_solve_batch(xh, u0[:S], N, dt, a.method)
         par = parity_check(gr, res)
+        decided = [i for i in par["mismatched_problems"]
+                   if hard_order_decided(ctx, xh, u0[:S], N, dt, a.method, gr, i, res[i])]
+        par["order_decided"] = len(decided)
+        par["unexplained"] = par["mismatches"] - len(decided)
         par["note"] = ("oracle/sqp.py with oracle/hard.py's rows and pcg_canonical, the banded PCG's summation "
-                       "order; the QP-by-QP replay on the GPU's own S is tests/test_gpu_hard.py")
+                       "order.  order_decided: mismatched problems whose first differing PCG count the oracle's "
+                       "canonical-order PCG reproduces on the GPU's own S at the GPU's own iterate (the runs' S "
+                       "differ in the last bits; tests/test_gpu_hard.py replays every QP this way)")
     ctx.set_box_limits(None)
     value = B * a.hard_steps * world / elapsed
     return {"metric": f"MPC solves/sec (arm{n}.urdf, N={N}, SQP {a.method}, hard ACTIVE_SET torque + velocity "
