@@ -257,27 +257,19 @@ def _cpu_solve_hard(args):
     lims = [ohard.HardLimit(k, n, v["lb"], v["ub"], v["mode"]) for k, v in LIMIT_PRESETS["torque-velocity-as"].items()]
     with np.errstate(all="ignore"):
         r = osqp.sqp(m, cost, x, u, N, 0.1, "PCG-SS", {}, hard=ohard.HardConstraints(lims), order="canonical")
+    tr = r["trace"][1:]
     return dict(exit_sqp=int(r["exit_sqp"]), sqp_iter=int(r["sqp_iter"]), pcg_iters=list(r["pcg_iters"]),
-                x=r["x"], u=r["u"])
+                x=r["x"], u=r["u"], alpha=[float(t["alpha"]) for t in tr],
+                succeeded=[bool(t["succeeded_line_search"]) for t in tr])
 
 
-def hard_order_decided(ctx, x0, u0, N, dt, method, gr, i, ref):
-    """For a problem whose hard-limit run differs from the oracle's: at the first QP j where the two runs'
-    PCG counts differ, the GPU's own iterate j (the same solve stopped after j iterations) is re-solved on
-    the device (tmpc_qp_batch) and the oracle's canonical-order PCG (oracle/hard.py pcg_canonical) runs on
-    that QP's own S and gamma.  True when it takes the GPU's count: the runs part only because their S
-    differ in the last bits (the GPU's and the oracle's dynamics / Schur formation), on a count the
-    summation order decides -- the replay tests/test_gpu_hard.py applies to every QP."""
-    from oracle import hard as ohard
-    ex, it = int(gr["exit_sqp"][i]), int(gr["sqp_iter"][i])
-    g_counts = [int(v) for v in gr["trace"]["pcg_iters"][i, 1:it + (1 if ex == 3 else 0) + 1]]
-    o_counts = list(ref["pcg_iters"])
-    j = next((q for q in range(min(len(g_counts), len(o_counts))) if g_counts[q] != o_counts[q]), None)
-    if j is None:
-        return False
+def _gpu_iterate(ctx, x0, u0, N, dt, method, gr, i, j):
+    """the GPU's own iterate j of problem i (the same solve stopped after j iterations) and the rho its QP j
+    used (the schedule of check_for_exit_or_error, TrajoptMPCReference.py:457-481, from the trace's
+    line-search outcomes)"""
     o = ctx.options
     rho, drho = o.rho_init_SQP_DDP, 1.0
-    for q in range(j):   # the rho schedule up to QP j (check_for_exit_or_error, TrajoptMPCReference.py:457-481)
+    for q in range(j):
         if gr["trace"]["succeeded_line_search"][i, q + 1]:
             drho = min(drho / o.rho_factor_SQP_DDP, 1.0 / o.rho_factor_SQP_DDP)
         else:
@@ -292,21 +284,68 @@ def hard_order_decided(ctx, x0, u0, N, dt, method, gr, i, ref):
         finally:
             ctx.set_options(max_iter_SQP_DDP=keep)
         xi, ui = rj["x"], rj["u"]
-    q = ctx.qp_batch(xi, ui, N, dt, np.array([rho]), method, want_blocks=False, xs=x0[i:i + 1, :, 0])
-    if int(q["pcg_iters"][0]) != g_counts[j]:
-        return False
-    info = ctx.qp_hard_info(1, N)
-    D, W = int(info["dim"][0]), int(info["W"])
-    S = np.zeros((D, D))
-    for off in range(2 * W + 1):
-        a = np.arange(D)
-        c = a - W + off
-        ok = (c >= 0) & (c < D)
-        S[a[ok], c[ok]] = info["S_band"][0][a[ok], off]
+    return xi, ui, rho
+
+
+def classify_hard_mismatch(ctx, x0, u0, N, dt, method, gr, i, ref):
+    """Why a problem's hard-limit run differs from the oracle's, replayed on the GPU's own inputs
+    (tests/test_gpu_hard.py does this for every QP):
+      * "pcg_count": at the first QP j where the PCG counts differ, the GPU's own iterate j is re-solved on
+        the device (tmpc_qp_batch) and the oracle's canonical-order PCG (oracle/hard.py pcg_canonical)
+        runs on that QP's own S and gamma: it takes the GPU's count -- the runs' S differ in the last
+        bits (the GPU's and the oracle's dynamics / Schur formation) on a count the summation order
+        decides;
+      * "line_search": every common QP's count agrees and the runs part at the first iteration j whose
+        line-search outcome (alpha, success) differs: the oracle's line search (oracle/sqp.py
+        line_search), run at the GPU's iterate j along the GPU's own direction for it, takes the GPU's
+        outcome -- the runs' directions differ in the last bits (their QPs' S do), and the trial's
+        acceptance is decided there;
+      * None: not reproduced."""
+    from oracle import hard as ohard
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    ex, it = int(gr["exit_sqp"][i]), int(gr["sqp_iter"][i])
+    g_counts = [int(v) for v in gr["trace"]["pcg_iters"][i, 1:it + (1 if ex == 3 else 0) + 1]]
+    o_counts = list(ref["pcg_iters"])
+    o = ctx.options
     nx = x0.shape[1]
-    _, it_c = ohard.pcg_canonical(S, info["gamma"][0, :D], nx, method[4:], o.exit_tolerance_linSys,
-                                  o.max_iter_linSys)
-    return it_c == g_counts[j]
+    j = next((q for q in range(min(len(g_counts), len(o_counts))) if g_counts[q] != o_counts[q]), None)
+    if j is not None:
+        xi, ui, rho = _gpu_iterate(ctx, x0, u0, N, dt, method, gr, i, j)
+        q = ctx.qp_batch(xi, ui, N, dt, np.array([rho]), method, want_blocks=False, xs=x0[i:i + 1, :, 0])
+        if int(q["pcg_iters"][0]) != g_counts[j]:
+            return None
+        info = ctx.qp_hard_info(1, N)
+        D, W = int(info["dim"][0]), int(info["W"])
+        S = np.zeros((D, D))
+        for off in range(2 * W + 1):
+            a = np.arange(D)
+            c = a - W + off
+            ok = (c >= 0) & (c < D)
+            S[a[ok], c[ok]] = info["S_band"][0][a[ok], off]
+        _, it_c = ohard.pcg_canonical(S, info["gamma"][0, :D], nx, method[4:], o.exit_tolerance_linSys,
+                                      o.max_iter_linSys)
+        return "pcg_count" if it_c == g_counts[j] else None
+    g_ls = [(float(gr["trace"]["alpha"][i, q + 1]), bool(gr["trace"]["succeeded_line_search"][i, q + 1]))
+            for q in range(it)]
+    o_ls = list(zip(ref["alpha"], ref["succeeded"]))
+    j = next((q for q in range(min(len(g_ls), len(o_ls))) if g_ls[q] != o_ls[q]), None)
+    if j is None:
+        return None
+    xi, ui, rho = _gpu_iterate(ctx, x0, u0, N, dt, method, gr, i, j)
+    q = ctx.qp_batch(xi, ui, N, dt, np.array([rho]), method, want_blocks=False, xs=x0[i:i + 1, :, 0])
+    n = nx // 2
+    m = parse_urdf(planar_arm_urdf(n))
+    cost = osqp.QuadCost(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(n), np.zeros(nx))
+    lims = [ohard.HardLimit(k, n, v["lb"], v["ub"], v["mode"]) for k, v in LIMIT_PRESETS["torque-velocity-as"].items()]
+    hc = ohard.HardConstraints(lims)
+    xs = x0[i, :, 0].copy()
+    with np.errstate(all="ignore"):
+        J = osqp.total_cost(cost, xi[0], ui[0], N, None)
+        c = osqp.total_violation(m, xi[0], ui[0], xs, N, dt, hc)
+        r1 = osqp.line_search(cost, m, xi[0], ui[0], xs, N, dt, q["dxul"][0], J, J + 10 * c, 10,
+                              osqp.default_options({}), None, hc)
+    return "line_search" if (float(r1["alpha"]), bool(r1["succeeded_line_search"])) == g_ls[j] else None
 
 
 def parity_check(gpu, cpu):
@@ -852,14 +891,15 @@ def run_hard_line(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, 
         xh = x0_host(ctx, d_x0, B, nx, N)[:S]
         gr = ctx.sqp_solve_batch(xh, u0[:S], N, dt, a.method)
         par = parity_check(gr, res)
-        decided = [i for i in par["mismatched_problems"]
-                   if hard_order_decided(ctx, xh, u0[:S], N, dt, a.method, gr, i, res[i])]
-        par["order_decided"] = len(decided)
-        par["unexplained"] = par["mismatches"] - len(decided)
+        why = {i: classify_hard_mismatch(ctx, xh, u0[:S], N, dt, a.method, gr, i, res[i])
+               for i in par["mismatched_problems"]}
+        par["replayed"] = {str(i): w for i, w in why.items()}
+        par["unexplained"] = sum(1 for w in why.values() if w is None)
         par["note"] = ("oracle/sqp.py with oracle/hard.py's rows and pcg_canonical, the banded PCG's summation "
-                       "order.  order_decided: mismatched problems whose first differing PCG count the oracle's "
-                       "canonical-order PCG reproduces on the GPU's own S at the GPU's own iterate (the runs' S "
-                       "differ in the last bits; tests/test_gpu_hard.py replays every QP this way)")
+                       "order.  replayed: each mismatched problem replayed on the GPU's own inputs at the first "
+                       "point the runs part (bench.classify_hard_mismatch): 'pcg_count' -- the canonical-order "
+                       "PCG on the GPU's own S takes the GPU's count; 'line_search' -- the oracle's SQP "
+                       "line search on the GPU's own iterate and direction takes the GPU's outcome")
     ctx.set_box_limits(None)
     value = B * a.hard_steps * world / elapsed
     return {"metric": f"MPC solves/sec (arm{n}.urdf, N={N}, SQP {a.method}, hard ACTIVE_SET torque + velocity "

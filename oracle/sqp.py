@@ -260,6 +260,55 @@ def total_violation(model, x, u, xs, N, dt, hard=None):
 
 
 # ------------------------------------------------------------------- SQP
+def line_search(cost, model, x, u, xs, N, dt, dxul, J, merit, mu, o, soft=None, hard=None):
+    """The SQP's merit line search (TrajoptMPCReference.py:640-700): trials x - alpha dx, u - alpha du
+    for alpha = 1, alpha_factor, ... down to alpha_min; a trial is accepted when the merit does not
+    increase and its reduction ratio lies in [expected_reduction_min, expected_reduction_max].  Returns
+    the accepted (or last) trial: succeeded_line_search, alpha, ls (trials - 1), the new x, u, J, c,
+    merit, D, ratio and delta_J = J - J_new."""
+    nx = x.shape[0]
+    n = nx + u.shape[0]
+    dxul = np.asarray(dxul, dtype=float).reshape(-1, 1)
+    alpha = 1
+    ls = 0
+    while True:
+        x_new = copy.deepcopy(x)
+        u_new = copy.deepcopy(u)
+        for k in range(N):
+            x_new[:, k] = x_new[:, k] - alpha * dxul[n * k:n * k + nx, 0]
+            if k < N - 1:
+                u_new[:, k] = u_new[:, k] - alpha * dxul[n * k + nx:n * (k + 1), 0]
+        J_new = total_cost(cost, x_new, u_new, N, soft)
+        c_new = total_violation(model, x_new, u_new, xs, N, dt, hard)
+        D = 0
+        for k in range(N - 1):
+            D += float(cost.gradient(x_new[:, k], u_new[:, k], k) @ dxul[n * k:n * (k + 1), 0])
+            if soft is not None:
+                for j in soft.jacobians(x_new[:, k], u_new[:, k], k, N, n):
+                    D += float(j.dot(dxul[n * k:n * (k + 1), 0]))
+        D += float(cost.gradient(x_new[:, N - 1], None, N - 1) @ dxul[n * (N - 1):n * (N - 1) + nx, 0])
+        if soft is not None:
+            for j in soft.jacobians(x_new[:, N - 1], None, N - 1, N, nx):
+                D += float(j.dot(dxul[n * (N - 1):n * (N - 1) + nx, 0]))
+        merit_new = J_new + mu * c_new
+        delta_J = J - J_new
+        delta_merit = merit - merit_new
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = np.float64(delta_merit) / np.float64(alpha * (D - mu * c_new))
+        out = dict(alpha=alpha, ls=ls, x=x_new, u=u_new, J=J_new, c=c_new, merit=merit_new, D=D, ratio=ratio,
+                   delta_J=delta_J)
+        if (delta_merit >= 0 and ratio >= o["expected_reduction_min_SQP_DDP"]
+                and ratio <= o["expected_reduction_max_SQP_DDP"]):
+            out["succeeded_line_search"] = True
+            return out
+        elif alpha > o["alpha_min_SQP_DDP"]:
+            alpha *= o["alpha_factor_SQP_DDP"]
+            ls += 1
+        else:
+            out["succeeded_line_search"] = False
+            return out
+
+
 def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm=None, hard=None,
         order="numpy"):
     """TrajoptMPCReference.SQP (:510-760).  Returns a dict.  `soft` (oracle.soft.SoftConstraints)
@@ -319,51 +368,16 @@ def sqp(model, cost, x, u, N, dt, method="PCG-SS", options=None, soft=None, warm
             dxuls.append(dxul[:, 0].copy())
             if iters is not None:
                 pcg_iters.append(iters)
-            alpha = 1
-            error = False
-            ls = 0
-            while True:
-                x_new = copy.deepcopy(x)
-                u_new = copy.deepcopy(u)
-                for k in range(N):
-                    x_new[:, k] = x_new[:, k] - alpha * dxul[n * k:n * k + nx, 0]
-                    if k < N - 1:
-                        u_new[:, k] = u_new[:, k] - alpha * dxul[n * k + nx:n * (k + 1), 0]
-                J_new = total_cost(cost, x_new, u_new, N, soft)
-                c_new = total_violation(model, x_new, u_new, xs, N, dt, hard)
-                D = 0
-                for k in range(N - 1):
-                    D += float(cost.gradient(x_new[:, k], u_new[:, k], k) @ dxul[n * k:n * (k + 1), 0])
-                    if soft is not None:
-                        for j in soft.jacobians(x_new[:, k], u_new[:, k], k, N, n):
-                            D += float(j.dot(dxul[n * k:n * (k + 1), 0]))
-                D += float(cost.gradient(x_new[:, N - 1], None, N - 1) @ dxul[n * (N - 1):n * (N - 1) + nx, 0])
-                if soft is not None:
-                    for j in soft.jacobians(x_new[:, N - 1], None, N - 1, N, nx):
-                        D += float(j.dot(dxul[n * (N - 1):n * (N - 1) + nx, 0]))
-                merit_new = J_new + mu * c_new
-                delta_J = J - J_new
-                delta_merit = merit - merit_new
-                with np.errstate(divide="ignore", invalid="ignore"):
-                    ratio = np.float64(delta_merit) / np.float64(alpha * (D - mu * c_new))
-                if (delta_merit >= 0 and ratio >= o["expected_reduction_min_SQP_DDP"]
-                        and ratio <= o["expected_reduction_max_SQP_DDP"]):
-                    x, u, J, c, merit = x_new, u_new, J_new, c_new, merit_new
-                    drho = min(drho / o["rho_factor_SQP_DDP"], 1 / o["rho_factor_SQP_DDP"])
-                    rho = max(rho * drho, o["rho_min_SQP_DDP"])
-                    trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=ls, alpha=alpha,
-                                      rho=rho, J=J, c=c, merit=merit, D=D, reduction_ratio=ratio,
-                                      succeeded_line_search=True))
-                    break
-                elif alpha > o["alpha_min_SQP_DDP"]:
-                    alpha *= o["alpha_factor_SQP_DDP"]
-                    ls += 1
-                else:
-                    error = True
-                    trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=ls, alpha=alpha,
-                                      rho=rho, J=J, c=c, merit=merit, D=D, reduction_ratio=ratio,
-                                      succeeded_line_search=False))
-                    break
+            r = line_search(cost, model, x, u, xs, N, dt, dxul, J, merit, mu, o, soft, hard)
+            error = not r["succeeded_line_search"]
+            if not error:
+                x, u, J, c, merit = r["x"], r["u"], r["J"], r["c"], r["merit"]
+                drho = min(drho / o["rho_factor_SQP_DDP"], 1 / o["rho_factor_SQP_DDP"])
+                rho = max(rho * drho, o["rho_min_SQP_DDP"])
+            delta_J = r["delta_J"]
+            trace.append(dict(outer_iteration=outer, iteration=it, line_search_iteration=r["ls"], alpha=r["alpha"],
+                              rho=rho, J=J, c=c, merit=merit, D=r["D"], reduction_ratio=r["ratio"],
+                              succeeded_line_search=not error))
             # check_for_exit_or_error (:463-481)
             exit_flag = False
             if error:
