@@ -454,7 +454,7 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
     slots = -(-dmax // 1024)
     # tmpc_hard.hip hard_pcg_reg_diag (slot 0, in registers; TMPC_HARD_REG, a build constant)
     reg = int(os.environ.get("TMPC_TEST_HARD_REG", "24"))
-    REG = (16 if nx <= 4 else (reg - 4 if nx >= 14 else reg)) - (8 if slots >= 3 else 0)
+    REG = (16 if nx <= 4 else (reg - 4 if nx >= 14 or nx == 8 else reg)) - (8 if slots >= 3 else 0)
     tot = 0.0
     for S, it in zip(Ss, iters):
         D = S.shape[0]

@@ -397,7 +397,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
 #endif
 
 // band entries of each slot-0 row (its first ones) k_hard_pcg holds in registers for the whole solve:
-// 24 (48 VGPRs of its 128); fewer where that spills (nx = 14: 20; nx = 2, 4: 16; 8 fewer in the three- and
+// 24 (48 VGPRs of its 128); fewer where that spills (nx = 8, 14: 20; nx = 2, 4: 16; 8 fewer in the three- and
 // four-slot instances, which hold x of three / four rows)
 #ifndef TMPC_HARD_REG
 #define TMPC_HARD_REG 24
@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
 #define TMPC_HARD_U 8
 #endif
 __host__ __device__ constexpr int hard_pcg_reg_diag(int nx, int slots) {
-  return (nx <= 4 ? 16 : (nx >= 14 ? TMPC_HARD_REG - 4 : TMPC_HARD_REG)) - (slots >= 3 ? 8 : 0);
+  return (nx <= 4 ? 16 : (nx >= 14 || nx == 8 ? TMPC_HARD_REG - 4 : TMPC_HARD_REG)) - (slots >= 3 ? 8 : 0);
 }
 
 // doubles of LDS k_hard_pcg uses before its reduction slots: r and p of dmax rows, z and S p of the rows
@@ -573,6 +573,12 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   constexpr int REG = hard_pcg_reg_diag(NX, SLOTS);
   const int b = blockIdx.x;
   if (!active[b]) return;
+#if TMPC_HX_STAMPS
+  unsigned long long su_[8] = {}, su_prev_ = __builtin_amdgcn_s_memtime();
+#define HX_SETUP(i_) { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); su_[i_] += n_ - su_prev_; su_prev_ = n_; }
+#else
+#define HX_SETUP(i_)
+#endif
   const int D = dim[b];
   const int BW = 2 * W + 1;
   const int nb = D / NX;
@@ -609,89 +615,137 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     // The setup runs on the whole workgroup, element-parallel, staged in the LDS that r, p, z, S p use
     // later: each element of a block keeps the canonical (oracle/hard.py) operation sequence, so the
     // blocks equal the oracle's bit for bit.
-    // (1) diagonal blocks: Gauss-Jordan on the augmented [M | I] without pivoting (oracle/hard.py _gj_inverse), `cap` blocks
-    //     at a time; per pivot p the new pivot row and the old column p are snapshotted first
-    //     Staged in the scratch or, where larger, in the cache's tail past the diagonal blocks (the stair
-    //     blocks' place, written only in (2))
-    const int tail = (int)(lds_bytes / sizeof(double)) - hard_pcg_cache_offset(D, NX, SLOTS) - ncd * B2;
-    const bool in_tail = tail > hard_pcg_scratch(D, NX);
-    double* stg = in_tail ? pcache + (size_t)ncd * B2 : sh;
-    const int cap = (in_tail ? tail : hard_pcg_scratch(D, NX)) / (B2 + 2 * NX);
-    double* prow = stg + (size_t)cap * B2;
-    double* fcol = prow + (size_t)cap * NX;
-    for (int k0 = 0; k0 < nb; k0 += cap) {
-      const int kc = min(cap, nb - k0);
-      __syncthreads();
-      for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
-        const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
-        stg[e] = band_at(S, rg, dmax, (k0 + kk) * NX + i, (k0 + kk) * NX + j);
-      }
-      for (int p = 0; p < NX; ++p) {
-        __syncthreads();
-        for (int e = t; e < kc * NX; e += HARD_PCG_THREADS) {
-          const int kk = e / NX, j = e - kk * NX;
-          const double* M = stg + (size_t)kk * B2;
-          const double d = M[p * NX + p];
-          prow[e] = (j == p) ? 1.0 / d : M[p * NX + j] / d;
-          fcol[e] = M[j * NX + p];
+    // (1) diagonal blocks: Gauss-Jordan on the augmented [M | I] without pivoting (oracle/hard.py
+    //     _gj_inverse).  One row of one block per thread, in registers, `bpp` blocks per pass: per pivot p
+    //     the owner of each block's row p scales it into LDS (double-buffered by p, so one barrier per
+    //     pivot), and every other row takes it in with its own column-p entry as the snapshot -- the
+    //     operation sequence of every element is the oracle's.  (Element-parallel through LDS with two
+    //     barriers per pivot it took ~110k cycles at D = 768, profiles/r05/hard/stamps_r05m_setup.txt.)
+    const int bpp = min(HARD_PCG_THREADS / NX, hard_pcg_scratch(D, NX) / (2 * NX));
+    double* prow = sh;   // [2][bpp][NX] pivot rows, in the scratch (r and p are written after the setup)
+    for (int k0 = 0; k0 < nb; k0 += bpp) {
+      const int kk = t / NX, i = t - kk * NX;
+      const int k = k0 + kk;
+      const bool own = kk < bpp && k < nb;
+      double m[NX];
+      if (own) {   // row i of S_kk (band_at), the row's range read once and its NX loads in flight together
+        const int a = k * NX + i;
+        const int lo = rg[2 * a], hi = rg[2 * a + 1];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+          const int c = k * NX + j;
+          const double v = S[(size_t)min(max(c - lo, 0), BW - 1) * dmax + a];
+          m[j] = (c >= lo && c <= hi) ? v : 0.0;
         }
-        __syncthreads();
-        for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
-          const int kk = e / B2, r = (e - kk * B2) / NX, j = e - kk * B2 - r * NX;
-          if (r == p) {
-            stg[e] = prow[kk * NX + j];
-          } else {
-            const double f = fcol[kk * NX + r];
-            const double m0 = (j == p) ? 0.0 : stg[e];
-            stg[e] = m0 - f * prow[kk * NX + j];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      HX_SETUP(4);
+#pragma unroll
+      for (int p = 0; p < NX; ++p) {
+        double* pr = prow + (size_t)(p & 1) * bpp * NX + (size_t)kk * NX;
+        if (own && i == p) {
+          const double d = m[p];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) {
+            m[j] = (j == p) ? 1.0 / d : m[j] / d;
+            pr[j] = m[j];
           }
         }
+        __syncthreads();
+        if (own && i != p) {
+          const double f = m[p];
+#pragma unroll
+          for (int j = 0; j < NX; ++j) m[j] = ((j == p) ? 0.0 : m[j]) - f * pr[j];
+        }
       }
-      __syncthreads();
-      for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {   // P_kk and its transpose
-        const int kk = e / B2, i = (e - kk * B2) / NX, j = e - kk * B2 - i * NX;
-        P[(size_t)(k0 + kk) * B2 + i * NX + j] = stg[e];
-        if (k0 + kk < ncd) pcd[hp_off<NX>(k0 + kk, i, j)] = stg[e];
-        else PT[(size_t)(k0 + kk) * B2 + j * NX + i] = stg[e];
+      HX_SETUP(5);
+      if (own) {   // P_kk and its transpose
+#pragma unroll
+        for (int j = 0; j < NX; ++j) {
+          P[(size_t)k * B2 + i * NX + j] = m[j];
+          if (k < ncd) pcd[hp_off<NX>(k, i, j)] = m[j];
+          else PT[(size_t)k * B2 + j * NX + i] = m[j];
+        }
       }
     }
+    HX_SETUP(0);
     // (2) SS stair blocks (oracle/hard.py _neg_triple, both products summed in index order):
     //     odd k: P_{k,k-1} = -P_kk (S_{k,k-1} P_{k-1,k-1}); even k: P_{k-1,k} = -P_{k-1,k-1} (S_{k-1,k}
-    //     P_kk), stored transposed.  Pl[k-1] = P_{k,k-1} row-major.  yz = Y Z staged in LDS, `cap2`
-    //     stairs at a time.
+    //     P_kk), stored transposed.  Pl[k-1] = P_{k,k-1} row-major.  Per pass, one thread per (stair,
+    //     row) stages row `rr` of Y = S_{yr,yc} in LDS (the row's range once, its NX loads together) --
+    //     for the stairs the LDS block cache holds, in their own cache slots, which their results
+    //     overwrite once every read is done; the others in the scratch -- then the same thread forms
+    //     column c = rr of X (Y Z) from LDS (Y, and P_kk's cached copy where present), each yz_mc and each
+    //     acc_rc summed in index order.  (With every Y entry read from HBM by its consumer it took
+    //     180-230k cycles at D = 768, profiles/r05/hard/stamps_r05m_setup.txt.)
     if (precond == PRECOND_SS && nb > 1) {
-      const int cap2 = hard_pcg_scratch(D, NX) / B2;
-      for (int k0 = 1; k0 < nb; k0 += cap2) {
-        const int kc = min(cap2, nb - k0);
-        __syncthreads();   // P written (global, this workgroup) / the previous chunk's yz read
-        for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
-          const int kk = e / B2, r = (e - kk * B2) / NX, c = e - kk * B2 - r * NX;
-          const int k = k0 + kk;
-          const bool odd = k & 1;
-          const int yr = odd ? k : k - 1, yc = odd ? k - 1 : k;        // Y = S_{yr, yc}
-          const double* Z = P + (size_t)(odd ? k - 1 : k) * B2;
-          double yz = 0.0;
-          for (int l = 0; l < NX; ++l) yz += band_at(S, rg, dmax, yr * NX + r, yc * NX + l) * Z[l * NX + c];
-          sh[e] = yz;
+      __syncthreads();   // P (global, this workgroup) and its LDS copies written
+      constexpr int SPP = HARD_PCG_THREADS / NX;
+      const int scap = hard_pcg_scratch(D, NX) / B2;
+      for (int s0 = 0; s0 < nb - 1;) {
+        const bool cached = s0 < ncl;
+        const int s1 = cached ? min(ncl, s0 + SPP) : min(nb - 1, s0 + min(SPP, scap));
+        double* stage = cached ? pcl + (size_t)s0 * B2 : sh;
+        const int q = t / NX, rr = t - q * NX;
+        const bool act = q < s1 - s0;
+        const int k = s0 + q + 1;
+        const bool odd = k & 1;
+        const int yr = odd ? k : k - 1, yc = odd ? k - 1 : k;   // Y = S_{yr, yc}
+        const int zk = odd ? k - 1 : k, xk = odd ? k : k - 1;   // Z, X = P_zk, P_xk
+        double* Yq = stage + (size_t)q * B2;
+        if (act) {
+          const int a = yr * NX + rr;
+          const int lo = rg[2 * a], hi = rg[2 * a + 1];
+#pragma unroll
+          for (int l = 0; l < NX; ++l) {
+            const int col = yc * NX + l;
+            const double v = S[(size_t)min(max(col - lo, 0), BW - 1) * dmax + a];
+            Yq[rr * NX + l] = (col >= lo && col <= hi) ? v : 0.0;   // band_at
+          }
         }
         __syncthreads();
-        for (int e = t; e < kc * B2; e += HARD_PCG_THREADS) {
-          const int kk = e / B2, r = (e - kk * B2) / NX, c = e - kk * B2 - r * NX;
-          const int k = k0 + kk;
-          const bool odd = k & 1;
-          const double* X = P + (size_t)(odd ? k : k - 1) * B2;
-          const double* yz = sh + (size_t)kk * B2;
-          double acc = 0.0;
-          for (int m = 0; m < NX; ++m) acc += X[r * NX + m] * yz[m * NX + c];
-          const double v = -acc;
-          const int pr = odd ? r : c, pc = odd ? c : r;                 // element of P_{k,k-1}
-          PL[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
-          if (k - 1 < ncl) pcl[hp_off<NX>(k - 1, pr, pc)] = v;
+        double acc[NX];
+        if (act) {
+          double z[NX];
+          if (zk < ncd) {
+#pragma unroll
+            for (int l = 0; l < NX; ++l) z[l] = pcd[hp_off<NX>(zk, l, rr)];
+          } else {
+#pragma unroll
+            for (int l = 0; l < NX; ++l) z[l] = P[(size_t)zk * B2 + l * NX + rr];
+          }
+#pragma unroll
+          for (int r = 0; r < NX; ++r) acc[r] = 0.0;
+#pragma unroll 1
+          for (int m = 0; m < NX; ++m) {
+            double yz = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) yz += Yq[m * NX + l] * z[l];
+            if (xk < ncd) {   // (separate loops: a select between the LDS and the HBM copy made flat loads)
+#pragma unroll
+              for (int r = 0; r < NX; ++r) acc[r] += pcd[hp_off<NX>(xk, r, m)] * yz;
+            } else {
+#pragma unroll
+              for (int r = 0; r < NX; ++r) acc[r] += P[(size_t)xk * B2 + r * NX + m] * yz;
+            }
+          }
         }
+        __syncthreads();   // every read of this pass's staged Y done
+        if (act) {
+#pragma unroll
+          for (int r = 0; r < NX; ++r) {
+            const double v = -acc[r];
+            const int pr = odd ? r : rr, pc = odd ? rr : r;   // element of P_{k,k-1}
+            PL[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
+            if (k - 1 < ncl) pcl[hp_off<NX>(k - 1, pr, pc)] = v;
+          }
+        }
+        s0 = s1;
       }
     }
     __syncthreads();
   }
+  HX_SETUP(1);
   // z = P^-1 r for row a (r read from LDS)
   auto apply_P = [&](int a) -> double {
     if (precond == PRECOND_NONE || TMPC_HX_NOPREC) return rv[a];
@@ -793,6 +847,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       nnz += hi + 1;
     }
   }
+  HX_SETUP(2);
   if (work) {
     nnz = h_block_sum_db(nnz, red, nsum);
     nnz_reg = h_block_sum_db(nnz_reg, red, nsum);
@@ -822,6 +877,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     }
   }
   double nu = h_block_sum_db(part, red, nsum);
+  HX_SETUP(3);
   int it_done = max_iter;
 #if TMPC_HX_STAMPS   // timing experiment: per-phase shader-clock sums of every wave of problem 0
   unsigned long long hs_[8] = {}, hs_prev_ = __builtin_amdgcn_s_memtime();
@@ -892,8 +948,12 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
   if (b == 0 && (t & 63) == 0 && t < D)
     printf("hx_stamps wave %d it %d D %d: top %llu spmv %llu sum_a %llu upd %llu bar %llu precond %llu sum_nu %llu pupd %llu\n",
            t >> 6, it_done, D, hs_[0], hs_[1], hs_[2], hs_[3], hs_[4], hs_[5], hs_[6], hs_[7]);
+  if (b == 0 && t == 0)
+    printf("hx_setup D %d: gj_loads %llu gj_pivots %llu gj_writes %llu stairs %llu ranges %llu z0 %llu\n", D,
+           su_[4], su_[5], su_[0], su_[1], su_[2], su_[3]);
 #endif
 #undef HX_STAMP
+#undef HX_SETUP
 #pragma unroll
   for (int m = 0; m < SLOTS; ++m) {
     const int a = t + m * HARD_PCG_THREADS;
