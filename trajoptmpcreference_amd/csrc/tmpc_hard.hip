@@ -189,6 +189,13 @@ __device__ __forceinline__ double hard_grad(const CostDev* __restrict__ C, const
   return g;
 }
 
+// pointers typed with their address space (LDS / HBM): a plain pointer that may point to either makes
+// every read through it a flat load
+typedef __attribute__((address_space(3))) const double lds_cdouble;
+typedef __attribute__((address_space(1))) const double glb_cdouble;
+__device__ __forceinline__ lds_cdouble* lds_ptr(const double* p) { return (lds_cdouble*)p; }
+__device__ __forceinline__ glb_cdouble* glb_ptr(const double* p) { return (glb_cdouble*)p; }
+
 // piece p of row a: the knot and the coefficient vector over [x_knot; u_knot]
 //   R_0 row i: (0, e_i);  R_j row i: (j-1, -[A_{j-1} B_{j-1}] row i), (j, e_i);  H_k row s: (k, sgn e_col)
 template <int NJ>
@@ -232,9 +239,16 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
                                                     double* __restrict__ Y, int* __restrict__ PK,
                                                     double* __restrict__ Sb, double* __restrict__ gam,
                                                     int* __restrict__ rng) {
+#if TMPC_HX_STAMPS
+  unsigned long long sc_[4] = {}, sc_prev_ = __builtin_amdgcn_s_memtime();
+#define HS_STAMP(i_) { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); sc_[i_] += n_ - sc_prev_; sc_prev_ = n_; }
+#else
+#define HS_STAMP(i_)
+#endif
   constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
   extern __shared__ double s_grad[];   // [N][NXU] cost gradient per knot, then s_piece
   int* s_piece = reinterpret_cast<int*>(s_grad + N * NXU);   // [N] first row, [N] last row touching each knot piece
+  int* s_pk = s_piece + 2 * N;   // [dmax][2] each row's piece knots (PK), read by phase 2 for every S entry
   const int b = blockIdx.x;
   if (!active[b]) return;
   const int K = N - 1;
@@ -257,49 +271,68 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     s_grad[e] = (m < NX || k < K) ? hard_grad<NJ>(C, xb, ub, js, N, k, m) : 0.0;
   }
   __syncthreads();
-  // phase 1
-  for (int a = threadIdx.x; a < D; a += blockDim.x) {
-    const int kind = rk[a], knot = rn[a], idx = ri[a];
-    const int* hc = hcol + hb + (size_t)knot * rmax;
-    const double* hs = hsgn + hb + (size_t)knot * rmax;
-    double g_dot = 0.0;
-    for (int p = 0; p < 2; ++p) {
-      double cf[3 * NJ];
-      const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
-      PKb[a * 2 + p] = kp;
-      if (kp < 0) continue;
-      // y = Ghat_kp cf (terminal knot: x block only), written out row by row, and s = y . g in the
-      // same order; the row loops stay rolled so one Ghat row's loads are live at a time
-      double* yo = Yb + ((size_t)a * 2 + p) * NXU;
-      const double* gk = s_grad + kp * NXU;
-      const double* Gx = Gh.x(C, kp, N);
-      double s = 0.0;
-#pragma unroll 1
-      for (int r = 0; r < NX; ++r) {
-        double acc = 0.0;
-#pragma unroll
-        for (int c = 0; c < NX; ++c) acc += Gx[r * NX + c] * cf[c];
-        yo[r] = acc;
-        s += acc * gk[r];
-      }
-      const double* Gu = Gh.u(kp);
-#pragma unroll 1
-      for (int r = 0; r < NU; ++r) {
-        double acc = 0.0;
-        if (kp < K) {
-#pragma unroll
-          for (int c = 0; c < NU; ++c) acc += Gu[r * NU + c] * cf[NX + c];
-        }
-        yo[NX + r] = acc;
-        s += acc * gk[NX + r];
-      }
-      g_dot += s;
-    }
-    double ca;
-    if (kind == 0) ca = cvec[((size_t)b * N + knot) * NX + idx];
-    else ca = hval[hb + (size_t)knot * rmax + idx];
-    gam[(size_t)b * dmax + a] = ca - g_dot;
+  HS_STAMP(0);
+  // phase 1.  With one shared Ghat (no per-knot soft blocks: Q, QF and R blocks, 2 NX^2 + NU^2 doubles)
+  // the rows read it from an LDS copy; per-knot blocks stay in HBM.  (From HBM, each row's 2 x 18 Ghat
+  // row loads were dependent round trips.)
+  double* s_gh = reinterpret_cast<double*>(s_pk + ((dmax * 2 + 3) & ~3));
+  constexpr int GH = 2 * NX * NX + NU * NU;
+  if (!per_knot) {
+    for (int e = threadIdx.x; e < GH; e += blockDim.x) s_gh[e] = Ghat[(size_t)b * 3 * NX * NX + e];
+    __syncthreads();
   }
+  auto phase1 = [&](auto gx_of, auto gu_of) {
+    for (int a = threadIdx.x; a < D; a += blockDim.x) {
+      const int kind = rk[a], knot = rn[a], idx = ri[a];
+      const int* hc = hcol + hb + (size_t)knot * rmax;
+      const double* hs = hsgn + hb + (size_t)knot * rmax;
+      double g_dot = 0.0;
+      for (int p = 0; p < 2; ++p) {
+        double cf[3 * NJ];
+        const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
+        PKb[a * 2 + p] = kp;
+        s_pk[a * 2 + p] = kp;
+        if (kp < 0) continue;
+        // y = Ghat_kp cf (terminal knot: x block only), written out row by row, and s = y . g in the
+        // same order; the row loops stay rolled so one Ghat row's loads are live at a time
+        double* yo = Yb + ((size_t)a * 2 + p) * NXU;
+        const double* gk = s_grad + kp * NXU;
+        const auto Gx = gx_of(kp);
+        double s = 0.0;
+#pragma unroll 1
+        for (int r = 0; r < NX; ++r) {
+          double acc = 0.0;
+#pragma unroll
+          for (int c = 0; c < NX; ++c) acc += Gx[r * NX + c] * cf[c];
+          yo[r] = acc;
+          s += acc * gk[r];
+        }
+        const auto Gu = gu_of(kp);
+#pragma unroll 1
+        for (int r = 0; r < NU; ++r) {
+          double acc = 0.0;
+          if (kp < K) {
+#pragma unroll
+            for (int c = 0; c < NU; ++c) acc += Gu[r * NU + c] * cf[NX + c];
+          }
+          yo[NX + r] = acc;
+          s += acc * gk[NX + r];
+        }
+        g_dot += s;
+      }
+      double ca;
+      if (kind == 0) ca = cvec[((size_t)b * N + knot) * NX + idx];
+      else ca = hval[hb + (size_t)knot * rmax + idx];
+      gam[(size_t)b * dmax + a] = ca - g_dot;
+    }
+  };
+  if (!per_knot) {
+    lds_cdouble* gl = lds_ptr(s_gh);
+    phase1([&](int kp) { return gl + (h_use_QF(C, kp, N) ? NX * NX : 0); }, [&](int) { return gl + 2 * NX * NX; });
+  } else {
+    phase1([&](int kp) { return glb_ptr(Gh.x(C, kp, N)); }, [&](int kp) { return glb_ptr(Gh.u(kp)); });
+  }
+  HS_STAMP(1);
   // the rows of each knot piece: S_ac is structurally nonzero only where rows a and c share a piece,
   // so row a's nonzeros lie in [min, max] of the rows of its pieces -- a much narrower range than
   // the worst-case band W, which the PCG's products and the elimination then stay inside
@@ -310,7 +343,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
   __syncthreads();
   for (int a = threadIdx.x; a < D; a += blockDim.x)
     for (int p = 0; p < 2; ++p) {
-      const int kp = PKb[a * 2 + p];
+      const int kp = s_pk[a * 2 + p];
       if (kp < 0) continue;
       atomicMin(&s_piece[kp], a);
       atomicMax(&s_piece[N + kp], a);
@@ -320,7 +353,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
   for (int a = threadIdx.x; a < D; a += blockDim.x) {
     int lo = a, hi = a;
     for (int p = 0; p < 2; ++p) {
-      const int kp = PKb[a * 2 + p];
+      const int kp = s_pk[a * 2 + p];
       if (kp < 0) continue;
       lo = min(lo, s_piece[kp]);
       hi = max(hi, s_piece[N + kp]);
@@ -335,6 +368,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
   // outside the ranges are never read (band_at / the PCG product / k_hard_direct's copy).  Each thread
   // keeps its row's two coefficient vectors in registers and the wave walks j up to its longest row (the
   // stores of one j are contiguous); S_ac = -(sum over pieces p of a, q of c on one knot of cf_ap . Y_cq)
+  HS_STAMP(2);
   const int BW = 2 * W + 1;
   double* S = Sb + (size_t)b * dmax * BW;
   for (int a0 = threadIdx.x & ~63; a0 < D; a0 += blockDim.x) {   // wave-uniform: the wave's first row
@@ -365,7 +399,7 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
         continue;
       }
       const int c = rb[2 * a] + o;
-      const int pc0 = PKb[c * 2], pc1 = PKb[c * 2 + 1];
+      const int pc0 = s_pk[c * 2], pc1 = s_pk[c * 2 + 1];   // (LDS: from HBM it was a dependent round trip per entry)
       double sum = 0.0;
       auto piece = [&](const double(&cf)[3 * NJ], int kp) {   // pieces q of column c on row a's knot kp
         if (kp < 0) return;
@@ -384,6 +418,13 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
       S[(size_t)o * dmax + a] = -sum;
     }
   }
+  HS_STAMP(3);
+#if TMPC_HX_STAMPS
+  if (b == 0 && (threadIdx.x & 63) == 0)
+    printf("hs_stamps wave %d D %d: grad %llu Y %llu ranges %llu S %llu\n", (int)(threadIdx.x >> 6), D, sc_[0], sc_[1],
+           sc_[2], sc_[3]);
+#endif
+#undef HS_STAMP
 }
 
 #ifndef TMPC_HX_NOSTREAM
@@ -485,10 +526,6 @@ __device__ __forceinline__ double h_block_sum(double v, double* red) {
 // A preconditioner block's row / column from the LDS cache or from HBM, through pointers typed with
 // their address space: a plain pointer that may point to either (or two branches the compiler merges)
 // makes every read a flat load, issued one at a time here.  s += M_ij r_j in j order (canonical).
-typedef __attribute__((address_space(3))) const double lds_cdouble;
-typedef __attribute__((address_space(1))) const double glb_cdouble;
-__device__ __forceinline__ lds_cdouble* lds_ptr(const double* p) { return (lds_cdouble*)p; }
-__device__ __forceinline__ glb_cdouble* glb_ptr(const double* p) { return (glb_cdouble*)p; }
 // The LDS copies of the preconditioner blocks are row-major with each row's 16-byte pieces swizzled:
 // piece c of row i of block k sits at c ^ sw, sw = bit 3 of the global row k NX + i (NX a multiple of 4,
 // so that c ^ 1 stays in the row).  A wave reads its rows' pieces with ds_read_b128: the 16 lanes of a
@@ -1212,7 +1249,7 @@ struct LaunchHard {
                          h.hcol, h.hsgn, h.hval, h.hslot, h.amask, h.iter, h.Wtr, h.tr_active);
       hipLaunchKernelGGL(k_hard_layout, dim3(B), dim3(64), 0, s, B, N, NX, h.rmax, h.active, h.cnt, h.roff, h.hoff,
                          h.dim, h.rkind, h.rknot, h.ridx, h.dmax);
-      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), N * (3 * NJ * sizeof(double) + 2 * sizeof(int)), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
+      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), N * (3 * NJ * sizeof(double) + 2 * sizeof(int)) + ((h.dmax * 2 + 3) & ~3) * sizeof(int) + (2 * 4 * NJ * NJ + NJ * NJ) * sizeof(double), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
                          h.per_knot, h.A, h.Bm, h.cvec, h.x, h.u, h.jsoft, h.dim, h.rkind, h.rknot, h.ridx, h.hoff,
                          h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam, h.rng);
     } else if (h.phase == 1) {
