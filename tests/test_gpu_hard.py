@@ -471,8 +471,10 @@ def _hard_pcg_bytes(Ss, iters, nx, ptype, dmax):
         ncap = max(0, 160 * 1024 // 8 - offset) // b2
         ncd = min(nb, ncap) if ptype in ("BJ", "SS") else 0
         ncl = min(nb - 1, ncap - ncd) if ptype == "SS" and nb > 1 else 0
-        pnnz, setup = {"0": (0, 0), "J": (D, 0), "BJ": ((nb - ncd) * b2, 2 * nb * b2),
-                       "SS": ((2 * nb - 1 - ncd - ncl) * b2, (4 * nb - 2) * b2) if nb else (0, 0)}[ptype]
+        # setup: the band blocks read, and the HBM writes of the blocks the LDS cache does not hold
+        pnnz, setup = {"0": (0, 0), "J": (D, 0), "BJ": ((nb - ncd) * b2, (nb + 2 * (nb - ncd)) * b2),
+                       "SS": ((2 * nb - 1 - ncd - ncl) * b2,
+                              (2 * nb - 1 + 2 * (nb - ncd) + (nb - 1 - ncl)) * b2) if nb else (0, 0)}[ptype]
         tot += 8.0 * (2.0 * D + int(it) * nnz + (int(it) + 1.0) * pnnz + setup + nnz_reg)
     return tot
 

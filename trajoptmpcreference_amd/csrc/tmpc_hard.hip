@@ -225,8 +225,16 @@ __device__ __forceinline__ int row_piece(int kind, int knot, int idx, int p, con
 
 // S band and gamma.  Phase 1: per row and piece, Y = Ghat cf (global scratch [dmax][2][NXU] per
 // problem); phase 2: S_ab = -sum over shared knots cf_a . Y_b, gamma_a = c_a - sum_p Y_a . g.
+#ifndef TMPC_SCHUR_WPE
+#define TMPC_SCHUR_WPE 1
+#endif
+// S entries per step of k_hard_schur's phase 2 (their Y loads in flight together): 2 (four measured the
+// same at NJ = 6, profiles/r05/hard/probe_r05s.txt, at 254 VGPRs)
+#ifndef TMPC_SCHUR_EPS
+#define TMPC_SCHUR_EPS 2
+#endif
 template <int NJ>
-__global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ C, int B, int N, int W, int dmax,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_SCHUR_WPE))) k_hard_schur(const CostDev* __restrict__ C, int B, int N, int W, int dmax,
                                                     int rmax, const int* __restrict__ active,
                                                     const double* __restrict__ Ghat, int per_knot,
                                                     const double* __restrict__ Aall, const double* __restrict__ Ball,
@@ -392,30 +400,50 @@ __global__ void __launch_bounds__(256) k_hard_schur(const CostDev* __restrict__ 
     }
     l = __builtin_amdgcn_readfirstlane(l);
     h = __builtin_amdgcn_readfirstlane(h);
-    for (int o = l; o <= h; ++o) {
-      if (!own) continue;
-      if (o > oh) {   // zero up to the wave's longest row: k_hard_pcg's products read it (exact zeros)
-        S[(size_t)o * dmax + a] = 0.0;
-        continue;
-      }
-      const int c = rb[2 * a] + o;
-      const int pc0 = s_pk[c * 2], pc1 = s_pk[c * 2 + 1];   // (LDS: from HBM it was a dependent round trip per entry)
-      double sum = 0.0;
-      auto piece = [&](const double(&cf)[3 * NJ], int kp) {   // pieces q of column c on row a's knot kp
-        if (kp < 0) return;
-#pragma unroll 1
-        for (int q = 0; q < 2; ++q) {
-          if ((q ? pc1 : pc0) != kp) continue;   // (q loop rolled: one Y vector's loads live at a time)
-          const double* y = Yb + ((size_t)c * 2 + q) * NXU;
-          double d = 0.0;
+    // EPS entries per step, each piece's Y vectors of all of them loaded together (per entry and piece a
+    // dependent HBM round trip kept one Y vector in flight per lane); S_ac = -(sum over the pieces p of a,
+    // in order, of cf_ap . Y_cq for the piece q of c on a's knot kp_p), zero past the row up to the wave's
+    // longest row (k_hard_pcg's products read it: exact zeros)
+    constexpr int EPS = TMPC_SCHUR_EPS;
+    const int lo_a = own ? rb[2 * a] : 0;
+    for (int o = l; o <= h; o += EPS) {
+      bool in[EPS];
+      int pc0[EPS], pc1[EPS];
+      double sm[EPS];
 #pragma unroll
-          for (int m = 0; m < NXU; ++m) d += cf[m] * y[m];
-          sum += d;
+      for (int e = 0; e < EPS; ++e) {
+        in[e] = own && o + e <= oh;
+        const int c = lo_a + o + e;
+        pc0[e] = in[e] ? s_pk[c * 2] : -2;
+        pc1[e] = in[e] ? s_pk[c * 2 + 1] : -2;
+        sm[e] = 0.0;
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int kp = p ? kp1 : kp0;
+        const double(&cf)[3 * NJ] = p ? cf1 : cf0;
+        int q[EPS];
+        double v[EPS][NXU];
+#pragma unroll
+        for (int e = 0; e < EPS; ++e) {
+          q[e] = kp < 0 ? -1 : (pc0[e] == kp ? 0 : (pc1[e] == kp ? 1 : -1));
+          const double* y = Yb + (size_t)(q[e] >= 0 ? (lo_a + o + e) * 2 + q[e] : 0) * NXU;
+#pragma unroll
+          for (int m = 0; m < NXU; ++m) v[e][m] = y[m];
         }
-      };
-      piece(cf0, kp0);
-      piece(cf1, kp1);
-      S[(size_t)o * dmax + a] = -sum;
+#pragma unroll
+        for (int e = 0; e < EPS; ++e) {
+          if (q[e] >= 0) {
+            double d = 0.0;
+#pragma unroll
+            for (int m = 0; m < NXU; ++m) d += cf[m] * v[e][m];
+            sm[e] += d;
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EPS; ++e)
+        if (own && o + e <= h) S[(size_t)(o + e) * dmax + a] = o + e <= oh ? -sm[e] : 0.0;
     }
   }
   HS_STAMP(3);
@@ -653,17 +681,21 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     // later: each element of a block keeps the canonical (oracle/hard.py) operation sequence, so the
     // blocks equal the oracle's bit for bit.
     // (1) diagonal blocks: Gauss-Jordan on the augmented [M | I] without pivoting (oracle/hard.py
-    //     _gj_inverse).  One row of one block per thread, in registers, `bpp` blocks per pass: per pivot p
-    //     the owner of each block's row p scales it into LDS (double-buffered by p, so one barrier per
-    //     pivot), and every other row takes it in with its own column-p entry as the snapshot -- the
-    //     operation sequence of every element is the oracle's.  (Element-parallel through LDS with two
-    //     barriers per pivot it took ~110k cycles at D = 768, profiles/r05/hard/stamps_r05m_setup.txt.)
-    const int bpp = min(HARD_PCG_THREADS / NX, hard_pcg_scratch(D, NX) / (2 * NX));
-    double* prow = sh;   // [2][bpp][NX] pivot rows, in the scratch (r and p are written after the setup)
-    for (int k0 = 0; k0 < nb; k0 += bpp) {
-      const int kk = t / NX, i = t - kk * NX;
-      const int k = k0 + kk;
-      const bool own = kk < bpp && k < nb;
+    //     _gj_inverse).  One row of one block per thread, in registers, each block inside one wave (64 / NX
+    //     whole blocks per wave): per pivot p the owner of each block's row p scales it into LDS and every
+    //     other row of the block takes it in with its own column-p entry as the snapshot -- the operation
+    //     sequence of every element is the oracle's.  A wave's LDS accesses complete in order, so a pivot
+    //     needs no workgroup barrier.  (Element-parallel through LDS with two barriers per pivot it took
+    //     ~110k cycles at D = 768, profiles/r05/hard/stamps_r05m_setup.txt; rows in registers with one
+    //     workgroup barrier per pivot ~35k, stamps_r05t.)
+    constexpr int BPW = 64 / NX;                          // whole blocks per wave
+    constexpr int BPP = (HARD_PCG_THREADS / 64) * BPW;    // blocks per pass
+    const int lane = t & 63, bw = lane / NX, i = lane - bw * NX;
+    const int kkp = (t >> 6) * BPW + bw;                  // this thread's block within the pass
+    for (int k0 = 0; k0 < nb; k0 += BPP) {
+      const int k = k0 + kkp;
+      const bool own = bw < BPW && k < nb;
+      double* pr = sh + (size_t)kkp * NX;   // the block's pivot row (scratch: at most D doubles per pass)
       double m[NX];
       if (own) {   // row i of S_kk (band_at), the row's range read once and its NX loads in flight together
         const int a = k * NX + i;
@@ -679,7 +711,6 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
       HX_SETUP(4);
 #pragma unroll
       for (int p = 0; p < NX; ++p) {
-        double* pr = prow + (size_t)(p & 1) * bpp * NX + (size_t)kk * NX;
         if (own && i == p) {
           const double d = m[p];
 #pragma unroll
@@ -688,22 +719,31 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
             pr[j] = m[j];
           }
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (own && i != p) {
           const double f = m[p];
 #pragma unroll
           for (int j = 0; j < NX; ++j) m[j] = ((j == p) ? 0.0 : m[j]) - f * pr[j];
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
       HX_SETUP(5);
-      if (own) {   // P_kk and its transpose
+      if (own) {   // P_kk: its LDS copy where cached, else in HBM row-major (stairs) and transposed (P^-1 r)
 #pragma unroll
         for (int j = 0; j < NX; ++j) {
-          P[(size_t)k * B2 + i * NX + j] = m[j];
-          if (k < ncd) pcd[hp_off<NX>(k, i, j)] = m[j];
-          else PT[(size_t)k * B2 + j * NX + i] = m[j];
+          if (k < ncd) {
+            pcd[hp_off<NX>(k, i, j)] = m[j];
+          } else {
+            P[(size_t)k * B2 + i * NX + j] = m[j];
+            PT[(size_t)k * B2 + j * NX + i] = m[j];
+          }
         }
       }
+      __syncthreads();   // (the next pass reuses the pivot rows)
     }
     HX_SETUP(0);
     // (2) SS stair blocks (oracle/hard.py _neg_triple, both products summed in index order):
@@ -741,6 +781,7 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
           }
         }
         __syncthreads();
+        HX_SETUP(6);
         double acc[NX];
         if (act) {
           double z[NX];
@@ -767,14 +808,15 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
             }
           }
         }
+        HX_SETUP(7);
         __syncthreads();   // every read of this pass's staged Y done
         if (act) {
 #pragma unroll
           for (int r = 0; r < NX; ++r) {
             const double v = -acc[r];
             const int pr = odd ? r : rr, pc = odd ? rr : r;   // element of P_{k,k-1}
-            PL[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
-            if (k - 1 < ncl) pcl[hp_off<NX>(k - 1, pr, pc)] = v;
+            if (k - 1 < ncl) pcl[hp_off<NX>(k - 1, pr, pc)] = v;   // cached: LDS only
+            else PL[(size_t)(k - 1) * B2 + pr * NX + pc] = v;
           }
         }
         s0 = s1;
@@ -986,8 +1028,8 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     printf("hx_stamps wave %d it %d D %d: top %llu spmv %llu sum_a %llu upd %llu bar %llu precond %llu sum_nu %llu pupd %llu\n",
            t >> 6, it_done, D, hs_[0], hs_[1], hs_[2], hs_[3], hs_[4], hs_[5], hs_[6], hs_[7]);
   if (b == 0 && t == 0)
-    printf("hx_setup D %d: gj_loads %llu gj_pivots %llu gj_writes %llu stairs %llu ranges %llu z0 %llu\n", D,
-           su_[4], su_[5], su_[0], su_[1], su_[2], su_[3]);
+    printf("hx_setup D %d: gj_loads %llu gj_pivots %llu gj_writes %llu stair_stage %llu stair_compute %llu "
+           "stair_rest %llu ranges %llu z0 %llu\n", D, su_[4], su_[5], su_[0], su_[6], su_[7], su_[1], su_[2], su_[3]);
 #endif
 #undef HX_STAMP
 #undef HX_SETUP
@@ -1002,13 +1044,16 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_hard_pcg(int B, int W, int
     // band's structural entries (S p) not held in registers, and the distinct preconditioner entries
     // one P^-1 r needs that are not resident in LDS (SS: of the nb diagonal and nb - 1 stair blocks,
     // each once, all but the ncd + ncl cached ones), it_done + 1 of those; once: the register-held band
-    // entries, and the setup's reads of the band's diagonal (and for SS sub-diagonal) blocks and writes
-    // of P (and Pl)
+    // entries, and the setup's reads of the band's diagonal (and for SS sub-diagonal) blocks and its HBM
+    // writes: the blocks the LDS cache does not hold (P_kk row-major and transposed, Pl)
     const double b2 = (double)NX * NX;
     double pnnz = 0.0, setup = 0.0;
     if (precond == PRECOND_J) pnnz = D;
-    if (precond == PRECOND_BJ) { pnnz = (double)(nb - ncd) * b2; setup = 2.0 * nb * b2; }
-    if (precond == PRECOND_SS && nb > 0) { pnnz = (double)(2 * nb - 1 - ncd - ncl) * b2; setup = (4.0 * nb - 2.0) * b2; }
+    if (precond == PRECOND_BJ) { pnnz = (double)(nb - ncd) * b2; setup = (nb + 2.0 * (nb - ncd)) * b2; }
+    if (precond == PRECOND_SS && nb > 0) {
+      pnnz = (double)(2 * nb - 1 - ncd - ncl) * b2;
+      setup = (2.0 * nb - 1.0 + 2.0 * (nb - ncd) + (nb - 1 - ncl)) * b2;
+    }
     work[b] += 8.0 * (2.0 * D + it_done * nnz + (it_done + 1.0) * pnnz + setup + nnz_reg);
   }
 }
