@@ -223,6 +223,32 @@ __device__ __forceinline__ int row_piece(int kind, int knot, int idx, int p, con
   return knot - 1;
 }
 
+// s_pk entry of one row piece: (knot + 1) | unit code << 16, the unit code 0 for a -[A B] row, else
+// 1 + 3 uc + (uv > 0 ? 1 : uv < 0 ? 2 : 0) for the unit piece uv e_uc (uv = a hard row's sign or 1)
+__device__ __forceinline__ int pk_pack(int kp, int uc, double uv) {
+  return (kp + 1) | (uc < 0 ? 0 : 1 + 3 * uc + (uv > 0.0 ? 1 : (uv < 0.0 ? 2 : 0))) << 16;
+}
+__device__ __forceinline__ int pk_knot(int v) { return (v & 0xffff) - 1; }
+__device__ __forceinline__ int pk_unit(int v) { return v >> 16; }
+__device__ __forceinline__ int pk_uc(int code) { return (code - 1) / 3; }
+__device__ __forceinline__ double pk_uv(int code) {
+  const int sc = (code - 1) % 3;
+  return sc == 1 ? 1.0 : (sc == 2 ? -1.0 : 0.0);
+}
+
+// the unit piece of row (kind, knot, idx), piece p (row_piece): its entry (-1: a -[A B] row or no piece)
+__device__ __forceinline__ int piece_unit(int kind, int knot, int idx, int p, const int* hc, const double* hs,
+                                          double& uv) {
+  uv = 1.0;
+  if (kind == 1) {
+    if (p) return -1;
+    uv = hs[idx];
+    return hc[idx];
+  }
+  if (knot == 0) return p ? -1 : idx;
+  return p ? idx : -1;
+}
+
 // S band and gamma.  Phase 1: per row and piece, Y = Ghat cf (global scratch [dmax][2][NXU] per
 // problem); phase 2: S_ab = -sum over shared knots cf_a . Y_b, gamma_a = c_a - sum_p Y_a . g.
 #ifndef TMPC_SCHUR_WPE
@@ -299,7 +325,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
         double cf[3 * NJ];
         const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
         PKb[a * 2 + p] = kp;
-        s_pk[a * 2 + p] = kp;
+        double uv;
+        const int uc = piece_unit(kind, knot, idx, p, hc, hs, uv);
+        s_pk[a * 2 + p] = pk_pack(kp, uc, uv);
         if (kp < 0) continue;
         // y = Ghat_kp cf (terminal knot: x block only), written out row by row, and s = y . g in the
         // same order; the row loops stay rolled so one Ghat row's loads are live at a time
@@ -351,7 +379,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
   __syncthreads();
   for (int a = threadIdx.x; a < D; a += blockDim.x)
     for (int p = 0; p < 2; ++p) {
-      const int kp = s_pk[a * 2 + p];
+      const int kp = pk_knot(s_pk[a * 2 + p]);
       if (kp < 0) continue;
       atomicMin(&s_piece[kp], a);
       atomicMax(&s_piece[N + kp], a);
@@ -361,7 +389,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
   for (int a = threadIdx.x; a < D; a += blockDim.x) {
     int lo = a, hi = a;
     for (int p = 0; p < 2; ++p) {
-      const int kp = s_pk[a * 2 + p];
+      const int kp = pk_knot(s_pk[a * 2 + p]);
       if (kp < 0) continue;
       lo = min(lo, s_piece[kp]);
       hi = max(hi, s_piece[N + kp]);
@@ -382,14 +410,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
   for (int a0 = threadIdx.x & ~63; a0 < D; a0 += blockDim.x) {   // wave-uniform: the wave's first row
     const int a = a0 + (threadIdx.x & 63);
     const bool own = a < D;
-    double cf0[3 * NJ], cf1[3 * NJ];
+    double cf0[3 * NJ];   // piece 0's coefficients (piece 1 is always a unit piece, or none: row_piece)
     int kp0 = -1, kp1 = -1, ol = BW, oh = -1;
+    // the unit pieces (row_piece: e_idx, or sgn e_col for a hard row): entry uc of cf, value uv (-1: a
+    // -[A B] row, the full product)
+    int uc0 = -1, uc1 = -1;
+    double uv0 = 0.0, uv1 = 0.0;
     if (own) {
       const int kind = rk[a], knot = rn[a], idx = ri[a];
       const int* hc = hcol + hb + (size_t)knot * rmax;
       const double* hs = hsgn + hb + (size_t)knot * rmax;
       kp0 = row_piece<NJ>(kind, knot, idx, 0, A, Bm, hc, hs, cf0);
-      kp1 = row_piece<NJ>(kind, knot, idx, 1, A, Bm, hc, hs, cf1);
+      kp1 = kind == 1 || knot == 0 ? -1 : knot;   // row_piece(.., p = 1, ..)
+      uc0 = piece_unit(kind, knot, idx, 0, hc, hs, uv0);
+      uc1 = piece_unit(kind, knot, idx, 1, hc, hs, uv1);
       ol = 0;
       oh = rb[2 * a + 1] - rb[2 * a];
     }
@@ -414,30 +448,57 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
       for (int e = 0; e < EPS; ++e) {
         in[e] = own && o + e <= oh;
         const int c = lo_a + o + e;
-        pc0[e] = in[e] ? s_pk[c * 2] : -2;
-        pc1[e] = in[e] ? s_pk[c * 2 + 1] : -2;
+        pc0[e] = in[e] ? s_pk[c * 2] : -1;   // packed (pk_pack); -1: no entry
+        pc1[e] = in[e] ? s_pk[c * 2 + 1] : -1;
         sm[e] = 0.0;
       }
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         const int kp = p ? kp1 : kp0;
-        const double(&cf)[3 * NJ] = p ? cf1 : cf0;
+        const int uc = p ? uc1 : uc0;
         int q[EPS];
-        double v[EPS][NXU];
 #pragma unroll
-        for (int e = 0; e < EPS; ++e) {
-          q[e] = kp < 0 ? -1 : (pc0[e] == kp ? 0 : (pc1[e] == kp ? 1 : -1));
-          const double* y = Yb + (size_t)(q[e] >= 0 ? (lo_a + o + e) * 2 + q[e] : 0) * NXU;
+        for (int e = 0; e < EPS; ++e)
+          q[e] = kp < 0 || pc0[e] < 0 ? -1 : (pk_knot(pc0[e]) == kp ? 0 : (pk_knot(pc1[e]) == kp ? 1 : -1));
+        if (uc >= 0) {
+          // a unit piece: of the product's sequential chain from +0 (d += cf_m y_m) only the one nonzero
+          // term changes d, so d = uv y_uc + 0 exactly (for finite Y): one Y load instead of NXU
+          const double uv = p ? uv1 : uv0;
+          double yv[EPS];
 #pragma unroll
-          for (int m = 0; m < NXU; ++m) v[e][m] = y[m];
-        }
+          for (int e = 0; e < EPS; ++e) yv[e] = q[e] >= 0 ? Yb[((size_t)(lo_a + o + e) * 2 + q[e]) * NXU + uc] : 0.0;
 #pragma unroll
-        for (int e = 0; e < EPS; ++e) {
-          if (q[e] >= 0) {
-            double d = 0.0;
+          for (int e = 0; e < EPS; ++e)
+            if (q[e] >= 0) sm[e] += uv * yv[e] + 0.0;
+        } else if (p == 0) {
+          // a -[A B] row (piece 0 only).  Where c's piece is the unit uv e_uc, cf_ap . Y_cq = uv (Ghat cf_ap)_uc = uv Y_ap[uc]
+          // (Ghat symmetric), one entry of row a's own Y; else the full product with c's Y vector
+          double v[EPS][NXU], dv[EPS];
+          bool full[EPS];
 #pragma unroll
-            for (int m = 0; m < NXU; ++m) d += cf[m] * v[e][m];
-            sm[e] += d;
+          for (int e = 0; e < EPS; ++e) {
+            const int code = q[e] < 0 ? 0 : pk_unit(q[e] ? pc1[e] : pc0[e]);
+            full[e] = q[e] >= 0 && code == 0;
+            dv[e] = code ? pk_uv(code) * Yb[((size_t)a * 2 + p) * NXU + pk_uc(code)] + 0.0 : 0.0;
+          }
+#pragma unroll
+          for (int e = 0; e < EPS; ++e) {
+            const double* y = Yb + (size_t)(full[e] ? (lo_a + o + e) * 2 + q[e] : 0) * NXU;
+            if (full[e]) {
+#pragma unroll
+              for (int m = 0; m < NXU; ++m) v[e][m] = y[m];
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < EPS; ++e) {
+            if (full[e]) {
+              double d = 0.0;
+#pragma unroll
+              for (int m = 0; m < NXU; ++m) d += cf0[m] * v[e][m];
+              sm[e] += d;
+            } else if (q[e] >= 0) {
+              sm[e] += dv[e];
+            }
           }
         }
       }
