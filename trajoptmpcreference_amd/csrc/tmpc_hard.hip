@@ -259,6 +259,18 @@ __device__ __forceinline__ int piece_unit(int kind, int knot, int idx, int p, co
 #ifndef TMPC_SCHUR_EPS
 #define TMPC_SCHUR_EPS 2
 #endif
+// Y scratch layout: 1 (shipped) [2][NXU][dmax], a wave's rows consecutive: phase 1's writes coalesce
+// (row-major [dmax][2][NXU], 0: Y 84k -> 63k cycles per problem, hard_schur 0.48 -> 0.43 ms per launch at
+// B = 4096, profiles/r05/hard/probe_r05z.txt; while phase 2 read a full Y row per entry and piece the
+// row-major layout was the faster one, probe_r05w_ytransposed_rejected.txt)
+#ifndef TMPC_SCHUR_YT
+#define TMPC_SCHUR_YT 1
+#endif
+#if TMPC_SCHUR_YT
+#define Y_AT(row, q, m) Yb[((size_t)(q) * NXU + (m)) * dmax + (row)]
+#else
+#define Y_AT(row, q, m) Yb[((size_t)(row) * 2 + (q)) * NXU + (m)]
+#endif
 template <int NJ>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_SCHUR_WPE))) k_hard_schur(const CostDev* __restrict__ C, int B, int N, int W, int dmax,
                                                     int rmax, const int* __restrict__ active,
@@ -331,7 +343,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
         if (kp < 0) continue;
         // y = Ghat_kp cf (terminal knot: x block only), written out row by row, and s = y . g in the
         // same order; the row loops stay rolled so one Ghat row's loads are live at a time
-        double* yo = Yb + ((size_t)a * 2 + p) * NXU;
+        double* yo = &Y_AT(a, p, 0);
+        const size_t ys = TMPC_SCHUR_YT ? (size_t)dmax : 1;   // the stride of the entries
         const double* gk = s_grad + kp * NXU;
         const auto Gx = gx_of(kp);
         double s = 0.0;
@@ -340,7 +353,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
           double acc = 0.0;
 #pragma unroll
           for (int c = 0; c < NX; ++c) acc += Gx[r * NX + c] * cf[c];
-          yo[r] = acc;
+          yo[r * ys] = acc;
           s += acc * gk[r];
         }
         const auto Gu = gu_of(kp);
@@ -351,7 +364,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
 #pragma unroll
             for (int c = 0; c < NU; ++c) acc += Gu[r * NU + c] * cf[NX + c];
           }
-          yo[NX + r] = acc;
+          yo[(NX + r) * ys] = acc;
           s += acc * gk[NX + r];
         }
         g_dot += s;
@@ -466,7 +479,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
           const double uv = p ? uv1 : uv0;
           double yv[EPS];
 #pragma unroll
-          for (int e = 0; e < EPS; ++e) yv[e] = q[e] >= 0 ? Yb[((size_t)(lo_a + o + e) * 2 + q[e]) * NXU + uc] : 0.0;
+          for (int e = 0; e < EPS; ++e) yv[e] = q[e] >= 0 ? Y_AT(lo_a + o + e, q[e], uc) : 0.0;
 #pragma unroll
           for (int e = 0; e < EPS; ++e)
             if (q[e] >= 0) sm[e] += uv * yv[e] + 0.0;
@@ -479,14 +492,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
           for (int e = 0; e < EPS; ++e) {
             const int code = q[e] < 0 ? 0 : pk_unit(q[e] ? pc1[e] : pc0[e]);
             full[e] = q[e] >= 0 && code == 0;
-            dv[e] = code ? pk_uv(code) * Yb[((size_t)a * 2 + p) * NXU + pk_uc(code)] + 0.0 : 0.0;
+            dv[e] = code ? pk_uv(code) * Y_AT(a, p, pk_uc(code)) + 0.0 : 0.0;
           }
 #pragma unroll
           for (int e = 0; e < EPS; ++e) {
-            const double* y = Yb + (size_t)(full[e] ? (lo_a + o + e) * 2 + q[e] : 0) * NXU;
             if (full[e]) {
 #pragma unroll
-              for (int m = 0; m < NXU; ++m) v[e][m] = y[m];
+              for (int m = 0; m < NXU; ++m) v[e][m] = Y_AT(lo_a + o + e, q[e], m);
             }
           }
 #pragma unroll
@@ -514,6 +526,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
            sc_[2], sc_[3]);
 #endif
 #undef HS_STAMP
+#undef Y_AT
 }
 
 #ifndef TMPC_HX_NOSTREAM
