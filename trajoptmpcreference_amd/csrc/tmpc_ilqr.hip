@@ -637,6 +637,24 @@ struct FwdPf {
   static __host__ __device__ size_t lds_doubles(int T) { return 2 * (rk(T) + rs(T)); }
 };
 
+// The knot loop's memory waits (config 3, profiles/r05/configs/c3_fwd_*_r05a[e-g]*; each switch 0 restores
+// the round-4 form for comparison): the next knot's prefetch issued after this knot's stores and feedback
+// reads (PF_LATE: in front of them, the compiler's wait pass put a vmcnt(0) before the feedback's LDS
+// reads -- the LDS-DMA may alias them -- exposing the DMA's latency), explicit waits after the loads into
+// xh / uh (WAITS), the DMA sources precomputed (PFR), the knot's wait through the builtin (BWAIT):
+// ilqr_forward 0.472 -> 0.401 ms per launch, config 3 4.37k -> 4.65k solves/s
+#ifndef TMPC_FWD_PF_LATE
+#define TMPC_FWD_PF_LATE 1
+#endif
+#ifndef TMPC_FWD_WAITS
+#define TMPC_FWD_WAITS 1
+#endif
+#ifndef TMPC_FWD_PFR
+#define TMPC_FWD_PFR 1
+#endif
+#ifndef TMPC_FWD_BWAIT
+#define TMPC_FWD_BWAIT 1
+#endif
 template <int NJ, bool CHAIN, bool SOFT, class MT, class R, bool PF>
 __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __restrict__ C,
                                                      const ConstrDev* __restrict__ Cs, const double* __restrict__ mu,
@@ -689,8 +707,52 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
     if (lane < npt) s_pb[lane] = P.at(min(p0 + lane, np - 1));
     __syncthreads();
   }
+  // TMPC_FWD_PFR: each lane's LDS-DMA sources for knot 0 computed once, here, while no LDS-DMA is in
+  // flight (up to PFJ wave-instructions per kind: T >= 5 trials); knot kn's are base + kn x stride.
+  // Reading the problem slot from LDS per instruction inside the prefetch made the compiler wait for
+  // the previous LDS-DMA before every read (the DMA writes LDS): ~3.7k cycles per knot to issue 13
+  // instructions (profiles/r05/configs/c3_fwd_stamps_r05ae.txt)
+  constexpr int PFJ = 12;
+  const int nkj = (npf * PF_::CK + 63) / 64, nsj = (npf * 2 * PF_::SS + 63) / 64;
+  const bool pfr = TMPC_FWD_PFR && pf && nkj <= PFJ && nsj <= PFJ;
+  const double* kbase[PFJ];
+  const char* sbase[PFJ];
+  int sstride[PFJ];   // bytes per knot
+  if (pfr) {
+#pragma unroll
+    for (int j = 0; j < PFJ; ++j) {
+      const int c = j * 64 + lane;
+      const int p = c / PF_::CK, w = c - p * PF_::CK;
+      const int bb = s_pb[min(p, npt - 1)];
+      kbase[j] = Kg + (size_t)bb * K * PF_::SK + 2 * w;
+      const int q = j * 64 + lane;
+      const int ps = q / (2 * PF_::SS), r = q - ps * (2 * PF_::SS), item = r >> 1, half = r & 1;
+      const int bs = s_pb[min(ps, npt - 1)];
+      const double* src = item < NU ? dg + (size_t)bs * K * NU + item
+                        : item < NU + NX ? x + ((size_t)bs * NX + (item - NU)) * N
+                                         : u + ((size_t)bs * NU + (item - NU - NX)) * K;
+      sbase[j] = (const char*)src + 4 * half;
+      sstride[j] = item < NU ? NU * 8 : 8;
+    }
+  }
   auto prefetch = [&](int kn, int slot) {
     double* buf = pfb + (size_t)slot * (PF_::rk(T) + PF_::rs(T));
+    if (pfr) {
+#pragma unroll
+      for (int j = 0; j < PFJ; ++j)
+        if (j < nkj) {
+          const double* src = kbase[j] + (size_t)kn * PF_::SK;
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + (size_t)j * 128), 16, 0, 0);
+        }
+      double* sb = buf + PF_::rk(T);
+#pragma unroll
+      for (int j = 0; j < PFJ; ++j)
+        if (j < nsj) {
+          const char* src = sbase[j] + (size_t)kn * sstride[j];
+          __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sb + (size_t)j * 32), 4, 0, 0);
+        }
+      return;
+    }
     // K_kn: 16-byte pieces, lane-linear destinations
     for (int j = 0; j * 64 < npf * PF_::CK; ++j) {
       const int c = j * 64 + lane;
@@ -716,6 +778,11 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
   double xh[NX];
 #pragma unroll
   for (int m = 0; m < NX; ++m) xh[m] = xb[m * N];
+  // vmcnt(0) through the builtin (the compiler's wait pass sees it, an asm one it does not): loads
+  // that could still be in flight into xh / uh when the loop's paths join made the pass put a full
+  // vmcnt(0) inside the knot loop, which also waited for the next knot's prefetch (its latency on
+  // every knot's critical path instead of under the dynamics)
+  if (TMPC_FWD_WAITS) __builtin_amdgcn_s_waitcnt(0x0F70);
   double J = 0.0;
 #ifdef TMPC_ILQR_STAMPS
   unsigned long long st_[8] = {}, st_prev_ = __builtin_amdgcn_s_memtime();
@@ -725,21 +792,30 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
     const bool term = k == K;
     double uh[NU];
     if (pf && !term) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // knot k's operands have landed in LDS
-      if (k + 1 < K) prefetch(k + 1, (k + 1) & 1);
+      // knot k's operands have landed in LDS.  TMPC_FWD_BWAIT: through the builtin, which is no
+      // compiler memory barrier (the asm's "memory" clobber made every knot reload the cost's
+      // constants); the compiler's own wait pass orders LDS reads after the LDS-DMA writing them
+      if (TMPC_FWD_BWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      IL_STAMP(4);
+      if (!TMPC_FWD_PF_LATE && k + 1 < K) prefetch(k + 1, (k + 1) & 1);
+      IL_STAMP(5);
     }
     if (live) {
     if (!init) {
 #pragma unroll
       for (int m = 0; m < NX; ++m) xo[k * NX + m] = xh[m];
+      IL_STAMP(6);
     } else {
 #pragma unroll
       for (int m = 0; m < NX; ++m) xh[m] = xb[m * N + k];
+      if (TMPC_FWD_WAITS) __builtin_amdgcn_s_waitcnt(0x0F70);
     }
     if (!term) {
       if (init) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) uh[i] = ub[i * K + k];
+        if (TMPC_FWD_WAITS) __builtin_amdgcn_s_waitcnt(0x0F70);
       } else if (pf) {
         const double* buf = pfb + (size_t)(k & 1) * (PF_::rk(T) + PF_::rs(T));
         const double* Kk = buf + (size_t)pl * PF_::SK;
@@ -768,6 +844,10 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
         }
       }
     }
+    }   // live
+    // TMPC_FWD_PF_LATE: the next knot's prefetch after this knot's stores
+    if (TMPC_FWD_PF_LATE && pf && k + 1 < K) prefetch(k + 1, (k + 1) & 1);
+    if (live) {
     IL_STAMP(0);
     J = J + knot_quad_cost<NJ>(C, k, N, xh, uh, term);
     IL_STAMP(1);
@@ -813,8 +893,8 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
   }
 #ifdef TMPC_ILQR_STAMPS
   if (gid == 0 && !init)
-    printf("ilqr_fwd_stamps K=%d loads+feedback %llu cost %llu aba %llu euler %llu soft %llu\n", K, st_[0], st_[1],
-           st_[2], st_[3] + st_[7], 0ull);
+    printf("ilqr_fwd_stamps K=%d wait %llu prefetch %llu xstore %llu feedback %llu cost %llu aba %llu euler %llu\n", K,
+           st_[4] + st_[7], st_[5], st_[6], st_[0], st_[1], st_[2], st_[3]);
 #endif
   Jt[bt] = J;
 }
