@@ -820,15 +820,30 @@ __global__ void __launch_bounds__(64) k_ilqr_forward(MT Mg, const CostDev* __res
         const double* buf = pfb + (size_t)(k & 1) * (PF_::rk(T) + PF_::rs(T));
         const double* Kk = buf + (size_t)pl * PF_::SK;
         const double* sk = buf + PF_::rk(T) + (size_t)pl * PF_::SS;   // d_k | x_k | u_k
+        // the LDS reads issued ahead of their products: d_k, x_k, u_k and row 0 of K_k together, then
+        // row i + 1 of K_k before row i's products (the scheduler fences keep them there; left alone it
+        // put each read next to its product with a full LDS wait between, ~4k cycles per knot,
+        // profiles/r05/configs/c3_fwd_stamps_r05ag.txt).  Same operands, same chains.
+        double sv[PF_::SS], kr[2][NX];
+#pragma unroll
+        for (int m = 0; m < PF_::SS; ++m) sv[m] = sk[m];
+#pragma unroll
+        for (int m = 0; m < NX; ++m) kr[0][m] = Kk[m];
+        __builtin_amdgcn_sched_barrier(0);
         double dx[NX];
 #pragma unroll
-        for (int m = 0; m < NX; ++m) dx[m] = xh[m] - sk[NU + m];
+        for (int m = 0; m < NX; ++m) dx[m] = xh[m] - sv[NU + m];
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
+          if (i + 1 < NU) {
+#pragma unroll
+            for (int m = 0; m < NX; ++m) kr[(i + 1) & 1][m] = Kk[(i + 1) * NX + m];
+          }
+          __builtin_amdgcn_sched_barrier(0);
           double fb = 0.0;
 #pragma unroll
-          for (int m = 0; m < NX; ++m) fb += Kk[i * NX + m] * dx[m];
-          uh[i] = (sk[NU + NX + i] + al * sk[i]) + fb;
+          for (int m = 0; m < NX; ++m) fb += kr[i & 1][m] * dx[m];
+          uh[i] = (sv[NU + NX + i] + al * sv[i]) + fb;
           uo[k * NU + i] = uh[i];
         }
       } else {
