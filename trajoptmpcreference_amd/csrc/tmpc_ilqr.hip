@@ -240,15 +240,21 @@ __global__ void __launch_bounds__(64) k_ilqr_backward(const CostDev* __restrict_
       constexpr int KS = (NX + 3) / 4;
       const int lo = t & 15, hi = t >> 4;
       double vf[KS], abf[2][KS];
+      // each fragment entry is one LDS read from a selected, always valid address, then a select
+      // against 0 (the nested conditional reads compiled to exec-masked branches with an LDS wait in
+      // each); the same values
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const int kk = 4 * s + hi;
-        vf[s] = kk < NX ? (lo < NX ? double(L.Vxx[lo * NX + kk]) : (lo == NX ? double(L.Vx[kk]) : 0.0)) : 0.0;
+        const int kk = 4 * s + hi, kc = kk < NX ? kk : NX - 1;
+        const R* vp = lo < NX ? &L.Vxx[lo * NX + kc] : &L.Vx[kc];
+        const double vv = double(*vp);
+        vf[s] = (kk < NX && lo <= NX) ? vv : 0.0;
 #pragma unroll
         for (int tl = 0; tl < 2; ++tl) {
           const int c = 16 * tl + lo;
-          abf[tl][s] = kk < NX ? (c < NX ? double(A[kk * NX + c]) : (c < NX + NU ? double(Bm[kk * NU + c - NX]) : 0.0))
-                               : 0.0;
+          const R* ap = c < NX ? &A[kc * NX + c] : &Bm[kc * NU + (c < NX + NU ? c - NX : 0)];
+          const double av = double(*ap);
+          abf[tl][s] = (kk < NX && c < NX + NU) ? av : 0.0;
         }
       }
       // P | VB (rows < NX) and [A B]^T V_x (row NX) = V_xx' [A B]
