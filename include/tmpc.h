@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define TMPC_ABI_VERSION 9   /* 9: tmpc_pcg_dense_batch; 8: tmpc_qp_blocks_batch; 7: tmpc_kernel_bytes */
+#define TMPC_ABI_VERSION 10  /* 10: tmpc_*_solve_stream_device; 9: tmpc_pcg_dense_batch; 8: tmpc_qp_blocks_batch */
 
 /* SQPSolverMethods (TrajoptMPCReference.py:13-18). */
 #define TMPC_LINSYS_S 1      /* Schur complement, direct block-tridiagonal solve (:441-446; np.linalg.solve in the reference) */
@@ -225,6 +225,38 @@ int tmpc_ilqr_solve_batch(tmpc_ctx* ctx, int B, int N, double dt, double* x, dou
                           int32_t* exit_soft, int32_t* outer_iter, int32_t* iters, tmpc_trace* trace);
 int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u,
                                  int32_t* exit_code, int32_t* iters);
+
+/* Continuous batching (ABI 10): `problems` independent problems solved through `slots` resident slots.
+ * The batch entry points above run B problems in lock step until the slowest one exits, so the GPU's
+ * work per batch iteration shrinks to a few problems in the tail.  Here a slot whose problem finishes
+ * (its last outer pass, i.e. its exit) takes the next pending problem in the same batch iteration, so
+ * every batch iteration runs `slots` problems until the stream drains.  This is how the reference's own
+ * drivers use the solver: a pool of independent problems (examples/test_multiple.py:123-128).  Each
+ * problem's operations are those of a batch solve from the same input, so its results (x, u, exit
+ * codes, iteration counts, trace) are bitwise those of tmpc_sqp_solve_batch / tmpc_ilqr_solve_batch;
+ * with soft limits every problem starts from the limits' initial constants (a fresh BoxConstraint).
+ * All arrays are device memory (tmpc_device_alloc):
+ *   x_in [period][nx][N], u_in [period][nu][N-1]   problem p starts from input p % period (iLQR: only
+ *                                                   x_in[:, :, 0] and u_in are read, as tmpc_ilqr_solve_batch);
+ *   x_out [problems][nx][N], u_out [problems][nu][N-1]   results (nullable);
+ *   status [problems][4]   exit code, iterations, exit_soft, outer_iter (nullable);
+ *   trace                  device arrays [problems][max_iter_SQP_DDP + 1] per field (each nullable;
+ *                          hard_active must be NULL).
+ * The context's soft-constraint state is left unset (tmpc_get_soft_state fails until the next solve). */
+typedef struct tmpc_stream {
+  int32_t problems;
+  int32_t slots;
+  int32_t period;
+  int32_t reserved;
+  const double* x_in;
+  const double* u_in;
+  double* x_out;
+  double* u_out;
+  int32_t* status;
+  tmpc_trace trace;
+} tmpc_stream;
+int tmpc_sqp_solve_stream_device(tmpc_ctx* ctx, int N, double dt, int linsys, const tmpc_stream* stream);
+int tmpc_ilqr_solve_stream_device(tmpc_ctx* ctx, int N, double dt, const tmpc_stream* stream);
 
 /* Receding-horizon MPC loop for B problems (the reference has only the hooks --
  * shift_QF_start, shift_soft_constraint_constants -- and no loop, F1; algorithm: oracle/mpc.py).

@@ -37,7 +37,7 @@ def test_binding_matches_header():
     from trajoptmpcreference_amd import _native
     assert sorted(_native.SIGNATURES) == header_functions()
     lib = _native.load_library()
-    assert lib.tmpc_abi_version() == 9
+    assert lib.tmpc_abi_version() == 10
 
 
 def test_options_struct_layout_and_defaults():
@@ -79,3 +79,19 @@ def test_trace_struct_layout():
     assert names == ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
                      "succeeded_line_search", "pcg_iters", "singular", "hard_active"]
     assert ctypes.sizeof(_native.tmpc_trace) == 13 * 8
+
+
+def test_stream_struct_layout():
+    """tmpc_stream (ABI 10): four int32, five device pointers, then a tmpc_trace of device pointers."""
+    from trajoptmpcreference_amd import _native
+    names = [f[0] for f in _native.tmpc_stream._fields_]
+    assert names == ["problems", "slots", "period", "reserved", "x_in", "u_in", "x_out", "u_out", "status", "trace"]
+    assert ctypes.sizeof(_native.tmpc_stream) == 16 + 5 * 8 + 13 * 8
+
+
+def test_stream_argument_errors_without_a_gpu():
+    """the stream entry points validate before any device work: a null context fails, not crashes"""
+    from trajoptmpcreference_amd import _native
+    lib = _native.load_library()
+    assert lib.tmpc_sqp_solve_stream_device(None, 8, 0.1, 4, None) < 0
+    assert lib.tmpc_ilqr_solve_stream_device(None, 8, 0.1, None) < 0

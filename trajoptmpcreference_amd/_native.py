@@ -65,6 +65,19 @@ class tmpc_trace(C.Structure):
     ]
 
 
+class tmpc_stream(C.Structure):
+    """continuous batching (tmpc_*_solve_stream_device): device arrays, include/tmpc.h"""
+    _fields_ = [("problems", C.c_int32), ("slots", C.c_int32), ("period", C.c_int32), ("reserved", C.c_int32),
+                ("x_in", C.c_void_p), ("u_in", C.c_void_p), ("x_out", C.c_void_p), ("u_out", C.c_void_p),
+                ("status", C.c_void_p), ("trace", tmpc_trace)]
+
+
+TRACE_FIELDS = [("iteration", np.int32), ("line_search_iteration", np.int32), ("alpha", np.float64),
+                ("rho", np.float64), ("J", np.float64), ("c", np.float64), ("merit", np.float64),
+                ("D", np.float64), ("reduction_ratio", np.float64), ("succeeded_line_search", np.int32),
+                ("pcg_iters", np.int32), ("singular", np.int32)]
+
+
 # every symbol include/tmpc.h declares, with its ctypes signature
 SIGNATURES = {
     "tmpc_abi_version": (C.c_int, []),
@@ -88,6 +101,8 @@ SIGNATURES = {
                                         C.POINTER(tmpc_trace)]),
     "tmpc_ilqr_solve_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p,
                                                _ip, _ip]),
+    "tmpc_sqp_solve_stream_device": (C.c_int, [C.c_void_p, C.c_int, C.c_double, C.c_int, C.POINTER(tmpc_stream)]),
+    "tmpc_ilqr_solve_stream_device": (C.c_int, [C.c_void_p, C.c_int, C.c_double, C.POINTER(tmpc_stream)]),
     "tmpc_mpc_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, _dp, _dp, _dp, _dp,
                                  _ip, _ip]),
     "tmpc_mpc_batch_device": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_int, C.c_int, C.c_void_p,
@@ -303,10 +318,7 @@ class Context:
     def _trace_arrays(self, B, N=None, hard_active=False):
         W = int(self.options.max_iter_SQP_DDP) + 1
         arrays = {}
-        for name, dt_ in [("iteration", np.int32), ("line_search_iteration", np.int32), ("alpha", np.float64),
-                          ("rho", np.float64), ("J", np.float64), ("c", np.float64), ("merit", np.float64),
-                          ("D", np.float64), ("reduction_ratio", np.float64),
-                          ("succeeded_line_search", np.int32), ("pcg_iters", np.int32), ("singular", np.int32)]:
+        for name, dt_ in TRACE_FIELDS:
             arrays[name] = np.zeros((B, W), dtype=dt_)
         if hard_active:
             arrays["hard_active"] = np.zeros((B, W, N), dtype=np.uint64)
@@ -544,6 +556,62 @@ class Context:
         self._check(self.lib.tmpc_sqp_solve_batch_device(self.h, B, int(N), float(dt), LINSYS[method], d_x, d_u,
                                                          _ptr(ex), _ptr(it)), "tmpc_sqp_solve_batch_device")
         return ex, it
+
+    def solve_stream_device(self, solver, P, slots, N, dt, d_x_in, d_u_in, period, d_x_out=None, d_u_out=None,
+                            d_status=None, d_trace=None):
+        """Continuous batching (tmpc_sqp_solve_stream_device / tmpc_ilqr_solve_stream_device): P problems
+        through `slots` resident slots, problem p from input p % period; device pointers (d_trace: dict of
+        trace field -> device pointer [P][max_iter+1])."""
+        st = tmpc_stream(problems=int(P), slots=int(slots), period=int(period), reserved=0, x_in=d_x_in,
+                         u_in=d_u_in, x_out=d_x_out, u_out=d_u_out, status=d_status)
+        for name, dt_ in TRACE_FIELDS:
+            p = (d_trace or {}).get(name)
+            if p is not None:
+                setattr(st.trace, name, C.cast(p, _ip if dt_ == np.int32 else _dp))
+        if solver == "iLQR":
+            self._check(self.lib.tmpc_ilqr_solve_stream_device(self.h, int(N), float(dt), C.byref(st)),
+                        "tmpc_ilqr_solve_stream_device")
+        else:
+            self._check(self.lib.tmpc_sqp_solve_stream_device(self.h, int(N), float(dt), LINSYS[solver], C.byref(st)),
+                        "tmpc_sqp_solve_stream_device")
+
+    def solve_stream(self, x, u, N, dt, solver="PCG-SS", slots=64, copies=1, with_trace=True):
+        """Host convenience of solve_stream_device: problems x [P0][nx][N], u [P0][nu][N-1], each solved
+        `copies` times (stream problem p = input p % P0) through `slots` slots.  Returns x, u [P][..],
+        status fields (exit, iters, exit_soft, outer_iter) [P] and the trace [P][max_iter+1]."""
+        x, u = _c64(x), _c64(u)
+        self._check_traj(x, u, N)
+        P0 = x.shape[0]
+        P = P0 * int(copies)
+        W = int(self.options.max_iter_SQP_DDP) + 1
+        bufs = []
+        try:
+            def dev(nbytes):
+                p = self.alloc(max(8, nbytes))
+                bufs.append(p)
+                return p
+            dxi, dui = dev(x.nbytes), dev(u.nbytes)
+            self.h2d(dxi, x)
+            self.h2d(dui, u)
+            dxo, duo, dst = dev(x.nbytes * copies), dev(u.nbytes * copies), dev(P * 4 * 4)
+            dtr = {name: dev(P * W * np.dtype(dt_).itemsize) for name, dt_ in TRACE_FIELDS} if with_trace else None
+            self.solve_stream_device(solver, P, slots, N, dt, dxi, dui, P0, dxo, duo, dst, dtr)
+            xo = np.empty((P,) + x.shape[1:])
+            uo = np.empty((P,) + u.shape[1:])
+            status = np.empty((P, 4), dtype=np.int32)
+            self.d2h(xo, dxo)
+            self.d2h(uo, duo)
+            self.d2h(status, dst)
+            trace = {}
+            if with_trace:
+                for name, dt_ in TRACE_FIELDS:
+                    trace[name] = np.empty((P, W), dtype=dt_)
+                    self.d2h(trace[name], dtr[name])
+        finally:
+            for p in bufs:
+                self.free(p)
+        return dict(x=xo, u=uo, exit=status[:, 0].copy(), iters=status[:, 1].copy(), exit_soft=status[:, 2].copy(),
+                    outer_iter=status[:, 3].copy(), trace=trace)
 
     def kernel_stats(self, name):
         n = C.c_int64(0)

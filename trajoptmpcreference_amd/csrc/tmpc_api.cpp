@@ -607,8 +607,11 @@ static int lockstep_loop(tmpc_ctx* ctx, long cap, int* active_count, AliveList& 
   return rc;
 }
 
+// sd (nullable): continuous batching -- d_x, d_u are the B slots of a stream of sd->P problems
+// (tmpc_sqp_solve_stream_device); each problem's results go to its rows of sd's outputs
 static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double* d_x, double* d_u,
-                      TraceDev* tr_out, bool keep_warm = false, bool hard_trace = false) {
+                      TraceDev* tr_out, bool keep_warm = false, bool hard_trace = false,
+                      const StreamDev* sd = nullptr) {
   int rc = check_ready(ctx, B, N);
   if (rc) return rc;
   const int precond = precond_of(linsys);
@@ -636,14 +639,17 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
   const bool soft = ctx->hlim.any != 0;
+  // the outer loop per problem (k_soft_outer with act_init): soft limits, and every stream (a slot's problem
+  // is finished when it leaves its outer loop, which without soft limits is check_and_update's exit 1)
+  const bool per_problem = soft || sd;
   AliveList alv;
-  if ((rc = alloc_alive(ctx, B, soft ? outer_active : st.active, alv))) return rc;
+  if ((rc = alloc_alive(ctx, B, per_problem ? outer_active : st.active, alv))) return rc;
   // UrdfCost has a state-dependent Hessian: it takes the per-knot Ghat path of the soft limits
   const bool perknot = soft || ctx->hcost.kind == COST_EE;
   double *smu = nullptr, *slam = nullptr, *sphi = nullptr;
   if (perknot) {
     if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
-    if (ctx->soft_B != B || ctx->soft_N != N) {
+    if (sd || ctx->soft_B != B || ctx->soft_N != N) {   // a stream's problems start from the initial constants
       launch_soft_init(ctx->stream, ctx->dlim, (size_t)B * N * 6 * nj, 6 * nj, smu, slam, sphi);
       HIP_OK(hipGetLastError());
       ctx->soft_B = B;
@@ -681,7 +687,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     // PCG warm start: each QP starts from the problem's previous lambda (in place: a workgroup reads
     // its guess before it writes its lambda)
     BUF(double, lam_warm, (size_t)B * N * nx);
-    if (!keep_warm) HIP_OK(hipMemsetAsync(lam_warm, 0, (size_t)B * N * nx * sizeof(double), ctx->stream));
+    if (!keep_warm || sd) HIP_OK(hipMemsetAsync(lam_warm, 0, (size_t)B * N * nx * sizeof(double), ctx->stream));
     w.guess = lam_warm;
     w.lam_keep = lam_warm;
   }
@@ -690,20 +696,25 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   std::vector<double> al_h(al);
   al_h.push_back(0.0);  // slot T: alpha = 0 for the initial merit evaluation
   HIP_OK(hipMemcpyAsync(alphas, al_h.data(), al_h.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (sd) {   // slot s starts with problem s
+    launch_stream_init(ctx->stream, B, *sd, d_x, d_u);
+    HIP_OK(hipGetLastError());
+  }
   // xs = x[:, 0] (:527)
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
   launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
-  // initial J, c, merit (:541-548) of the problems in `mask` (st.active: all, act_init: restarted passes)
-  auto init_merit = [&](int* mask, int* ac) -> int {
+  // initial J, c, merit (:541-548) of the problems in `mask` (st.active: all; act_init: restarted passes
+  // and a stream's new problems, which k_ls_decide then moves into their inner loop: activate = st.active)
+  auto init_merit = [&](int* mask, int* ac, int* activate) -> int {
     ProbState sti = st;
     sti.active = mask;
     LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
                               alv.P, alv.nb, N, 1, dt, alphas + T, d_x, d_u, w.xs, nullptr, nullptr, mask, terms));
     if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, mask));
     launch_ls_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
-                     sti, nullptr, tr, ac, nullptr, hterms);
+                     sti, nullptr, tr, ac, nullptr, hterms, nullptr, activate);
     HIP_OK(hipGetLastError());
     return 0;
   };
@@ -724,8 +735,8 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     return 0;
   };
   HIP_OK(hipMemsetAsync(active_count, 0, 8 * sizeof(int), ctx->stream));
-  if ((rc = init_merit(st.active, active_count))) return rc;
-  if (!soft) {
+  if ((rc = init_merit(st.active, active_count, nullptr))) return rc;
+  if (!per_problem) {
     // unconstrained: one inner loop (at most max_iter iterations, + 1 for the lag of the exit test);
     // check_and_update_soft_constraints then exits 1 (:531-757)
     rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, alv, [&](int* ac) { return sqp_iteration(ac); });
@@ -742,20 +753,23 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     // sequence of operations is the lock-step one, so its results are identical.
     BUF(int, act_init, B);
     HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
-    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
+    const long per = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
+    // a stream: every batch iteration advances some problem by one iteration, so P x per bounds it
+    const long cap = sd ? per * sd->P + 3 : per;
     rc = lockstep_loop(ctx, cap, active_count, alv, [&](int* ac) -> int {
       int r = sqp_iteration(ac);
       if (r) return r;
-      launch_soft_outer(ctx->stream, ctx->dlim, alv.P, alv.nb, N, nj, o.exit_tolerance_softConstraints,
-                        o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
-                        ac + 1, &st, act_init, o.rho_init_SQP_DDP);
-      HIP_OK(hipGetLastError());
-      // restarted passes (act_init, set by k_soft_outer): initial merit, then into the inner loop;
-      // masked by act_init, so a no-op when no pass restarted
-      if ((r = init_merit(act_init, ac))) return r;
-      launch_activate(ctx->stream, alv.P, alv.nb, act_init, st.active);
-      HIP_OK(hipGetLastError());
-      return 0;
+      {   // a stream: k_soft_outer also hands finished slots on (finished problems out, pending ones in)
+        Timed t(ctx, "soft_outer");
+        launch_soft_outer(ctx->stream, ctx->dlim, alv.P, alv.nb, N, nj, o.exit_tolerance_softConstraints,
+                          o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
+                          ac + 1, &st, act_init, o.rho_init_SQP_DDP, sd, w.xs, &tr, w.lam_keep);
+        HIP_OK(hipGetLastError());
+      }
+      // restarted passes (act_init, set by k_soft_outer) and a stream's new problems: initial merit, then
+      // into the inner loop; masked by act_init, so a no-op when no pass restarted
+      Timed t(ctx, "init_merit");
+      return init_merit(act_init, ac, st.active);
     });
     if (rc) return rc;
   }
@@ -768,13 +782,15 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   ctx->last_counters[2] = (int64_t)hc[2];
   ctx->last_counters[3] = (int64_t)T;
   if (w.hard && (rc = collect_hard_work(ctx, hard))) return rc;
+  if (sd && perknot) ctx->soft_B = ctx->soft_N = -1;   // the slots' constants are no caller's state
   resolve_timings(ctx);
   if (tr_out) *tr_out = tr;
   return 0;
 }
 
 // ------------------------------------------------------------------ iLQR driver (oracle/ilqr.py)
-static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u, TraceDev* tr_out) {
+static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, double* d_u, TraceDev* tr_out,
+                       const StreamDev* sd = nullptr) {
   int rc = check_ready(ctx, B, N, false);
   if (rc) return rc;
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "iLQR supports QuadraticCost only (UrdfCost: use SQP)");
@@ -806,14 +822,17 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   BUF(int, outer_iter, B);
   BUF(int, exit_soft, B);
   BUF(unsigned long long, counters, 4);
+  BUF(unsigned long long, il_prob_counters, (size_t)B * 3);   // per-problem tallies of k_ilqr_decide
   HIP_OK(hipMemsetAsync(counters, 0, 4 * sizeof(unsigned long long), ctx->stream));
+  HIP_OK(hipMemsetAsync(il_prob_counters, 0, (size_t)B * 3 * sizeof(unsigned long long), ctx->stream));
   const bool soft = ctx->hlim.any != 0;
+  const bool per_problem = soft || sd;   // as sqp_device
   AliveList alv;
-  if ((rc = alloc_alive(ctx, B, soft ? outer_active : st.active, alv))) return rc;
+  if ((rc = alloc_alive(ctx, B, per_problem ? outer_active : st.active, alv))) return rc;
   double *smu = nullptr, *slam = nullptr, *sphi = nullptr, *il_jac = nullptr;
   if (soft) {
     if ((rc = alloc_soft(ctx, B, N, &smu, &slam, &sphi))) return rc;
-    if (ctx->soft_B != B || ctx->soft_N != N) {
+    if (sd || ctx->soft_B != B || ctx->soft_N != N) {
       launch_soft_init(ctx->stream, ctx->dlim, (size_t)B * N * 6 * nj, 6 * nj, smu, slam, sphi);
       HIP_OK(hipGetLastError());
       ctx->soft_B = B;
@@ -823,20 +842,37 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     il_jac = il_jac_buf;
   }
   HIP_OK(hipMemcpyAsync(alphas, al.data(), al.size() * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  // iLQR iterates are rollouts: start from the rollout of u from x[:, 0]
-  LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
+  StreamDev sdr{};
+  if (sd) {
+    // a stream's problems start from the rollout of u from x[:, 0] too: roll the `period` inputs out once
+    // (the same kernel on the same x[:, 0], u as a batch solve's rollout, so the same trajectories) and
+    // let the slots copy from there -- a pending problem then enters its slot without a serial rollout
+    sdr = *sd;
+    BUF(double, stream_xr, (size_t)sd->period * nx * N);
+    HIP_OK(hipMemcpyAsync(stream_xr, sd->x_in, (size_t)sd->period * nx * N * sizeof(double), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+    LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, sd->period, N, dt,
+                             stream_xr, sd->u_in));
+    sdr.x_in = stream_xr;
+    launch_stream_init(ctx->stream, B, sdr, d_x, d_u);   // slot s starts with problem s
+    HIP_OK(hipGetLastError());
+  } else {
+    // iLQR iterates are rollouts: start from the rollout of u from x[:, 0]
+    LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
+  }
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
   launch_outer_init(ctx->stream, B, outer_active, outer_iter, exit_soft);
   launch_init_state(ctx->stream, B, o.rho_init_SQP_DDP, st, outer_active);
-  // J at the current trajectory of the problems in `mask` (st.active: all, act_init: restarted passes)
-  auto init_cost = [&](int* mask, int* ac) -> int {
+  // J at the current trajectory of the problems in `mask` (st.active: all; act_init: restarted passes and a
+  // stream's new problems, moved into their inner loop by k_ilqr_decide: activate = st.active)
+  auto init_cost = [&](int* mask, int* ac, int* activate) -> int {
     ProbState sti = st;
     sti.active = mask;
     LAUNCH_OK(launch_ilqr_init_cost(ctx->stream, nj, ctx->dcost, ctx->dlim, smu, slam, alv.P, alv.nb, N, d_x, d_u,
                                     mask, il_J));
     launch_ilqr_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, 1, 1, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, sti,
-                       tr, ac, nullptr);
+                       tr, ac, nullptr, activate);
     HIP_OK(hipGetLastError());
     return 0;
   };
@@ -871,13 +907,13 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     }
     Timed t(ctx, "ilqr_decide");
     launch_ilqr_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, T, 0, alphas, so, il_J, il_dV, il_ok, il_xt, il_ut, d_x, d_u, st, tr,
-                       ac, counters);
+                       ac, il_prob_counters);
     HIP_OK(hipGetLastError());
     return 0;
   };
   HIP_OK(hipMemsetAsync(active_count, 0, 8 * sizeof(int), ctx->stream));
-  if ((rc = init_cost(st.active, active_count))) return rc;
-  if (!soft) {
+  if ((rc = init_cost(st.active, active_count, nullptr))) return rc;
+  if (!per_problem) {
     rc = lockstep_loop(ctx, (long)o.max_iter_SQP_DDP + 1, active_count, alv, [&](int* ac) { return ilqr_iteration(ac); });
     if (rc) return rc;
     launch_soft_outer(ctx->stream, ctx->dlim, PList{nullptr, nullptr}, B, N, nj, o.exit_tolerance_softConstraints,
@@ -889,26 +925,30 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     // as its own inner loop exits
     BUF(int, act_init, B);
     HIP_OK(hipMemsetAsync(act_init, 0, sizeof(int) * B, ctx->stream));
-    const long cap = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
+    const long per = (long)(o.max_iter_softConstraints + 1) * (o.max_iter_SQP_DDP + 1) + 3;
+    const long cap = sd ? per * sd->P + 3 : per;   // as sqp_device
     rc = lockstep_loop(ctx, cap, active_count, alv, [&](int* ac) -> int {
       int r = ilqr_iteration(ac);
       if (r) return r;
-      launch_soft_outer(ctx->stream, ctx->dlim, alv.P, alv.nb, N, nj, o.exit_tolerance_softConstraints,
-                        o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
-                        ac + 1, &st, act_init, o.rho_init_SQP_DDP);
-      HIP_OK(hipGetLastError());
-      if ((r = init_cost(act_init, ac))) return r;   // masked by act_init: a no-op when no pass restarted
-      launch_activate(ctx->stream, alv.P, alv.nb, act_init, st.active);
-      HIP_OK(hipGetLastError());
-      return 0;
+      {   // a stream: k_soft_outer also hands finished slots on (pending problems from the rolled-out inputs)
+        Timed t(ctx, "soft_outer");
+        launch_soft_outer(ctx->stream, ctx->dlim, alv.P, alv.nb, N, nj, o.exit_tolerance_softConstraints,
+                          o.max_iter_softConstraints, d_x, d_u, smu, slam, sphi, outer_active, outer_iter, exit_soft,
+                          ac + 1, &st, act_init, o.rho_init_SQP_DDP, sd ? &sdr : nullptr, w.xs, &tr, nullptr);
+        HIP_OK(hipGetLastError());
+      }
+      Timed t(ctx, "init_merit");
+      return init_cost(act_init, ac, st.active);   // masked by act_init: a no-op when no pass restarted
     });
     if (rc) return rc;
   }
+  launch_sum_counters(ctx->stream, B, il_prob_counters, counters);
   unsigned long long hc[4] = {0, 0, 0, 0};
   HIP_OK(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   for (int i = 0; i < 3; ++i) ctx->last_counters[i] = (int64_t)hc[i];
   ctx->last_counters[3] = (int64_t)T;
+  if (sd && soft) ctx->soft_B = ctx->soft_N = -1;   // as sqp_device
   resolve_timings(ctx);
   if (tr_out) *tr_out = tr;
   return 0;
@@ -1286,6 +1326,70 @@ int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double*
   if (exit_code) HIP_OK(hipMemcpy(exit_code, ctx->bufs["st_exit"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
   if (iters) HIP_OK(hipMemcpy(iters, ctx->bufs["st_iter"].ptr, sizeof(int) * B, hipMemcpyDeviceToHost));
   return 0;
+}
+
+// ------------------------------------------------------------------ continuous batching (include/tmpc.h, ABI 10)
+// The stream's device descriptor and its B = min(slots, problems) slot buffers.
+static int stream_setup(tmpc_ctx* ctx, int N, const tmpc_stream* s, StreamDev& sd, int& B, double** d_x,
+                        double** d_u) {
+  if (!s) return fail(ctx, "null stream");
+  if (s->problems < 0 || s->slots < 1 || s->period < 1)
+    return fail(ctx, "stream: problems %d (>= 0), slots %d and period %d (>= 1)", s->problems, s->slots, s->period);
+  if (!s->x_in || !s->u_in) return fail(ctx, "stream: null x_in / u_in");
+  if (s->trace.hard_active) return fail(ctx, "stream: trace.hard_active is not supported (set it to NULL)");
+  B = std::min(s->slots, s->problems);
+  const int nj = ctx->hmodel.n, nx = 2 * nj;
+  BUF(double, stream_x, (size_t)std::max(B, 1) * nx * N);
+  BUF(double, stream_u, (size_t)std::max(B, 1) * nj * (N - 1));
+  BUF(int, stream_pid, std::max(B, 1));
+  BUF(int, stream_next, 1);
+  *d_x = stream_x;
+  *d_u = stream_u;
+  sd = StreamDev{};
+  sd.P = s->problems;
+  sd.period = s->period;
+  sd.NX = nx;
+  sd.NU = nj;
+  sd.N = N;
+  sd.W = ctx->opts.max_iter_SQP_DDP + 1;
+  sd.MC = 6 * nj;
+  sd.x_in = s->x_in;
+  sd.u_in = s->u_in;
+  sd.x_out = s->x_out;
+  sd.u_out = s->u_out;
+  sd.status = s->status;
+  const tmpc_trace& t = s->trace;
+  sd.tr_out = TraceDev{t.iteration, t.line_search_iteration, t.alpha, t.rho, t.J, t.c, t.merit, t.D,
+                       t.reduction_ratio, t.succeeded_line_search, t.pcg_iters, t.singular, nullptr};
+  sd.slot_pid = stream_pid;
+  sd.next = stream_next;
+  return 0;
+}
+
+int tmpc_sqp_solve_stream_device(tmpc_ctx* ctx, int N, double dt, int linsys, const tmpc_stream* stream) {
+  if (!ctx) return -1;
+  int rc = check_ready(ctx, 1, N);
+  if (rc) return rc;
+  hipSetDevice(ctx->device);
+  StreamDev sd;
+  int B = 0;
+  double *d_x = nullptr, *d_u = nullptr;
+  if ((rc = stream_setup(ctx, N, stream, sd, B, &d_x, &d_u))) return rc;
+  if (B == 0) return 0;
+  return sqp_device(ctx, B, N, dt, linsys, d_x, d_u, nullptr, false, false, &sd);
+}
+
+int tmpc_ilqr_solve_stream_device(tmpc_ctx* ctx, int N, double dt, const tmpc_stream* stream) {
+  if (!ctx) return -1;
+  int rc = check_ready(ctx, 1, N, false);
+  if (rc) return rc;
+  hipSetDevice(ctx->device);
+  StreamDev sd;
+  int B = 0;
+  double *d_x = nullptr, *d_u = nullptr;
+  if ((rc = stream_setup(ctx, N, stream, sd, B, &d_x, &d_u))) return rc;
+  if (B == 0) return 0;
+  return ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr, &sd);
 }
 
 // ------------------------------------------------------------------ receding-horizon MPC (oracle/mpc.py)

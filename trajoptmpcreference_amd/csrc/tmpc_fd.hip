@@ -262,11 +262,14 @@ __global__ void __launch_bounds__(256) k_unit_fd(MT M, int K, double dt,
 
 // sequential Euler rollout, one lane per problem (workload setup: §8d)
 template <int NJ, bool CHAIN, class MT, class R>
-__global__ void __launch_bounds__(64) k_rollout(MT M, int B, int N, double dt,
-                                                double* __restrict__ x, const double* __restrict__ u) {
+__global__ void __launch_bounds__(64) k_rollout(MT M, PList P, int B, int N, double dt,
+                                                double* __restrict__ x, const double* __restrict__ u,
+                                                const int* __restrict__ mask) {
   constexpr int NX = 2 * NJ;
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (!P.has(p, B)) return;
+  const int b = P.at(p);
+  if (mask && !mask[b]) return;
   const int K = N - 1;
   double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NJ * K;
@@ -387,11 +390,12 @@ struct LaunchFD {
     hipLaunchKernelGGL((k_mpc_shift<NJ, CHAIN, MT>), dim3(B), dim3(64), 0, s, MT::make(M), B, N, dt, step, steps, x,
                        u, xe, ue);
   }
-  static void rollout(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u) {
+  static void rollout(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u,
+                      PList P, const int* mask) {
     if (f32)
-      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, float>), TMPC_GRID(B, 64), 0, s, MT::make(M), B, N, dt, x, u);
+      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, float>), TMPC_GRID(B, 64), 0, s, MT::make(M), P, B, N, dt, x, u, mask);
     else
-      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, double>), TMPC_GRID(B, 64), 0, s, MT::make(M), B, N, dt, x, u);
+      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, double>), TMPC_GRID(B, 64), 0, s, MT::make(M), P, B, N, dt, x, u, mask);
   }
 };
 
@@ -430,8 +434,8 @@ int launch_unit_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const M
   TMPC_DISPATCH_NJ(nj, chain, unit_fd(f32, s, M, K, dt, x, u, xnext, qdd))
 }
 int launch_rollout(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt,
-                   double* x, const double* u) {
-  TMPC_DISPATCH_NJ(nj, chain, rollout(f32, s, M, B, N, dt, x, u))
+                   double* x, const double* u, PList P, const int* mask) {
+  TMPC_DISPATCH_NJ(nj, chain, rollout(f32, s, M, B, N, dt, x, u, P, mask))
 }
 
 int launch_mpc_shift(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, int step,

@@ -1024,7 +1024,8 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int N
                                                     const double* __restrict__ ut, double* __restrict__ x,
                                                     double* __restrict__ u, ProbState st, TraceDev tr,
                                                     int* __restrict__ active_count,
-                                                    unsigned long long* __restrict__ counters) {
+                                                    unsigned long long* __restrict__ counters,
+                                                    int* __restrict__ activate) {
   if (!P.has(blockIdx.x, B)) return;
   const int b = P.at(blockIdx.x);
   if (!st.active[b]) return;
@@ -1043,6 +1044,10 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int N
       tr.J[e] = J; tr.c[e] = 0.0; tr.merit[e] = J; tr.D[e] = __builtin_nan(""); tr.ratio[e] = __builtin_nan("");
       tr.accepted[e] = 0; tr.pcg_iters[e] = 0;
       *active_count = 1;   // the host only tests for zero
+      if (activate) {      // a restarted pass / a stream's new problem enters its inner loop (st.active: act_init)
+        st.active[b] = 0;
+        activate[b] = 1;
+      }
       s_choice = -1;
     } else {
       const double J = st.J[b];
@@ -1068,9 +1073,11 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int N
       const int it = st.iter[b];
       const size_t e = (size_t)b * W + it + 1;
       if (counters) {
-        // [0] problem-iterations, [2] iterations with a fresh dynamics gradient
-        atomicAdd(&counters[0], 1ull);
-        atomicAdd(&counters[2], (unsigned long long)st.need_grad[b]);
+        // per-problem tallies [B][3], summed once per solve (k_sum_counters): [0] problem-iterations,
+        // [2] iterations with a fresh dynamics gradient (same-address atomics serialised the launch)
+        unsigned long long* pc = counters + (size_t)b * 3;
+        pc[0] += 1ull;
+        pc[2] += (unsigned long long)st.need_grad[b];
       }
       if (!error) {
         st.J[b] = Jn;
@@ -1237,9 +1244,9 @@ int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrD
 void launch_ilqr_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int T, int init, const double* alphas,
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
-                        int* active_count, unsigned long long* counters) {
+                        int* active_count, unsigned long long* counters, int* activate) {
   hipLaunchKernelGGL(k_ilqr_decide, dim3(B), dim3(64), 0, s, P, B, N, NX, NU, T, init, alphas, o, Jt, dV, ok, xt, ut, x,
-                     u, st, tr, active_count, counters);
+                     u, st, tr, active_count, counters, activate);
 }
 
 }  // namespace tmpc

@@ -101,8 +101,10 @@ int launch_unit_fd(bool f32, hipStream_t s, int nj, bool chain, int mid, const M
 int launch_unit_minv(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, const double* x, double* minv);
 int launch_unit_grad(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int K, double dt, const double* x,
                      const double* qdd, const double* minv, double* A, double* Bm, double* dqdd);
+// P / mask: the problems to roll out (the identity and every problem by default; the stream's refilled
+// slots: the alive list and act_init)
 int launch_rollout(bool f32, hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, double* x,
-                   const double* u);
+                   const double* u, PList P = PList{nullptr, nullptr}, const int* mask = nullptr);
 int launch_ginv(hipStream_t s, int nj, const CostDev* C, PList P, int B, const double* rho, const int* active, double* G);
 // dt: the Euler step of A_k / B_k (their structural rows are not read, tmpc_kernels.hip qp_schur_row)
 int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, double dt, int precond, int mode,
@@ -139,18 +141,41 @@ int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const
                    const double* gam, double* U, double* Y, double* lam);
 int pcg_set_max_lds();
 void launch_sum_counters(hipStream_t s, int B, const unsigned long long* pc, unsigned long long* out);
+// Continuous batching (tmpc_sqp_solve_stream_device / tmpc_ilqr_solve_stream_device): B resident slots
+// work through a stream of P problems.  The workgroup of k_soft_outer that ends a problem's outer loop
+// (outer_active 1 -> 0) writes the problem's results to its output rows and, when a problem is pending
+// (one atomic on `next`; which slot gets which problem changes no problem's results), loads the next
+// one's inputs with the state a fresh solve starts from -- act_init, so its initial merit / cost is
+// evaluated in the same batch iteration.  Each problem's own operation sequence is the one of a batch
+// solve, so its results are bitwise those of tmpc_*_solve_batch.
+struct StreamDev {
+  int P, period, NX, NU, N, W, MC;   // problems, input period, sizes, trace rows, soft slots per knot (6 n)
+  const double* x_in;                // [period][NX][N]: problem p starts from input p % period
+  const double* u_in;                // [period][NU][N-1]
+  double* x_out;                     // [P][NX][N] (nullable)
+  double* u_out;                     // [P][NU][N-1] (nullable)
+  int* status;                       // [P][4]: exit code, iterations, exit_soft, outer_iter (nullable)
+  TraceDev tr_out;                   // [P][W] per field (each nullable; hard_active unused)
+  int* slot_pid;                     // [B] problem in the slot (-1: none)
+  int* next;                         // [1] next pending problem
+};
+void launch_stream_init(hipStream_t s, int B, const StreamDev& sd, double* x, double* u);
+
 void launch_ls_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int T, int mode, int soft, const double* alphas,
                       const SolverOpts& o, const double* terms, double* x, double* u, const double* dx,
                       const double* du, const ProbState& st, const int* pcg_iters, const TraceDev& tr,
                       int* active_count, unsigned long long* counters, const double* hterms,
-                      const int* qp_singular = nullptr);
+                      const int* qp_singular = nullptr, int* activate = nullptr);   // activate: as launch_ilqr_decide
 void launch_init_state(hipStream_t s, int B, double rho_init, const ProbState& st, const int* outer_active);
-// st / act_init / rho_init: the per-problem outer loop (null act_init: lock-step, tmpc_kernels.hip)
+// st / act_init / rho_init: the per-problem outer loop (null act_init: lock-step, tmpc_kernels.hip);
+// sd / xs / tr / lam_warm: a stream's hand-over of finished slots (nullable; per-problem mode only)
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, PList P, int B, int N, int nj, double tol, int max_iter,
-                       const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
+                       double* x, double* u, double* mu, double* lam, double* phi, int* outer_active,
                        int* outer_iter, int* exit_soft, int* outer_count, const ProbState* st = nullptr,
-                       int* act_init = nullptr, double rho_init = 0.0);
-void launch_activate(hipStream_t s, PList P, int B, int* act_init, int* active);
+                       int* act_init = nullptr, double rho_init = 0.0, const StreamDev* sd = nullptr,
+                       double* xs = nullptr, const TraceDev* tr = nullptr, double* lam_warm = nullptr);
+
+
 int launch_ilqr_backward(bool f32, hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N, const double* x,
                          const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                          const double* mu, const double* lam, double* jscratch, double* K, double* d, double* dV,
@@ -162,10 +187,13 @@ int launch_ilqr_forward(bool f32, hipStream_t s, int nj, bool chain, int mid, co
 int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, const double* mu,
                           const double* lam, PList P, int B, int N, const double* x, const double* u, const int* mask,
                           double* Jt);
+// counters: per-problem tallies [B][3] (problem-iterations, -, fresh gradients), summed by
+// launch_sum_counters; activate (init only, nullable): the real active flags -- st.active is then the
+// act_init mask, cleared as the problem enters its inner loop
 void launch_ilqr_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int T, int init, const double* alphas,
                         const SolverOpts& o, const double* Jt, const double* dV, const int* ok, const double* xt,
                         const double* ut, double* x, double* u, const ProbState& st, const TraceDev& tr,
-                        int* active_count, unsigned long long* counters);
+                        int* active_count, unsigned long long* counters, int* activate = nullptr);
 int launch_mpc_shift(hipStream_t s, int nj, bool chain, int mid, const ModelDev* M, int B, int N, double dt, int step,
                      int steps, double* x, double* u, double* xe, double* ue);
 void launch_soft_shift(hipStream_t s, const ConstrDev* Cs, int B, int N, int nj, double* mu, double* lam,

@@ -871,7 +871,8 @@ __global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX,
                                                   int* __restrict__ active_count,
                                                   unsigned long long* __restrict__ counters,
                                                   const double* __restrict__ hterms,
-                                                  const int* __restrict__ qp_singular) {
+                                                  const int* __restrict__ qp_singular,
+                                                  int* __restrict__ activate) {
   if (!P.has(blockIdx.x, B)) return;
   const int b = P.at(blockIdx.x);
   if (!st.active[b]) return;
@@ -911,6 +912,10 @@ __global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX,
       tr.iteration[e] = 0; tr.ls_iter[e] = 0; tr.alpha[e] = 1.0; tr.rho[e] = st.rho[b];
       tr.J[e] = J; tr.c[e] = c; tr.merit[e] = J + o.mu * c; tr.D[e] = __builtin_nan(""); tr.ratio[e] = __builtin_nan("");
       tr.accepted[e] = 0; tr.pcg_iters[e] = 0; tr.singular[e] = 0;
+      if (activate) {   // a restarted pass / a stream's new problem enters its inner loop (st.active: act_init)
+        st.active[b] = 0;
+        activate[b] = 1;
+      }
       s_choice = -2;
     } else {
       const double J = st.J[b], c = st.c[b], merit = st.merit[b];
@@ -1235,9 +1240,9 @@ void launch_ls_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int 
                       const double* alphas, const SolverOpts& o, const double* terms, double* x, double* u,
                       const double* dx, const double* du, const ProbState& st, const int* pcg_iters,
                       const TraceDev& tr, int* active_count, unsigned long long* counters, const double* hterms,
-                      const int* qp_singular) {
+                      const int* qp_singular, int* activate) {
   hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, P, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u, dx,
-                     du, st, pcg_iters, tr, active_count, counters, hterms, qp_singular);
+                     du, st, pcg_iters, tr, active_count, counters, hterms, qp_singular, activate);
 }
 
 // The problems still alive in the lock-step loop (mask != 0), ascending, and their count: one
@@ -1301,13 +1306,93 @@ __device__ __forceinline__ double soft_v(const ConstrDev* Cs, int t, int e, int 
   return e < n ? z - Cs->lb[t][i] : Cs->ub[t][i] - z;
 }
 
+// A stream's hand-over of slot s, whose problem has just left its outer loop (tmpc_internal.h StreamDev),
+// by the workgroup of k_soft_outer that ended it: the finished problem's trajectory, status and trace rows
+// to its output rows; then, when a problem is pending, its x, u, x[:, 0] and the state a fresh solve
+// starts from -- k_init_state's reset, k_outer_init's, BoxConstraint.__init__'s constants (k_soft_init),
+// a zero PCG warm start -- and act_init, so that its initial merit / cost is evaluated this iteration.
+__device__ void stream_handover(int s, const StreamDev& sd, double* __restrict__ x, double* __restrict__ u,
+                                double* __restrict__ xs, const ProbState& st, int* __restrict__ outer_active,
+                                int* __restrict__ outer_iter, int* __restrict__ exit_soft,
+                                int* __restrict__ act_init, double rho_init, const TraceDev& tr,
+                                const ConstrDev* __restrict__ Cs, double* __restrict__ mu, double* __restrict__ lam,
+                                double* __restrict__ phi, double* __restrict__ lam_warm) {
+  __shared__ int s_next;
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int old = sd.slot_pid[s];
+  const int XN = sd.NX * sd.N, UN = sd.NU * (sd.N - 1), W = sd.W;
+  double* xb = x + (size_t)s * XN;
+  double* ub = u + (size_t)s * UN;
+  if (t == 0) s_next = atomicAdd(sd.next, 1);
+  if (old >= 0) {
+    if (sd.x_out)
+      for (int e = t; e < XN; e += nt) sd.x_out[(size_t)old * XN + e] = xb[e];
+    if (sd.u_out)
+      for (int e = t; e < UN; e += nt) sd.u_out[(size_t)old * UN + e] = ub[e];
+    if (sd.status && t == 0) {
+      int* so = sd.status + (size_t)old * 4;
+      so[0] = st.exit_sqp[s];
+      so[1] = st.iter[s];
+      so[2] = exit_soft[s];
+      so[3] = outer_iter[s];
+    }
+    const TraceDev& to = sd.tr_out;
+    const size_t ri = (size_t)s * W, ro = (size_t)old * W;
+    for (int r = t; r < W; r += nt) {
+#define TMPC_TR_COPY(f) \
+  if (to.f) to.f[ro + r] = tr.f[ri + r];
+      TMPC_TR_COPY(iteration) TMPC_TR_COPY(ls_iter) TMPC_TR_COPY(alpha) TMPC_TR_COPY(rho) TMPC_TR_COPY(J)
+      TMPC_TR_COPY(c) TMPC_TR_COPY(merit) TMPC_TR_COPY(D) TMPC_TR_COPY(ratio) TMPC_TR_COPY(accepted)
+      TMPC_TR_COPY(pcg_iters) TMPC_TR_COPY(singular)
+#undef TMPC_TR_COPY
+    }
+  }
+  __syncthreads();   // every read of the finished problem precedes the writes of the next one
+  const int nw = s_next;
+  if (nw >= sd.P) {
+    if (t == 0) sd.slot_pid[s] = -1;
+    return;
+  }
+  const size_t src = (size_t)(nw % sd.period);
+  for (int e = t; e < XN; e += nt) xb[e] = sd.x_in[src * XN + e];
+  for (int e = t; e < UN; e += nt) ub[e] = sd.u_in[src * UN + e];
+  for (int m = t; m < sd.NX; m += nt) xs[(size_t)s * sd.NX + m] = sd.x_in[src * XN + (size_t)m * sd.N];
+  if (mu) {
+    const int MC = sd.MC;
+    for (int i = t; i < sd.N * MC; i += nt) {
+      const int ty = (i % MC) / (MC / 3);
+      const size_t o = (size_t)s * sd.N * MC + i;
+      mu[o] = Cs->mu_init[ty];
+      lam[o] = 0.0;
+      phi[o] = Cs->phi_init[ty];
+    }
+  }
+  if (lam_warm)
+    for (int e = t; e < sd.NX * sd.N; e += nt) lam_warm[(size_t)s * sd.NX * sd.N + e] = 0.0;
+  if (t == 0) {
+    st.rho[s] = rho_init;
+    st.drho[s] = 1.0;
+    st.iter[s] = 0;
+    st.active[s] = 0;   // set by the initial merit's decision (act_init)
+    st.need_grad[s] = 1;
+    st.exit_sqp[s] = 0;
+    outer_active[s] = 1;
+    outer_iter[s] = 0;
+    exit_soft[s] = 0;
+    act_init[s] = 1;
+    sd.slot_pid[s] = nw;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__ Cs, PList P, int B, int N, int NJ,
-                                                   double tol, int max_iter, const double* __restrict__ x,
-                                                   const double* __restrict__ u, double* __restrict__ mu,
+                                                   double tol, int max_iter, double* __restrict__ x,
+                                                   double* __restrict__ u, double* __restrict__ mu,
                                                    double* __restrict__ lam, double* __restrict__ phi,
                                                    int* __restrict__ outer_active, int* __restrict__ outer_iter,
                                                    int* __restrict__ exit_soft, int* __restrict__ outer_count,
-                                                   ProbState st, int* __restrict__ act_init, double rho_init) {
+                                                   ProbState st, int* __restrict__ act_init, double rho_init,
+                                                   StreamDev sd, double* __restrict__ xs, TraceDev tr,
+                                                   double* __restrict__ lam_warm) {
   if (!P.has(blockIdx.x, B)) return;
   const int b = P.at(blockIdx.x);
   if (!outer_active[b]) return;
@@ -1333,7 +1418,7 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
     mx = fmax(mx, fabs(mn));
   }
   __shared__ double smax[64];
-  __shared__ int s_exit, s_changed;
+  __shared__ int s_exit, s_changed, s_done;
   smax[t0] = mx;
   if (t0 == 0) s_changed = 0;
   __syncthreads();
@@ -1371,6 +1456,7 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
   if (t0 == 0) {
     int ex = s_exit;
     if (ex == 0 && !s_changed) ex = 3;
+    s_done = ex != 0;
     if (ex) {
       exit_soft[b] = ex;
       outer_active[b] = 0;
@@ -1386,29 +1472,24 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
       }
     }
   }
-}
-
-// act_init -> active once the initial merit of a restarted pass is set
-__global__ void k_activate(PList P, int B, int* __restrict__ act_init, int* __restrict__ active) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (!P.has(p, B)) return;
-  const int b = P.at(p);
-  if (!act_init[b]) return;
-  act_init[b] = 0;
-  active[b] = 1;
-}
-
-void launch_activate(hipStream_t s, PList P, int B, int* act_init, int* active) {
-  hipLaunchKernelGGL(k_activate, TMPC_GRID(B, 256), 0, s, P, B, act_init, active);
+  if (sd.P > 0) {   // a stream (per-problem mode): a finished problem hands its slot on
+    __syncthreads();
+    if (s_done)
+      stream_handover(b, sd, x, u, xs, st, outer_active, outer_iter, exit_soft, act_init, rho_init, tr, Cs, mu, lam,
+                      phi, lam_warm);
+  }
 }
 
 void launch_soft_outer(hipStream_t s, const ConstrDev* Cs, PList P, int B, int N, int nj, double tol, int max_iter,
-                       const double* x, const double* u, double* mu, double* lam, double* phi, int* outer_active,
+                       double* x, double* u, double* mu, double* lam, double* phi, int* outer_active,
                        int* outer_iter, int* exit_soft, int* outer_count, const ProbState* st, int* act_init,
-                       double rho_init) {
+                       double rho_init, const StreamDev* sd, double* xs, const TraceDev* tr, double* lam_warm) {
   ProbState none{};
+  StreamDev nosd{};
+  TraceDev notr{};
   hipLaunchKernelGGL(k_soft_outer, dim3(B), dim3(64), 0, s, Cs, P, B, N, nj, tol, max_iter, x, u, mu, lam, phi,
-                     outer_active, outer_iter, exit_soft, outer_count, st ? *st : none, act_init, rho_init);
+                     outer_active, outer_iter, exit_soft, outer_count, st ? *st : none, act_init, rho_init,
+                     sd ? *sd : nosd, xs, tr ? *tr : notr, lam_warm);
 }
 
 // BoxConstraint.__init__ (:21-24): mu = mu_init, lambda = 0, phi = phi_init
@@ -1464,6 +1545,27 @@ void launch_soft_init(hipStream_t s, const ConstrDev* Cs, size_t total, int MC, 
   hipLaunchKernelGGL(k_soft_init, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, Cs, total, MC, mu, lam,
                      phi);
 }
+
+// ======================================================================= continuous batching (tmpc_internal.h)
+// slot s starts with problem s: one 256-thread workgroup per slot copies its inputs (x, u are read and
+// written with unit stride, so a workgroup's loads and stores coalesce)
+__global__ void __launch_bounds__(256) k_stream_init(int B, StreamDev sd, double* __restrict__ x,
+                                                     double* __restrict__ u) {
+  const int s = blockIdx.x, t = threadIdx.x;
+  const int XN = sd.NX * sd.N, UN = sd.NU * (sd.N - 1);
+  const size_t src = (size_t)(s % sd.period);
+  for (int e = t; e < XN; e += blockDim.x) x[(size_t)s * XN + e] = sd.x_in[src * XN + e];
+  for (int e = t; e < UN; e += blockDim.x) u[(size_t)s * UN + e] = sd.u_in[src * UN + e];
+  if (t == 0) {
+    sd.slot_pid[s] = s;
+    if (s == 0) *sd.next = B;   // the next pending problem (stream_handover takes them with atomics)
+  }
+}
+
+void launch_stream_init(hipStream_t s, int B, const StreamDev& sd, double* x, double* u) {
+  hipLaunchKernelGGL(k_stream_init, dim3(B), dim3(256), 0, s, B, sd, x, u);
+}
+
 
 // dispatch tables over the joint count and the chain specialisation
 #ifdef TMPC_DEV_NJ
