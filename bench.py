@@ -96,14 +96,23 @@ def parse(argv=None):
                          "is set, else os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the config-4 line the default (headline) run adds after its own measurement")
-    ap.add_argument("--secondary-steps", type=int, default=3)
+                    help="skip the other BASELINE configurations' lines the default (headline) run adds after its "
+                         "own measurement")
+    ap.add_argument("--skip-lines", default="", help="comma-separated lines to skip: secondary, hard_limits, config2, "
+                                                     "config3, config3_fp32, config5")
+    ap.add_argument("--secondary-steps", type=int, default=16)
     ap.add_argument("--secondary-parity", type=int, default=64, help="config-4 problems checked against the oracle")
-    ap.add_argument("--no-hard-line", action="store_true",
-                    help="skip the hard-limit line (ACTIVE_SET torque + velocity) after the headline")
-    ap.add_argument("--hard-steps", type=int, default=3)
-    ap.add_argument("--hard-parity", type=int, default=16, help="hard-limit problems checked against the oracle")
-    return ap.parse_args(argv)
+    ap.add_argument("--hard-steps", type=int, default=16)
+    ap.add_argument("--hard-parity", type=int, default=64, help="hard-limit problems checked against the oracle")
+    ap.add_argument("--config-steps", type=int, default=16, help="timed steps of the config 2 / 3 lines")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="time each step as one lock-step batched solve (D2D restore + solve to every problem's "
+                         "exit) instead of the continuous-batching stream")
+    ap.add_argument("--lockstep-steps", type=int, default=2,
+                    help="lock-step steps timed beside each streamed line (its `lockstep` rate; 0: skip)")
+    a = ap.parse_args(argv)
+    a.skip_lines = [v for v in a.skip_lines.split(",") if v]
+    return a
 
 
 def initial_states(n, B, seed0, scale=1.0):
@@ -287,20 +296,22 @@ def _gpu_iterate(ctx, x0, u0, N, dt, method, gr, i, j):
     return xi, ui, rho
 
 
-def classify_hard_mismatch(ctx, x0, u0, N, dt, method, gr, i, ref):
-    """Why a problem's hard-limit run differs from the oracle's, replayed on the GPU's own inputs
-    (tests/test_gpu_hard.py does this for every QP):
+def classify_hard_mismatch(ctx, x0, u0, N, dt, method, gr, i, ref, limits="torque-velocity-as"):
+    """Why a problem's hard-limit run differs from the oracle's, replayed at the first point the runs part,
+    on the GPU's own inputs (tests/test_gpu_hard_arm6.py does this for every QP of every fixture problem).
+    Returns a dict whose "kind" is:
       * "pcg_count": at the first QP j where the PCG counts differ, the GPU's own iterate j is re-solved on
-        the device (tmpc_qp_batch) and the oracle's canonical-order PCG (oracle/hard.py pcg_canonical)
-        runs on that QP's own S and gamma: it takes the GPU's count -- the runs' S differ in the last
-        bits (the GPU's and the oracle's dynamics / Schur formation) on a count the summation order
-        decides;
+        the device (tmpc_qp_batch) and takes the run's count, and the oracle's canonical-order PCG
+        (oracle/hard.py pcg_canonical) on that QP's own S and gamma takes it too -- the runs' S differ in the
+        last bits (the GPU's and the oracle's dynamics / Schur formation) on a count the rounding decides;
       * "line_search": every common QP's count agrees and the runs part at the first iteration j whose
-        line-search outcome (alpha, success) differs: the oracle's line search (oracle/sqp.py
-        line_search), run at the GPU's iterate j along the GPU's own direction for it, takes the GPU's
-        outcome -- the runs' directions differ in the last bits (their QPs' S do), and the trial's
-        acceptance is decided there;
-      * None: not reproduced."""
+        line-search outcome (alpha, success) differs.  At the GPU's iterate j the oracle's line search
+        (oracle/sqp.py line_search) along the GPU's direction takes the GPU's outcome, AND along the
+        oracle's own direction (its own dense KKT solve in the canonical PCG order at that iterate and rho)
+        takes the oracle run's outcome: the two directions -- whose relative difference is reported -- decide
+        the step, not the line search;
+      * None: not reproduced (the dict says which replay failed).
+    The cost, limits and options are the bench's (the arguments), not fixed."""
     from oracle import hard as ohard
     from oracle import sqp as osqp
     from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
@@ -309,12 +320,13 @@ def classify_hard_mismatch(ctx, x0, u0, N, dt, method, gr, i, ref):
     o_counts = list(ref["pcg_iters"])
     o = ctx.options
     nx = x0.shape[1]
+    n = nx // 2
     j = next((q for q in range(min(len(g_counts), len(o_counts))) if g_counts[q] != o_counts[q]), None)
     if j is not None:
         xi, ui, rho = _gpu_iterate(ctx, x0, u0, N, dt, method, gr, i, j)
         q = ctx.qp_batch(xi, ui, N, dt, np.array([rho]), method, want_blocks=False, xs=x0[i:i + 1, :, 0])
         if int(q["pcg_iters"][0]) != g_counts[j]:
-            return None
+            return {"kind": None, "j": j, "failed": "the GPU's QP at its own iterate did not retake its count"}
         info = ctx.qp_hard_info(1, N)
         D, W = int(info["dim"][0]), int(info["W"])
         S = np.zeros((D, D))
@@ -325,27 +337,45 @@ def classify_hard_mismatch(ctx, x0, u0, N, dt, method, gr, i, ref):
             S[a[ok], c[ok]] = info["S_band"][0][a[ok], off]
         _, it_c = ohard.pcg_canonical(S, info["gamma"][0, :D], nx, method[4:], o.exit_tolerance_linSys,
                                       o.max_iter_linSys)
-        return "pcg_count" if it_c == g_counts[j] else None
+        return {"kind": "pcg_count" if it_c == g_counts[j] else None, "j": j, "gpu_count": g_counts[j],
+                "oracle_count": o_counts[j], "canonical_on_gpu_S": it_c}
     g_ls = [(float(gr["trace"]["alpha"][i, q + 1]), bool(gr["trace"]["succeeded_line_search"][i, q + 1]))
-            for q in range(it)]
+            for q in range(it + (1 if ex == 3 else 0))]
     o_ls = list(zip(ref["alpha"], ref["succeeded"]))
     j = next((q for q in range(min(len(g_ls), len(o_ls))) if g_ls[q] != o_ls[q]), None)
     if j is None:
-        return None
+        return {"kind": None, "failed": "no differing PCG count or line-search outcome"}
     xi, ui, rho = _gpu_iterate(ctx, x0, u0, N, dt, method, gr, i, j)
     q = ctx.qp_batch(xi, ui, N, dt, np.array([rho]), method, want_blocks=False, xs=x0[i:i + 1, :, 0])
-    n = nx // 2
     m = parse_urdf(planar_arm_urdf(n))
     cost = osqp.QuadCost(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(n), np.zeros(nx))
-    lims = [ohard.HardLimit(k, n, v["lb"], v["ub"], v["mode"]) for k, v in LIMIT_PRESETS["torque-velocity-as"].items()]
+    lims = [ohard.HardLimit(k, n, v["lb"], v["ub"], v["mode"]) for k, v in LIMIT_PRESETS[limits].items()]
     hc = ohard.HardConstraints(lims)
     xs = x0[i, :, 0].copy()
+    opts = {k: getattr(o, k) for k in ("exit_tolerance_linSys", "max_iter_linSys", "alpha_factor_SQP_DDP",
+                                       "alpha_min_SQP_DDP", "expected_reduction_min_SQP_DDP",
+                                       "expected_reduction_max_SQP_DDP")}
+    oo = osqp.default_options(opts)
     with np.errstate(all="ignore"):
         J = osqp.total_cost(cost, xi[0], ui[0], N, None)
         c = osqp.total_violation(m, xi[0], ui[0], xs, N, dt, hc)
-        r1 = osqp.line_search(cost, m, xi[0], ui[0], xs, N, dt, q["dxul"][0], J, J + 10 * c, 10,
-                              osqp.default_options({}), None, hc)
-    return "line_search" if (float(r1["alpha"]), bool(r1["succeeded_line_search"])) == g_ls[j] else None
+        merit = J + o.merit_mu * c
+        d_g = q["dxul"][0]
+        r_g = osqp.line_search(cost, m, xi[0], ui[0], xs, N, dt, d_g, J, merit, o.merit_mu, oo, None, hc)
+        G, g, Cm, cc = ohard.kkt_dense(m, cost, xi[0], ui[0], xs, N, dt, hc, None)
+        d_o, _, _ = ohard.solve_qp_dense(G, g, Cm, cc, rho, method, oo, nx, {}, "canonical")
+        r_o = osqp.line_search(cost, m, xi[0], ui[0], xs, N, dt, d_o, J, merit, o.merit_mu, oo, None, hc)
+    npr = (nx + n) * (N - 1) + nx   # the primal part the line search steps along
+    d_o = np.asarray(d_o, dtype=float).reshape(-1)[:npr]
+    delta = float(np.max(np.abs(d_g[:npr] - d_o)) / max(1e-300, float(np.max(np.abs(d_o)))))
+    out_g = (float(r_g["alpha"]), bool(r_g["succeeded_line_search"]))
+    out_o = (float(r_o["alpha"]), bool(r_o["succeeded_line_search"]))
+    gpu_ok = out_g == g_ls[j]
+    ora_ok = out_o == o_ls[j]
+    return {"kind": "line_search" if gpu_ok and ora_ok else None, "j": j, "gpu_outcome": g_ls[j],
+            "oracle_outcome": o_ls[j], "oracle_ls_on_gpu_direction": out_g, "oracle_ls_on_oracle_direction": out_o,
+            "direction_rel_diff": delta, "pcg_counts_at_j": [g_counts[j] if j < len(g_counts) else None,
+                                                            o_counts[j] if j < len(o_counts) else None]}
 
 
 def parity_check(gpu, cpu):
@@ -360,7 +390,7 @@ def parity_check(gpu, cpu):
             mism.append(i)
         for a, b in ((gpu["x"][i], c["x"]), (gpu["u"][i], c["u"])):
             worst = max(worst, float(np.max(np.abs(a - b))) / max(1.0, float(np.max(np.abs(b)))))
-    return {"checked": len(cpu), "mismatches": len(mism), "mismatched_problems": mism[:16],
+    return {"checked": len(cpu), "mismatches": len(mism), "mismatched_problems": mism[:64],
             "compared": "exit_sqp, sqp_iter, per-QP PCG iteration counts (exact); final x, u",
             "max_traj_rel_diff": worst}
 
@@ -599,6 +629,294 @@ def _standin():
     return mod
 
 
+def solver_name(a):
+    """the stream / batch entry points' solver argument: "iLQR" or the SQP linear-system method"""
+    return "iLQR" if a.solver == "ilqr" else a.method
+
+
+def setup_workload(ctx, a):
+    """model, cost, limits and options of workload `a` on the context (every line of the run re-does this)"""
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    n = a.links
+    nx, nu = 2 * n, n
+    model = parse_urdf(planar_arm_urdf(n))
+    ctx.set_model(model)
+    if a.cost == "ee":
+        if n != 2:
+            raise SystemExit("--cost ee needs --links 2 (UrdfCost is 2-link only, SURVEY F5)")
+        ctx.set_cost_ee(np.eye(4), 100 * np.eye(4), 0.1 * np.eye(2), np.array([-1.0, 1.5, 0.0, 0.0]), None,
+                        model.H0[:2], model.Ha[:2], model.Hb[:2])
+    else:
+        ctx.set_cost_quadratic(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
+    ctx.set_options(precision=0, pcg_warm_start=0)
+    ctx.set_box_limits(LIMIT_PRESETS[a.limits])
+    return model
+
+
+def workload_inputs(ctx, comm, rank, a):
+    """§8d workload of `a` for this rank: rank 0 draws every rank's start states, RCCL broadcast, the rank's
+    slice resident in HBM, x = the fp64 Euler rollout of u = 0 on the device.  Returns the device buffers
+    (initial x0, u0 and working x, u) and the host u0."""
+    n, N, B, dt = a.links, a.N, a.batch, 0.1
+    nx, nu = 2 * n, n
+    from trajoptmpcreference_amd import dist
+    q0 = dist.scatter_from_root(comm, rank, B, lambda count: initial_states(n, count, a.seed0, a.q0_scale), (n,))
+    x0 = np.zeros((B, nx, N))
+    x0[:, :n, 0] = q0
+    u0 = np.zeros((B, nu, N - 1))
+    d = dict(x0=ctx.alloc(x0.nbytes), u0=ctx.alloc(u0.nbytes), x=ctx.alloc(x0.nbytes), u=ctx.alloc(u0.nbytes),
+             xb=x0.nbytes, ub=u0.nbytes)
+    ctx.h2d(d["x0"], x0)
+    ctx.h2d(d["u0"], u0)
+    ctx.rollout_device(B, N, dt, d["x0"], d["u0"])
+    # after the fp64 workload rollout: the line's precision and PCG warm start
+    ctx.set_options(precision={"fp64": 0, "fp32": 1, "mixed": 2}[a.precision], pcg_warm_start=int(a.pcg_warm_start))
+    if a.erm is not None:
+        ctx.set_options(expected_reduction_min_SQP_DDP=float(a.erm))
+    return d, u0
+
+
+def free_inputs(ctx, d):
+    for k in ("x0", "u0", "x", "u"):
+        ctx.free(d[k])
+
+
+def soft_limits(a):
+    return a.limits != "none" and not hard_limits(a.limits)
+
+
+def batch_solve(ctx, a, d, want_status=False, mpc=None):
+    """one lock-step batched solve of the B resident problems from their initial trajectories (D2D restore
+    first; soft limits from their initial constants); mpc: the MPC loop's output buffers"""
+    B, N, dt = a.batch, a.N, 0.1
+    ctx.d2d(d["x"], d["x0"], d["xb"])
+    ctx.d2d(d["u"], d["u0"], d["ub"])
+    if soft_limits(a):
+        ctx.set_soft_state(B, N)
+    if a.mpc_steps > 0:
+        ctx.mpc_batch_device(B, N, dt, solver_name(a), a.mpc_steps, d["x"], d["u"], mpc["xe"], mpc["ue"],
+                             mpc["codes"], mpc["iters"])
+        if want_status:
+            codes = np.zeros((B, a.mpc_steps), dtype=np.int32)
+            its = np.zeros((B, a.mpc_steps), dtype=np.int32)
+            ctx.d2h(codes, mpc["codes"])
+            ctx.d2h(its, mpc["iters"])
+            return codes.reshape(-1), its.reshape(-1)
+        return None, None
+    if a.solver == "ilqr":
+        return ctx.ilqr_solve_batch_device(B, N, dt, d["x"], d["u"], want_status=want_status)
+    return ctx.sqp_solve_batch_device(B, N, dt, d["x"], d["u"], a.method, want_status=want_status)
+
+
+KERNEL_NAMES = ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "schur", "btsolve", "dxu", "ls_terms", "ls_decide",
+                "hard_schur", "hard_pcg", "hard_direct", "ilqr_backward", "ilqr_forward", "ilqr_decide", "mpc_shift",
+                "soft_outer", "init_merit"]
+
+
+def kernel_table(ctx):
+    kernels = {}
+    for name in KERNEL_NAMES:
+        cnt, ms = ctx.kernel_stats(name)
+        if cnt:
+            kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
+    return kernels
+
+
+def measure(ctx, comm, a, d, steps, warmup, stream, sbuf=None, mpc=None):
+    """The timed region of one line: `warmup` untimed steps, then `steps` timed ones between barrier +
+    synchronize, the max over ranks.  stream: the steps' B x steps problems go through the B slots of one
+    continuous-batching solve (tmpc_*_solve_stream_device: problem p starts from resident input p % B,
+    results to the sbuf output rows); else each step is a D2D restore + one lock-step batched solve.
+    Returns (elapsed s, work counters, kernel table, k_hard_pcg's counted bytes or None)."""
+    B, N, dt = a.batch, a.N, 0.1
+
+    def stream_solve(copies):
+        ctx.solve_stream_device(solver_name(a), B * copies, B, N, dt, d["x0"], d["u0"], B, sbuf["x"], sbuf["u"],
+                                sbuf["st"])
+
+    if stream:
+        if warmup > 0:
+            stream_solve(warmup)
+    else:
+        for _ in range(warmup):
+            batch_solve(ctx, a, d, mpc=mpc)
+    ctx.synchronize()
+    ctx.set_options(profile=1)
+    ctx.reset_stats()
+    counters = np.zeros(4, dtype=np.int64)
+    comm.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    if stream:
+        stream_solve(steps)
+        counters += np.array(ctx.solve_counters(), dtype=np.int64)
+    else:
+        for _ in range(steps):
+            batch_solve(ctx, a, d, mpc=mpc)
+            counters += np.array(ctx.solve_counters(), dtype=np.int64)
+    ctx.synchronize()
+    comm.barrier()
+    elapsed = comm.max(time.perf_counter() - t0)
+    ctx.set_options(profile=0)
+    if not stream:
+        counters[3] = counters[3] // max(1, steps)   # line-search trials per QP (each solve reports it)
+    hard_bytes = ctx.kernel_bytes("hard_pcg") if hard_limits(a.limits) and a.method != "S" else None
+    return elapsed, counters, kernel_table(ctx), hard_bytes
+
+
+def stream_buffers(ctx, a, copies):
+    n, N, B = a.links, a.N, a.batch
+    P = B * copies
+    return dict(x=ctx.alloc(P * 2 * n * N * 8), u=ctx.alloc(P * n * (N - 1) * 8), st=ctx.alloc(P * 4 * 4), P=P)
+
+
+def free_stream_buffers(ctx, sbuf):
+    for k in ("x", "u", "st"):
+        ctx.free(sbuf[k])
+
+
+def stream_check(ctx, a, d, sbuf, copies, ex_b, it_b, xb):
+    """The streamed problems against the lock-step batch solve of the same inputs (ex_b, it_b, xb: its exit
+    codes, iteration counts and x): every stream problem's exit code and iteration count, and the final x of
+    the first and the last copy of the batch bitwise (each problem's operations are the batch solve's)."""
+    n, N, B = a.links, a.N, a.batch
+    P = B * copies
+    st = np.empty((P, 4), dtype=np.int32)
+    ctx.d2h(st, sbuf["st"])
+    mism = int(np.sum((st[:, 0] != np.tile(ex_b, copies)) | (st[:, 1] != np.tile(it_b, copies))))
+    xs = np.empty((B, 2 * n, N))
+    xm = []
+    for c in sorted({0, copies - 1}):
+        ctx.d2h(xs, sbuf["x"], offset=c * xs.nbytes)
+        xm.append(int(np.sum(np.any(xs != xb, axis=(1, 2)))))
+    return {"problems": P, "status_mismatches": mism, "x_copies_compared": sorted({0, copies - 1}),
+            "x_mismatches": int(sum(xm)),
+            "compared": "each streamed problem's exit code and iteration count against the lock-step batch solve of "
+                        "its input; final x of the first and last copies bitwise"}
+
+
+STREAM_BASIS = ("continuous batching (tmpc_sqp_solve_stream_device / tmpc_ilqr_solve_stream_device): the timed "
+                "region solves steps x B problems (problem p starts from resident input p mod B) through B resident "
+                "slots; a slot whose problem exits takes the next pending one in the same batch iteration, so the "
+                "GPU never runs a near-empty lock-step tail.  Inputs resident in HBM before the timed region; every "
+                "problem's results (x, u, exit code, iterations) are written to its own output rows.  ms_per_step = "
+                "time / steps, i.e. per B problems.  Each problem's results equal its lock-step batch solve's "
+                "bitwise (stream_check; tests/test_gpu_stream.py).  lockstep: the same workload one batch at a "
+                "time (D2D restore + solve to every problem's exit), the round-5 definition")
+
+
+def run_line(ctx, comm, rank, world, a, steps, warmup, stream, lockstep_steps):
+    """Measure workload `a` (B = a.batch problems per rank): the line's value (solves/s over all ranks), its
+    kernel table and work counters, the stream's check against the lock-step solve, and the lock-step rate.
+    Returns (line dict, device inputs, host u0, the lock-step batch's status / x)."""
+    setup_workload(ctx, a)
+    d, u0 = workload_inputs(ctx, comm, rank, a)
+    B, N = a.batch, a.N
+    mpc = None
+    if a.mpc_steps > 0:
+        n = a.links
+        K1 = a.mpc_steps
+        mpc = dict(xe=ctx.alloc(B * 2 * n * (K1 + 1) * 8), ue=ctx.alloc(B * n * K1 * 8),
+                   codes=ctx.alloc(B * K1 * 4), iters=ctx.alloc(B * K1 * 4))
+        stream = False   # the MPC loop's horizon solves are lock-step batches (tmpc_mpc_batch_device)
+    sbuf = stream_buffers(ctx, a, max(steps, warmup, 1)) if stream else None
+    elapsed, counters, kernels, hard_bytes = measure(ctx, comm, a, d, steps, warmup, stream, sbuf, mpc)
+    units = max(1, a.mpc_steps)
+    value = B * steps * world * units / elapsed
+    line = {"value": value, "unit": "solves/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": 1000.0 * elapsed / steps, "higher_is_better": True, "scaling": "weak",
+            "mode": "stream" if stream else ("lockstep MPC loop" if mpc else "lockstep")}
+    # the lock-step batch solve of the same inputs: status for the gather and the stream check
+    ex_b, it_b = batch_solve(ctx, a, d, want_status=True, mpc=mpc)
+    if stream:
+        xb = np.empty((B, 2 * a.links, N))
+        ctx.d2h(xb, d["x"])
+        line["stream_check"] = stream_check(ctx, a, d, sbuf, steps, ex_b, it_b, xb)   # the timed stream's rows
+        free_stream_buffers(ctx, sbuf)
+        if lockstep_steps > 0:
+            el, _, _, _ = measure(ctx, comm, a, d, lockstep_steps, 1, False)
+            line["lockstep"] = {"value": B * lockstep_steps * world / el, "ms_per_step": 1000.0 * el / lockstep_steps,
+                                "steps": lockstep_steps}
+    it_name = "ilqr_decide" if a.solver == "ilqr" else "ls_decide"
+    if it_name in kernels:
+        line["batch_iterations"] = {
+            "per_step": kernels[it_name]["launches"] / steps / units,
+            "problem_iterations_mean": int(counters[0]) / (B * steps * units),
+            "slot_utilization": int(counters[0]) / max(1, kernels[it_name]["launches"] * B)}
+    line["work"] = {"problem_qps_per_step": int(counters[0]) / steps, "pcg_iters_per_step": int(counters[1]) / steps,
+                    "grad_evals_per_step": int(counters[2]) / steps, "ls_trials_per_qp": int(counters[3])}
+    line["kernels"] = kernels
+    line["dominant_kernel"] = max(kernels, key=lambda k: kernels[k]["total_ms"]) if kernels else None
+    from trajoptmpcreference_amd import dist
+    g = dist.gather_summaries(comm, exit_codes=ex_b.astype(np.int32), iters=it_b.astype(np.int32))
+    line["exit_codes"] = {str(k): int(v) for k, v in zip(*np.unique(g["exit_codes"], return_counts=True))}
+    line["iters_mean"] = float(np.mean(g["iters"]))
+    line["iters_max"] = int(np.max(g["iters"]))
+    line["problems_gathered"] = int(g["exit_codes"].size)
+    if mpc:
+        for k in ("xe", "ue", "codes", "iters"):
+            ctx.free(mpc[k])
+    return line, d, u0, counters, kernels, hard_bytes
+
+
+def line_roofline(a, N, nx, nu, kernels, counters, hard_bytes=None):
+    if a.solver == "sqp" and a.method.startswith("PCG") and "qp" in kernels and (a.mpc_steps == 0 or N * nx > 1024):
+        return sqp_roofline(a, N, nx, nu, kernels, counters)
+    if hard_bytes and "hard_pcg" in kernels:
+        return hard_roofline(a, kernels, hard_bytes)
+    if a.solver == "ilqr" and "ilqr_backward" in kernels:
+        bw = kernels["ilqr_backward"]
+        per_launch = int(counters[0]) / max(1, bw["launches"])
+        flops = per_launch * (N - 1) * ilqr_backward_flops_per_knot(nx, nu)
+        ach = flops / (bw["avg_ms"] / 1e3) / 1e12
+        f32 = a.precision == "fp32"
+        peak = FP32_PEAK_TFLOPS if f32 else FP64_PEAK_TFLOPS
+        traffic, src = measured_traffic("void tmpc::k_ilqr_backward<", workload_key(a))
+        r = {"kernel": "k_ilqr_backward", "bound": "fp32-valu" if f32 else "fp64-valu", "achieved": ach,
+             "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": traffic,
+             "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
+             "note": "sequential Riccati sweep, latency-bound (one 64-lane wave per problem)"}
+        if traffic:
+            r.update(hbm_GBps=traffic / (bw["avg_ms"] / 1e3) / 1e9, traffic_source=src)
+        fw = kernels.get("ilqr_forward")
+        if fw:
+            ft, fsrc = measured_traffic("void tmpc::k_ilqr_forward<", workload_key(a))
+            r["forward"] = {"kernel": "k_ilqr_forward", "avg_launch_ms": fw["avg_ms"], "traffic": ft,
+                            "hbm_GBps": ft / (fw["avg_ms"] / 1e3) / 1e9 if ft else None}
+        return r
+    return None
+
+
+def line_config(a, world, name):
+    B = a.batch
+    return {"workload": f"arm{a.links}.urdf{' (joint6 fixed)' if a.links == 6 else ''} N={a.N} {name}, batch {B} per GPU"
+                        + ("" if a.limits == "none" else f", limits {a.limits}")
+                        + (", UrdfCost" if a.cost == "ee" else "")
+                        + ("" if a.precision == "fp64" else f", precision {a.precision}")
+                        + (f", MPC loop of {a.mpc_steps} steps" if a.mpc_steps > 0 else "")
+                        + (", PCG warm start" if a.pcg_warm_start else ""),
+            "global_batch": B * world, "N": a.N, "method": a.method if a.solver == "sqp" else "iLQR",
+            "parallelism": f"shard{world} (RCCL broadcast of start states, gather of results)"}
+
+
+def workload_name(a):
+    name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
+    if a.limits != "none":
+        name += f", {'hard' if hard_limits(a.limits) else 'soft'} box constraints {a.limits}"
+    if a.cost == "ee":
+        name += ", UrdfCost end-effector cost (twolinks.py goal)"
+    if a.mpc_steps > 0:
+        name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
+    if a.precision != "fp64":
+        name += ", fp32 dynamics + Riccati" if a.precision == "fp32" else ", mixed fp32 dynamics / fp64 PCG"
+    return name
+
+
+def is_headline(a):
+    return a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and a.limits == "none" and \
+        a.cost == "quadratic" and a.N == 64 and a.precision == "fp64" and a.links == 6
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -618,181 +936,37 @@ def main():
     cfg = dist.config_hash({k: v for k, v in sorted(vars(a).items()) if k != "cpu_procs"}, model.X0, model.Xa,
                            model.Xb, model.I, np.asarray(model.parent), bytes(ctx.options))
     comm = standin.make_comm(ctx, rank, world, cfg) if standin else dist.make_comm(ctx, rank, world, cfg)
-    ctx.set_model(model)
-    if a.cost == "ee":
-        if n != 2:
-            raise SystemExit("--cost ee needs --links 2 (UrdfCost is 2-link only, SURVEY F5)")
-        ctx.set_cost_ee(np.eye(4), 100 * np.eye(4), 0.1 * np.eye(2), np.array([-1.0, 1.5, 0.0, 0.0]), None,
-                        model.H0[:2], model.Ha[:2], model.Hb[:2])
-    else:
-        ctx.set_cost_quadratic(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(nu), np.zeros(nx))
-    limits = LIMIT_PRESETS[a.limits]
-    ctx.set_box_limits(limits)
-
-    # ---- workload: rank 0 draws every rank's start states, RCCL broadcast, own slice resident in HBM
-    q0 = dist.scatter_from_root(comm, rank, B, lambda count: initial_states(n, count, a.seed0, a.q0_scale), (n,))
-    x0 = np.zeros((B, nx, N))
-    x0[:, :n, 0] = q0
-    u0 = np.zeros((B, nu, N - 1))
-    xb, ub = x0.nbytes, u0.nbytes
-    d_x0, d_u0, d_x, d_u = ctx.alloc(xb), ctx.alloc(ub), ctx.alloc(xb), ctx.alloc(ub)
-    ctx.h2d(d_x0, x0)
-    ctx.h2d(d_u0, u0)
-    ctx.rollout_device(B, N, dt, d_x0, d_u0)
-    prec_id = {"fp64": 0, "fp32": 1, "mixed": 2}[a.precision]
-    ctx.set_options(precision=prec_id, pcg_warm_start=int(a.pcg_warm_start))   # after the fp64 workload rollout
-    if a.erm is not None:
-        ctx.set_options(expected_reduction_min_SQP_DDP=float(a.erm))
-
-    if a.mpc_steps > 0:
-        K1 = a.mpc_steps
-        d_xe, d_ue = ctx.alloc(B * nx * (K1 + 1) * 8), ctx.alloc(B * nu * K1 * 8)
-        d_codes, d_iters = ctx.alloc(B * K1 * 4), ctx.alloc(B * K1 * 4)
-
-    def solve(want_status=False):
-        if a.mpc_steps > 0:
-            ctx.mpc_batch_device(B, N, dt, "iLQR" if a.solver == "ilqr" else a.method, a.mpc_steps, d_x, d_u, d_xe,
-                                 d_ue, d_codes, d_iters)
-            if want_status:
-                codes = np.zeros((B, a.mpc_steps), dtype=np.int32)
-                its = np.zeros((B, a.mpc_steps), dtype=np.int32)
-                ctx.d2h(codes, d_codes)
-                ctx.d2h(its, d_iters)
-                return codes.reshape(-1), its.reshape(-1)
-            return None, None
-        if a.solver == "ilqr":
-            return ctx.ilqr_solve_batch_device(B, N, dt, d_x, d_u, want_status=want_status)
-        return ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=want_status)
-
-    def step():
-        ctx.d2d(d_x, d_x0, xb)
-        ctx.d2d(d_u, d_u0, ub)
-        if limits:
-            ctx.set_soft_state(B, N)   # every step starts from the initial mu / lambda / phi
-        solve()
-
-    for _ in range(a.warmup):
-        step()
-    ctx.synchronize()
-    ctx.set_options(profile=1)
-    ctx.reset_stats()
-    counters = np.zeros(4, dtype=np.int64)
-    comm.barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-        counters += np.array(ctx.solve_counters(), dtype=np.int64)
-    ctx.synchronize()
-    comm.barrier()
-    t1 = time.perf_counter()
-    elapsed = comm.max(t1 - t0)
-    ctx.set_options(profile=0)
-    hard_bytes = ctx.kernel_bytes("hard_pcg") if limits and a.method != "S" and hard_limits(a.limits) else None
-
-    kernels = {}
-    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "schur", "btsolve", "dxu", "ls_terms", "ls_decide",
-                 "hard_schur", "hard_pcg", "hard_direct", "ilqr_backward", "ilqr_forward", "ilqr_decide",
-                 "mpc_shift"]:
-        cnt, ms = ctx.kernel_stats(name)
-        if cnt:
-            kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
-    dominant = max(kernels, key=lambda k: kernels[k]["total_ms"])
-
-    total_solves = B * a.steps * world * max(1, a.mpc_steps)
-    value = total_solves / elapsed
-    ms_per_step = 1000.0 * elapsed / a.steps
-
-    # ---- status of one solve (exit codes / iteration counts), gathered from every rank over RCCL
-    ctx.d2d(d_x, d_x0, xb)
-    ctx.d2d(d_u, d_u0, ub)
-    if limits:
-        ctx.set_soft_state(B, N)
-    exit_codes, iters = solve(want_status=True)
-    g = dist.gather_summaries(comm, exit_codes=exit_codes.astype(np.int32), iters=iters.astype(np.int32))
-    exit_all, iters_all = g["exit_codes"], g["iters"]
-
-    # ---- PCIe-inclusive rate: the same batch through the host-array entry point (H2D + solve + D2H)
+    stream = not a.lockstep and a.mpc_steps == 0
+    line, d, u0, counters, kernels, hard_bytes = run_line(ctx, comm, rank, world, a, a.steps, a.warmup, stream,
+                                                          a.lockstep_steps if stream else 0)
+    headline = is_headline(a)
+    # ---- PCIe-inclusive rate: the same steps x B problems with host inputs and outputs (H2D of x0 / u0, the
+    # stream, D2H of every problem's x, u and status) -- BASELINE.md section 3's wall-time definition
     pcie = None
-    if a.solver == "sqp" and a.mpc_steps == 0 and not limits and a.cost == "quadratic":
-        xh = np.empty((B, nx, N))
-        ctx.d2h(xh, d_x0)
-        ctx.synchronize()
-        tp = time.perf_counter()
-        ctx.sqp_solve_batch(xh, u0, N, dt, a.method, with_trace=False)
-        tp = time.perf_counter() - tp
-        pcie = {"value": B / tp, "unit": "solves/s", "ms_per_solve_batch": 1000.0 * tp,
-                "note": "tmpc_sqp_solve_batch with host x/u (H2D, solve, D2H of x, u and the status arrays), "
-                        "one batch, this GPU; `value` above is the HBM-resident rate"}
+    if headline:
+        xh = x0_host(ctx, d["x0"], B, nx, N)
+        pcie = pcie_inclusive(ctx, a, xh, u0, stream)
     comm.barrier()
-    headline = a.solver == "sqp" and a.method == "PCG-SS" and a.mpc_steps == 0 and not limits and \
-        a.cost == "quadratic" and N == 64 and a.precision == "fp64"
-    # BASELINE config 4 beside the headline (after its measurement; every rank takes part)
-    secondary = None
-    if headline and not a.no_secondary and n == 6:
-        secondary = run_secondary(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0)
-    hard_line = None
-    if headline and not a.no_hard_line and n == 6:
-        hard_line = run_hard_line(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0)
-
+    extra = {}
+    if headline and not a.no_secondary:
+        extra = run_config_lines(ctx, comm, rank, world, a)
     if rank != 0:
         comm.close()
         return
-
-    name = 'iLQR' if a.solver == 'ilqr' else 'SQP ' + a.method
-    if a.limits != "none":
-        name += f", {'hard' if hard_limits(a.limits) else 'soft'} box constraints {a.limits}"
-    if a.cost == "ee":
-        name += ", UrdfCost end-effector cost (twolinks.py goal)"
-    if a.mpc_steps > 0:
-        name = f"receding-horizon MPC loop of {a.mpc_steps} horizon solves, {name}"
-    if a.precision != "fp64":
-        name += ", fp32 dynamics + Riccati" if a.precision == "fp32" else ", mixed fp32 dynamics / fp64 PCG"
     out = {
         "metric": ("MPC solves/sec (arm6.urdf, N=64, SQP-PCG) at 1/2/4/8 GPUs; KKT residual vs ref" if headline
-                   else f"MPC solves/sec (arm{n}.urdf, N={N}, {name})"),
-        "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": {"fp64": "f64", "fp32": "f32", "mixed": "f32 dynamics / f64 Schur-PCG"}[a.precision], "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
-        "config": {"workload": f"arm{n}.urdf{' (joint6 fixed)' if n == 6 else ''} N={N} {a.solver.upper()} "
-                               f"{'' if a.solver == 'ilqr' else a.method}, batch {B} per GPU"
-                               + ("" if a.limits == "none" else f", limits {a.limits}")
-                               + (", UrdfCost" if a.cost == "ee" else "")
-                               + ("" if a.precision == "fp64" else f", precision {a.precision}")
-                               + (f", MPC loop of {a.mpc_steps} steps" if a.mpc_steps > 0 else "")
-                               + (", PCG warm start" if a.pcg_warm_start else ""),
-                   "global_batch": B * world, "N": N, "method": a.method if a.solver == "sqp" else "iLQR",
-                   "parallelism": f"shard{world} (RCCL broadcast of start states, gather of results)"},
+                   else f"MPC solves/sec (arm{n}.urdf, N={N}, {workload_name(a)})"),
+        "value": line["value"], "unit": "solves/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": line["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": {"fp64": "f64", "fp32": "f32", "mixed": "f32 dynamics / f64 Schur-PCG"}[a.precision],
+        "data": "synthetic (SURVEY §8d workload: seeded random start states, u=0 rollout)",
+        "config": line_config(a, world, f"{a.solver.upper()} {'' if a.solver == 'ilqr' else a.method}"),
     }
-    roofline = None
-    if a.solver == "sqp" and a.method.startswith("PCG") and a.mpc_steps == 0 and "qp" in kernels:
-        roofline = sqp_roofline(a, N, nx, nu, kernels, counters)
-    elif a.solver == "sqp" and a.method.startswith("PCG") and a.mpc_steps > 0 and "qp" in kernels and N * nx > 1024:
-        # config 5 with SQP horizon solves: the GM QP kernel streams S / P^-1 rows (HBM roofline)
-        roofline = sqp_roofline(a, N, nx, nu, kernels, counters)
-    elif hard_bytes and "hard_pcg" in kernels:
-        roofline = hard_roofline(a, kernels, hard_bytes)
-    elif a.solver == "ilqr" and "ilqr_backward" in kernels:
-        bw = kernels["ilqr_backward"]
-        per_launch = int(counters[0]) / max(1, bw["launches"])
-        flops = per_launch * (N - 1) * ilqr_backward_flops_per_knot(nx, nu)
-        ach = flops / (bw["avg_ms"] / 1e3) / 1e12
-        f32 = a.precision == "fp32"
-        peak = FP32_PEAK_TFLOPS if f32 else FP64_PEAK_TFLOPS
-        traffic, src = measured_traffic("void tmpc::k_ilqr_backward<", workload_key(a))
-        roofline = {"kernel": "k_ilqr_backward", "bound": "fp32-valu" if f32 else "fp64-valu", "achieved": ach,
-                    "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": traffic,
-                    "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
-                    "note": "sequential Riccati sweep, latency-bound (one 64-lane workgroup per problem)"}
-        if traffic:
-            roofline.update(hbm_GBps=traffic / (bw["avg_ms"] / 1e3) / 1e9, traffic_source=src)
-        fw = kernels.get("ilqr_forward")
-        if fw:
-            ft, fsrc = measured_traffic("void tmpc::k_ilqr_forward<", workload_key(a))
-            roofline["forward"] = {"kernel": "k_ilqr_forward", "avg_launch_ms": fw["avg_ms"], "traffic": ft,
-                                   "hbm_GBps": ft / (fw["avg_ms"] / 1e3) / 1e9 if ft else None}
-    out["roofline"] = roofline
-
+    if standin:
+        out["standin"] = os.environ.get("TMPC_BENCH_STANDIN")   # a test stand-in context, not libtmpc
+    out["roofline"] = line_roofline(a, N, nx, nu, kernels, counters, hard_bytes)
+    if headline:
+        out["value_pcie_inclusive"] = pcie["value"] if pcie else None
     cpu, par = None, None
     if headline and not a.no_cpu_baseline and world == 1:
         share, total, basis = host_cores()
@@ -804,195 +978,228 @@ def main():
                          f"oracle NumPy restatement (no SymPy), {procs} processes x 1 BLAS thread, {wall:.1f} s",
                "cores_basis": f"{basis}: this job may use {share} cores of the {total} os.cpu_count() reports"}
         # the GPU's own results for those problems (rank 0's first `sample` problems), with trace
-        gr = ctx.sqp_solve_batch(x0_host(ctx, d_x0, B, nx, N)[:sample], u0[:sample], N, dt, a.method)
+        gr = ctx.sqp_solve_batch(x0_host(ctx, d["x0"], B, nx, N)[:sample], u0[:sample], N, dt, a.method)
         par = parity_check(gr, res)
     out["cpu_baseline"] = cpu
     if headline:
         out["parity"] = par
         out["kkt_residual"] = kkt_residual_check(ctx, n)
         out["pcie_inclusive"] = pcie
-        out["value_basis"] = ("HBM-resident: inputs resident on the GPU before the timed region, each step a D2D "
-                              "restore + one batched solve (the bench contract's definition); SURVEY 8(d) / "
-                              "BASELINE.md section 3 count H2D/D2H in wall time -- that rate is pcie_inclusive")
-        out["work"] = {"problem_qps_per_step": int(counters[0]) / a.steps,
-                       "pcg_iters_per_step": int(counters[1]) / a.steps,
-                       "grad_evals_per_step": int(counters[2]) / a.steps,
-                       "ls_trials_per_qp": int(counters[3]) // max(1, a.steps)}
-    out["kernels"] = kernels
-    out["dominant_kernel"] = dominant
-    # lock-step cost: every iteration launches the whole batch until its slowest problem exits
-    it_name = "ilqr_decide" if a.solver == "ilqr" else "ls_decide"
-    if it_name in kernels:
-        out["lockstep"] = {"batch_iterations_per_solve": kernels[it_name]["launches"] / a.steps / max(1, a.mpc_steps),
-                           "problem_iterations_mean": int(counters[0]) / (B * a.steps * max(1, a.mpc_steps))}
-    out["exit_codes"] = {str(k): int(v) for k, v in zip(*np.unique(exit_all, return_counts=True))}
-    out["iters_mean"] = float(np.mean(iters_all))
-    out["iters_max"] = int(np.max(iters_all))
-    out["problems_gathered"] = int(exit_all.size)
-    if secondary is not None:
-        out["secondary"] = secondary
-    if hard_line is not None:
-        out["hard_limits"] = hard_line
+    out["value_basis"] = STREAM_BASIS if stream else (
+        "lock-step: each step a D2D restore + one batched solve to every problem's exit" +
+        (" (MPC loop: a step = the receding-horizon loop over the batch)" if a.mpc_steps else ""))
+    for k in ("mode", "stream_check", "lockstep", "batch_iterations", "work", "kernels", "dominant_kernel",
+              "exit_codes", "iters_mean", "iters_max", "problems_gathered"):
+        if k in line:
+            out[k] = line[k]
+    out.update(extra)
     print(json.dumps(out))
     comm.close()
 
 
-def run_hard_line(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0):
-    """The headline workload under hard ACTIVE_SET torque + velocity limits (LIMIT_PRESETS
-    "torque-velocity-as": constraint rows in C, the banded Schur path, TrajoptMPCReference.py:238-248),
-    measured after the headline and the secondary, timed as the headline (barrier + synchronize around
-    --hard-steps solves, max over ranks), with k_hard_pcg's roofline and the GPU's exit codes /
-    iterations / per-QP PCG counts against the oracle (canonical order) on the first --hard-parity
-    problems (rank 0)."""
+def pcie_inclusive(ctx, a, xh, u0, stream):
+    """steps x B problems as a host-memory caller sees them: H2D of the inputs, the solve, D2H of every
+    problem's x, u and status (BASELINE.md section 3 counts host <-> device copies in wall time)."""
+    B, N, dt = a.batch, a.N, 0.1
+    ctx.synchronize()
+    if not stream:
+        tp = time.perf_counter()
+        ctx.sqp_solve_batch(xh, u0, N, dt, a.method, with_trace=False)
+        tp = time.perf_counter() - tp
+        return {"value": B / tp, "unit": "solves/s", "ms_per_solve_batch": 1000.0 * tp,
+                "note": "tmpc_sqp_solve_batch with host x/u (H2D, solve, D2H of x, u and the status arrays), one "
+                        "batch, this GPU"}
+    steps = a.steps
+    P = B * steps
+    xo = np.empty((P,) + xh.shape[1:])
+    uo = np.empty((P,) + u0.shape[1:])
+    st = np.empty((P, 4), dtype=np.int32)
+    dxi, dui = ctx.alloc(xh.nbytes), ctx.alloc(u0.nbytes)
+    sb = dict(x=ctx.alloc(xo.nbytes), u=ctx.alloc(uo.nbytes), st=ctx.alloc(st.nbytes))
+    try:
+        ctx.synchronize()
+        tp = time.perf_counter()
+        ctx.h2d(dxi, xh)
+        ctx.h2d(dui, u0)
+        ctx.solve_stream_device(solver_name(a), P, B, N, dt, dxi, dui, B, sb["x"], sb["u"], sb["st"])
+        ctx.d2h(xo, sb["x"])
+        ctx.d2h(uo, sb["u"])
+        ctx.d2h(st, sb["st"])
+        tp = time.perf_counter() - tp
+    finally:
+        for p in (dxi, dui, sb["x"], sb["u"], sb["st"]):
+            ctx.free(p)
+    return {"value": P / tp, "unit": "solves/s", "ms_per_step": 1000.0 * tp / steps,
+            "note": f"{steps} x {B} problems with host inputs and outputs: H2D of x0 / u0 ({(xh.nbytes + u0.nbytes) / 1e6:.0f}"
+                    f" MB), the stream, D2H of every problem's x, u and status ({(xo.nbytes + uo.nbytes + st.nbytes) / 1e6:.0f} MB, "
+                    "pageable host memory); `value` is the HBM-resident rate"}
+
+
+def line_args(a, **kw):
     import copy
-    nx, nu = 2 * n, n
-    ah = copy.copy(a)
-    ah.limits = "torque-velocity-as"
-    ctx.set_box_limits(LIMIT_PRESETS[ah.limits])
-    xb, ub = B * nx * N * 8, B * nu * (N - 1) * 8
+    b = copy.copy(a)
+    b.cost, b.erm, b.mpc_steps, b.pcg_warm_start, b.precision, b.solver = "quadratic", None, 0, False, "fp64", "sqp"
+    b.method, b.limits, b.N, b.links = "PCG-SS", "none", 64, 6
+    for k, v in kw.items():
+        setattr(b, k, v)
+    return b
 
-    def step():
-        ctx.d2d(d_x, d_x0, xb)
-        ctx.d2d(d_u, d_u0, ub)
-        ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method)
 
-    step()
-    ctx.synchronize()
-    ctx.set_options(profile=1)
-    ctx.reset_stats()
-    comm.barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.hard_steps):
-        step()
-    ctx.synchronize()
-    comm.barrier()
-    elapsed = comm.max(time.perf_counter() - t0)
-    ctx.set_options(profile=0)
-    hard_bytes = ctx.kernel_bytes("hard_pcg")
-    kernels = {}
-    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "hard_schur", "hard_pcg", "dxu", "ls_terms", "ls_decide"]:
-        cnt, ms = ctx.kernel_stats(name)
-        if cnt:
-            kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
-    ctx.d2d(d_x, d_x0, xb)
-    ctx.d2d(d_u, d_u0, ub)
-    exit_codes, iters = ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=True)
-    from trajoptmpcreference_amd import dist
-    dist.gather_summaries(comm, exit_codes=exit_codes.astype(np.int32), iters=iters.astype(np.int32))
-    par = None
-    if rank == 0 and a.hard_parity > 0:
-        S = min(B, a.hard_parity)
-        share, _, _ = host_cores()
-        jobs = [(a.seed0 + i, n, N) for i in range(S)]
-        with mp.get_context("fork").Pool(min(share, S), initializer=os.environ.__setitem__,
-                                          initargs=("OMP_NUM_THREADS", "1")) as pool:
-            res = pool.map(_cpu_solve_hard, jobs, chunksize=1)
-        xh = x0_host(ctx, d_x0, B, nx, N)[:S]
-        gr = ctx.sqp_solve_batch(xh, u0[:S], N, dt, a.method)
+def run_config_lines(ctx, comm, rank, world, a):
+    """The other BASELINE.json configurations beside the headline, each measured after it with its own
+    timed region (barrier + synchronize, max over ranks), kernel table, roofline and parity sample:
+      secondary    config 4: arm6 N = 64 SQP PCG-SS, soft torque + joint limits by augmented Lagrangian;
+      hard_limits  the headline under hard ACTIVE_SET torque + velocity limits (the banded Schur path);
+      config2      arm3 N = 32 SQP PCG-SS, B = 1024;
+      config3      arm6 N = 64 iLQR, soft torque limits by augmented Lagrangian, fp64 and fp32 (BASELINE's
+                   stated precision);
+      config5      arm6 N = 128 receding-horizon MPC loop of 4 SQP PCG-SS horizon solves, mixed fp32
+                   dynamics / fp64 PCG, PCG warm start, B = 8192."""
+    out = {}
+    lines = [
+        ("secondary", line_args(a, limits="torque-joint-al"), a.secondary_steps, "config 4's per-GPU slice"),
+        ("hard_limits", line_args(a, limits="torque-velocity-as"), a.hard_steps, "hard ACTIVE_SET limits"),
+        ("config2", line_args(a, links=3, N=32, batch=1024), a.config_steps, "BASELINE config 2"),
+        ("config3", line_args(a, solver="ilqr", limits="torque-al"), a.config_steps, "BASELINE config 3 (fp64)"),
+        ("config3_fp32", line_args(a, solver="ilqr", limits="torque-al", precision="fp32"), a.config_steps,
+         "BASELINE config 3 at its stated precision (fp32)"),
+        ("config5", line_args(a, N=128, batch=8192, mpc_steps=4, precision="mixed", pcg_warm_start=True), 2,
+         "BASELINE config 5's per-GPU slice"),
+    ]
+    for key, b, steps, label in lines:
+        if key in a.skip_lines:
+            continue
+        stream = not a.lockstep and b.mpc_steps == 0
+        line, d, u0, counters, kernels, hb = run_line(ctx, comm, rank, world, b, steps, 1, stream,
+                                                      a.lockstep_steps if stream else 0)
+        nx, nu = 2 * b.links, b.links
+        line["metric"] = f"MPC solves/sec (arm{b.links}.urdf, N={b.N}, {workload_name(b)}) -- {label}"
+        if b.mpc_steps:
+            line["metric"] = f"MPC horizon solves/sec (arm{b.links}.urdf, N={b.N}, {workload_name(b)}) -- {label}"
+        line["config"] = line_config(b, world, workload_name(b))
+        line["dtype"] = {"fp64": "f64", "fp32": "f32", "mixed": "f32 dynamics / f64 Schur-PCG"}[b.precision]
+        line["roofline"] = line_roofline(b, b.N, nx, nu, kernels, counters, hb)
+        line["value_basis"] = STREAM_BASIS if stream else "lock-step MPC loop: a step = 4 horizon solves of every problem"
+        if rank == 0:
+            line["parity"] = line_parity(ctx, key, b, d, u0)
+        free_inputs(ctx, d)
+        out[key] = line
+        comm.barrier()
+    setup_workload(ctx, a)
+    return out
+
+
+def _pool_map(fn, jobs):
+    share, _, _ = host_cores()
+    with mp.get_context("fork").Pool(max(1, min(share, len(jobs))), initializer=os.environ.__setitem__,
+                                      initargs=("OMP_NUM_THREADS", "1")) as pool:
+        return pool.map(fn, jobs, chunksize=1)
+
+
+def _rel(x, y):
+    return float(np.max(np.abs(np.asarray(x) - np.asarray(y)))) / max(1.0, float(np.max(np.abs(y))))
+
+
+def line_parity(ctx, key, b, d, u0):
+    """each line's parity sample on rank 0 (the GPU's lock-step batch solve of the same problems; the stream
+    equals it per problem bitwise, stream_check):
+      secondary   the oracle (oracle/sqp.py + oracle/soft.py) on the first --secondary-parity problems:
+                  exit codes, SQP iterations, outer passes and per-QP PCG counts exact;
+      hard_limits the oracle in the banded PCG's canonical order on the first --hard-parity problems, exact
+                  integers; a problem whose run parts is replayed on the GPU's own inputs at the first
+                  point the runs part (classify_hard_mismatch), and counts as unexplained otherwise;
+      config2     the oracle on the first 64 problems, exact integers;
+      config3     the committed oracle fixture (tests/golden/oracle_config3_arm6_N64_ilqr_al.npz, 8 problems):
+                  exit codes, iterations, outer passes and alpha paths exact, x / u within 1e-5; at fp32 the
+                  fixture's fp64 solves bound the deviation (parity unpinned: the reference is fp64 only);
+      config5     the committed fp64 oracle MPC loop (oracle_config5_arm6_N128_mpc_sqp_pcgss.npz, 2 problems x
+                  3 steps): per-step exit codes and SQP iterations exact, executed states within 1e-4."""
+    n, N, B, dt = b.links, b.N, b.batch, 0.1
+    nx = 2 * n
+    if key in ("secondary", "hard_limits", "config2"):
+        S = min(B, {"secondary": b.secondary_parity, "hard_limits": b.hard_parity, "config2": 64}[key])
+        if S <= 0:
+            return None
+        fn = {"secondary": _cpu_solve_config4, "hard_limits": _cpu_solve_hard, "config2": _cpu_solve}[key]
+        res = _pool_map(fn, [(b.seed0 + i, n, N) for i in range(S)])
+        xh = x0_host(ctx, d["x0"], B, nx, N)[:S]
+        if key == "secondary":
+            ctx.set_soft_state(S, N)
+        gr = ctx.sqp_solve_batch(xh, u0[:S], N, dt, b.method)
         par = parity_check(gr, res)
-        why = {i: classify_hard_mismatch(ctx, xh, u0[:S], N, dt, a.method, gr, i, res[i])
-               for i in par["mismatched_problems"]}
-        par["replayed"] = {str(i): w for i, w in why.items()}
-        par["unexplained"] = sum(1 for w in why.values() if w is None)
-        par["note"] = ("oracle/sqp.py with oracle/hard.py's rows and pcg_canonical, the banded PCG's summation "
-                       "order.  replayed: each mismatched problem replayed on the GPU's own inputs at the first "
-                       "point the runs part (bench.classify_hard_mismatch): 'pcg_count' -- the canonical-order "
-                       "PCG on the GPU's own S takes the GPU's count; 'line_search' -- the oracle's SQP "
-                       "line search on the GPU's own iterate and direction takes the GPU's outcome")
-    ctx.set_box_limits(None)
-    value = B * a.hard_steps * world / elapsed
-    return {"metric": f"MPC solves/sec (arm{n}.urdf, N={N}, SQP {a.method}, hard ACTIVE_SET torque + velocity "
-                      "box limits)",
-            "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.hard_steps, "warmup": 1,
-            "ms_per_step": 1000.0 * elapsed / a.hard_steps, "higher_is_better": True, "scaling": "weak",
-            "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} SQP {a.method}, batch {B} per GPU, limits "
-                                   f"{ah.limits} (torque +-0.5, velocity +-1, ACTIVE_SET)",
-                       "global_batch": B * world},
-            "roofline": hard_roofline(ah, kernels, hard_bytes) if "hard_pcg" in kernels and hard_bytes else None,
-            "kernels": kernels, "parity": par,
-            "lockstep": {"batch_iterations_per_solve": kernels["ls_decide"]["launches"] / a.hard_steps}
-            if "ls_decide" in kernels else None}
+        if key == "secondary":
+            soft_mism = [i for i, c in enumerate(res) if (int(gr["exit_soft"][i]), int(gr["outer_iter"][i]))
+                         != (c["exit_soft"], c["outer_iter"])]
+            par["mismatches"] += len([i for i in soft_mism if i not in par["mismatched_problems"]])
+            par["compared"] += "; exit_soft, outer_iter (exact)"
+        if key == "hard_limits":
+            why = {i: classify_hard_mismatch(ctx, xh, u0[:S], N, dt, b.method, gr, i, res[i], b.limits)
+                   for i in par["mismatched_problems"]}
+            par["replayed"] = {str(i): w for i, w in why.items()}
+            par["unexplained"] = sum(1 for w in why.values() if w["kind"] is None)
+            par["mismatch_rate"] = par["mismatches"] / S
+            par["note"] = HARD_PARITY_NOTE
+        return par
+    from oracle import sqp as osqp
+    from trajoptmpcreference_amd.urdf import parse_urdf, planar_arm_urdf
+    m = parse_urdf(planar_arm_urdf(n))
+    if key in ("config3", "config3_fp32"):
+        f = np.load(os.path.join(ROOT, "tests", "golden", "oracle_config3_arm6_N64_ilqr_al.npz"))
+        xs, us = zip(*[osqp.initial_problem(m, N, dt, int(s)) for s in f["seeds"]])
+        ctx.set_options(max_iter_softConstraints=int(f["max_iter_softConstraints"]),
+                        max_iter_SQP_DDP=int(f["max_iter_SQP_DDP"]))
+        ctx.set_soft_state(len(xs), N)
+        try:
+            r = ctx.ilqr_solve_batch(np.array(xs), np.array(us), N, dt)
+        finally:
+            ctx.set_options(max_iter_softConstraints=10, max_iter_SQP_DDP=100)
+        cost = osqp.QuadCost(np.eye(nx), 100 * np.eye(nx), 0.1 * np.eye(n), np.zeros(nx))
+        ints, alph, xerr, jerr = [], [], [], []
+        for i in range(len(xs)):
+            got = (int(r["exit_code"][i]), int(r["iter"][i]), int(r["exit_soft"][i]), int(r["outer_iter"][i]))
+            ref = (int(f["exit_code"][i]), int(f["iter"][i]), int(f["exit_soft"][i]), int(f["outer_iter"][i]))
+            ints.append(got == ref)
+            al = f["alpha"][i]
+            al = list(al[~np.isnan(al)])
+            alph.append(list(r["trace"]["alpha"][i, 1:len(al) + 1]) == al)
+            xerr.append(max(_rel(r["x"][i], f["x"][i]), _rel(r["u"][i], f["u"][i])))
+            J = osqp.total_cost(cost, r["x"][i], r["u"][i], N)
+            J64 = osqp.total_cost(cost, f["x"][i], f["u"][i], N)
+            jerr.append(abs(J - J64) / abs(J64))
+        out = {"checked": len(xs), "source": "tests/golden/oracle_config3_arm6_N64_ilqr_al.npz (oracle/ilqr.py)",
+               "integers_identical": int(sum(ints)), "alpha_paths_identical": int(sum(alph)),
+               "max_traj_rel_diff": max(xerr), "max_cost_rel_diff": max(jerr)}
+        if key == "config3":
+            out["mismatches"] = len(xs) - sum(a_ and b_ and e < 1e-5 for a_, b_, e in zip(ints, alph, xerr))
+            out["compared"] = "exit code, iterations, exit_soft, outer_iter, alpha path (exact); x, u within 1e-5"
+        else:
+            out["compared"] = ("parity unpinned (no fp32 reference): deviation of the fp32 solves from the fp64 "
+                               "oracle's; tests/test_gpu_precision.py bounds cost 1e-2, states 1e-1")
+        return out
+    if key == "config5":
+        f = np.load(os.path.join(ROOT, "tests", "golden", "oracle_config5_arm6_N128_mpc_sqp_pcgss.npz"))
+        steps = int(f["steps"])
+        xs, us = zip(*[osqp.initial_problem(m, N, dt, int(s)) for s in f["seeds"]])
+        r = ctx.mpc_batch(np.array(xs), np.array(us), N, dt, b.method, steps)
+        ints = [list(r["exit_codes"][i]) == list(f["exit_codes"][i]) and list(r["iters"][i]) == list(f["iters"][i])
+                for i in range(len(xs))]
+        xerr = [_rel(r["x_exec"][i], f["x_exec"][i]) for i in range(len(xs))]
+        return {"checked": len(xs), "steps": steps,
+                "source": "tests/golden/oracle_config5_arm6_N128_mpc_sqp_pcgss.npz (oracle/mpc.py, fp64)",
+                "mismatches": len(xs) - sum(ok and e < 1e-4 for ok, e in zip(ints, xerr)),
+                "max_x_exec_rel_diff": max(xerr),
+                "compared": "per-step exit codes and SQP iterations (exact); executed states within 1e-4 (mixed "
+                            "precision against the fp64 oracle: parity unpinned for the floats)"}
+    return None
 
 
-def run_secondary(a, ctx, comm, rank, world, n, N, B, dt, d_x0, d_u0, d_x, d_u, u0):
-    """BASELINE config 4 beside the headline, measured after it (the headline's timed region is untouched):
-    the same workload under soft torque + joint limits by augmented Lagrangian (LIMIT_PRESETS
-    "torque-joint-al", SQP PCG-SS), timed exactly as the headline (barrier + synchronize around
-    --secondary-steps solves, max over ranks), with its own kernel stats and k_qp roofline, and the GPU's
-    exit codes / iterations / outer passes / per-QP PCG counts against the oracle on the first
-    --secondary-parity problems (rank 0)."""
-    import copy
-    nx, nu = 2 * n, n
-    a4 = copy.copy(a)
-    a4.limits = "torque-joint-al"
-    limits = LIMIT_PRESETS[a4.limits]
-    ctx.set_box_limits(limits)
-    xb, ub = B * nx * N * 8, B * nu * (N - 1) * 8
-
-    def step():
-        ctx.d2d(d_x, d_x0, xb)
-        ctx.d2d(d_u, d_u0, ub)
-        ctx.set_soft_state(B, N)
-        ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method)
-
-    step()
-    ctx.synchronize()
-    ctx.set_options(profile=1)
-    ctx.reset_stats()
-    counters = np.zeros(4, dtype=np.int64)
-    comm.barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.secondary_steps):
-        step()
-        counters += np.array(ctx.solve_counters(), dtype=np.int64)
-    ctx.synchronize()
-    comm.barrier()
-    elapsed = comm.max(time.perf_counter() - t0)
-    ctx.set_options(profile=0)
-    kernels = {}
-    for name in ["qp_fd", "qp_minv", "qp_grad", "ginv", "qp", "ls_terms", "ls_decide"]:
-        cnt, ms = ctx.kernel_stats(name)
-        if cnt:
-            kernels[name] = {"launches": cnt, "total_ms": ms, "avg_ms": ms / cnt}
-    ctx.d2d(d_x, d_x0, xb)
-    ctx.d2d(d_u, d_u0, ub)
-    ctx.set_soft_state(B, N)
-    exit_codes, iters = ctx.sqp_solve_batch_device(B, N, dt, d_x, d_u, a.method, want_status=True)
-    from trajoptmpcreference_amd import dist
-    g = dist.gather_summaries(comm, exit_codes=exit_codes.astype(np.int32), iters=iters.astype(np.int32))
-    par = None
-    if rank == 0 and a.secondary_parity > 0:
-        S = min(B, a.secondary_parity)
-        share, _, _ = host_cores()
-        jobs = [(a.seed0 + i, n, N) for i in range(S)]
-        with mp.get_context("fork").Pool(min(share, S), initializer=os.environ.__setitem__,
-                                          initargs=("OMP_NUM_THREADS", "1")) as pool:
-            res = pool.map(_cpu_solve_config4, jobs, chunksize=1)
-        ctx.set_soft_state(S, N)
-        gr = ctx.sqp_solve_batch(x0_host(ctx, d_x0, B, nx, N)[:S], u0[:S], N, dt, a.method)
-        par = parity_check(gr, res)
-        soft_mism = [i for i, c in enumerate(res) if (int(gr["exit_soft"][i]), int(gr["outer_iter"][i]))
-                     != (c["exit_soft"], c["outer_iter"])]
-        par["mismatches"] += len([i for i in soft_mism if i not in par["mismatched_problems"]])
-        par["compared"] += "; exit_soft, outer_iter (exact)"
-    ctx.set_box_limits(None)
-    value = B * a.secondary_steps * world / elapsed
-    return {"metric": f"MPC solves/sec (arm{n}.urdf, N={N}, SQP {a.method}, soft torque + joint box limits by "
-                      "augmented Lagrangian) -- BASELINE config 4's per-GPU slice",
-            "value": value, "unit": "solves/s", "n_gpus": world, "steps": a.secondary_steps, "warmup": 1,
-            "ms_per_step": 1000.0 * elapsed / a.secondary_steps, "higher_is_better": True, "scaling": "weak",
-            "config": {"workload": f"arm{n}.urdf (joint6 fixed) N={N} SQP {a.method}, batch {B} per GPU, limits "
-                                   f"{a4.limits} (torque +-0.5, joint +-1, AUGMENTED_LAGRANGIAN)",
-                       "global_batch": B * world},
-            "roofline": sqp_roofline(a4, N, nx, nu, kernels, counters) if "qp" in kernels else None,
-            "kernels": kernels, "parity": par,
-            "lockstep": {"batch_iterations_per_solve": kernels["ls_decide"]["launches"] / a.secondary_steps,
-                         "problem_iterations_mean": int(counters[0]) / (B * a.secondary_steps)}
-            if "ls_decide" in kernels else None,
-            "exit_codes": {str(k): int(v) for k, v in zip(*np.unique(g["exit_codes"], return_counts=True))},
-            "iters_mean": float(np.mean(g["iters"])), "iters_max": int(np.max(g["iters"]))}
+HARD_PARITY_NOTE = (
+    "oracle/sqp.py with oracle/hard.py's rows and pcg_canonical, the banded PCG's summation order.  replayed: each "
+    "mismatched problem replayed on the GPU's own inputs at the first point the runs part (bench."
+    "classify_hard_mismatch): 'pcg_count' -- the canonical-order PCG on the GPU's own S takes the GPU's count; "
+    "'line_search' -- at the GPU's iterate the oracle's line search along the GPU's direction takes the GPU's "
+    "outcome AND along the oracle's own direction (its own QP at that iterate) takes the oracle run's outcome, "
+    "with the two directions apart by less than the PCG tolerance allows")
 
 
 def x0_host(ctx, d_x0, B, nx, N):

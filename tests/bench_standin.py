@@ -53,9 +53,9 @@ class Context:
         b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
         self.mem[dst][:b.size] = b
 
-    def d2h(self, arr, src):
+    def d2h(self, arr, src, offset=0):
         b = arr.view(np.uint8).reshape(-1)
-        b[:] = self.mem[src][:b.size]
+        b[:] = self.mem[src][offset:offset + b.size]
 
     def d2d(self, dst, src, nbytes):
         self.mem[dst][:nbytes] = self.mem[src][:nbytes]
@@ -92,6 +92,26 @@ class Context:
             x[b], u[b] = r["x"], r["u"]
             ex[b], it[b] = r["exit_sqp"], r["sqp_iter"]
         return (ex, it) if want_status else (None, None)
+
+    def solve_stream_device(self, solver, P, slots, N, dt, d_x_in, d_u_in, period, d_x_out=None, d_u_out=None,
+                            d_status=None, d_trace=None):
+        """the continuous-batching entry point's contract: problem p from input p % period, its results to
+        output row p (the stand-in solves them one by one)"""
+        n = self.model.n
+        xi, ui = self._view(d_x_in, (period, 2 * n, N)), self._view(d_u_in, (period, n, N - 1))
+        xo = self._view(d_x_out, (P, 2 * n, N)) if d_x_out else None
+        uo = self._view(d_u_out, (P, n, N - 1)) if d_u_out else None
+        st = self.mem[d_status][:16 * P].view(np.int32).reshape(P, 4) if d_status else None
+        counters = [0, 0, 0, 9]
+        for p in range(P):
+            r = self._solve(xi[p % period].copy(), ui[p % period].copy(), N, dt, solver)
+            counters[0] += len(r["pcg_iters"])
+            counters[1] += int(sum(r["pcg_iters"]))
+            if xo is not None:
+                xo[p], uo[p] = r["x"], r["u"]
+            if st is not None:
+                st[p] = (r["exit_sqp"], r["sqp_iter"], r["exit_soft"], r["outer_iter"])
+        self.counters = counters
 
     def sqp_solve_batch(self, x, u, N, dt, method="PCG-SS", with_trace=True, hard_active=False):
         rs = [self._solve(np.array(x[b]), np.array(u[b]), N, dt, method) for b in range(x.shape[0])]

@@ -538,7 +538,10 @@ class Context:
         arr = np.ascontiguousarray(arr)
         self._check(self.lib.tmpc_memcpy_h2d(self.h, dst, arr.ctypes.data_as(C.c_void_p), arr.nbytes), "h2d")
 
-    def d2h(self, arr, src):
+    def d2h(self, arr, src, offset=0):
+        """device -> host copy of arr.nbytes bytes starting `offset` bytes into the device buffer src"""
+        if offset:
+            src = C.c_void_p((src.value if isinstance(src, C.c_void_p) else int(src)) + int(offset))
         self._check(self.lib.tmpc_memcpy_d2h(self.h, arr.ctypes.data_as(C.c_void_p), src, arr.nbytes), "d2h")
 
     def d2d(self, dst, src, nbytes):
