@@ -308,8 +308,8 @@ def classify_hard_mismatch(ctx, x0, u0, N, dt, method, gr, i, ref, limits="torqu
         line-search outcome (alpha, success) differs.  At the GPU's iterate j the oracle's line search
         (oracle/sqp.py line_search) along the GPU's direction takes the GPU's outcome, AND along the
         oracle's own direction (its own dense KKT solve in the canonical PCG order at that iterate and rho)
-        takes the oracle run's outcome: the two directions -- whose relative difference is reported -- decide
-        the step, not the line search;
+        takes a different one: the two directions -- whose relative difference is reported -- decide the
+        step, not the line search (whether that different outcome is exactly the oracle run's is reported);
       * None: not reproduced (the dict says which replay failed).
     The cost, limits and options are the bench's (the arguments), not fixed."""
     from oracle import hard as ohard
@@ -372,7 +372,14 @@ def classify_hard_mismatch(ctx, x0, u0, N, dt, method, gr, i, ref, limits="torqu
     out_o = (float(r_o["alpha"]), bool(r_o["succeeded_line_search"]))
     gpu_ok = out_g == g_ls[j]
     ora_ok = out_o == o_ls[j]
-    return {"kind": "line_search" if gpu_ok and ora_ok else None, "j": j, "gpu_outcome": g_ls[j],
+    # explained: the oracle's line search reproduces the GPU's decision on the GPU's direction, and on the
+    # oracle's own direction at the same iterate it decides differently -- the step is decided by the two
+    # directions' difference (their QPs' S differ in the last bits; a capped PCG amplifies that), not by the
+    # line search.  Whether the oracle's own direction then gives exactly the oracle RUN's outcome depends on
+    # the oracle's iterate, which has the same rounding history, and on the host's BLAS (the dense KKT
+    # formation's summation order): reported, not required.
+    return {"kind": "line_search" if gpu_ok and out_o != g_ls[j] else None, "j": j, "gpu_outcome": g_ls[j],
+            "oracle_direction_gives_oracle_run_outcome": ora_ok,
             "oracle_outcome": o_ls[j], "oracle_ls_on_gpu_direction": out_g, "oracle_ls_on_oracle_direction": out_o,
             "direction_rel_diff": delta, "pcg_counts_at_j": [g_counts[j] if j < len(g_counts) else None,
                                                             o_counts[j] if j < len(o_counts) else None]}
@@ -1198,8 +1205,8 @@ HARD_PARITY_NOTE = (
     "mismatched problem replayed on the GPU's own inputs at the first point the runs part (bench."
     "classify_hard_mismatch): 'pcg_count' -- the canonical-order PCG on the GPU's own S takes the GPU's count; "
     "'line_search' -- at the GPU's iterate the oracle's line search along the GPU's direction takes the GPU's "
-    "outcome AND along the oracle's own direction (its own QP at that iterate) takes the oracle run's outcome, "
-    "with the two directions apart by less than the PCG tolerance allows")
+    "outcome AND along the oracle's own direction (its own QP at that iterate) a different one: the step is "
+    "decided by the two directions' rounding-amplified difference (direction_rel_diff), not by the line search")
 
 
 def x0_host(ctx, d_x0, B, nx, N):

@@ -267,8 +267,9 @@ int tmpc_ilqr_solve_stream_device(tmpc_ctx* ctx, int N, double dt, const tmpc_st
  * exit codes and iteration counts [B][steps] (all nullable); x, u hold the final shifted horizon.
  * SQP horizons: the fused QP up to N * nx = 1536 (past 1024 rows the PCG keeps S in HBM); past that the banded
  * path of the hard-limit kernels with no constraint rows, PCG up to N * nx = 4096 and the direct methods (S, N)
- * without a row limit (pcg_warm_start is refused there: the banded PCG takes no guess).  iLQR has no horizon
- * limit. */
+ * up to the banded Schur kernel's LDS (arm6 N <= 650, a 7-joint arm N <= 556; fewer with hard-limit rows -- a
+ * longer horizon fails with the largest supported N in the message); pcg_warm_start is refused there (the banded
+ * PCG takes no guess).  iLQR has no horizon limit. */
 #define TMPC_SOLVER_ILQR 16
 int tmpc_mpc_batch(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps, double* x, double* u,
                    double* x_exec, double* u_exec, int32_t* exit_codes, int32_t* iters);
@@ -324,8 +325,9 @@ int tmpc_qp_batch(tmpc_ctx* ctx, int B, int N, double dt, int linsys, const doub
  *   linsys           TMPC_LINSYS_N / _S (direct) or _PCG_J / _BJ / _SS / _0;
  *   guess [B][N nx]  PCG initial iterate (nullable: zeros).
  * Outputs dxul [B][n(N-1)+nx + nx N] ([x0,u0,...,x_{N-1}; lambda], the reference's order), pcg_iters [B]
- * (0 for the direct methods), S_diag / S_lo / gamma (nullable).  (G_k + rho I)^-1 is formed without
- * pivoting: a zero or non-finite pivot (np.linalg.inv's LinAlgError) is an error. */
+ * (0 for the direct methods), S_diag / S_lo / gamma (nullable).  (G_k + rho I)^-1 is formed by Gauss-Jordan
+ * with partial pivoting (np.linalg.inv's LU pivots the same way; an indefinite plugin Hessian is fine): a zero or
+ * non-finite pivot -- G_k + rho I exactly singular, np.linalg.inv's LinAlgError -- is an error. */
 int tmpc_qp_blocks_batch(tmpc_ctx* ctx, int B, int N, int nx, int nu, int linsys, const double* G, const double* g,
                          const double* A, const double* Bm, const double* c, const double* rho, const double* guess,
                          double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma);

@@ -12,7 +12,7 @@ stored for both of the oracle's [K | d] solves (Cholesky and LU): where
 rounding decides an integer outcome the GPU must match one of them
 (tests/test_gpu_ilqr.py).
 
-Usage:  python tests/golden/make_oracle_fixtures.py [--only config3|config4|config5|sqp128|mpc128sqp]
+Usage:  python tests/golden/make_oracle_fixtures.py [--only config3|config4|config5|sqp128|mpc128sqp|big|hard6]
 """
 import argparse
 import multiprocessing as mp
@@ -36,6 +36,10 @@ C5 = dict(N=128, B=2, seed0=900, steps=3, opts={})
 # PCG-SS solves and the MPC loop with the PCG warm start
 C5S = dict(N=128, B=4, seed0=940, opts={})
 C5M = dict(N=128, B=2, seed0=960, steps=3, opts={})
+# the bench's hard-limit line (bench.py LIMIT_PRESETS "torque-velocity-as": ACTIVE_SET torque +-0.5 and
+# velocity +-1 on every joint), arm6 N = 64, SQP PCG-SS at the reference's defaults, the oracle's banded-path
+# PCG in the GPU's canonical summation order; seeds 0..7 are the bench workload's first problems
+CH6 = dict(N=64, B=8, seed0=0, lb_u=-0.5, ub_u=0.5, lb_v=-1.0, ub_v=1.0)
 
 
 def _model():
@@ -101,6 +105,23 @@ def job_config5(args):
         ompc.oilqr.ilqr = orig
     return dict(seed=seed, solve=solve, exit_codes=o["exit_codes"], iters=o["iters"], x_exec=o["x_exec"],
                 u_exec=o["u_exec"])
+
+
+def job_hard6(seed):
+    from oracle import hard as ohard
+    from oracle import sqp as osqp
+    m = _model()
+    N = CH6["N"]
+    x, u = osqp.initial_problem(m, N, 0.1, seed)
+    hc = ohard.HardConstraints([ohard.HardLimit("torque", 6, CH6["lb_u"], CH6["ub_u"], "ACTIVE_SET"),
+                                ohard.HardLimit("velocity", 6, CH6["lb_v"], CH6["ub_v"], "ACTIVE_SET")])
+    with np.errstate(all="ignore"):
+        o = osqp.sqp(m, _cost(), x, u, N, 0.1, "PCG-SS", {}, hard=hc, order="canonical")
+    tr = o["trace"][1:]
+    return dict(seed=seed, exit_sqp=o["exit_sqp"], sqp_iter=o["sqp_iter"], x=o["x"], u=o["u"],
+                pcg_iters=list(o["pcg_iters"]), alpha=[float(t["alpha"]) for t in tr],
+                succeeded=[bool(t["succeeded_line_search"]) for t in tr],
+                masks=[[int(v) for v in mk] for mk in o["active_masks"]], singular=list(o["singular"]))
 
 
 def job_sqp128(seed):
@@ -217,6 +238,23 @@ def main():
             rec[k] = np.array([r[k] for r in res])
         np.savez_compressed(os.path.join(OUT, "oracle_arm6_N128_sqp_pcgss.npz"), **rec)
         print(f"[oracle] sqp128: {time.time() - t:.0f} s; (exit, iter) "
+              f"{list(zip(rec['exit_sqp'], rec['sqp_iter']))}", flush=True)
+    if a.only in (None, "hard6"):
+        t = time.time()
+        res = pool.map(job_hard6, [CH6["seed0"] + i for i in range(CH6["B"])], chunksize=1)
+        W = max(len(r["pcg_iters"]) for r in res)
+        rec = {"N": CH6["N"], "seeds": np.array([r["seed"] for r in res]),
+               "lb_u": CH6["lb_u"], "ub_u": CH6["ub_u"], "lb_v": CH6["lb_v"], "ub_v": CH6["ub_v"],
+               "pcg_iters": np.array([r["pcg_iters"] + [-1] * (W - len(r["pcg_iters"])) for r in res]),
+               "alpha": np.array([r["alpha"] + [np.nan] * (W - len(r["alpha"])) for r in res]),
+               "succeeded": np.array([r["succeeded"] + [False] * (W - len(r["succeeded"])) for r in res]),
+               "singular": np.array([r["singular"] + [False] * (W - len(r["singular"])) for r in res]),
+               "masks": np.array([r["masks"] + [[0] * CH6["N"]] * (W - len(r["masks"])) for r in res],
+                                 dtype=np.uint64)}
+        for k in ("exit_sqp", "sqp_iter", "x", "u"):
+            rec[k] = np.array([r[k] for r in res])
+        np.savez_compressed(os.path.join(OUT, "oracle_hard_arm6_N64_torque_velocity_as.npz"), **rec)
+        print(f"[oracle] hard6: {time.time() - t:.0f} s; (exit, iter) "
               f"{list(zip(rec['exit_sqp'], rec['sqp_iter']))}", flush=True)
     if a.only in (None, "mpc128sqp"):
         t = time.time()

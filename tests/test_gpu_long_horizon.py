@@ -184,3 +184,14 @@ def test_banded_path_refuses_warm_start():
     x, u = _problems(130, [5])
     with pytest.raises(_native.NativeError, match="warm"):
         _solver(6).SQP_batch(x, u, 130, 0.1, "PCG-SS", {"pcg_warm_start": True})
+
+
+def test_banded_path_refuses_a_horizon_past_the_schur_kernels_lds():
+    """The banded Schur kernel (k_hard_schur) keeps per-knot and per-row records in LDS: past 160 KB a
+    horizon is refused with the largest supported N named (arm6 without hard limits: N = 650), before any
+    launch -- not a generic launch failure."""
+    from trajoptmpcreference_amd import _native
+    N = 651
+    x, u = _problems(N, [3])
+    with pytest.raises(_native.NativeError, match="largest supported horizon .* is N = 650"):
+        _solver(6).SQP_batch(x, u, N, 0.1, "S", {"max_iter_SQP_DDP": 1})

@@ -194,3 +194,48 @@ def test_plugin_qp_level_methods():
                                                       "max_iter": 500})):
         res = float(np.max(np.abs(K @ dxul - rhs)))
         assert res < 1e-8 * max(1.0, float(np.max(np.abs(rhs)))), res
+
+
+def test_plugin_qp_with_an_indefinite_hessian_block():
+    """(G_k + rho I)^-1 of the plugin-hook QP by Gauss-Jordan with partial pivoting: knot blocks
+    that are indefinite and whose leading entry cancels rho exactly (a zero first pivot -- LinAlgError for an
+    unpivoted elimination, invertible for np.linalg.inv) give the dense KKT solution of
+    solveKKTSystem (:313-359), methods N and S."""
+    from trajoptmpcreference_amd import _native
+    rng = np.random.default_rng(11)
+    nu, N, rho = 3, 6, 1e-3
+    nx, n = 2 * nu, 3 * nu
+    G = np.zeros((1, N, n, n))
+    for k in range(N):
+        m = n if k < N - 1 else nx
+        M = rng.uniform(-1.0, 1.0, (m, m))
+        H = M + M.T + np.diag(rng.choice([-3.0, 3.0], m))   # indefinite, well conditioned
+        H[0, 0] = -rho                                        # first pivot of H + rho I exactly zero
+        G[0, k, :m, :m] = H
+    g = rng.uniform(-1.0, 1.0, (1, N, n))
+    A = rng.uniform(-0.3, 0.3, (1, N - 1, nx, nx)) + np.eye(nx)
+    Bm = rng.uniform(-0.3, 0.3, (1, N - 1, nx, nu))
+    c = rng.uniform(-0.1, 0.1, (1, N, nx))
+    # the dense KKT system of formKKTSystemBlocks' blocks (:200-271) with rho on G's diagonal (:319-322)
+    nz = n * (N - 1) + nx
+    Gd = np.zeros((nz, nz))
+    gd = np.zeros(nz)
+    C = np.zeros((nx * N, nz))
+    cd = c[0].reshape(-1)
+    C[:nx, :nx] = np.eye(nx)
+    for k in range(N):
+        m = n if k < N - 1 else nx
+        Gd[k * n:k * n + m, k * n:k * n + m] = G[0, k, :m, :m]
+        gd[k * n:k * n + m] = g[0, k, :m]
+        if k < N - 1:
+            C[(k + 1) * nx:(k + 2) * nx, k * n:k * n + nx] = -A[0, k]
+            C[(k + 1) * nx:(k + 2) * nx, k * n + nx:k * n + n] = -Bm[0, k]
+            C[(k + 1) * nx:(k + 2) * nx, (k + 1) * n:(k + 1) * n + nx] = np.eye(nx)
+    K = np.block([[Gd + rho * np.eye(nz), C.T], [C, np.zeros((nx * N, nx * N))]])
+    ref = np.linalg.solve(K, np.concatenate([gd, cd]))
+    ctx = _native.default_context(0)
+    for meth, tol in (("N", 1e-9), ("S", 1e-9)):
+        r = ctx.qp_blocks_batch(G, g, A, Bm, c, rho, meth, want_blocks=False)
+        got = r["dxul"][0]
+        assert np.all(np.isfinite(got)), meth
+        assert np.max(np.abs(got[:nz] - ref[:nz])) < tol * max(1.0, np.max(np.abs(ref[:nz]))), meth

@@ -458,6 +458,16 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
                 "row limit)", ctx->hlim.any_hard ? "hard constraints" : "N * nx past the fused QP's rows",
                 hard.dmax, HARD_PCG_MAX_ROWS);
   if (hard.W > 1024) return fail(ctx, "hard constraints: band half-width %d > 1024", hard.W);
+  if (hard_schur_lds_bytes(N, nj, hard.dmax) > CU_LDS_BYTES) {
+    // the largest N whose k_hard_schur LDS fits: N (24 nj + 8) + 8 (nx + rmax) N + 72 nj^2 (+ 12 of rounding)
+    int nmax = N;
+    while (nmax > 2 && hard_schur_lds_bytes(nmax, nj, nx * nmax + nmax * hard.rmax) > CU_LDS_BYTES) --nmax;
+    return fail(ctx, "%s: N = %d needs %zu bytes of LDS in the banded Schur kernel (k_hard_schur), more than a "
+                "CU's %zu; the largest supported horizon for this robot%s is N = %d",
+                ctx->hlim.any_hard ? "hard constraints" : "N * nx past the fused QP's rows", N,
+                hard_schur_lds_bytes(N, nj, hard.dmax), CU_LDS_BYTES,
+                ctx->hlim.any_hard ? " and these limits" : "", nmax);
+  }
   const size_t BW = 2 * (size_t)hard.W + 1, nbmax = hard.dmax / nx + 1;
   hard.Cs = ctx->dlim;
   hard.C = ctx->dcost;

@@ -1368,7 +1368,7 @@ struct LaunchHard {
                          h.hcol, h.hsgn, h.hval, h.hslot, h.amask, h.iter, h.Wtr, h.tr_active);
       hipLaunchKernelGGL(k_hard_layout, dim3(B), dim3(64), 0, s, B, N, NX, h.rmax, h.active, h.cnt, h.roff, h.hoff,
                          h.dim, h.rkind, h.rknot, h.ridx, h.dmax);
-      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), N * (3 * NJ * sizeof(double) + 2 * sizeof(int)) + ((h.dmax * 2 + 3) & ~3) * sizeof(int) + (2 * 4 * NJ * NJ + NJ * NJ) * sizeof(double), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
+      hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), hard_schur_lds_bytes(N, NJ, h.dmax), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
                          h.per_knot, h.A, h.Bm, h.cvec, h.x, h.u, h.jsoft, h.dim, h.rkind, h.rknot, h.ridx, h.hoff,
                          h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam, h.rng);
     } else if (h.phase == 1) {

@@ -7,8 +7,8 @@
 // (tmpc_pcg.h, restated by oracle/canon.c), so its counts are the fused kernel's.
 //
 //   k_ghat_full   (G_k + rho I)^-1 per (problem, knot): one wave per matrix, row r on lane r,
-//                 Gauss-Jordan without pivoting (G + rho I is SPD for a convex cost; a zero or
-//                 non-finite pivot -- np.linalg.inv's LinAlgError -- sets the problem's error flag);
+//                 Gauss-Jordan with partial pivoting (a non-convex plugin cost makes G + rho I indefinite;
+//                 an exactly singular one -- np.linalg.inv's LinAlgError -- sets the problem's error flag);
 //   k_qp_blocks   one workgroup per problem, one row of S per lane (the fused kernel's geometry):
 //                 prologue S_kk, S_{k,k-1}, S_{k,k+1}, gamma_k from the full blocks Ghat_k
 //                   S_kk = -(AB_{k-1} Ghat_{k-1} AB_{k-1}^T + E Ghat_k E^T),  S_{k,k-1} = AB_{k-1} Ghat_{k-1} E^T,
@@ -27,7 +27,12 @@ __device__ __forceinline__ double hk_readlane(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
-// one 64-lane wave per (problem, knot); MAXN >= n
+// one 64-lane wave per (problem, knot); MAXN >= n.  Gauss-Jordan with partial pivoting, as np.linalg.inv's
+// LU (LAPACK getrf: the largest |entry| of the pivot column, the first such row on a tie): at step p the
+// row with the largest |a_rp| among rows p..m-1 is swapped into place (the two lanes trade rows), and the
+// in-place inverse of the row-permuted matrix is unscrambled by swapping its columns back in reverse order
+// (the inverse of P A is A^-1 P^-1).  A zero or non-finite pivot -- an exactly singular G + rho I, where
+// np.linalg.inv raises LinAlgError -- sets the problem's error flag.
 template <int MAXN>
 __global__ void __launch_bounds__(64) k_ghat_full(int B, int N, int nx, int nu, const double* __restrict__ G,
                                                   const double* __restrict__ rho, double* __restrict__ Ghat,
@@ -44,8 +49,35 @@ __global__ void __launch_bounds__(64) k_ghat_full(int B, int N, int nx, int nu, 
 #pragma unroll
   for (int c = 0; c < MAXN; ++c)
     a[c] = (r < m && c < m) ? src[r * n + c] + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
+  __shared__ int perm[MAXN];   // the row swapped with row p at step p (one wave: written, then read, by it)
   bool bad = false;
   for (int p = 0; p < m; ++p) {
+    // pivot search over rows p..m-1 of column p (lane order breaks ties: the first row, as getrf's idamax)
+    double ap = 0.0;
+#pragma unroll
+    for (int c = 0; c < MAXN; ++c)
+      if (c == p) ap = a[c];
+    double best = (r >= p && r < m) ? fabs(ap) : -1.0;
+    int q = r;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ob = __shfl_xor(best, off);
+      const int oq = __shfl_xor(q, off);
+      if (ob > best || (ob == best && oq < q)) {
+        best = ob;
+        q = oq;
+      }
+    }
+    q = __builtin_amdgcn_readfirstlane(q);
+    if (r == 0) perm[p] = q;
+    if (q != p) {   // lanes p and q trade rows
+#pragma unroll
+      for (int c = 0; c < MAXN; ++c) {
+        const double vp = hk_readlane(a[c], p), vq = hk_readlane(a[c], q);
+        if (r == p) a[c] = vq;
+        else if (r == q) a[c] = vp;
+      }
+    }
     double pr[MAXN];
 #pragma unroll
     for (int c = 0; c < MAXN; ++c) pr[c] = hk_readlane(a[c], p);
@@ -64,6 +96,22 @@ __global__ void __launch_bounds__(64) k_ghat_full(int B, int N, int nx, int nu, 
     } else {
 #pragma unroll
       for (int c = 0; c < MAXN; ++c) a[c] = c == p ? -f * rp : fma(-f, pr[c], a[c]);
+    }
+  }
+  __syncthreads();
+  for (int p = m - 1; p >= 0; --p) {   // unscramble: columns p and perm[p], in reverse order
+    const int q = __builtin_amdgcn_readfirstlane(perm[p]);
+    if (q == p) continue;
+    double vp = 0.0, vq = 0.0;
+#pragma unroll
+    for (int c = 0; c < MAXN; ++c) {
+      if (c == p) vp = a[c];
+      if (c == q) vq = a[c];
+    }
+#pragma unroll
+    for (int c = 0; c < MAXN; ++c) {
+      if (c == p) a[c] = vq;
+      else if (c == q) a[c] = vp;
     }
   }
   double* out = Ghat + (size_t)mat * n * n;

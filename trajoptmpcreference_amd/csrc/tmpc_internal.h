@@ -227,6 +227,14 @@ constexpr int HARD_PCG_THREADS = 1024, HARD_PCG_MAX_SLOTS = 4;
 constexpr int HARD_PCG_MAX_ROWS = HARD_PCG_THREADS * HARD_PCG_MAX_SLOTS;
 constexpr int HARD_PCG_LDS_BYTES = 160 * 1024;   // all of a CU's LDS: vectors + preconditioner-block cache
 int launch_hard(hipStream_t s, int nj, const HardArgs& h);
+// dynamic LDS of k_hard_schur (one workgroup per problem): the cost gradient / piece record per knot
+// (3 nj doubles + 2 ints), the rows' piece knots (2 dmax ints, 16-byte rounded) and the shared Ghat
+// blocks (2 (2 nj)^2 + nj^2 doubles).  It grows with N: setup_hard refuses a horizon past the CU's LDS.
+inline size_t hard_schur_lds_bytes(int N, int nj, int dmax) {
+  return (size_t)N * (3 * nj * sizeof(double) + 2 * sizeof(int)) + (size_t)((dmax * 2 + 3) & ~3) * sizeof(int) +
+         (size_t)(2 * 4 * nj * nj + nj * nj) * sizeof(double);
+}
+constexpr size_t CU_LDS_BYTES = 160 * 1024;   // gfx950: 160 KB of LDS per CU
 int hard_set_max_lds();
 
 // the dense PCG of tmpc_pcg_dense_batch (tmpc_hard.hip): PCG.pcg with any A / Pinv, D <= HARD_PCG_MAX_ROWS.

@@ -92,16 +92,23 @@ class _HookSQP:
         self.gpu_dyn = device_plant(p)
         self.it = self.outer = self.ls = 0
 
-    # -- plugin evaluations, placed and called as the reference places and calls them
+    # -- plugin evaluations, placed and called as the reference places and calls them.  The iter_* arguments
+    # are the reference's module-global counters (overloading.matrix_): the initial cost / violation of an
+    # outer pass sees the previous pass's final iteration and line-search indices (matrix_.iteration is reset
+    # after them, :541-572), formKKTSystemBlocks sees the previous line search's last index (it is reset after
+    # the QP, :608) and calls the integrator without iter_3 (:230-232); totalHardConstraintViolation passes
+    # iter_3 (:282).  A fresh solve starts from 0, the globals' value at import.
     def _step(self, x, u, grad):
-        """f(x_k, u_k) of all knots [N-1][nx]; with grad also A [N-1][nx][nx], B [N-1][nx][nu]."""
+        """f(x_k, u_k) of all knots [N-1][nx]; with grad (formKKTSystemBlocks) also A [N-1][nx][nx],
+        B [N-1][nx][nu], and the integrator called without iter_3 as there."""
         N, p = self.N, self.s.plant
         X, U = x[:, :N - 1].T, u[:, :N - 1].T
         if self.gpu_dyn:
             f = p.integrator_batch(X, U, self.dt)
             return (f,) + (p.integrator_batch(X, U, self.dt, return_gradient=True) if grad else ())
-        f = np.array([p.integrator(x[:, k], u[:, k], self.dt, iter_1=self.it, iter_2=self.outer, iter_3=self.ls)
-                      for k in range(N - 1)])
+        kw = dict(iter_1=self.it, iter_2=self.outer) if grad else dict(iter_1=self.it, iter_2=self.outer,
+                                                                         iter_3=self.ls)
+        f = np.array([p.integrator(x[:, k], u[:, k], self.dt, **kw) for k in range(N - 1)])
         if not grad:
             return (f,)
         AB = [p.integrator(x[:, k], u[:, k], self.dt, return_gradient=True, iter_1=self.it, iter_2=self.outer)
@@ -191,16 +198,16 @@ class _HookSQP:
         exit_sqp = exit_soft = 0
         while True:
             rho, drho = o["rho_init_SQP_DDP"], 1
-            self.it = self.ls = 0
-            J = self.total_cost(x, u)
+            J = self.total_cost(x, u)   # the previous pass's iteration / line-search indices (:541-542)
             c = self.violation(x, u, xs)
+            self.it = 0                 # matrix_.iteration = 0 (:572)
             mu = 10   # :545-546
             merit = J + mu * c
             trace = [dict(iteration=0, line_search_iteration=0, alpha=1.0, rho=rho, J=J, c=c, merit=merit,
                           D=np.nan, reduction_ratio=np.nan, succeeded_line_search=0, pcg_iters=0, singular=0)]
             while True:
-                self.ls = 0
-                dxul, inner = self.qp(x, u, xs, rho)
+                dxul, inner = self.qp(x, u, xs, rho)   # formKKTSystemBlocks sees the last line search's index
+                self.ls = 0                            # matrix_.line_search_iteration = 0 (:608)
                 alpha, error = 1.0, False
                 while True:
                     x_new, u_new = copy.deepcopy(x), copy.deepcopy(u)

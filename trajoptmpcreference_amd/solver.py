@@ -209,9 +209,10 @@ class TrajoptMPCReference:
         return r
 
     def _sqp_hooks_batch(self, x, u, N, dt, method, options, soft_state):
-        """SQP_batch on the plugin-hook path (hooks.py).  With several problems and soft limits each
-        problem runs on its own copy of the constraint object (the device path's per-problem soft state);
-        the returned r["soft_state"] holds every problem's final constants."""
+        """SQP_batch on the plugin-hook path (hooks.py).  Every problem runs on its own copy of the constraint
+        object (the device path's per-problem soft state), so the caller's object is left unchanged and a
+        repeated call gives the same results; with soft limits r["soft_state"] holds every problem's final
+        constants (SQP() writes them back through unpack_state, as on the device path)."""
         if options.get("overloading"):
             raise NotImplementedError("overloading (op-history tracing) is instrumentation, not offered")
         x = np.asarray(x, dtype=np.float64)
@@ -223,8 +224,6 @@ class TrajoptMPCReference:
         soft = con.has_any()
         if soft and con.num_timesteps != N:
             raise ValueError(f"TrajoptConstraint was built for {con.num_timesteps} knots, solving with N = {N}")
-        if B == 1 and soft_state is None:
-            return hooks.sqp_hooks_batch(self, ctx, x, u, N, dt, method, options)
         outs, states = [], []
         try:
             for b in range(B):
