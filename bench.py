@@ -108,6 +108,9 @@ def parse(argv=None):
     ap.add_argument("--lockstep", action="store_true",
                     help="time each step as one lock-step batched solve (D2D restore + solve to every problem's "
                          "exit) instead of the continuous-batching stream")
+    ap.add_argument("--substreams", type=int, default=1,
+                    help="concurrent sub-streams of the headline's stream (tmpc_stream.substreams; the other lines use "
+                         "their own tuned count, LINE_SUBSTREAMS)")
     ap.add_argument("--lockstep-steps", type=int, default=2,
                     help="lock-step steps timed beside each streamed line (its `lockstep` rate; 0: skip)")
     a = ap.parse_args(argv)
@@ -729,7 +732,7 @@ def kernel_table(ctx):
     return kernels
 
 
-def measure(ctx, comm, a, d, steps, warmup, stream, sbuf=None, mpc=None):
+def measure(ctx, comm, a, d, steps, warmup, stream, sbuf=None, mpc=None, substreams=1):
     """The timed region of one line: `warmup` untimed steps, then `steps` timed ones between barrier +
     synchronize, the max over ranks.  stream: the steps' B x steps problems go through the B slots of one
     continuous-batching solve (tmpc_*_solve_stream_device: problem p starts from resident input p % B,
@@ -739,7 +742,7 @@ def measure(ctx, comm, a, d, steps, warmup, stream, sbuf=None, mpc=None):
 
     def stream_solve(copies):
         ctx.solve_stream_device(solver_name(a), B * copies, B, N, dt, d["x0"], d["u0"], B, sbuf["x"], sbuf["u"],
-                                sbuf["st"])
+                                sbuf["st"], substreams=substreams)
 
     if stream:
         if warmup > 0:
@@ -812,7 +815,7 @@ STREAM_BASIS = ("continuous batching (tmpc_sqp_solve_stream_device / tmpc_ilqr_s
                 "time (D2D restore + solve to every problem's exit), the round-5 definition")
 
 
-def run_line(ctx, comm, rank, world, a, steps, warmup, stream, lockstep_steps):
+def run_line(ctx, comm, rank, world, a, steps, warmup, stream, lockstep_steps, substreams=1):
     """Measure workload `a` (B = a.batch problems per rank): the line's value (solves/s over all ranks), its
     kernel table and work counters, the stream's check against the lock-step solve, and the lock-step rate.
     Returns (line dict, device inputs, host u0, the lock-step batch's status / x)."""
@@ -827,12 +830,14 @@ def run_line(ctx, comm, rank, world, a, steps, warmup, stream, lockstep_steps):
                    codes=ctx.alloc(B * K1 * 4), iters=ctx.alloc(B * K1 * 4))
         stream = False   # the MPC loop's horizon solves are lock-step batches (tmpc_mpc_batch_device)
     sbuf = stream_buffers(ctx, a, max(steps, warmup, 1)) if stream else None
-    elapsed, counters, kernels, hard_bytes = measure(ctx, comm, a, d, steps, warmup, stream, sbuf, mpc)
+    elapsed, counters, kernels, hard_bytes = measure(ctx, comm, a, d, steps, warmup, stream, sbuf, mpc, substreams)
     units = max(1, a.mpc_steps)
     value = B * steps * world * units / elapsed
     line = {"value": value, "unit": "solves/s", "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": 1000.0 * elapsed / steps, "higher_is_better": True, "scaling": "weak",
             "mode": "stream" if stream else ("lockstep MPC loop" if mpc else "lockstep")}
+    if stream:
+        line["substreams"] = substreams
     # the lock-step batch solve of the same inputs: status for the gather and the stream check
     ex_b, it_b = batch_solve(ctx, a, d, want_status=True, mpc=mpc)
     if stream:
@@ -945,7 +950,7 @@ def main():
     comm = standin.make_comm(ctx, rank, world, cfg) if standin else dist.make_comm(ctx, rank, world, cfg)
     stream = not a.lockstep and a.mpc_steps == 0
     line, d, u0, counters, kernels, hard_bytes = run_line(ctx, comm, rank, world, a, a.steps, a.warmup, stream,
-                                                          a.lockstep_steps if stream else 0)
+                                                          a.lockstep_steps if stream else 0, a.substreams)
     headline = is_headline(a)
     # ---- PCIe-inclusive rate: the same steps x B problems with host inputs and outputs (H2D of x0 / u0, the
     # stream, D2H of every problem's x, u and status) -- BASELINE.md section 3's wall-time definition
@@ -1052,6 +1057,12 @@ def line_args(a, **kw):
     return b
 
 
+# concurrent sub-streams per line (tmpc_stream.substreams), measured (profiles/r06/stream/probe_r06e.jsonl, 16
+# copies): two overlap the latency-bound phases of config 3 / config 4 / the hard line by 3-5 %; the
+# headline's k_qp fills every CU alone (no gain) and config 2's short iterations lose to the second stream
+LINE_SUBSTREAMS = {"secondary": 2, "hard_limits": 2, "config3": 2, "config3_fp32": 2}
+
+
 def run_config_lines(ctx, comm, rank, world, a):
     """The other BASELINE.json configurations beside the headline, each measured after it with its own
     timed region (barrier + synchronize, max over ranks), kernel table, roofline and parity sample:
@@ -1078,7 +1089,7 @@ def run_config_lines(ctx, comm, rank, world, a):
             continue
         stream = not a.lockstep and b.mpc_steps == 0
         line, d, u0, counters, kernels, hb = run_line(ctx, comm, rank, world, b, steps, 1, stream,
-                                                      a.lockstep_steps if stream else 0)
+                                                      a.lockstep_steps if stream else 0, LINE_SUBSTREAMS.get(key, 1))
         nx, nu = 2 * b.links, b.links
         line["metric"] = f"MPC solves/sec (arm{b.links}.urdf, N={b.N}, {workload_name(b)}) -- {label}"
         if b.mpc_steps:

@@ -242,12 +242,14 @@ int tmpc_ilqr_solve_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double*
  *   status [problems][4]   exit code, iterations, exit_soft, outer_iter (nullable);
  *   trace                  device arrays [problems][max_iter_SQP_DDP + 1] per field (each nullable;
  *                          hard_active must be NULL).
- * The context's soft-constraint state is left unset (tmpc_get_soft_state fails until the next solve). */
+ * The context's soft-constraint state is left unset (tmpc_get_soft_state fails until the next solve).
+ * Work counters (tmpc_solve_counters) and kernel timings sum over the sub-streams. */
 typedef struct tmpc_stream {
   int32_t problems;
   int32_t slots;
   int32_t period;
-  int32_t reserved;
+  int32_t substreams;   /* 0 / 1: one stream; K = 2..8: K concurrent sub-streams (own HIP stream, slots / K slots,
+                           a contiguous 1 / K of the problems each), whose kernels overlap on the GPU */
   const double* x_in;
   const double* u_in;
   double* x_out;

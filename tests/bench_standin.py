@@ -94,7 +94,7 @@ class Context:
         return (ex, it) if want_status else (None, None)
 
     def solve_stream_device(self, solver, P, slots, N, dt, d_x_in, d_u_in, period, d_x_out=None, d_u_out=None,
-                            d_status=None, d_trace=None):
+                            d_status=None, d_trace=None, substreams=1):
         """the continuous-batching entry point's contract: problem p from input p % period, its results to
         output row p (the stand-in solves them one by one)"""
         n = self.model.n

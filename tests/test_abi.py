@@ -85,7 +85,7 @@ def test_stream_struct_layout():
     """tmpc_stream (ABI 10): four int32, five device pointers, then a tmpc_trace of device pointers."""
     from trajoptmpcreference_amd import _native
     names = [f[0] for f in _native.tmpc_stream._fields_]
-    assert names == ["problems", "slots", "period", "reserved", "x_in", "u_in", "x_out", "u_out", "status", "trace"]
+    assert names == ["problems", "slots", "period", "substreams", "x_in", "u_in", "x_out", "u_out", "status", "trace"]
     assert ctypes.sizeof(_native.tmpc_stream) == 16 + 5 * 8 + 13 * 8
 
 

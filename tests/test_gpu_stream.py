@@ -49,9 +49,9 @@ def _batch(ctx, solver, x, u, N, dt, soft):
                 outer_iter=r["outer_iter"], trace=r["trace"])
 
 
-def _assert_stream_equals_batch(ctx, solver, x, u, N, slots, copies, dt=0.1, soft=False):
+def _assert_stream_equals_batch(ctx, solver, x, u, N, slots, copies, dt=0.1, soft=False, substreams=1):
     ref = _batch(ctx, solver, x, u, N, dt, soft)
-    s = ctx.solve_stream(x, u, N, dt, solver, slots=slots, copies=copies)
+    s = ctx.solve_stream(x, u, N, dt, solver, slots=slots, copies=copies, substreams=substreams)
     P0 = x.shape[0]
     for p in range(P0 * copies):
         i = p % P0
@@ -142,3 +142,22 @@ def test_stream_counts_every_problem_once(ctx):
     ctx.solve_stream(x, u, 12, 0.1, "PCG-SS", slots=2, copies=2, with_trace=False)
     cs = ctx.solve_counters()
     assert cs[0] == 2 * cb[0] and cs[1] == 2 * cb[1] and cs[2] == 2 * cb[2], (cs, cb)
+
+
+@pytest.mark.parametrize("solver,K", [("PCG-SS", 2), ("PCG-SS", 3), ("iLQR", 2)])
+def test_stream_substreams_equal_batch(ctx, solver, K):
+    """K concurrent sub-streams (own HIP stream, slots / K slots, a contiguous 1 / K of the problems each, host
+    threads): every problem's results still equal its batch solve's bitwise, at its global output row"""
+    _setup(ctx, 3, {"torque": dict(mode="AUGMENTED_LAGRANGIAN", lb=-0.5, ub=0.5)})
+    x, u = _problems(3, 16, range(800, 811))
+    _assert_stream_equals_batch(ctx, solver, x, u, 16, slots=6, copies=2, soft=True, substreams=K)
+
+
+def test_stream_substreams_count_every_problem_once(ctx):
+    _setup(ctx, 3)
+    x, u = _problems(3, 12, range(900, 907))
+    ctx.sqp_solve_batch(x, u, 12, 0.1, "PCG-SS", with_trace=False)
+    cb = ctx.solve_counters()
+    ctx.solve_stream(x, u, 12, 0.1, "PCG-SS", slots=4, copies=3, with_trace=False, substreams=2)
+    cs = ctx.solve_counters()
+    assert cs[:3] == [3 * v for v in cb[:3]], (cs, cb)

@@ -26,7 +26,7 @@ WL = {
 }
 
 
-def run(name, copies=4):
+def run(name, copies=4, substreams=1):
     w = WL[name]
     n, N, B, dt = w["n"], w["N"], w["B"], 0.1
     nx, nu = 2 * n, n
@@ -69,7 +69,7 @@ def run(name, copies=4):
     ctx.set_options(profile=1)
     ctx.reset_stats()
     t = time.perf_counter()
-    ctx.solve_stream_device(w["solver"], P, B, N, dt, d_x0, d_u0, B, d_xo, d_uo, d_st)
+    ctx.solve_stream_device(w["solver"], P, B, N, dt, d_x0, d_u0, B, d_xo, d_uo, d_st, substreams=substreams)
     ctx.synchronize()
     t_stream = time.perf_counter() - t
     ctx.set_options(profile=0)
@@ -85,7 +85,7 @@ def run(name, copies=4):
     ctx.d2d(d_x, d_xo, x0.nbytes)
     ctx.d2h(xo, d_x)
     mism = int(np.sum((st[:, 0] != np.tile(ex_b, copies)) | (st[:, 1] != np.tile(it_b, copies))))
-    out = dict(workload=name, B=B, copies=copies, batch_solves_per_s=B / t_batch,
+    out = dict(workload=name, B=B, copies=copies, substreams=substreams, batch_solves_per_s=B / t_batch,
                stream_solves_per_s=P / t_stream, speedup=(P / t_stream) / (B / t_batch),
                status_mismatches=mism, x_copy0_bitwise=bool(np.array_equal(xo, xb)), kernels=kern,
                iters_mean=float(np.mean(it_b)), iters_max=int(np.max(it_b)))
@@ -94,5 +94,7 @@ def run(name, copies=4):
 
 
 if __name__ == "__main__":
-    for name in sys.argv[1:] or ["head"]:
-        run(name)
+    # args: workload[:copies[:substreams]] ...
+    for spec in sys.argv[1:] or ["head"]:
+        parts = spec.split(":")
+        run(parts[0], int(parts[1]) if len(parts) > 1 else 4, int(parts[2]) if len(parts) > 2 else 1)

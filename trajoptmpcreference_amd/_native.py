@@ -67,7 +67,7 @@ class tmpc_trace(C.Structure):
 
 class tmpc_stream(C.Structure):
     """continuous batching (tmpc_*_solve_stream_device): device arrays, include/tmpc.h"""
-    _fields_ = [("problems", C.c_int32), ("slots", C.c_int32), ("period", C.c_int32), ("reserved", C.c_int32),
+    _fields_ = [("problems", C.c_int32), ("slots", C.c_int32), ("period", C.c_int32), ("substreams", C.c_int32),
                 ("x_in", C.c_void_p), ("u_in", C.c_void_p), ("x_out", C.c_void_p), ("u_out", C.c_void_p),
                 ("status", C.c_void_p), ("trace", tmpc_trace)]
 
@@ -561,11 +561,11 @@ class Context:
         return ex, it
 
     def solve_stream_device(self, solver, P, slots, N, dt, d_x_in, d_u_in, period, d_x_out=None, d_u_out=None,
-                            d_status=None, d_trace=None):
+                            d_status=None, d_trace=None, substreams=1):
         """Continuous batching (tmpc_sqp_solve_stream_device / tmpc_ilqr_solve_stream_device): P problems
         through `slots` resident slots, problem p from input p % period; device pointers (d_trace: dict of
-        trace field -> device pointer [P][max_iter+1])."""
-        st = tmpc_stream(problems=int(P), slots=int(slots), period=int(period), reserved=0, x_in=d_x_in,
+        trace field -> device pointer [P][max_iter+1]); substreams: K concurrent sub-streams."""
+        st = tmpc_stream(problems=int(P), slots=int(slots), period=int(period), substreams=int(substreams), x_in=d_x_in,
                          u_in=d_u_in, x_out=d_x_out, u_out=d_u_out, status=d_status)
         for name, dt_ in TRACE_FIELDS:
             p = (d_trace or {}).get(name)
@@ -578,7 +578,7 @@ class Context:
             self._check(self.lib.tmpc_sqp_solve_stream_device(self.h, int(N), float(dt), LINSYS[solver], C.byref(st)),
                         "tmpc_sqp_solve_stream_device")
 
-    def solve_stream(self, x, u, N, dt, solver="PCG-SS", slots=64, copies=1, with_trace=True):
+    def solve_stream(self, x, u, N, dt, solver="PCG-SS", slots=64, copies=1, with_trace=True, substreams=1):
         """Host convenience of solve_stream_device: problems x [P0][nx][N], u [P0][nu][N-1], each solved
         `copies` times (stream problem p = input p % P0) through `slots` slots.  Returns x, u [P][..],
         status fields (exit, iters, exit_soft, outer_iter) [P] and the trace [P][max_iter+1]."""
@@ -598,7 +598,7 @@ class Context:
             self.h2d(dui, u)
             dxo, duo, dst = dev(x.nbytes * copies), dev(u.nbytes * copies), dev(P * 4 * 4)
             dtr = {name: dev(P * W * np.dtype(dt_).itemsize) for name, dt_ in TRACE_FIELDS} if with_trace else None
-            self.solve_stream_device(solver, P, slots, N, dt, dxi, dui, P0, dxo, duo, dst, dtr)
+            self.solve_stream_device(solver, P, slots, N, dt, dxi, dui, P0, dxo, duo, dst, dtr, substreams)
             xo = np.empty((P,) + x.shape[1:])
             uo = np.empty((P,) + u.shape[1:])
             status = np.empty((P, 4), dtype=np.int32)

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tmpc.h"
@@ -67,6 +68,8 @@ struct tmpc_ctx {
   // other user of those buffers (setup_hard) and by a change of the limits, so stale data is refused
   struct { int B, N, dmax, W, rmax; } hard_last{0, 0, 0, 0, 0};
   std::map<std::string, double> kbytes;   // bytes beyond registers / LDS of counting kernels since tmpc_reset_stats
+  std::vector<tmpc_ctx*> subs;            // a stream's concurrent sub-streams (tmpc_stream.substreams): own HIP
+                                          // stream and buffers each, the configuration copied from this context
 };
 
 static int fail(tmpc_ctx* c, const char* fmt, ...) {
@@ -1010,6 +1013,7 @@ void tmpc_destroy(tmpc_ctx* ctx) {
     hipEventDestroy(p.stop);
   }
   for (auto e : ctx->event_pool) hipEventDestroy(e);
+  for (tmpc_ctx* sub : ctx->subs) tmpc_destroy(sub);
   for (auto& kv : ctx->bufs)
     if (kv.second.ptr) hipFree(kv.second.ptr);
   if (ctx->dmodel) hipFree(ctx->dmodel);
@@ -1347,6 +1351,7 @@ static int stream_setup(tmpc_ctx* ctx, int N, const tmpc_stream* s, StreamDev& s
     return fail(ctx, "stream: problems %d (>= 0), slots %d and period %d (>= 1)", s->problems, s->slots, s->period);
   if (!s->x_in || !s->u_in) return fail(ctx, "stream: null x_in / u_in");
   if (s->trace.hard_active) return fail(ctx, "stream: trace.hard_active is not supported (set it to NULL)");
+  if (s->substreams < 0 || s->substreams > 8) return fail(ctx, "stream: substreams %d (0..8)", s->substreams);
   B = std::min(s->slots, s->problems);
   const int nj = ctx->hmodel.n, nx = 2 * nj;
   BUF(double, stream_x, (size_t)std::max(B, 1) * nx * N);
@@ -1357,6 +1362,7 @@ static int stream_setup(tmpc_ctx* ctx, int N, const tmpc_stream* s, StreamDev& s
   *d_u = stream_u;
   sd = StreamDev{};
   sd.P = s->problems;
+  sd.pbase = 0;
   sd.period = s->period;
   sd.NX = nx;
   sd.NU = nj;
@@ -1376,30 +1382,99 @@ static int stream_setup(tmpc_ctx* ctx, int N, const tmpc_stream* s, StreamDev& s
   return 0;
 }
 
-int tmpc_sqp_solve_stream_device(tmpc_ctx* ctx, int N, double dt, int linsys, const tmpc_stream* stream) {
-  if (!ctx) return -1;
-  int rc = check_ready(ctx, 1, N);
-  if (rc) return rc;
-  hipSetDevice(ctx->device);
+// One (sub-)stream on one context: problems [pbase, pbase + s->problems) of the caller's stream.
+static int stream_one(tmpc_ctx* ctx, int N, double dt, int linsys, const tmpc_stream* s, int pbase) {
   StreamDev sd;
   int B = 0;
   double *d_x = nullptr, *d_u = nullptr;
-  if ((rc = stream_setup(ctx, N, stream, sd, B, &d_x, &d_u))) return rc;
-  if (B == 0) return 0;
-  return sqp_device(ctx, B, N, dt, linsys, d_x, d_u, nullptr, false, false, &sd);
+  int rc = stream_setup(ctx, N, s, sd, B, &d_x, &d_u);
+  if (rc || B == 0) return rc;
+  sd.pbase = pbase;
+  return linsys < 0 ? ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr, &sd)
+                    : sqp_device(ctx, B, N, dt, linsys, d_x, d_u, nullptr, false, false, &sd);
+}
+
+// The stream, split over K = substreams concurrent sub-streams: sub-stream c has its own context (HIP stream,
+// buffers, lock-step loop on its own host thread), slots / K of the slots and a contiguous 1 / K of the
+// problems.  Their kernels run side by side on the GPU, so one sub-stream's latency-bound phases (a one-wave
+// Riccati sweep, a rollout with fewer lanes than SIMDs) overlap the other's.  Each problem's operations are
+// unchanged, so its results are too.  linsys < 0: iLQR.
+static int stream_solve(tmpc_ctx* ctx, int N, double dt, int linsys, const tmpc_stream* s) {
+  int rc = linsys < 0 ? check_ready(ctx, 1, N, false) : check_ready(ctx, 1, N);
+  if (rc) return rc;
+  if (!s) return fail(ctx, "null stream");
+  hipSetDevice(ctx->device);
+  const int K = std::max(1, std::min({s->substreams, s->slots, std::max(1, s->problems), 8}));
+  if (K == 1 || s->substreams <= 1) return stream_one(ctx, N, dt, linsys, s, 0);
+  if (s->slots < 1 || s->problems < 0 || s->period < 1 || !s->x_in || !s->u_in)
+    return stream_one(ctx, N, dt, linsys, s, 0);   // the argument errors, as for one stream
+  while ((int)ctx->subs.size() < K) {
+    tmpc_ctx* sub = nullptr;
+    if (tmpc_create(ctx->device, &sub) != 0) return fail(ctx, "stream: creating sub-stream context failed");
+    ctx->subs.push_back(sub);
+  }
+  for (int c = 0; c < K; ++c) {   // the configuration of this context
+    tmpc_ctx* sub = ctx->subs[c];
+    sub->hmodel = ctx->hmodel;
+    sub->hcost = ctx->hcost;
+    sub->hlim = ctx->hlim;
+    sub->model_id = ctx->model_id;
+    sub->opts = ctx->opts;
+    sub->has_model = ctx->has_model;
+    sub->has_cost = ctx->has_cost;
+    sub->soft_B = sub->soft_N = -1;
+    sub->stats.clear();
+    sub->kbytes.clear();
+    sub->err.clear();
+    HIP_OK(hipMemcpyAsync(sub->dmodel, &sub->hmodel, sizeof(ModelDev), hipMemcpyHostToDevice, sub->stream));
+    HIP_OK(hipMemcpyAsync(sub->dcost, &sub->hcost, sizeof(CostDev), hipMemcpyHostToDevice, sub->stream));
+    HIP_OK(hipMemcpyAsync(sub->dlim, &sub->hlim, sizeof(ConstrDev), hipMemcpyHostToDevice, sub->stream));
+    HIP_OK(hipStreamSynchronize(sub->stream));
+  }
+  std::vector<tmpc_stream> part(K, *s);
+  std::vector<int> pbase(K, 0), rcs(K, 0);
+  for (int c = 0, p0 = 0; c < K; ++c) {
+    part[c].problems = s->problems / K + (c < s->problems % K ? 1 : 0);
+    part[c].slots = s->slots / K + (c < s->slots % K ? 1 : 0);
+    part[c].substreams = 1;
+    pbase[c] = p0;
+    p0 += part[c].problems;
+  }
+  std::vector<std::thread> th;
+  for (int c = 0; c < K; ++c)
+    th.emplace_back([&, c]() {
+      hipSetDevice(ctx->device);
+      rcs[c] = stream_one(ctx->subs[c], N, dt, linsys, &part[c], pbase[c]);
+    });
+  for (auto& t : th) t.join();
+  for (int c = 0; c < K; ++c)
+    if (rcs[c]) return fail(ctx, "sub-stream %d: %s", c, ctx->subs[c]->err.c_str());
+  for (int i = 0; i < 3; ++i) {
+    ctx->last_counters[i] = 0;
+    for (int c = 0; c < K; ++c) ctx->last_counters[i] += ctx->subs[c]->last_counters[i];
+  }
+  ctx->last_counters[3] = ctx->subs[0]->last_counters[3];
+  for (int c = 0; c < K; ++c) {   // kernel timings and counted bytes of every sub-stream
+    for (auto& kv : ctx->subs[c]->stats) {
+      ctx->stats[kv.first].launches += kv.second.launches;
+      ctx->stats[kv.first].total_ms += kv.second.total_ms;
+    }
+    for (auto& kv : ctx->subs[c]->kbytes) ctx->kbytes[kv.first] += kv.second;
+  }
+  ctx->soft_B = ctx->soft_N = -1;
+  return 0;
+}
+
+int tmpc_sqp_solve_stream_device(tmpc_ctx* ctx, int N, double dt, int linsys, const tmpc_stream* stream) {
+  if (!ctx) return -1;
+  if (precond_of(linsys) < 0)
+    return fail(ctx, "linear system method %d is not available on the GPU (use S/PCG-J/BJ/SS = 1/2/3/4)", linsys);
+  return stream_solve(ctx, N, dt, linsys, stream);
 }
 
 int tmpc_ilqr_solve_stream_device(tmpc_ctx* ctx, int N, double dt, const tmpc_stream* stream) {
   if (!ctx) return -1;
-  int rc = check_ready(ctx, 1, N, false);
-  if (rc) return rc;
-  hipSetDevice(ctx->device);
-  StreamDev sd;
-  int B = 0;
-  double *d_x = nullptr, *d_u = nullptr;
-  if ((rc = stream_setup(ctx, N, stream, sd, B, &d_x, &d_u))) return rc;
-  if (B == 0) return 0;
-  return ilqr_device(ctx, B, N, dt, d_x, d_u, nullptr, &sd);
+  return stream_solve(ctx, N, dt, -1, stream);
 }
 
 // ------------------------------------------------------------------ receding-horizon MPC (oracle/mpc.py)

@@ -150,12 +150,13 @@ void launch_sum_counters(hipStream_t s, int B, const unsigned long long* pc, uns
 // solve, so its results are bitwise those of tmpc_*_solve_batch.
 struct StreamDev {
   int P, period, NX, NU, N, W, MC;   // problems, input period, sizes, trace rows, soft slots per knot (6 n)
-  const double* x_in;                // [period][NX][N]: problem p starts from input p % period
+  int pbase;                         // global index of this (sub-)stream's problem 0 (inputs and output rows)
+  const double* x_in;                // [period][NX][N]: problem p starts from input (pbase + p) % period
   const double* u_in;                // [period][NU][N-1]
-  double* x_out;                     // [P][NX][N] (nullable)
-  double* u_out;                     // [P][NU][N-1] (nullable)
-  int* status;                       // [P][4]: exit code, iterations, exit_soft, outer_iter (nullable)
-  TraceDev tr_out;                   // [P][W] per field (each nullable; hard_active unused)
+  double* x_out;                     // [pbase + P][NX][N] (nullable): problem p's row is pbase + p
+  double* u_out;                     // [pbase + P][NU][N-1] (nullable)
+  int* status;                       // [pbase + P][4]: exit code, iterations, exit_soft, outer_iter (nullable)
+  TraceDev tr_out;                   // [pbase + P][W] per field (each nullable; hard_active unused)
   int* slot_pid;                     // [B] problem in the slot (-1: none)
   int* next;                         // [1] next pending problem
 };

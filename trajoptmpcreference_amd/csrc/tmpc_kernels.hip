@@ -1319,12 +1319,13 @@ __device__ void stream_handover(int s, const StreamDev& sd, double* __restrict__
                                 double* __restrict__ phi, double* __restrict__ lam_warm) {
   __shared__ int s_next;
   const int t = threadIdx.x, nt = blockDim.x;
-  const int old = sd.slot_pid[s];
+  const int old_l = sd.slot_pid[s];
+  const int old = sd.pbase + old_l;   // the output row (global problem index)
   const int XN = sd.NX * sd.N, UN = sd.NU * (sd.N - 1), W = sd.W;
   double* xb = x + (size_t)s * XN;
   double* ub = u + (size_t)s * UN;
   if (t == 0) s_next = atomicAdd(sd.next, 1);
-  if (old >= 0) {
+  if (old_l >= 0) {
     if (sd.x_out)
       for (int e = t; e < XN; e += nt) sd.x_out[(size_t)old * XN + e] = xb[e];
     if (sd.u_out)
@@ -1353,7 +1354,7 @@ __device__ void stream_handover(int s, const StreamDev& sd, double* __restrict__
     if (t == 0) sd.slot_pid[s] = -1;
     return;
   }
-  const size_t src = (size_t)(nw % sd.period);
+  const size_t src = (size_t)((sd.pbase + nw) % sd.period);
   for (int e = t; e < XN; e += nt) xb[e] = sd.x_in[src * XN + e];
   for (int e = t; e < UN; e += nt) ub[e] = sd.u_in[src * UN + e];
   for (int m = t; m < sd.NX; m += nt) xs[(size_t)s * sd.NX + m] = sd.x_in[src * XN + (size_t)m * sd.N];
@@ -1553,7 +1554,7 @@ __global__ void __launch_bounds__(256) k_stream_init(int B, StreamDev sd, double
                                                      double* __restrict__ u) {
   const int s = blockIdx.x, t = threadIdx.x;
   const int XN = sd.NX * sd.N, UN = sd.NU * (sd.N - 1);
-  const size_t src = (size_t)(s % sd.period);
+  const size_t src = (size_t)((sd.pbase + s) % sd.period);
   for (int e = t; e < XN; e += blockDim.x) x[(size_t)s * XN + e] = sd.x_in[src * XN + e];
   for (int e = t; e < UN; e += blockDim.x) u[(size_t)s * UN + e] = sd.u_in[src * UN + e];
   if (t == 0) {
