@@ -193,6 +193,8 @@ def workload_key(a):
         key += "_warm"
     if a.cost != "quadratic":
         key += "_" + a.cost
+    if not getattr(a, "lockstep", True) and a.mpc_steps == 0:   # continuous batching: its own launches
+        key += f"_stream{max(1, getattr(a, 'substreams', 1))}"
     return key.replace("/", "-")
 
 
@@ -449,29 +451,37 @@ def hard_limits(preset):
     return any(v["mode"] in ("ACTIVE_SET", "FULL_SET") for v in LIMIT_PRESETS[preset].values())
 
 
-def hard_roofline(a, kernels, hard_bytes):
-    """Roofline of k_hard_pcg, the hard-limit path's dominant kernel.  `achieved` = the bytes the kernel
-    itself counts (tmpc_kernel_bytes): everything it reads and writes beyond its registers and
-    LDS -- per iteration the band entries not held in registers and the preconditioner blocks not held in
-    LDS, gamma in, lambda out, the setup blocks -- / the average launch time, against the HBM peak.  After
-    the first iteration those re-reads are L2 hits (a problem's streamed part is ~85 kB; 32 problems per
-    XCD fit its 4 MB L2): `traffic`, the PMC bytes, is what reaches the fabric, and hbm_GBps / hbm_frac
-    show how little HBM the kernel uses.  It is bound by one problem's iteration latency, not by memory."""
+def hard_roofline(a, kernels, hard_bytes, counters=None):
+    """Roofline of k_hard_pcg, the hard-limit path's dominant kernel: one 16-wave workgroup per problem keeps
+    each row's first band entries in registers and the preconditioner blocks in LDS for the whole solve, so
+    an iteration is bound by its LDS traffic and its two workgroup reductions' latency, not by
+    HBM.  `achieved` = the LDS bytes an iteration serves (lds_model: per row and PCG iteration the 3 nx band
+    entries' p, the SS preconditioner's 3 nx block entries and the 3 nx r entries they multiply, 9 nx doubles,
+    plus 3 vector writes; D = N nx rows, the hard rows not counted, so a lower bound) x PCG iterations per launch
+    / the HIP-event launch time, against the CUs' LDS bandwidth.  `traffic` / hbm_frac: the PMC bytes that reach
+    HBM.  `self_counted`: the bytes the kernel reads and writes beyond registers and LDS
+    (tmpc_kernel_bytes), served by L2 after the first iteration."""
     hp = kernels["hard_pcg"]
-    per_launch = hard_bytes / hp["launches"]
     avg_s = hp["avg_ms"] / 1e3
-    ach = per_launch / avg_s / 1e9
+    nx, N = 2 * a.links, a.N
+    iters = int(counters[1]) / max(1, hp["launches"]) if counters is not None else None
+    lds = iters * 8.0 * N * nx * (9 * nx + 3) if iters is not None else None
     traffic, src = measured_traffic("void tmpc::k_hard_pcg<", workload_key(a))
-    out = {"kernel": "k_hard_pcg", "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "avg_launch_ms": hp["avg_ms"],
-           "algorithmic_bytes_per_launch": per_launch,
-           "bytes_basis": "counted by the kernel per problem: 8 B x (2 D + iterations x band entries not in "
-                          "registers + (iterations + 1) x distinct preconditioner entries not in LDS + once: "
-                          "register-held band entries, setup blocks), DESIGN.md 4f; served by L2 after the first "
-                          "iteration",
-           "note": "each row's first band entries stay in registers and the preconditioner blocks in LDS for "
-                   "the whole solve, so memory is not what binds: one 16-wave workgroup per problem, the PCG "
-                   "iteration's barrier-separated phases (DESIGN.md 4f)"}
+    out = {"kernel": "k_hard_pcg", "bound": "lds",
+           "bound_note": "LDS bandwidth and the two workgroup reductions' latency per PCG iteration (the contract's "
+                         "enum has hbm / mfma only; HBM is what this kernel does NOT use: hbm_frac)",
+           "achieved": lds / avg_s / 1e9 if lds else None, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+           "frac": lds / avg_s / 1e9 / LDS_PEAK_GBS if lds else None, "traffic": traffic,
+           "avg_launch_ms": hp["avg_ms"], "pcg_iters_per_launch": iters, "lds_bytes_per_launch": lds,
+           "lds_basis": "8 B x N nx rows x (9 nx + 3) per PCG iteration (DESIGN.md 4h: a row reads 3 nx p, 3 nx "
+                        "preconditioner and 3 nx r entries from LDS)"}
+    if hard_bytes:
+        per_launch = hard_bytes / hp["launches"]
+        out["self_counted"] = {"bytes_per_launch": per_launch, "GBps": per_launch / avg_s / 1e9,
+                               "basis": "counted by the kernel per problem: 8 B x (2 D + iterations x band entries not "
+                                        "in registers + (iterations + 1) x distinct preconditioner entries not in LDS "
+                                        "+ once: register-held band entries, setup blocks), DESIGN.md 4f; L2 hits after "
+                                        "the first iteration"}
     if traffic:
         out.update(hbm_GBps=traffic / avg_s / 1e9, hbm_frac=traffic / avg_s / 1e9 / HBM_PEAK_GBS,
                    traffic_source=src,
@@ -874,8 +884,8 @@ def run_line(ctx, comm, rank, world, a, steps, warmup, stream, lockstep_steps, s
 def line_roofline(a, N, nx, nu, kernels, counters, hard_bytes=None):
     if a.solver == "sqp" and a.method.startswith("PCG") and "qp" in kernels and (a.mpc_steps == 0 or N * nx > 1024):
         return sqp_roofline(a, N, nx, nu, kernels, counters)
-    if hard_bytes and "hard_pcg" in kernels:
-        return hard_roofline(a, kernels, hard_bytes)
+    if hard_limits(a.limits) and "hard_pcg" in kernels:
+        return hard_roofline(a, kernels, hard_bytes, counters)
     if a.solver == "ilqr" and "ilqr_backward" in kernels:
         bw = kernels["ilqr_backward"]
         per_launch = int(counters[0]) / max(1, bw["launches"])
@@ -1088,8 +1098,9 @@ def run_config_lines(ctx, comm, rank, world, a):
         if key in a.skip_lines:
             continue
         stream = not a.lockstep and b.mpc_steps == 0
+        b.substreams = LINE_SUBSTREAMS.get(key, 1)
         line, d, u0, counters, kernels, hb = run_line(ctx, comm, rank, world, b, steps, 1, stream,
-                                                      a.lockstep_steps if stream else 0, LINE_SUBSTREAMS.get(key, 1))
+                                                      a.lockstep_steps if stream else 0, b.substreams)
         nx, nu = 2 * b.links, b.links
         line["metric"] = f"MPC solves/sec (arm{b.links}.urdf, N={b.N}, {workload_name(b)}) -- {label}"
         if b.mpc_steps:
