@@ -334,7 +334,27 @@ int tmpc_qp_blocks_batch(tmpc_ctx* ctx, int B, int N, int nx, int nu, int linsys
                          const double* A, const double* Bm, const double* c, const double* rho, const double* guess,
                          double* dxul, int32_t* pcg_iters, double* S_diag, double* S_lo, double* gamma);
 
-/* Hard-limit detail of the last tmpc_qp_batch call with hard box limits (same B, N): sizes[2] = {dmax, W} of
+/* The plugin-hook QP on the banded path (ABI 10): solveKKTSystem / solveKKTSystem_Schur
+ * (TrajoptMPCReference.py:313-455) on the caller's formKKTSystemBlocks blocks (:200-271) WITH hard rows
+ * (ACTIVE_SET / FULL_SET, :238-248) and / or past tmpc_qp_blocks_batch's 1024 rows.  G, g, A, Bm, c, rho as
+ * tmpc_qp_blocks_batch; the hard rows of each knot in the reference's order, from the caller's constraint
+ * hooks (value_hard_constraints / jacobian_hard_constraints): hcnt [B][N] rows per knot, hcol [B][N][rmax]
+ * the row's column in [x_k; u_k], hsgn [B][N][rmax] its jacobian entry (+1 / -1, or 0 for a FULL_SET row that
+ * is not violated), hval [B][N][rmax] its value; every row a box row (one entry of [x_k; u_k]), which is what
+ * the reference's BoxConstraint produces.  Outputs: dxul [B][n(N-1)+nx + nx N] (the lambda part: the N nx
+ * dynamics / initial-state rows' multipliers in knot order), pcg_iters [B], lambda_hard [B][N][rmax] the hard
+ * rows' multipliers, singular [B] (the direct methods' least-squares flag); all nullable.  The banded kernels of
+ * the device path (k_hard_schur / k_hard_pcg / k_hard_direct / k_hard_dxu) with the caller's full
+ * (G_k + rho I)^-1 blocks (partial-pivoting Gauss-Jordan) and gradient; summation order oracle/hard.py. */
+int tmpc_qp_blocks_banded_batch(tmpc_ctx* ctx, int B, int N, int nx, int nu, int linsys, const double* G,
+                                const double* g, const double* A, const double* Bm, const double* c,
+                                const int32_t* hcnt, const int32_t* hcol, const double* hsgn, const double* hval,
+                                int rmax, const double* rho, double* dxul, int32_t* pcg_iters, double* lambda_hard,
+                                int32_t* singular);
+
+/* Hard-limit detail of the last tmpc_qp_batch call with hard box limits, or of the last
+ * tmpc_qp_blocks_banded_batch call (same B, N; there the bits and slots are t * 2 nu + e over the given
+ * rows' columns, 6 n slots of the context's model): sizes[2] = {dmax, W} of
  * the banded Schur complement (rows padded to dmax, half band W), dim [B] its dimension per problem
  * (N nx + hard rows), active [B][N] the per-knot active-set bitmasks (as tmpc_trace.hard_active),
  * lambda_hard [B][N][6 n] the hard rows' multipliers by slot t * 2n + e (0 where no row), S_band

@@ -756,6 +756,92 @@ def run_plugins(args):
            f"pcg={list(pcg_iters)}"
 
 
+def run_plugins_hard(args):
+    """The reference's SQP with a user cost plugin (tests/plugin_models.py CoupledCost, written against the
+    reference's TrajoptCost: an x-u cross term, time-varying) AND hard ACTIVE_SET torque limits on the
+    1-link arm (constraint_size 1, the size the reference's BoxConstraint runs): the hard rows are
+    appended to C after each knot's dynamics rows (TrajoptMPCReference.py:238-248) on the plugin's own
+    blocks.  Records run_hard's fields (per-QP active rows from the reference's own C, PCG counts)."""
+    method, N, q0, seed, dt = args
+    _setup_reference()
+    sys.path.insert(0, os.path.dirname(OUT))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    import plugin_models as pm
+    from trajoptmpcreference_amd.urdf import planar_arm_urdf
+    from TrajoptPlant import URDFPlant
+    from TrajoptCost import TrajoptCost
+    from TrajoptConstraint import TrajoptConstraint
+    from TrajoptMPCReference import TrajoptMPCReference, SQPSolverMethods
+    from overloading import matrix_
+    matrix_.iteration = 0
+    matrix_.soft_constraint_iteration = 0
+    matrix_.line_search_iteration = 0
+
+    class CoupledCost(TrajoptCost):
+        def __init__(self, nx, nu):
+            self.arrs = pm.coupled_arrays(nx, nu)
+
+        def value(self, x, u=None, timestep=None, *a, **k):
+            return pm.coupled_value(x, u, timestep, self.arrs)
+
+        def gradient(self, x, u=None, timestep=None, *a, **k):
+            return pm.coupled_gradient(x, u, timestep, self.arrs)
+
+        def hessian(self, x, u=None, timestep=None, *a, **k):
+            return pm.coupled_hessian(x, u, timestep, self.arrs)
+
+    urdf = planar_arm_urdf(1)
+    d = tempfile.mkdtemp(prefix="tmpc_urdf_")
+    path = os.path.join(d, "arm1.urdf")
+    with open(path, "w") as f:
+        f.write(urdf)
+    plant = URDFPlant(options={"path_to_urdf": path, "overloading": False})
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((2, N))
+    x0[0, 0] = q0 + rng.uniform(-0.1, 0.1)
+    u0 = np.zeros((1, N - 1))
+    for k in range(N - 1):
+        x0[:, k + 1] = plant.integrator(x0[:, k], u0[:, k], dt)
+    lb, ub = -0.2, 0.2
+    con = TrajoptConstraint(1, 1, 1, N)
+    con.overloading = False   # attribute the reference reads but never sets (SURVEY F6)
+    con.set_torque_limits([ub], [lb], "ACTIVE_SET", {"overloading": False})
+    solver = TrajoptMPCReference(plant, CoupledCost(2, 1), con)
+    m = {"S": SQPSolverMethods.S, "PCG-J": SQPSolverMethods.PCG_J, "PCG-BJ": SQPSolverMethods.PCG_BJ,
+         "PCG-SS": SQPSolverMethods.PCG_SS, "N": SQPSolverMethods.N}[method]
+    import io
+    import contextlib
+    with contextlib.redirect_stdout(io.StringIO()):
+        x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(copy.deepcopy(x0), copy.deepcopy(u0), N, dt, m,
+                                                                     {"overloading": False})
+    tr = solver.trace
+    keys = ["iteration", "line_search_iteration", "alpha", "rho", "J", "c", "merit", "D", "reduction_ratio",
+            "succeeded_line_search", "singular"]
+    rec = {"tr_" + k: np.array([np.nan if t[k] is None else float(np.asarray(t[k]).reshape(-1)[0]) for t in tr])
+           for k in keys}
+    nx, n = 2, 3
+    act_knot, act_sign, act_qp = [], [], []
+    for q, dC in enumerate(solver.saved_C):
+        C = np.asarray(dC["value"])
+        for r in range(C.shape[0]):
+            row = C[r]
+            nzc = np.nonzero(row)[0]
+            if r >= nx and len(nzc) == 1 and (nzc[0] % n) == nx:   # a torque row: one entry in a u column
+                act_qp.append(q)
+                act_knot.append(int(nzc[0] // n))
+                act_sign.append(int(np.sign(row[nzc[0]])))
+    pcg_iters = np.array([len(t[0][0]) - 1 for t in solver.saved_inner_traces], dtype=np.int32)
+    rows = np.array([np.asarray(dC["value"]).shape[0] for dC in solver.saved_C], dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, f"plugin_hard_arm1_N{N}_s{seed}_{method}.npz"),
+                        urdf=np.array(urdf), x0=x0, u0=u0, x=np.asarray(x), u=np.asarray(u), dt=dt, lb=lb, ub=ub,
+                        exit_sqp=exit_sqp, exit_soft=exit_soft, outer_iter=outer_iter, sqp_iter=sqp_iter,
+                        pcg_iters=pcg_iters, C_rows=rows, act_qp=np.array(act_qp, dtype=np.int32),
+                        act_knot=np.array(act_knot, dtype=np.int32), act_sign=np.array(act_sign, dtype=np.int32),
+                        **rec)
+    return f"[golden] plugin+hard {method} N={N} seed={seed}: exit_sqp={exit_sqp} iters={sqp_iter} rows={list(rows)} " \
+           f"pcg={list(pcg_iters)}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="skip the slow arm6 N=64 solves")
@@ -826,6 +912,12 @@ def main():
                 ("plant", 20, 1, "N", 0.1), ("plant", 20, 2, "PCG-BJ", 0.1)]
         with mp.get_context("fork").Pool(len(jobs)) as pool:
             for msg in pool.imap_unordered(run_plugins, jobs):
+                print(msg, flush=True)
+    if a.only in (None, "plugins_hard"):
+        jobs = [("PCG-SS", 10, 2.0, 20, 0.1), ("S", 10, 2.0, 21, 0.1), ("N", 12, 2.5, 22, 0.1),
+                ("PCG-BJ", 12, 2.2, 23, 0.1)]
+        with mp.get_context("fork").Pool(len(jobs)) as pool:
+            for msg in pool.imap_unordered(run_plugins_hard, jobs):
                 print(msg, flush=True)
     if a.only in (None, "soft"):
         jobs = [("QUADRATIC_PENALTY", "PCG-SS", 8, 2.0, 0, 0.1), ("AUGMENTED_LAGRANGIAN", "PCG-SS", 8, 2.0, 0, 0.1),

@@ -6,7 +6,10 @@ TrajoptCost / TrajoptPlant base classes):
   * CoupledCost -- a QuadraticCost subclass here that overrides value / gradient / hessian with a
     time-varying cost with an x-u cross term (its G_k is not block-diagonal) -- on arm3 N = 10;
   * SpringPlant -- a TrajoptPlant subclass without URDF (closed-form dynamics and gradient) with
-    CoupledCost, N = 20.
+    CoupledCost, N = 20;
+  * CoupledCost with hard ACTIVE_SET torque limits on the 1-link arm (plugin_hard_*.npz, make_golden.py
+    run_plugins_hard): the hooks' hard rows (TrajoptConstraint.py's value/jacobian at each knot) go through
+    tmpc_qp_blocks_banded_batch -- the banded Schur path on the plugin's own blocks.
 
 Integers exact against the reference's run: exit code, SQP iterations, line-search iterations, the
 alpha path, the PCG count of every QP; J / c / merit / trajectories at 1e-7 relative.  Every QP is also
@@ -26,7 +29,9 @@ from conftest import GOLDEN, quad_cost_arrays
 
 pytestmark = pytest.mark.gpu
 
-FILES = sorted(glob.glob(os.path.join(GOLDEN, "plugin_*.npz")))
+FILES = sorted(f for f in glob.glob(os.path.join(GOLDEN, "plugin_*.npz"))
+               if not os.path.basename(f).startswith("plugin_hard_"))
+HARD_FILES = sorted(glob.glob(os.path.join(GOLDEN, "plugin_hard_*.npz")))
 
 
 def _classes():
@@ -239,3 +244,131 @@ def test_plugin_qp_with_an_indefinite_hessian_block():
         got = r["dxul"][0]
         assert np.all(np.isfinite(got)), meth
         assert np.max(np.abs(got[:nz] - ref[:nz])) < tol * max(1.0, np.max(np.abs(ref[:nz]))), meth
+
+
+@pytest.mark.parametrize("f", HARD_FILES, ids=lambda f: os.path.basename(f))
+def test_plugin_cost_with_hard_limits_matches_reference(f, monkeypatch):
+    """A user cost plugin AND hard ACTIVE_SET torque limits (TrajoptMPCReference.py:238-248 appends the
+    constraint's rows to C after each knot's dynamics rows, on the plugin's own blocks) against the
+    reference's own run: exit code, SQP iterations, every QP's active set (bit 4 = a row of sign +1 active at
+    the knot, bit 5 = sign -1, read back from the reference's own C), the alpha path, line-search iterations,
+    every PCG count exact; J / c / merit / trajectories at 1e-7.  Every PCG QP is replayed on its own S:
+    the canonical-order PCG (oracle/hard.py) takes the GPU's count."""
+    from oracle import hard as ohard
+    from trajoptmpcreference_amd import TrajoptConstraint, TrajoptMPCReference, URDFPlant, _native
+    _, CoupledCost, _ = _classes()
+    d = np.load(f)
+    N = d["x0"].shape[1]
+    method = os.path.basename(f)[:-4].split("_")[-1]
+    con = TrajoptConstraint(1, 1, 1, N)
+    con.set_torque_limits([float(d["ub"])], [float(d["lb"])], "ACTIVE_SET")
+    solver = TrajoptMPCReference(URDFPlant(options={"path_to_urdf": str(d["urdf"])}), CoupledCost(2, 1), con)
+    assert solver._hooks()
+    calls = []
+    orig = _native.Context.qp_blocks_banded_batch
+
+    def spy(self, G, *a, **k):
+        r = orig(self, G, *a, **k)
+        calls.append((r, self.qp_hard_info(G.shape[0], G.shape[1]) if method.startswith("PCG") else None))
+        return r
+
+    monkeypatch.setattr(_native.Context, "qp_blocks_banded_batch", spy)
+    x, u, exit_sqp, exit_soft, outer_iter, sqp_iter = solver.SQP(d["x0"], d["u0"], N, float(d["dt"]), method, {})
+    monkeypatch.setattr(_native.Context, "qp_blocks_banded_batch", orig)
+    assert (exit_sqp, sqp_iter, exit_soft, outer_iter) == (int(d["exit_sqp"]), int(d["sqp_iter"]),
+                                                           int(d["exit_soft"]), int(d["outer_iter"]))
+    ref_masks = [[0] * N for _ in range(len(d["C_rows"]))]
+    for q, k, sg in zip(d["act_qp"], d["act_knot"], d["act_sign"]):
+        ref_masks[int(q)][int(k)] |= 1 << (4 if int(sg) > 0 else 5)
+    assert solver.active_sets == ref_masks
+    assert max(max(m) for m in ref_masks) > 0   # the limits bind
+    tr = solver.trace
+    assert [t["alpha"] for t in tr] == list(d["tr_alpha"])
+    assert [t["line_search_iteration"] for t in tr] == list(d["tr_line_search_iteration"].astype(int))
+    assert [t["succeeded_line_search"] for t in tr] == list(d["tr_succeeded_line_search"].astype(bool))
+    if method.startswith("PCG"):
+        assert [t["inner_iters"] for t in tr[1:]] == list(d["pcg_iters"])
+    for key in ("J", "c", "merit"):
+        assert np.allclose([t[key] for t in tr], d["tr_" + key], rtol=1e-7, atol=1e-12), key
+    assert np.allclose(x, d["x"], rtol=1e-7, atol=1e-10)
+    assert np.allclose(u, d["u"], rtol=1e-7, atol=1e-10)
+    assert len(calls) == len(tr) - 1
+    if not method.startswith("PCG"):
+        return
+    opts = {}
+    solver.set_default_options(opts)
+    for j, (r, info) in enumerate(calls):
+        D = int(info["dim"][0])
+        assert D >= N * 2
+        S = _unband_S(info["S_band"][0], info["W"], D)
+        _, it = ohard.pcg_canonical(S, info["gamma"][0, :D], 2, method[4:], opts["exit_tolerance_linSys"],
+                                    opts["max_iter_linSys"])
+        assert it == int(r["pcg_iters"][0]), (j, it, int(r["pcg_iters"][0]))
+
+
+def _unband_S(Sb, W, D):
+    S = np.zeros((D, D))
+    for o in range(2 * W + 1):
+        a = np.arange(D)
+        c = a - W + o
+        ok = (c >= 0) & (c < D)
+        S[a[ok], c[ok]] = Sb[a[ok], o]
+    return S
+
+
+@pytest.mark.parametrize("method", ["S", "N", "PCG-SS", "PCG-BJ"])
+def test_plugin_qp_past_1024_rows(method):
+    """The plugin-hook QP past the 1024-row dense kernels (N * nx = 1200: arm6-sized blocks, N = 100) goes
+    through tmpc_qp_blocks_banded_batch with no hard rows: the direct methods give the dense KKT solution of
+    the same blocks (solveKKTSystem, TrajoptMPCReference.py:313-359); the PCG's count is the canonical-order
+    PCG's on the QP's own S and its lambda solves S lambda = gamma to the PCG's tolerance."""
+    from oracle import hard as ohard
+    from trajoptmpcreference_amd import _native
+    rng = np.random.default_rng(21)
+    nu, N, rho = 6, 100, 1e-3
+    nx, n = 2 * nu, 3 * nu
+    G = np.zeros((1, N, n, n))
+    for k in range(N):
+        m = n if k < N - 1 else nx
+        M = rng.uniform(-1.0, 1.0, (m, m))
+        G[0, k, :m, :m] = M @ M.T / m + np.eye(m)
+    g = rng.uniform(-1.0, 1.0, (1, N, n))
+    A = rng.uniform(-0.05, 0.05, (1, N - 1, nx, nx)) + np.eye(nx)
+    A[0, :, :nu, nu:] += 0.1 * np.eye(nu)
+    Bm = rng.uniform(-0.1, 0.1, (1, N - 1, nx, nu))
+    c = rng.uniform(-0.1, 0.1, (1, N, nx))
+    nz = n * (N - 1) + nx
+    Gd = np.zeros((nz, nz))
+    gd = np.zeros(nz)
+    C = np.zeros((nx * N, nz))
+    C[:nx, :nx] = np.eye(nx)
+    for k in range(N):
+        m = n if k < N - 1 else nx
+        Gd[k * n:k * n + m, k * n:k * n + m] = G[0, k, :m, :m]
+        gd[k * n:k * n + m] = g[0, k, :m]
+        if k < N - 1:
+            C[(k + 1) * nx:(k + 2) * nx, k * n:k * n + nx] = -A[0, k]
+            C[(k + 1) * nx:(k + 2) * nx, k * n + nx:k * n + n] = -Bm[0, k]
+            C[(k + 1) * nx:(k + 2) * nx, (k + 1) * n:(k + 1) * n + nx] = np.eye(nx)
+    K = np.block([[Gd + rho * np.eye(nz), C.T], [C, np.zeros((nx * N, nx * N))]])
+    ref = np.linalg.solve(K, np.concatenate([gd, c[0].reshape(-1)]))
+    ctx = _native.default_context(0)
+    rows = [[[] for _ in range(N)]]
+    r = ctx.qp_blocks_banded_batch(G, g, A, Bm, c, rho, rows, method)
+    got = r["dxul"][0]
+    assert got.shape == ref.shape and np.all(np.isfinite(got))
+    if not method.startswith("PCG"):
+        assert np.max(np.abs(got - ref)) < 1e-8 * max(1.0, np.max(np.abs(ref))), method
+        return
+    info = ctx.qp_hard_info(1, N)
+    D = int(info["dim"][0])
+    assert D == N * nx
+    S = _unband_S(info["S_band"][0], info["W"], D)
+    gam = info["gamma"][0, :D]
+    tol, max_iter = ctx.options.exit_tolerance_linSys, ctx.options.max_iter_linSys
+    lam_c, it = ohard.pcg_canonical(S, gam, nx, method[4:], tol, max_iter)
+    assert it == int(r["pcg_iters"][0]), (it, int(r["pcg_iters"][0]))
+    lam = got[nz:]
+    assert np.max(np.abs(lam - lam_c)) < 1e-9 * max(1.0, np.max(np.abs(lam_c)))
+    # the primal step from lambda: within the PCG's tolerance of the exact KKT solution
+    assert np.max(np.abs(got[:nz] - ref[:nz])) < 1e-3 * max(1.0, np.max(np.abs(ref[:nz])))

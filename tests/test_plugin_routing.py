@@ -115,15 +115,31 @@ def test_entry_points_without_a_hook_path_raise():
 
 
 def test_hook_path_refuses_what_it_cannot_run():
+    """Hard rows and long horizons take the banded plugin QP (tmpc_qp_blocks_banded_batch, GPU tests); what it
+    cannot run is refused before any solve: FULL_SET with a PCG method (S singular, the reference's
+    preconditioner raises), a hard row that is not a box row."""
     from trajoptmpcreference_amd import TrajoptConstraint, TrajoptMPCReference, hooks
     Scaled, _, _, _ = _costs()
     con = TrajoptConstraint(3, 3, 3, 8)
-    con.set_torque_limits([1.0] * 3, [-1.0] * 3, "ACTIVE_SET")
+    con.set_torque_limits([1.0] * 3, [-1.0] * 3, "FULL_SET")
     s = TrajoptMPCReference(_plant(), Scaled(*quad_cost_arrays(3)), con)
     o = {}
     s.set_default_options(o)
-    with pytest.raises(NotImplementedError, match="hard box"):
+    with pytest.raises(NotImplementedError, match="FULL_SET"):
         hooks.sqp_hooks_batch(s, None, np.zeros((1, 6, 8)), np.zeros((1, 3, 7)), 8, 0.1, "PCG-SS", o)
-    s2 = TrajoptMPCReference(_plant(), Scaled(*quad_cost_arrays(3)))
-    with pytest.raises(NotImplementedError, match="1024"):
-        hooks.sqp_hooks_batch(s2, None, np.zeros((1, 6, 200)), np.zeros((1, 3, 199)), 200, 0.1, "PCG-SS", o)
+
+    class SkewRows(TrajoptConstraint):   # a hard row over two entries: not a box row
+        def jacobian_hard_constraints(self, xk, uk=None, timestep=None):
+            J = super().jacobian_hard_constraints(xk, uk, timestep)
+            if J is not None:
+                J = J.copy()
+                J[:, 0] += 0.5
+            return J
+
+    con2 = SkewRows(3, 3, 3, 8)
+    con2.set_torque_limits([0.1] * 3, [-0.1] * 3, "ACTIVE_SET")
+    s2 = TrajoptMPCReference(_plant(), Scaled(*quad_cost_arrays(3)), con2)
+    q = hooks._HookSQP(s2, None, 8, 0.1, "PCG-SS", o)
+    u = np.full((3, 7), 0.5)   # every torque above its bound: active rows at every knot
+    with pytest.raises(NotImplementedError, match="box row"):
+        q.hard_rows(np.zeros((6, 8)), u)

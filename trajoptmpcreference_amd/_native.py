@@ -114,6 +114,8 @@ SIGNATURES = {
                                 _dp, _dp, _dp, _dp]),
     "tmpc_qp_blocks_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp, _dp,
                                        _dp, _dp, _dp, _dp, _ip, _dp, _dp, _dp]),
+    "tmpc_qp_blocks_banded_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp, _dp,
+                                              _dp, _dp, _ip, _ip, _dp, _dp, C.c_int, _dp, _dp, _ip, _dp, _ip]),
     "tmpc_qp_hard_info": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _ip, _ip, _up, _dp, _dp, _dp, _ip]),
     "tmpc_hard_pcg_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _ip, C.c_int, _dp, _dp,
                                       C.c_double, C.c_int, _dp, _ip]),
@@ -456,6 +458,39 @@ class Context:
                                                   _ptr(Sd), _ptr(Sl), _ptr(gam)), "tmpc_qp_blocks_batch")
         return dict(dxul=dxul, pcg_iters=iters, S_diag=Sd, S_lo=Sl, gamma=gam)
 
+    def qp_blocks_banded_batch(self, G, g, A, Bm, c, rho, rows, method="PCG-SS"):
+        """tmpc_qp_blocks_banded_batch: the plugin-hook QP with hard box rows and / or past 1024 rows.  G, g, A, Bm,
+        c, rho as qp_blocks_batch; rows[b][k] = [(column in [x_k; u_k], sign, value), ...] of knot k of problem b
+        in the reference's row order (sign +1 / -1, 0 for an inactive FULL_SET row).  Returns dict(dxul,
+        pcg_iters, lambda_hard [B][N][rmax], singular)."""
+        G, g, A, Bm, c = _c64(G), _c64(g), _c64(A), _c64(Bm), _c64(c)
+        B, N, n, _ = G.shape
+        nx, nu = A.shape[2], Bm.shape[3]
+        rmax = max([len(rk) for rb in rows for rk in rb] + [0])
+        rb_ = max(rmax, 1)
+        cnt = np.zeros((B, N), dtype=np.int32)
+        col = np.zeros((B, N, rb_), dtype=np.int32)
+        sgn = np.zeros((B, N, rb_))
+        val = np.zeros((B, N, rb_))
+        for b in range(B):
+            for k in range(N):
+                cnt[b, k] = len(rows[b][k])
+                for r, (cl, sg, v) in enumerate(rows[b][k]):
+                    col[b, k, r], sgn[b, k, r], val[b, k, r] = cl, sg, v
+        rho = _c64(np.broadcast_to(np.asarray(rho, dtype=np.float64), (B,)))
+        dxul = np.zeros((B, n * (N - 1) + nx + nx * N))
+        iters = np.zeros(B, dtype=np.int32)
+        lam_h = np.zeros((B, N, rb_))
+        sing = np.zeros(B, dtype=np.int32)
+        if rmax > 0:
+            col, sgn, val = np.ascontiguousarray(col[:, :, :rmax]), np.ascontiguousarray(sgn[:, :, :rmax]), \
+                np.ascontiguousarray(val[:, :, :rmax])
+        self._check(self.lib.tmpc_qp_blocks_banded_batch(
+            self.h, B, N, nx, nu, LINSYS[method], _ptr(G), _ptr(g), _ptr(A), _ptr(Bm), _ptr(c), _ptr(cnt), _ptr(col),
+            _ptr(sgn), _ptr(val), int(rmax), _ptr(rho), _ptr(dxul), _ptr(iters), _ptr(lam_h), _ptr(sing)),
+            "tmpc_qp_blocks_banded_batch")
+        return dict(dxul=dxul, pcg_iters=iters, lambda_hard=lam_h, singular=sing)
+
     def qp_hard_info(self, B, N):
         """Hard-limit detail of the last qp_batch (tmpc_qp_hard_info): dict with dim [B], active [B][N]
         (uint64 bitmasks), lambda_hard [B][N][6n], S_band [B][dmax][2W+1], gamma [B][dmax], singular [B], W."""
@@ -464,7 +499,7 @@ class Context:
                                                None), "tmpc_qp_hard_info")
         dmax, W = int(sizes[0]), int(sizes[1])
         out = dict(dim=np.zeros(B, dtype=np.int32), active=np.zeros((B, N), dtype=np.uint64),
-                   lambda_hard=np.zeros((B, N, 6 * self.model.n)), S_band=np.zeros((B, dmax, 2 * W + 1)),
+                   lambda_hard=np.zeros((B, N, 6 * (self.model.n if self.model is not None else 0))), S_band=np.zeros((B, dmax, 2 * W + 1)),
                    gamma=np.zeros((B, dmax)), singular=np.zeros(B, dtype=np.int32))
         self._check(self.lib.tmpc_qp_hard_info(self.h, int(B), int(N), _ptr(sizes), _ptr(out["dim"]),
                                                _ptr(out["active"]), _ptr(out["lambda_hard"]), _ptr(out["S_band"]),

@@ -432,19 +432,23 @@ static int alloc_soft(tmpc_ctx* ctx, int B, int N, double** mu, double** lam, do
 }
 
 // Buffers of the hard-constraint QP (tmpc_hard.hip) for B problems of N knots; T line-search trials.
-static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs& hard) {
-  const int nj = ctx->hmodel.n, nx = 2 * nj;
+// nj_given / rmax_given >= 0: the plugin-hook QP's joint count and rows per knot (its rows come from the
+// caller's constraint hooks, not from the context's limits)
+static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs& hard, int nj_given = -1,
+                      int rmax_given = -1) {
+  const int nj = nj_given >= 0 ? nj_given : ctx->hmodel.n, nx = 2 * nj;
   // rows per knot, at most: FULL_SET both bounds of every entry; ACTIVE_SET one per entry when lb < ub
   // (z - lb < 0 and ub - z < 0 cannot hold together), else both
   int rmax = 0;
   bool full = false;
-  for (int t = 0; t < 3; ++t) {
+  for (int t = 0; t < 3 && rmax_given < 0; ++t) {
     if (ctx->hlim.hard[t] == HARD_NONE) continue;
     bool ordered = ctx->hlim.hard[t] == HARD_ACTIVE;
     for (int i = 0; i < nj; ++i) ordered = ordered && ctx->hlim.lb[t][i] < ctx->hlim.ub[t][i];
     rmax += ordered ? nj : 2 * nj;
     if (ctx->hlim.hard[t] == HARD_FULL) full = true;
   }
+  if (rmax_given >= 0) rmax = rmax_given;
   if (full && precond != 0)
     return fail(ctx, "FULL_SET box constraints with a PCG method: the inactive rows of C are zero, so S is "
                 "singular and the reference's preconditioner raises LinAlgError (PCG.py:168-188); use method S");
@@ -457,8 +461,8 @@ static int setup_hard(tmpc_ctx* ctx, int B, int N, int T, int precond, HardArgs&
   const int gmax = nx + 2 * hard.rmax;         // the last group holds two knots' hard rows
   hard.W = 2 * gmax - 1;
   if (precond != 0 && hard.dmax > HARD_PCG_MAX_ROWS)
-    return fail(ctx, "%s: Schur dimension up to %d exceeds the banded PCG's %d rows (methods S / N have no "
-                "row limit)", ctx->hlim.any_hard ? "hard constraints" : "N * nx past the fused QP's rows",
+    return fail(ctx, "%s: Schur dimension up to %d exceeds the banded PCG's %d rows (methods S / N go further)",
+                ctx->hlim.any_hard || rmax_given > 0 ? "hard constraints" : "N * nx past the fused QP's rows",
                 hard.dmax, HARD_PCG_MAX_ROWS);
   if (hard.W > 1024) return fail(ctx, "hard constraints: band half-width %d > 1024", hard.W);
   if (hard_schur_lds_bytes(N, nj, hard.dmax) > CU_LDS_BYTES) {
@@ -1842,6 +1846,155 @@ int tmpc_qp_blocks_batch(tmpc_ctx* ctx, int B, int N, int nx, int nu, int linsys
   return 0;
 }
 
+int tmpc_qp_blocks_banded_batch(tmpc_ctx* ctx, int B, int N, int nx, int nu, int linsys, const double* G,
+                                const double* g, const double* A, const double* Bm, const double* c,
+                                const int32_t* hcnt, const int32_t* hcol, const double* hsgn, const double* hval,
+                                int rmax, const double* rho, double* dxul, int32_t* pcg_iters, double* lambda_hard,
+                                int32_t* singular) {
+  if (!ctx) return -1;
+  if (B < 1 || N < 2) return fail(ctx, "bad sizes B=%d N=%d (B >= 1, N >= 2)", B, N);
+  if (nu < 1 || nu > 7 || nx != 2 * nu)
+    return fail(ctx, "tmpc_qp_blocks_banded_batch: nx = %d, nu = %d; the device QP takes nx = 2 nu, 1 <= nu <= 7",
+                nx, nu);
+  const int n = nx + nu, K = N - 1;
+  if (rmax < 0 || rmax > 2 * n) return fail(ctx, "tmpc_qp_blocks_banded_batch: rmax = %d (0..%d)", rmax, 2 * n);
+  const int precond = precond_of(linsys);
+  if (precond < 0) return fail(ctx, "linear system method %d is not available on the GPU", linsys);
+  if (!G || !g || !A || !Bm || !c || !rho || (rmax > 0 && (!hcnt || !hcol || !hsgn || !hval)))
+    return fail(ctx, "null input");
+  const int rbuf = rmax > 0 ? rmax : 1;
+  std::vector<int> cnt((size_t)B * N, 0);
+  if (rmax > 0) memcpy(cnt.data(), hcnt, sizeof(int) * B * N);
+  for (size_t e = 0; e < cnt.size(); ++e) {
+    if (cnt[e] < 0 || cnt[e] > rmax) return fail(ctx, "hard rows: %d rows at (problem, knot) %zu (0..%d)", cnt[e], e, rmax);
+    for (int r = 0; r < cnt[e]; ++r) {
+      const int col = hcol[e * rmax + r];
+      const double sg = hsgn[e * rmax + r];
+      const int k = (int)(e % N);
+      if (col < 0 || col >= (k < K ? n : nx) || !(sg == 1.0 || sg == -1.0 || sg == 0.0))
+        return fail(ctx, "hard row %d at (problem, knot) %zu: column %d, sign %g -- the banded QP takes box rows "
+                    "(+-1 or 0 times one entry of [x_k; u_k])", r, e, col, sg);
+      if (sg == 0.0 && precond != 0)
+        return fail(ctx, "FULL_SET box constraints with a PCG method: the inactive rows of C are zero, so S is "
+                    "singular and the reference's preconditioner raises LinAlgError (PCG.py:168-188); use method S");
+    }
+  }
+  hipSetDevice(ctx->device);
+  BUF(double, hb_G, (size_t)B * N * n * n);
+  BUF(double, hb_Gh, (size_t)B * N * n * n);
+  BUF(double, hb_g, (size_t)B * N * n);
+  BUF(double, hb_A, (size_t)B * K * nx * nx);
+  BUF(double, hb_B, (size_t)B * K * nx * nu);
+  BUF(double, hb_c, (size_t)B * N * nx);
+  BUF(double, hb_rho, (size_t)B);
+  BUF(int, hb_err, (size_t)B);
+  BUF(int, hb_it, (size_t)B);
+  BUF(int, hb_act, (size_t)B);
+  BUF(double, hb_dx, (size_t)B * N * nx);
+  BUF(double, hb_du, (size_t)B * K * nu);
+  HIP_OK(hipMemcpyAsync(hb_G, G, sizeof(double) * B * N * n * n, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_g, g, sizeof(double) * B * N * n, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_A, A, sizeof(double) * B * K * nx * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_B, Bm, sizeof(double) * B * K * nx * nu, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_c, c, sizeof(double) * B * N * nx, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemcpyAsync(hb_rho, rho, sizeof(double) * B, hipMemcpyHostToDevice, ctx->stream));
+  HIP_OK(hipMemsetAsync(hb_err, 0, sizeof(int) * B, ctx->stream));
+  HIP_OK(hipMemsetAsync(hb_it, 0, sizeof(int) * B, ctx->stream));
+  std::vector<int> act(B, 1);
+  HIP_OK(hipMemcpyAsync(hb_act, act.data(), sizeof(int) * B, hipMemcpyHostToDevice, ctx->stream));
+  {
+    Timed t(ctx, "ghat_full");
+    LAUNCH_OK(launch_ghat_full(ctx->stream, nu, B, N, hb_G, hb_rho, hb_Gh, hb_err));
+  }
+  HardArgs hard{};
+  int rc = setup_hard(ctx, B, N, 0, precond, hard, nu, rmax);
+  if (rc) return rc;
+  HIP_OK(hipMemcpyAsync(hard.cnt, cnt.data(), sizeof(int) * B * N, hipMemcpyHostToDevice, ctx->stream));
+  // the per-knot active-set bitmasks (tmpc_qp_hard_info), bit t * 2 nu + e of the box row over [q; qd; u]
+  // and each row's slot t * 2 nu + e (the lambda_hard layout)
+  std::vector<unsigned long long> amask((size_t)B * N, 0ull);
+  std::vector<int> hslot((size_t)B * N * std::max(rmax, 1), 0);
+  for (size_t e = 0; e < amask.size(); ++e)
+    for (int r = 0; r < cnt[e]; ++r) {
+      const double sg = hsgn[e * rmax + r];
+      const int col = hcol[e * rmax + r], t = col / nu, i = col % nu;
+      hslot[e * rmax + r] = t * 2 * nu + (sg >= 0.0 ? i : nu + i);
+      if (sg != 0.0) amask[e] |= 1ull << hslot[e * rmax + r];
+    }
+  HIP_OK(hipMemcpyAsync(hard.amask, amask.data(), sizeof(unsigned long long) * B * N, hipMemcpyHostToDevice,
+                        ctx->stream));
+  if (rmax > 0)
+    HIP_OK(hipMemcpyAsync(hard.hslot, hslot.data(), sizeof(int) * B * N * rmax, hipMemcpyHostToDevice, ctx->stream));
+  if (rmax > 0) {
+    HIP_OK(hipMemcpyAsync(hard.hcol, hcol, sizeof(int) * B * N * rbuf, hipMemcpyHostToDevice, ctx->stream));
+    HIP_OK(hipMemcpyAsync(hard.hsgn, hsgn, sizeof(double) * B * N * rbuf, hipMemcpyHostToDevice, ctx->stream));
+    HIP_OK(hipMemcpyAsync(hard.hval, hval, sizeof(double) * B * N * rbuf, hipMemcpyHostToDevice, ctx->stream));
+  }
+  hard.rows_given = 1;
+  hard.precond = precond;
+  hard.Ghat = hb_Gh;
+  hard.per_knot = 2;
+  hard.gvec = hb_g;
+  hard.A = hb_A;
+  hard.Bm = hb_B;
+  hard.cvec = hb_c;
+  hard.x = hb_g;   // not read: the gradient is the caller's (gvec), the rows are given
+  hard.u = hb_g;
+  hard.jsoft = nullptr;
+  hard.active = hb_act;
+  hard.iters = hb_it;
+  hard.dx = hb_dx;
+  hard.du = hb_du;
+  hard.tol = ctx->opts.exit_tolerance_linSys;
+  hard.max_iter = ctx->opts.max_iter_linSys;
+  const char* names[3] = {"hard_schur", precond == 0 ? "hard_direct" : "hard_pcg", "dxu"};
+  for (int ph = 0; ph < 3; ++ph) {
+    Timed t(ctx, names[ph]);
+    hard.phase = ph;
+    LAUNCH_OK(launch_hard(ctx->stream, nu, hard));
+  }
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if ((rc = collect_hard_work(ctx, hard))) return rc;
+  resolve_timings(ctx);
+  std::vector<int> err(B);
+  HIP_OK(hipMemcpy(err.data(), hb_err, sizeof(int) * B, hipMemcpyDeviceToHost));
+  for (int b = 0; b < B; ++b)
+    if (err[b])
+      return fail(ctx, "problem %d: G_k + rho I has a zero or non-finite pivot (singular matrix, the reference's "
+                  "np.linalg.inv raises LinAlgError)", b);
+  std::vector<int> roff((size_t)B * N), hoff((size_t)B * N);
+  std::vector<double> lh((size_t)B * hard.dmax);
+  HIP_OK(hipMemcpy(roff.data(), hard.roff, roff.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(hoff.data(), hard.hoff, hoff.size() * sizeof(int), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(lh.data(), hard.lam, lh.size() * sizeof(double), hipMemcpyDeviceToHost));
+  if (dxul) {
+    std::vector<double> dx((size_t)B * N * nx), du((size_t)B * K * nu);
+    HIP_OK(hipMemcpy(dx.data(), hb_dx, dx.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(du.data(), hb_du, du.size() * sizeof(double), hipMemcpyDeviceToHost));
+    const size_t L = (size_t)n * K + nx + (size_t)nx * N;
+    for (int b = 0; b < B; ++b) {
+      double* o = dxul + b * L;
+      for (int k = 0; k < N; ++k) {
+        for (int i = 0; i < nx; ++i) o[(size_t)k * n + i] = dx[((size_t)b * N + k) * nx + i];
+        if (k < K)
+          for (int i = 0; i < nu; ++i) o[(size_t)k * n + nx + i] = du[((size_t)b * K + k) * nu + i];
+        for (int i = 0; i < nx; ++i)
+          o[(size_t)n * K + nx + (size_t)k * nx + i] = lh[(size_t)b * hard.dmax + roff[(size_t)b * N + k] + i];
+      }
+    }
+  }
+  if (lambda_hard)
+    for (int b = 0; b < B; ++b)
+      for (int k = 0; k < N; ++k)
+        for (int r = 0; r < rbuf; ++r)
+          lambda_hard[((size_t)b * N + k) * rbuf + r] =
+              r < cnt[(size_t)b * N + k] ? lh[(size_t)b * hard.dmax + hoff[(size_t)b * N + k] + r] : 0.0;
+  if (pcg_iters) HIP_OK(hipMemcpy(pcg_iters, hb_it, sizeof(int) * B, hipMemcpyDeviceToHost));
+  if (singular) HIP_OK(hipMemcpy(singular, hard.sing, sizeof(int) * B, hipMemcpyDeviceToHost));
+  ctx->hard_last = {B, N, hard.dmax, hard.W, hard.rmax};   // tmpc_qp_hard_info reads this QP's S band and gamma
+  return 0;
+}
+
 int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim, uint64_t* active,
                       double* lambda_hard, double* S_band, double* gamma, int32_t* singular) {
   if (!ctx) return -1;
@@ -1895,8 +2048,10 @@ int tmpc_qp_hard_info(tmpc_ctx* ctx, int B, int N, int32_t* sizes, int32_t* dim,
     for (int b = 0; b < B; ++b)
       for (int k = 0; k < N; ++k) {
         const size_t bk = (size_t)b * N + k;
-        for (int r = 0; r < cnt[bk] && r < rmax; ++r)
-          lambda_hard[bk * S6 + slot[bk * rmax + r]] = lam[(size_t)b * hl.dmax + hoff[bk] + r];
+        for (int r = 0; r < cnt[bk] && r < rmax; ++r) {
+          const int sl = slot[bk * rmax + r];
+          if (sl >= 0 && sl < S6) lambda_hard[bk * S6 + sl] = lam[(size_t)b * hl.dmax + hoff[bk] + r];
+        }
       }
   }
   return 0;

@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
                                                     const double* __restrict__ hsgn, const double* __restrict__ hval,
                                                     double* __restrict__ Y, int* __restrict__ PK,
                                                     double* __restrict__ Sb, double* __restrict__ gam,
-                                                    int* __restrict__ rng) {
+                                                    int* __restrict__ rng, const double* __restrict__ gvec) {
 #if TMPC_HX_STAMPS
   unsigned long long sc_[4] = {}, sc_prev_ = __builtin_amdgcn_s_memtime();
 #define HS_STAMP(i_) { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); sc_[i_] += n_ - sc_prev_; sc_prev_ = n_; }
@@ -305,6 +305,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
   const double* ub = u + (size_t)b * NU * K;
   const double* js = jsoft ? jsoft + (size_t)b * N * NXU : nullptr;
   const HGhat<NJ> Gh{per_knot ? Ghat + (size_t)b * N * HGhat<NJ>::GS : Ghat + (size_t)b * 3 * NX * NX, per_knot != 0};
+  // per_knot 2: the plugin-hook QP's full (G_k + rho I)^-1 blocks [N][NXU][NXU] (x-u coupling; the terminal
+  // knot's NX x NX block top-left, k_ghat_full) and the caller's gradient gvec [N][NXU]
+  const double* Gf = Ghat + (size_t)b * N * NXU * NXU;
   const int* rk = rkind + (size_t)b * dmax;
   const int* rn = rknot + (size_t)b * dmax;
   const int* ri = ridx + (size_t)b * dmax;
@@ -314,7 +317,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
   // phase 0: the cost gradient of every knot (0 for the terminal knot's u part)
   for (int e = threadIdx.x; e < N * NXU; e += blockDim.x) {
     const int k = e / NXU, m = e - k * NXU;
-    s_grad[e] = (m < NX || k < K) ? hard_grad<NJ>(C, xb, ub, js, N, k, m) : 0.0;
+    s_grad[e] = (m < NX || k < K) ? (gvec ? gvec[(size_t)b * N * NXU + e] : hard_grad<NJ>(C, xb, ub, js, N, k, m))
+                                  : 0.0;
   }
   __syncthreads();
   HS_STAMP(0);
@@ -375,7 +379,45 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TMPC_S
       gam[(size_t)b * dmax + a] = ca - g_dot;
     }
   };
-  if (!per_knot) {
+  if (per_knot == 2) {   // full blocks: y = Ghat_kp cf over all NXU entries (terminal: the NX x NX block)
+    for (int a = threadIdx.x; a < D; a += blockDim.x) {
+      const int kind = rk[a], knot = rn[a], idx = ri[a];
+      const int* hc = hcol + hb + (size_t)knot * rmax;
+      const double* hs = hsgn + hb + (size_t)knot * rmax;
+      double g_dot = 0.0;
+      for (int p = 0; p < 2; ++p) {
+        double cf[3 * NJ];
+        const int kp = row_piece<NJ>(kind, knot, idx, p, A, Bm, hc, hs, cf);
+        PKb[a * 2 + p] = kp;
+        double uv;
+        const int uc = piece_unit(kind, knot, idx, p, hc, hs, uv);
+        s_pk[a * 2 + p] = pk_pack(kp, uc, uv);
+        if (kp < 0) continue;
+        double* yo = &Y_AT(a, p, 0);
+        const size_t ys = TMPC_SCHUR_YT ? (size_t)dmax : 1;
+        const double* gk = s_grad + kp * NXU;
+        glb_cdouble* G = glb_ptr(Gf + (size_t)kp * NXU * NXU);
+        const int m = kp < K ? NXU : NX;
+        double s = 0.0;
+#pragma unroll 1
+        for (int r = 0; r < NXU; ++r) {
+          double acc = 0.0;
+          if (r < m) {
+#pragma unroll
+            for (int c = 0; c < NXU; ++c)
+              if (c < m) acc += G[r * NXU + c] * cf[c];
+          }
+          yo[r * ys] = acc;
+          s += acc * gk[r];
+        }
+        g_dot += s;
+      }
+      double ca;
+      if (kind == 0) ca = cvec[((size_t)b * N + knot) * NX + idx];
+      else ca = hval[hb + (size_t)knot * rmax + idx];
+      gam[(size_t)b * dmax + a] = ca - g_dot;
+    }
+  } else if (!per_knot) {
     lds_cdouble* gl = lds_ptr(s_gh);
     phase1([&](int kp) { return gl + (h_use_QF(C, kp, N) ? NX * NX : 0); }, [&](int) { return gl + 2 * NX * NX; });
   } else {
@@ -1270,7 +1312,8 @@ __global__ void __launch_bounds__(64) k_hard_dxu(const CostDev* __restrict__ C, 
                                                  const int* __restrict__ roff, const int* __restrict__ hoff,
                                                  const int* __restrict__ cnt, const int* __restrict__ hcol,
                                                  const double* __restrict__ hsgn, const double* __restrict__ lam,
-                                                 double* __restrict__ dx, double* __restrict__ du) {
+                                                 double* __restrict__ dx, double* __restrict__ du,
+                                                 const double* __restrict__ gvec) {
   constexpr int NX = 2 * NJ, NU = NJ, NXU = NX + NU;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= B * N) return;
@@ -1305,7 +1348,21 @@ __global__ void __launch_bounds__(64) k_hard_dxu(const CostDev* __restrict__ C, 
   const double* ub = u + (size_t)b * NU * K;
   const double* js = jsoft ? jsoft + (size_t)b * N * NXU : nullptr;
   double rhs[3 * NJ];
-  for (int m = 0; m < NXU; ++m) rhs[m] = (m < NX || k < K) ? hard_grad<NJ>(C, xb, ub, js, N, k, m) - ctl[m] : 0.0;
+  for (int m = 0; m < NXU; ++m)
+    rhs[m] = (m < NX || k < K) ? (gvec ? gvec[((size_t)b * N + k) * NXU + m] : hard_grad<NJ>(C, xb, ub, js, N, k, m))
+                                     - ctl[m]
+                               : 0.0;
+  if (per_knot == 2) {   // the plugin-hook QP's full block (k_ghat_full): dxu_k = Ghat_k (g_k - (C^T lambda)_k)
+    const double* G = Ghat + ((size_t)b * N + k) * NXU * NXU;
+    const int m = k < K ? NXU : NX;
+    for (int i = 0; i < m; ++i) {
+      double acc = 0.0;
+      for (int j = 0; j < m; ++j) acc += G[i * NXU + j] * rhs[j];
+      if (i < NX) dx[((size_t)b * N + k) * NX + i] = acc;
+      else du[((size_t)b * K + k) * NU + (i - NX)] = acc;
+    }
+    return;
+  }
   const double* Gx = Gh.x(C, k, N);
   for (int i = 0; i < NX; ++i) {
     double acc = 0.0;
@@ -1364,13 +1421,14 @@ struct LaunchHard {
     constexpr int NX = 2 * NJ;
     const int B = h.B, N = h.N;
     if (h.phase == 0) {
-      hipLaunchKernelGGL((k_hard_rows<NJ>), HGRID(B * N, 256), 0, s, h.Cs, B, N, h.rmax, h.x, h.u, h.active, h.cnt,
-                         h.hcol, h.hsgn, h.hval, h.hslot, h.amask, h.iter, h.Wtr, h.tr_active);
+      if (!h.rows_given)   // the plugin-hook QP brings its rows (cnt / hcol / hsgn / hval) from the host
+        hipLaunchKernelGGL((k_hard_rows<NJ>), HGRID(B * N, 256), 0, s, h.Cs, B, N, h.rmax, h.x, h.u, h.active, h.cnt,
+                           h.hcol, h.hsgn, h.hval, h.hslot, h.amask, h.iter, h.Wtr, h.tr_active);
       hipLaunchKernelGGL(k_hard_layout, dim3(B), dim3(64), 0, s, B, N, NX, h.rmax, h.active, h.cnt, h.roff, h.hoff,
                          h.dim, h.rkind, h.rknot, h.ridx, h.dmax);
       hipLaunchKernelGGL((k_hard_schur<NJ>), dim3(B), dim3(256), hard_schur_lds_bytes(N, NJ, h.dmax), s, h.C, B, N, h.W, h.dmax, h.rmax, h.active, h.Ghat,
                          h.per_knot, h.A, h.Bm, h.cvec, h.x, h.u, h.jsoft, h.dim, h.rkind, h.rknot, h.ridx, h.hoff,
-                         h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam, h.rng);
+                         h.hcol, h.hsgn, h.hval, h.Y, h.PK, h.Sb, h.gam, h.rng, h.gvec);
     } else if (h.phase == 1) {
       if (h.precond == 0) {
         hipLaunchKernelGGL(k_hard_direct, dim3(B), dim3(256), 0, s, B, N, NX, h.W, h.dmax, h.rmax, h.active, h.dim,
@@ -1395,7 +1453,7 @@ struct LaunchHard {
     } else if (h.phase == 2) {
       hipLaunchKernelGGL((k_hard_dxu<NJ>), HGRID(B * N, 64), 0, s, h.C, B, N, h.dmax, h.rmax, h.active, h.Ghat,
                          h.per_knot, h.A, h.Bm, h.x, h.u, h.jsoft, h.roff, h.hoff, h.cnt, h.hcol, h.hsgn, h.lam, h.dx,
-                         h.du);
+                         h.du, h.gvec);
     } else {
       hipLaunchKernelGGL((k_hard_ls<NJ>), HGRID(B * h.T * N, 256), 0, s, h.Cs, B, N, h.T, h.alphas, h.x, h.u, h.dx,
                          h.du, h.active, h.hterms);

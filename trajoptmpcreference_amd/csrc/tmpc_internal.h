@@ -222,6 +222,11 @@ struct HardArgs {
   int Wtr;                        // trace row stride (max_iter_SQP_DDP + 1)
   unsigned long long* tr_active;  // [B][Wtr][N] trace copy of amask (nullable)
   double* work;                   // [B] algorithmic HBM bytes of k_hard_pcg, accumulated per problem (nullable)
+  // the plugin-hook QP (tmpc_qp_blocks_banded_batch): per_knot = 2 -- Ghat holds full (G_k + rho I)^-1 blocks
+  // [B][N][nx+nu][nx+nu] -- the caller's cost gradient gvec [B][N][nx+nu] (null: the context's cost), and
+  // rows_given: cnt / hcol / hsgn / hval were filled from the caller's constraint hooks (k_hard_rows skipped)
+  const double* gvec;
+  int rows_given;
 };
 // k_hard_pcg: 1024 threads per problem, row a on thread a % 1024 (row slot a / 1024, at most 4 slots)
 constexpr int HARD_PCG_THREADS = 1024, HARD_PCG_MAX_SLOTS = 4;

@@ -14,9 +14,11 @@ plant is a URDFPlant whose dynamics hooks are not overridden (one batched launch
 There is no CPU fallback for the QP: without the library the solve raises.
 
 Supported: methods N, S, PCG-J / BJ / SS; soft constraints (QUADRATIC_PENALTY / AUGMENTED_LAGRANGIAN and
-the outer loop, :483-508) through the constraint object's hooks.  Hard box constraints (ACTIVE_SET /
-FULL_SET) with plugin hooks raise NotImplementedError (their QP rows need the banded device path, which
-takes device-formed blocks only), as do nx != 2 nu and N nx > 1024.
+the outer loop, :483-508) through the constraint object's hooks; hard box constraints (ACTIVE_SET / FULL_SET,
+:238-248): the constraint hooks' rows (value_hard_constraints / jacobian_hard_constraints) go to the banded
+device QP with the plugin's blocks (tmpc_qp_blocks_banded_batch), which also takes QPs past the fused
+kernel's 1024 rows.  A hard row must be a box row (one +-1 entry of [x_k; u_k], or a zero FULL_SET row),
+as the reference's BoxConstraint produces; nx must be 2 nu.
 """
 import copy
 
@@ -91,6 +93,15 @@ class _HookSQP:
         self.n = self.nx + self.nu
         self.gpu_dyn = device_plant(p)
         self.it = self.outer = self.ls = 0
+        con = solver.other_constraints
+        # hard rows: the built-in box limits in a hard mode, or a subclass's own hard-constraint hooks
+        self.hard = any(c.is_hard_constraint_mode() for _, c in con.limits()) or bool(
+            overrides(con, TrajoptConstraint, ("total_hard_constraints", "value_hard_constraints",
+                                               "jacobian_hard_constraints", "_hard_slices")))
+        # the banded device QP: hard rows, or past the fused kernel's 1024 Schur rows
+        self.banded = self.hard or N * self.nx > 1024
+        self.mask = np.zeros(N, dtype=np.uint64)   # the last QP's active set per knot (trace hard_active)
+        self.singular = 0
 
     # -- plugin evaluations, placed and called as the reference places and calls them.  The iter_* arguments
     # are the reference's module-global counters (overloading.matrix_): the initial cost / violation of an
@@ -129,13 +140,64 @@ class _HookSQP:
         return J
 
     def violation(self, x, u, xs):
-        """totalHardConstraintViolation (:273-294) without hard limits (refused above): the initial-state
-        and dynamics defects' 1-norms, summed knot by knot."""
+        """totalHardConstraintViolation (:273-294): the initial-state and dynamics defects' 1-norms knot by
+        knot, then the hard constraints' (:286-293; the terminal value_hard_constraints call passes N - 1 in
+        the u position, as the reference's)."""
         (f,) = self._step(x, u, False)
         c = sum(map(abs, x[:, 0] - xs))
-        for k in range(self.N - 1):
+        N = self.N
+        for k in range(N - 1):
             c = c + sum(map(abs, x[:, k + 1] - f[k]))
+        if self.hard:
+            con = self.s.other_constraints
+            if con.total_hard_constraints(x, u) > 0:
+                for k in range(N - 1):
+                    if con.total_hard_constraints(x, u, k):
+                        c = c + sum(map(abs, con.value_hard_constraints(x[:, k], u[:, k], k)))
+                if con.total_hard_constraints(x, u, N - 1):
+                    c = c + sum(map(abs, con.value_hard_constraints(x[:, N - 1], N - 1)))
         return c
+
+    def hard_rows(self, x, u):
+        """formKKTSystemBlocks' hard rows (:238-248, 262-270) per knot as (column in [x_k; u_k], sign, value):
+        the constraint hooks' jacobian rows must be box rows (one +-1 entry; a zero row is FULL_SET's
+        inactive entry, sign 0).  Also sets the per-knot active-set bitmasks of the trace (bit t * 2n + e,
+        include/tmpc.h) for rows over [q; qd; u]."""
+        N, nx, n, nu = self.N, self.nx, self.n, self.nu
+        con = self.s.other_constraints
+        rows = [[] for _ in range(N)]
+        self.mask = np.zeros(N, dtype=np.uint64)
+        if not self.hard or con.total_hard_constraints(x, u) == 0:
+            return rows
+        for k in range(N):
+            if not con.total_hard_constraints(x, u, k):
+                continue
+            if k < N - 1:
+                jac = con.jacobian_hard_constraints(x[:, k], u[:, k], k)
+                val = con.value_hard_constraints(x[:, k], u[:, k], k)
+                width = n
+            else:
+                jac = con.jacobian_hard_constraints(x[:, N - 1], timestep=N - 1)
+                val = con.value_hard_constraints(x[:, N - 1], timestep=N - 1)
+                width = nx
+            if val is None or not len(val):
+                continue
+            val = np.asarray(val, dtype=np.float64).reshape(-1)
+            J = np.reshape(np.asarray(jac, dtype=np.float64), (len(val), width))
+            for r in range(len(val)):
+                nzc = np.nonzero(J[r])[0]
+                if len(nzc) == 0:
+                    rows[k].append((0, 0.0, float(val[r])))
+                    continue
+                if len(nzc) != 1 or abs(J[r, nzc[0]]) != 1.0:
+                    raise NotImplementedError(
+                        f"plugin-hook SQP: hard row {r} of knot {k} is not a box row (one +-1 entry of [x_k; u_k]); "
+                        "the banded device QP takes the rows BoxConstraint forms")
+                col, sg = int(nzc[0]), float(J[r, nzc[0]])
+                rows[k].append((col, sg, float(val[r])))
+                t, i = divmod(col, nu)
+                self.mask[k] |= np.uint64(1) << np.uint64(t * 2 * nu + (i if sg > 0 else nu + i))
+        return rows
 
     def blocks(self, x, u, xs):
         """formKKTSystemBlocks (:200-271) per knot: G [N][n][n], g [N][n], A, B, c."""
@@ -183,7 +245,13 @@ class _HookSQP:
 
     def qp(self, x, u, xs, rho):
         G, g, A, Bm, c = self.blocks(x, u, xs)
-        r = self.ctx.qp_blocks_batch(G[None], g[None], A[None], Bm[None], c[None], rho, self.method)
+        if self.banded:   # hard rows (the constraint hooks') and / or past 1024 Schur rows
+            rows = self.hard_rows(x, u)
+            r = self.ctx.qp_blocks_banded_batch(G[None], g[None], A[None], Bm[None], c[None], rho, [rows],
+                                                self.method)
+            self.singular = int(r["singular"][0])
+        else:
+            r = self.ctx.qp_blocks_batch(G[None], g[None], A[None], Bm[None], c[None], rho, self.method)
         return r["dxul"][0].reshape(-1, 1), int(r["pcg_iters"][0])
 
     # -- the loop
@@ -204,7 +272,8 @@ class _HookSQP:
             mu = 10   # :545-546
             merit = J + mu * c
             trace = [dict(iteration=0, line_search_iteration=0, alpha=1.0, rho=rho, J=J, c=c, merit=merit,
-                          D=np.nan, reduction_ratio=np.nan, succeeded_line_search=0, pcg_iters=0, singular=0)]
+                          D=np.nan, reduction_ratio=np.nan, succeeded_line_search=0, pcg_iters=0, singular=0,
+                          hard_active=np.zeros(N, dtype=np.uint64))]
             while True:
                 dxul, inner = self.qp(x, u, xs, rho)   # formKKTSystemBlocks sees the last line search's index
                 self.ls = 0                            # matrix_.line_search_iteration = 0 (:608)
@@ -229,7 +298,8 @@ class _HookSQP:
                         rho, drho = s.reduce_regularization(rho, drho, o)
                         trace.append(dict(iteration=self.it, line_search_iteration=self.ls, alpha=alpha, rho=rho,
                                           J=J, c=c, merit=merit, D=D, reduction_ratio=ratio,
-                                          succeeded_line_search=1, pcg_iters=inner, singular=0))
+                                          succeeded_line_search=1, pcg_iters=inner, singular=self.singular,
+                                          hard_active=self.mask.copy()))
                         break
                     elif alpha > o["alpha_min_SQP_DDP"]:
                         alpha *= o["alpha_factor_SQP_DDP"]
@@ -238,7 +308,8 @@ class _HookSQP:
                         error = True
                         trace.append(dict(iteration=self.it, line_search_iteration=self.ls, alpha=alpha, rho=rho,
                                           J=J, c=c, merit=merit, D=D, reduction_ratio=ratio,
-                                          succeeded_line_search=0, pcg_iters=inner, singular=0))
+                                          succeeded_line_search=0, pcg_iters=inner, singular=self.singular,
+                                          hard_active=self.mask.copy()))
                         break
                 exit_flag, self.it, rho, drho = s.check_for_exit_or_error(error, delta_J, self.it, rho, drho, o)
                 if exit_flag:
@@ -250,7 +321,8 @@ class _HookSQP:
                 break
         tr = {k: np.zeros(W, dtype=np.int32 if k in ("iteration", "line_search_iteration", "succeeded_line_search",
                                                        "pcg_iters", "singular") else np.float64)
-              for k in trace[0]}
+              for k in trace[0] if k != "hard_active"}
+        tr["hard_active"] = np.zeros((W, N), dtype=np.uint64)
         for i, row in enumerate(trace[:W]):
             for k, v in row.items():
                 tr[k][i] = v
@@ -266,16 +338,15 @@ def sqp_hooks_batch(solver, ctx, x, u, N, dt, method, options):
     if nx != 2 * nu or not 1 <= nu <= 7:
         raise NotImplementedError(f"plugin-hook SQP: the device QP takes nx = 2 nu with 1 <= nu <= 7 "
                                   f"(got nx = {nx}, nu = {nu})")
-    if N * nx > 1024:
-        raise NotImplementedError(f"plugin-hook SQP: N * nx = {N * nx} exceeds the hook QP's 1024 rows")
-    con = solver.other_constraints
-    if any(c.is_hard_constraint_mode() for _, c in con.limits()):
-        raise NotImplementedError("hard box constraints (ACTIVE_SET / FULL_SET) with plugin-hook costs or plants: "
-                                  "the hard-limit QP takes device-formed blocks only; use soft limits")
     if options.get("precision", "fp64") != "fp64":
         raise NotImplementedError("the fp32 / mixed precision modes need device plugins")
     if options.get("pcg_warm_start"):
         raise NotImplementedError("pcg_warm_start needs device plugins")
+    con = solver.other_constraints
+    if any(c.is_hard_constraint_mode() for _, c in con.limits()) and method.startswith("PCG") and \
+            any(c.mode == "FULL_SET" for _, c in con.limits() if c.is_hard_constraint_mode()):
+        raise NotImplementedError("FULL_SET box constraints with a PCG method: the inactive rows of C are zero, so S "
+                                  "is singular and the reference's preconditioner raises LinAlgError; use method S")
     B = x.shape[0]
     outs = [_HookSQP(solver, ctx, N, dt, method, options).solve(x[b], u[b]) for b in range(B)]
     r = {k: np.array([o[k] for o in outs], dtype=np.int32) for k in ("exit_sqp", "exit_soft", "outer_iter",
