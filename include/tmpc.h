@@ -104,11 +104,15 @@ typedef struct tmpc_options {
   int32_t pcg_warm_start;                /* 0      */
   /* Arithmetic precision (BASELINE configs 3 and 5; the reference is fp64 throughout):
    * TMPC_PRECISION_F64   everything fp64 (default, the reference's arithmetic);
-   * TMPC_PRECISION_F32   rigid-body dynamics (forward dynamics, M^-1, RNEA gradient: the QP build,
-   *                      line-search / rollout dynamics) and the iLQR Riccati sweep in fp32;
-   * TMPC_PRECISION_MIXED rigid-body dynamics in fp32, Schur complement / PCG and Riccati in fp64.
+   * TMPC_PRECISION_F32   the dynamics' derivatives (M^-1, RNEA gradient: A_k, B_k of the QP build and
+   *                      of the iLQR linearisation) and the iLQR Riccati sweep in fp32; every
+   *                      trajectory evaluation (the QP's defects, line-search trials, iLQR rollouts) in
+   *                      fp64, so costs, merit and the exit tests are the fp64 ones (round 6);
+   * TMPC_PRECISION_MIXED rigid-body dynamics (derivatives and trajectory evaluations) in fp32, Schur
+   *                      complement / PCG and Riccati in fp64.
    * In every mode the buffers, the merit / cost sums, the acceptance tests and the MPC loop's
-   * simulated plant step are fp64. */
+   * simulated plant step are fp64; the standalone dynamics entry points (tmpc_rollout_batch_device,
+   * tmpc_fd_batch, tmpc_fd_grad_batch) evaluate in fp32 under F32 and MIXED. */
   int32_t precision;                     /* 0      */
 } tmpc_options;
 
@@ -391,8 +395,11 @@ int tmpc_pcg_batch(tmpc_ctx* ctx, int B, int N, int nx, int precond, const doubl
  * guess [B][D] the initial iterate (nullable = zeros).  Outputs: x [B][D], iters [B], trace_nu /
  * trace_res [B][max_iter+1] (|nu| and ||b - A x|| per iteration as PCG.py:82-95, nullable: without
  * trace_res the explicit residual's extra product is skipped), Pinv_out [B][D][D] (nullable: the
- * preconditioner matrix the solve used).  1 <= D <= 4096: no block-tridiagonal structure is assumed,
- * the arbitrary-Pinv and the past-1024-row forms of the reference's PCG class.  Summation order:
+ * preconditioner matrix the solve used).  Any D >= 1 (B D^2 <= 2^34 entries, i.e. the device memory of
+ * three B x D x D matrices): no block-tridiagonal structure is assumed, the arbitrary-Pinv and the
+ * past-1024-row forms of the reference's PCG class.  Up to 4096 rows one workgroup per system holds the
+ * vectors (registers + LDS); past that each iteration's products and updates are separate launches with
+ * the vectors in HBM (host-synchronous every 4 iterations), the same operation order.  Summation order:
  * oracle/dense.py (bitwise reproducible on the CPU). */
 int tmpc_pcg_dense_batch(tmpc_ctx* ctx, int B, int D, const double* A, const double* b, const double* Pinv,
                          int precond, int nx, const double* guess, double tol, int max_iter, double* x,

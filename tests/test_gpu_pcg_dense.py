@@ -10,7 +10,9 @@ rows with the block preconditioner built on the device (compute_preconditioner, 
 * The preconditioner the device builds equals oracle/dense.py block_pinv bit for bit, and the
   reference's to 1e-12.
 * Arbitrary Pinv (no block structure) and dimensions past 1024 rows, including a trailing partial block,
-  through the PCG class: bit for bit against the oracle."""
+  through the PCG class: bit for bit against the oracle.
+* Past 4096 rows (the multi-launch form, vectors in HBM; round 6): the same operation order, bit for bit
+  against the oracle through the PCG class, with an arbitrary Pinv in a batch of two, and from a guess."""
 import numpy as np
 import pytest
 
@@ -146,3 +148,48 @@ def test_pcg_class_past_the_fused_rows(D, nx, ptype):
     assert np.array_equal(P, Po)
     x2, (trace2b, _) = pcg.pcg(S, g.reshape(-1, 1), P, np.zeros(D), dict(opts))
     assert np.array_equal(x2.reshape(-1), xo) and len(trace2b) == no + 1
+
+
+def test_pcg_class_past_4096_rows():
+    """PCG(A, b, nx, N).solve() at 5000 rows (10-row blocks, SS) and compute_preconditioner: the
+    multi-launch device PCG, iteration count, x and the |nu| trace bit for bit against the oracle."""
+    from oracle import dense as od
+    from trajoptmpcreference_amd import PCG
+    D, nx = 5000, 10
+    S, g = _random_system(D, nx, 17)
+    opts = {"preconditioner_type": "SS", "exit_tolerance": 1e-8, "max_iter": 150}
+    pcg = PCG(S, g.reshape(-1, 1), nx, D // nx, options=dict(opts))
+    x, (trace, trace2) = pcg.solve()
+    Po = od.block_pinv(S, nx, "SS")
+    xo, no, tno, tro = od.pcg(S, g, Po, tol=1e-8, max_iter=150)
+    assert 5 < no < 150
+    assert len(trace) == no + 1 and np.array_equal(x.reshape(-1), xo)
+    assert np.array_equal(np.array(trace), np.array(tno))
+    assert np.allclose(np.array(trace2), np.array(tro), rtol=1e-14, atol=0)
+    assert np.array_equal(pcg.compute_preconditioner(S, nx, "SS"), Po)
+
+
+def test_dense_pcg_past_4096_rows_arbitrary_pinv_batch_and_guess():
+    """Two 4200-row systems in one batch -- a dense arbitrary Pinv and the device's BJ blocks of a banded
+    system -- from a nonzero guess: per system bit for bit against the oracle; the system that converges
+    first stops (its later launches return) while the other continues."""
+    from oracle import dense as od
+    from trajoptmpcreference_amd import _native
+    D = 4200
+    S0, g0 = _random_system(D, 12, 31)
+    S1, g1 = _random_system(D, 12, 32, width=9)
+    rng = np.random.default_rng(33)
+    E = rng.uniform(-1.0, 1.0, (D, D)) * 1e-4
+    P0 = np.diag(1.0 / np.diag(S0)) + (E + E.T)
+    P1 = od.block_pinv(S1, 12, "BJ")
+    guess = rng.uniform(-0.1, 0.1, (2, D))
+    ctx = _native.default_context(0)
+    x, it, tn, tr, _ = ctx.pcg_dense_batch(np.stack([S0, S1]), np.stack([g0, g1]), np.stack([P0, P1]), guess=guess,
+                                           tol=1e-9, max_iter=400)
+    counts = []
+    for i, (S, g, P) in enumerate(((S0, g0, P0), (S1, g1, P1))):
+        ora = od.pcg(S, g, P, guess=guess[i], tol=1e-9, max_iter=400)
+        assert 3 < ora[1] < 400
+        _same((x[i], it[i], tn[i], tr[i]), ora, None)
+        counts.append(ora[1])
+    assert counts[0] != counts[1]

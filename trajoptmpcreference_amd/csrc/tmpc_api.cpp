@@ -176,9 +176,12 @@ static T* buf(tmpc_ctx* ctx, const char* name, size_t count) {
   if (!name) return fail(ctx, "device allocation of %s (%zu elements) failed", #name, \
                          (size_t)(count));
 
-// precision modes (tmpc_options.precision): rigid-body dynamics in fp32 for F32 and MIXED, the
-// Riccati sweep in fp32 for F32 only; Schur / PCG, merit sums and decisions stay fp64
+// precision modes (tmpc_options.precision): the dynamics' derivatives (M^-1, RNEA gradient: A_k, B_k) in
+// fp32 for F32 and MIXED; the trajectory values (the QP's defects, line-search trials, iLQR rollouts) in
+// fp32 for MIXED only -- F32 evaluates every trajectory, cost and merit in fp64, so its exit tests see the
+// fp64 objective; the Riccati sweep in fp32 for F32 only; Schur / PCG, merit sums and decisions stay fp64
 static bool dyn32(const tmpc_ctx* ctx) { return ctx->opts.precision != TMPC_PRECISION_F64; }
+static bool val32(const tmpc_ctx* ctx) { return ctx->opts.precision == TMPC_PRECISION_MIXED; }
 static bool ric32(const tmpc_ctx* ctx) { return ctx->opts.precision == TMPC_PRECISION_F32; }
 
 static SolverOpts solver_opts(const tmpc_options& o) {
@@ -269,7 +272,7 @@ static int run_qp(tmpc_ctx* ctx, int B, int N, double dt, int precond, const dou
   const double* G = soft ? w.Gk : w.G;
   {
     Timed t(ctx, "qp_fd");
-    LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, P, nb, N, dt, d_x, d_u, w.xs, st.need_grad,
+    LAUNCH_OK(launch_qp_fd(val32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, P, nb, N, dt, d_x, d_u, w.xs, st.need_grad,
                            w.qdd, w.cvec));
   }
   {
@@ -727,7 +730,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
   auto init_merit = [&](int* mask, int* ac, int* activate) -> int {
     ProbState sti = st;
     sti.active = mask;
-    LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
+    LAUNCH_OK(launch_ls_terms(val32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
                               alv.P, alv.nb, N, 1, dt, alphas + T, d_x, d_u, w.xs, nullptr, nullptr, mask, terms));
     if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, 1, alphas + T, d_x, d_u, nullptr, nullptr, mask));
     launch_ls_decide(ctx->stream, alv.P, alv.nb, N, nx, nj, 1, LS_MODE_INIT, soft, alphas + T, so, terms, d_x, d_u, w.dx, w.du,
@@ -741,7 +744,7 @@ static int sqp_device(tmpc_ctx* ctx, int B, int N, double dt, int linsys, double
     if (rc2) return rc2;
     {
       Timed t(ctx, "ls_terms");
-      LAUNCH_OK(launch_ls_terms(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
+      LAUNCH_OK(launch_ls_terms(val32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu, slam,
                                 alv.P, alv.nb, N, T, dt, alphas, d_x, d_u, w.xs, w.dx, w.du, st.active, terms));
       if (hterms) LAUNCH_OK(hard_ls(ctx, nj, hard, B, N, T, alphas, d_x, d_u, w.dx, w.du, st.active));
     }
@@ -868,14 +871,14 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     BUF(double, stream_xr, (size_t)sd->period * nx * N);
     HIP_OK(hipMemcpyAsync(stream_xr, sd->x_in, (size_t)sd->period * nx * N * sizeof(double), hipMemcpyDeviceToDevice,
                           ctx->stream));
-    LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, sd->period, N, dt,
+    LAUNCH_OK(launch_rollout(val32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, sd->period, N, dt,
                              stream_xr, sd->u_in));
     sdr.x_in = stream_xr;
     launch_stream_init(ctx->stream, B, sdr, d_x, d_u);   // slot s starts with problem s
     HIP_OK(hipGetLastError());
   } else {
     // iLQR iterates are rollouts: start from the rollout of u from x[:, 0]
-    LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
+    LAUNCH_OK(launch_rollout(val32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
   }
   HIP_OK(hipMemcpy2DAsync(w.xs, sizeof(double), d_x, (size_t)N * sizeof(double), sizeof(double), (size_t)B * nx,
                           hipMemcpyDeviceToDevice, ctx->stream));
@@ -897,7 +900,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
   auto ilqr_iteration = [&](int* ac) -> int {
     {
       Timed t(ctx, "qp_fd");
-      LAUNCH_OK(launch_qp_fd(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, alv.P, alv.nb, N, dt, d_x, d_u,
+      LAUNCH_OK(launch_qp_fd(val32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, alv.P, alv.nb, N, dt, d_x, d_u,
                              w.xs, st.need_grad, w.qdd, w.cvec));
     }
     {
@@ -918,7 +921,7 @@ static int ilqr_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, doub
     }
     {
       Timed t(ctx, "ilqr_forward");
-      LAUNCH_OK(launch_ilqr_forward(dyn32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu,
+      LAUNCH_OK(launch_ilqr_forward(val32(ctx), ctx->stream, nj, chain, ctx->model_id, ctx->dmodel, ctx->dcost, ctx->dlim, smu,
                                     slam, alv.P, alv.nb, N, T, dt, 0, alphas, d_x, d_u, il_K, il_d, st.active, il_ok, il_xt, il_ut,
                                     il_J));
     }
@@ -2196,8 +2199,8 @@ int tmpc_pcg_dense_batch(tmpc_ctx* ctx, int B, int D, const double* A, const dou
                          int precond, int nx, const double* guess, double tol, int max_iter, double* x,
                          int32_t* iters, double* trace_nu, double* trace_res, double* Pinv_out) {
   if (!ctx) return -1;
-  if (B < 1 || D < 1 || D > HARD_PCG_MAX_ROWS)
-    return fail(ctx, "bad sizes B=%d D=%d (the dense PCG takes 1 <= D <= %d)", B, D, HARD_PCG_MAX_ROWS);
+  if (B < 1 || D < 1 || (size_t)B * D * D > ((size_t)1 << 34))
+    return fail(ctx, "bad sizes B=%d D=%d (the dense PCG takes D >= 1 and B D^2 <= 2^34 entries)", B, D);
   if (!A || !b) return fail(ctx, "null input");
   if (max_iter < 0) return fail(ctx, "max_iter must be >= 0");
   if (!Pinv) {
@@ -2236,6 +2239,21 @@ int tmpc_pcg_dense_batch(tmpc_ctx* ctx, int B, int D, const double* A, const dou
   a.iters = dn_it;
   a.trace_nu = trace_nu ? dn_tn : nullptr;
   a.trace_res = trace_res ? dn_tr : nullptr;
+  const bool big = D > HARD_PCG_MAX_ROWS;   // past the one-workgroup kernel's registers / LDS
+  if (big) {
+    BUF(double, dn_r, (size_t)B * D);
+    BUF(double, dn_p, (size_t)B * D);
+    BUF(double, dn_y, (size_t)B * D);
+    BUF(double, dn_q, (size_t)B * D);
+    BUF(double, dn_nu, (size_t)B);
+    BUF(int, dn_done, (size_t)B);
+    a.r = dn_r;
+    a.p = dn_p;
+    a.y = dn_y;
+    a.q = dn_q;
+    a.nu = dn_nu;
+    a.done = dn_done;
+  }
   HIP_OK(hipMemcpyAsync(dn_stage, A, sizeof(double) * DD, hipMemcpyHostToDevice, ctx->stream));
   HIP_OK(hipMemcpyAsync(dn_b, b, sizeof(double) * B * D, hipMemcpyHostToDevice, ctx->stream));
   if (guess) HIP_OK(hipMemcpyAsync(dn_x0, guess, sizeof(double) * B * D, hipMemcpyHostToDevice, ctx->stream));
@@ -2249,7 +2267,8 @@ int tmpc_pcg_dense_batch(tmpc_ctx* ctx, int B, int D, const double* A, const dou
       HIP_OK(hipMemsetAsync(dn_PT, 0, sizeof(double) * DD, ctx->stream));
       LAUNCH_OK(launch_dense_precond(ctx->stream, a));   // reads A row-major from the stage
     }
-    LAUNCH_OK(launch_pcg_dense(ctx->stream, a));
+    if (big) LAUNCH_OK(launch_pcg_dense_big(ctx->stream, a));
+    else LAUNCH_OK(launch_pcg_dense(ctx->stream, a));
   }
   HIP_OK(hipStreamSynchronize(ctx->stream));
   resolve_timings(ctx);

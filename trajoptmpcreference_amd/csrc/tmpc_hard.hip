@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #pragma clang fp contract(off)
 
@@ -1722,6 +1723,157 @@ __global__ void __launch_bounds__(HARD_PCG_THREADS) k_pcg_dense(int D, const dou
     if (a < D) xo[(size_t)b * D + a] = xr[m];
   }
   if (t == 0) iters[b] = it_done;
+}
+
+// ---- the dense PCG past HARD_PCG_MAX_ROWS rows (launch_pcg_dense_big) ----
+// Past 4096 rows the vectors of a system no longer fit the workgroup's registers and LDS, so each phase of an
+// iteration is its own launch with the vectors in HBM scratch, every value in k_pcg_dense's order:
+//   k_pdb_mv:   y = M v (M given transposed: column c = row c of MT), row a on one thread, sequential over
+//               the columns from 0.0 -- the product of k_pcg_dense's mv; 64-thread workgroups so that a
+//               system's rows spread over D / 64 CUs; z selects one of two (M, v, y) products per launch;
+//   k_pdb_step: one HARD_PCG_THREADS workgroup per system, thread t over rows t, t + 1024, ... in order --
+//               the per-thread partials, butterfly and fan-in of h_block_sum_db, i.e. k_pcg_dense's sums --
+//               and the element updates of the phase.
+// A system that has met the tolerance sets done[b]; every later launch returns at once for it.
+__global__ void __launch_bounds__(64) k_pdb_mv(int D, const double* __restrict__ M0, const double* __restrict__ v0,
+                                               double* __restrict__ y0, const double* M1, const double* v1,
+                                               double* y1,
+                                               const int* __restrict__ done) {
+  const int b = blockIdx.y, a = blockIdx.x * 64 + threadIdx.x;
+  if (done[b] || a >= D) return;
+  const bool second = blockIdx.z == 1;
+  const size_t DD = (size_t)D * D;
+  const double* M = (second ? M1 : M0) + b * DD;
+  const double* v = (second ? v1 : v0) + (size_t)b * D;
+  double s = 0.0;
+  int c = 0;
+  for (; c + 4 <= D; c += 4) {   // four columns' loads in flight, summed in column order
+    const double m0 = M[(size_t)c * D + a], m1 = M[(size_t)(c + 1) * D + a];
+    const double m2 = M[(size_t)(c + 2) * D + a], m3 = M[(size_t)(c + 3) * D + a];
+    s = s + m0 * v[c];
+    s = s + m1 * v[c + 1];
+    s = s + m2 * v[c + 2];
+    s = s + m3 * v[c + 3];
+  }
+  for (; c < D; ++c) s = s + M[(size_t)c * D + a] * v[c];
+  (second ? y1 : y0)[(size_t)b * D + a] = s;
+}
+
+enum { PDB_INIT_R = 0, PDB_INIT_P = 1, PDB_A = 2, PDB_B = 3 };
+
+__global__ void __launch_bounds__(HARD_PCG_THREADS) k_pdb_step(int phase, int it, int D, const double* __restrict__ bv,
+                                                              double* __restrict__ xv, double* __restrict__ rv,
+                                                              double* __restrict__ pv, const double* __restrict__ yv,
+                                                              const double* __restrict__ qv, double* __restrict__ nuv,
+                                                              int* __restrict__ done, double tol, int max_iter,
+                                                              int* __restrict__ iters, double* __restrict__ tnu,
+                                                              double* __restrict__ tres) {
+  constexpr int T = HARD_PCG_THREADS;
+  __shared__ double red[32];
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (done[b]) return;
+  int nsum = 0;
+  const size_t o = (size_t)b * D;
+  const double* bb = bv + o;
+  double* x = xv + o;
+  double* r = rv + o;
+  double* p = pv + o;
+  const double* y = yv + o;
+  const int W = max_iter + 1;
+  double part = 0.0;
+  if (phase == PDB_INIT_R) {         // r = b - A x0, ||r||
+    for (int a = t; a < D; a += T) {
+      const double e = bb[a] - y[a];
+      r[a] = e;
+      part = part + e * e;
+    }
+    const double res0 = h_block_sum_db(part, red, nsum);
+    if (t == 0 && tres) tres[(size_t)b * W] = sqrt(res0);
+  } else if (phase == PDB_INIT_P) {  // p = z = Pinv r, nu = r . z
+    for (int a = t; a < D; a += T) {
+      p[a] = y[a];
+      part = part + r[a] * y[a];
+    }
+    const double nu = h_block_sum_db(part, red, nsum);
+    if (t == 0) {
+      nuv[b] = nu;
+      if (tnu) tnu[(size_t)b * W] = fabs(nu);
+    }
+  } else if (phase == PDB_A) {       // alpha = nu / p . A p; r -= A p alpha; x += p alpha
+    for (int a = t; a < D; a += T) part = part + p[a] * y[a];
+    const double alpha = nuv[b] / h_block_sum_db(part, red, nsum);
+    for (int a = t; a < D; a += T) {
+      r[a] = r[a] - y[a] * alpha;
+      x[a] = x[a] + p[a] * alpha;
+    }
+  } else {                           // nu' = r . z, ||b - A x||, the exit test, p = z + p beta
+    for (int a = t; a < D; a += T) part = part + r[a] * y[a];
+    const double nup = h_block_sum_db(part, red, nsum);
+    if (tres) {
+      double pq = 0.0;
+      for (int a = t; a < D; a += T) {
+        const double e = bb[a] - qv[o + a];
+        pq = pq + e * e;
+      }
+      const double rs = h_block_sum_db(pq, red, nsum);
+      if (t == 0) tres[(size_t)b * W + it + 1] = sqrt(rs);
+    }
+    if (t == 0 && tnu) tnu[(size_t)b * W + it + 1] = fabs(nup);
+    if (fabs(nup) < tol) {
+      __syncthreads();   // every thread has read nu / done before thread 0 changes them
+      if (t == 0) {
+        iters[b] = it + 1;
+        done[b] = 1;
+      }
+      return;
+    }
+    const double beta = nup / nuv[b];
+    for (int a = t; a < D; a += T) p[a] = y[a] + p[a] * beta;
+    __syncthreads();   // every thread has read nu
+    if (t == 0) nuv[b] = nup;
+  }
+}
+
+int launch_pcg_dense_big(hipStream_t s, const DenseArgs& a) {
+  const dim3 g1((a.D + 63) / 64, a.B, 1), g2((a.D + 63) / 64, a.B, 2);
+  const size_t vb = sizeof(double) * a.B * a.D;
+  if (a.guess) {
+    if (hipMemcpyAsync(a.x, a.guess, vb, hipMemcpyDeviceToDevice, s) != hipSuccess) return -1;
+  } else if (hipMemsetAsync(a.x, 0, vb, s) != hipSuccess) {
+    return -1;
+  }
+  if (hipMemsetAsync(a.done, 0, sizeof(int) * a.B, s) != hipSuccess) return -1;
+  std::vector<int> itn(a.B, a.max_iter), dn(a.B);
+  if (hipMemcpyAsync(a.iters, itn.data(), sizeof(int) * a.B, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+  auto mv = [&](const double* M, const double* v, double* y) {
+    hipLaunchKernelGGL(k_pdb_mv, g1, dim3(64), 0, s, a.D, M, v, y, M, v, y, a.done);
+  };
+  auto step = [&](int phase, int it) {
+    hipLaunchKernelGGL(k_pdb_step, dim3(a.B), dim3(HARD_PCG_THREADS), 0, s, phase, it, a.D, a.b, a.x, a.r, a.p, a.y,
+                       a.q, a.nu, a.done, a.tol, a.max_iter, a.iters, a.trace_nu, a.trace_res);
+  };
+  mv(a.AT, a.x, a.y);
+  step(PDB_INIT_R, 0);
+  mv(a.PT, a.r, a.y);
+  step(PDB_INIT_P, 0);
+  constexpr int CHECK = 4;   // iterations between host checks (later launches of a done system return at once)
+  for (int it = 0; it < a.max_iter; ++it) {
+    mv(a.AT, a.p, a.y);
+    step(PDB_A, it);
+    if (a.trace_res)   // z = Pinv r and A x in one launch
+      hipLaunchKernelGGL(k_pdb_mv, g2, dim3(64), 0, s, a.D, a.PT, a.r, a.y, a.AT, a.x, a.q, a.done);
+    else
+      mv(a.PT, a.r, a.y);
+    step(PDB_B, it);
+    if ((it + 1) % CHECK == 0 && it + 1 < a.max_iter) {
+      if (hipMemcpyAsync(dn.data(), a.done, sizeof(int) * a.B, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+      if (hipStreamSynchronize(s) != hipSuccess) return -1;
+      bool all = true;
+      for (int v : dn) all = all && v;
+      if (all) break;
+    }
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 static size_t pcg_dense_lds(int D) { return ((size_t)3 * D + 32) * sizeof(double); }

@@ -252,10 +252,16 @@ struct DenseArgs {
   const double *A, *b, *guess;
   double *AT, *PT, *Pd, *x, *trace_nu, *trace_res;
   int* iters;
+  // past HARD_PCG_MAX_ROWS (launch_pcg_dense_big): the vectors in HBM scratch [B][D] and per-system state
+  double *r, *p, *y, *q, *nu;
+  int *done;
 };
 int launch_dense_transpose(hipStream_t s, int B, int D, const double* in, double* out);
 int launch_dense_precond(hipStream_t s, const DenseArgs& a);
 int launch_pcg_dense(hipStream_t s, const DenseArgs& a);
+// the same PCG past HARD_PCG_MAX_ROWS rows: one launch per product / update phase, vectors in HBM, the same
+// operation order (oracle/dense.py); host-synchronous every few iterations to stop once every system is done
+int launch_pcg_dense_big(hipStream_t s, const DenseArgs& a);
 int dense_set_max_lds();
 
 }  // namespace tmpc

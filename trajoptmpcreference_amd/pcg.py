@@ -8,7 +8,7 @@ trace_res = ||b - A x_k|| (:83,95).  A block-tridiagonal A of at most 1024 rows
 (the Schur complement of the trajectory KKT system) runs in libtmpc's fused
 one-workgroup-per-system kernel on its blocks; any other A, and
 ``pcg(A, b, Pinv, guess, options)`` with any preconditioner matrix, run the
-dense device PCG (tmpc_pcg_dense_batch, up to 4096 rows).  Invalid options
+dense device PCG (tmpc_pcg_dense_batch, any size).  Invalid options
 raise ValueError instead of exit().
 """
 import numpy as np
@@ -18,7 +18,7 @@ from ._options import NO_OPTIONS, fresh
 
 VALID_PRECONDITIONERS = ("0", "J", "BJ", "SS")
 FUSED_MAX_ROWS = 1024   # tmpc_pcg_batch: one row of S per lane of one workgroup
-DENSE_MAX_ROWS = 4096   # tmpc_pcg_dense_batch (HARD_PCG_MAX_ROWS)
+DENSE_MAX_ROWS = 4096   # tmpc_pcg_dense_batch's one-workgroup kernel; past it the multi-launch form
 
 
 def extract_blocks(A, block_size):
@@ -96,7 +96,7 @@ class PCG:
     def _run(self, A, b, guess, options):
         """PCG.solve: the fused block-tridiagonal kernel (tmpc_pcg_batch) where A is block-tridiagonal with
         at most 1024 rows, else the dense PCG with the block preconditioner built on the device
-        (tmpc_pcg_dense_batch, up to 4096 rows)."""
+        (tmpc_pcg_dense_batch, any size)."""
         A = np.asarray(A, dtype=np.float64)
         n = A.shape[0]
         if n > FUSED_MAX_ROWS or A.shape != (n, n) or n % self.block_size:
@@ -127,8 +127,6 @@ class PCG:
         n = A.shape[0]
         if A.shape != (n, n):
             raise ValueError(f"A must be square, got {A.shape}")
-        if n > DENSE_MAX_ROWS:
-            raise NotImplementedError(f"PCG: {n} rows exceed the device PCG's {DENSE_MAX_ROWS}")
         b = np.asarray(b, dtype=np.float64).reshape(1, -1)
         g = None
         if guess is not None:
@@ -157,7 +155,7 @@ class PCG:
 
     def pcg(self, A, b, Pinv, guess, options=NO_OPTIONS):
         """PCG.pcg (PCG.py:66-111) with the caller's preconditioner matrix, whatever it is: z = Pinv r on
-        the device (tmpc_pcg_dense_batch, up to 4096 rows)."""
+        the device (tmpc_pcg_dense_batch, any size)."""
         options = fresh(options)
         self.set_default_options(options)
         x, traces, _ = self._run_dense(A, b, Pinv, guess, options)
@@ -167,7 +165,7 @@ class PCG:
         """PCG.compute_preconditioner (PCG.py:113-212) as a dense matrix: '0' identity, J diag(A)^-1, BJ the
         inverses of the floor(n / block_size) diagonal blocks, SS the symmetric stair (odd block rows carry
         -P_k A_k,k+-1 P_k+-1, mirrored to the even ones) -- built on the device from A (the dense PCG's
-        builder, k_dense_gj / k_dense_stair), any A up to 4096 rows."""
+        builder, k_dense_gj / k_dense_stair), any A."""
         self.validate_precon_type(preconditioner_type)
         A = np.asarray(A, dtype=np.float64)
         n = A.shape[0]
@@ -175,8 +173,6 @@ class PCG:
             return np.identity(n)
         if A.shape != (n, n):
             raise ValueError(f"A must be square, got {A.shape}")
-        if n > DENSE_MAX_ROWS:
-            raise NotImplementedError(f"PCG: {n} rows exceed the device PCG's {DENSE_MAX_ROWS}")
         ctx = _native.default_context(self.device)
         _, _, _, _, P = ctx.pcg_dense_batch(A[None], np.zeros((1, n)), None, precond=preconditioner_type,
                                             nx=int(block_size), tol=1.0, max_iter=0, trace=False, want_pinv=True)
