@@ -288,7 +288,8 @@ class Context:
             L.mode[t] = LIMIT_MODES[spec["mode"]]
             lb = np.broadcast_to(np.asarray(spec["lb"], dtype=np.float64), (n,))
             ub = np.broadcast_to(np.asarray(spec["ub"], dtype=np.float64), (n,))
-            for i in range(n):
+            # the ABI rows hold 8 joints; limits on a wider model are refused by the solve (check_ready)
+            for i in range(min(n, len(L.lb[t]))):
                 L.lb[t][i] = float(lb[i])
                 L.ub[t][i] = float(ub[i])
             o = spec.get("options", {})

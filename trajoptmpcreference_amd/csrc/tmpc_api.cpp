@@ -226,9 +226,32 @@ static int precond_of(int linsys) {
   }
 }
 
+// A wide model (NJ_FULL < n <= NJMAX joints) runs the dynamics on the runtime model and the SQP with the
+// fused register / two-rows-per-lane QP: fp64, QuadraticCost, no box limits, N * nx <= 1024 rows, no iLQR
+// (the Riccati sweep's MFMA tiles and the fp32 / soft / hard / HBM-row instances exist for up to NJ_FULL
+// joints)
+static int wide_ok(tmpc_ctx* ctx, const char* what) {
+  const int n = ctx->hmodel.n;
+  if (n <= NJ_FULL) return 0;
+  if (ctx->opts.precision != TMPC_PRECISION_F64)
+    return fail(ctx, "%s: %d joints run in fp64 only (precision modes up to %d joints)", what, n, NJ_FULL);
+  return 0;
+}
+
 static int check_ready(tmpc_ctx* ctx, int B, int N, bool qp = true) {
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model: call tmpc_set_model first");
+  if (ctx->hmodel.n > NJ_FULL) {
+    const int n = ctx->hmodel.n;
+    if (!qp) return fail(ctx, "iLQR supports up to %d joints (got %d); the SQP runs up to %d", NJ_FULL, n, NJMAX);
+    if (int rc = wide_ok(ctx, "SQP")) return rc;
+    if (ctx->hlim.any)
+      return fail(ctx, "box constraints with %d joints: supported up to %d joints (the soft / hard limit kernels)", n,
+                  NJ_FULL);
+    if (ctx->has_cost && ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "%d joints: QuadraticCost only", n);
+    if (N * 2 * n > 1024)
+      return fail(ctx, "%d joints: the QP takes N * nx <= 1024 rows (N <= %d; got N = %d)", n, 1024 / (2 * n), N);
+  }
   if (!ctx->has_cost) return fail(ctx, "no cost: call tmpc_set_cost_quadratic first");
   if (ctx->hcost.nx != 2 * ctx->hmodel.n || ctx->hcost.nu != ctx->hmodel.n)
     return fail(ctx, "cost sizes (nx=%d, nu=%d) do not match the model (n=%d)", ctx->hcost.nx, ctx->hcost.nu,
@@ -1036,7 +1059,7 @@ const char* tmpc_last_error(const tmpc_ctx* ctx) { return ctx ? ctx->err.c_str()
 int tmpc_set_model(tmpc_ctx* ctx, int n, const int32_t* parent, const int32_t* jtype, const int32_t* saxis,
                    const double* X0, const double* Xa, const double* Xb, const double* I, double gravity) {
   if (!ctx) return -1;
-  if (n < 1 || n > 7) return fail(ctx, "model must have 1..7 joints (got %d)", n);
+  if (n < 1 || n > NJMAX) return fail(ctx, "model must have 1..%d joints (got %d)", NJMAX, n);
   if (!parent || !jtype || !saxis || !X0 || !Xa || !Xb || !I) return fail(ctx, "null model array");
   ModelDev m{};
   m.n = n;
@@ -1171,9 +1194,10 @@ int tmpc_set_box_limits(tmpc_ctx* ctx, const tmpc_box_limits* L) {
         c.hard[t] = L->mode[t] == TMPC_LIMIT_ACTIVE_SET ? HARD_ACTIVE : HARD_FULL;
         c.any_hard = 1;
       }
-      for (int i = 0; i < NJMAX; ++i) {
-        c.lb[t][i] = L->lb[t][i];
-        c.ub[t][i] = L->ub[t][i];
+      constexpr int abi_row = (int)(sizeof(L->lb[0]) / sizeof(double));   // tmpc_box_limits rows: 8 joints
+      for (int i = 0; i < NJMAX; ++i) {   // (limits are refused past NJ_FULL joints, check_ready)
+        c.lb[t][i] = i < abi_row ? L->lb[t][i] : 0.0;
+        c.ub[t][i] = i < abi_row ? L->ub[t][i] : 0.0;
       }
       c.mu_init[t] = L->mu_init[t];
       c.mu_factor[t] = L->mu_factor[t];
@@ -1579,6 +1603,7 @@ int tmpc_mpc_batch(tmpc_ctx* ctx, int B, int N, double dt, int solver, int steps
 int tmpc_rollout_batch_device(tmpc_ctx* ctx, int B, int N, double dt, double* d_x, const double* d_u) {
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model");
+  if (int rc = wide_ok(ctx, "dynamics")) return rc;
   hipSetDevice(ctx->device);
   LAUNCH_OK(launch_rollout(dyn32(ctx), ctx->stream, ctx->hmodel.n, ctx->hmodel.chain != 0, ctx->model_id, ctx->dmodel, B, N, dt, d_x, d_u));
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -1589,6 +1614,7 @@ int tmpc_fd_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const double
                   double* Minv) {
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model");
+  if (int rc = wide_ok(ctx, "dynamics")) return rc;
   if (K < 1) return 0;
   hipSetDevice(ctx->device);
   const int nj = ctx->hmodel.n, nx = 2 * nj;
@@ -1612,6 +1638,7 @@ int tmpc_fd_grad_batch(tmpc_ctx* ctx, int K, double dt, const double* x, const d
                        double* dqdd) {
   if (!ctx) return -1;
   if (!ctx->has_model) return fail(ctx, "no model");
+  if (int rc = wide_ok(ctx, "dynamics")) return rc;
   if (K < 1) return 0;
   hipSetDevice(ctx->device);
   const int nj = ctx->hmodel.n, nx = 2 * nj;

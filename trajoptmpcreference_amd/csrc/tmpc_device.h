@@ -27,8 +27,22 @@
 
 namespace tmpc {
 
-constexpr int NJMAX = 8;
+constexpr int NJMAX = 12;
 constexpr int NXMAX = 2 * NJMAX;
+// joint counts with every kernel instance (fp32 / mixed, soft and hard limits, iLQR, the HBM-row QP, ...);
+// 8..NJMAX joints run the SQP on the runtime model (ModelRef), fp64, without box limits, up to 1024 Schur
+// rows: a "wide" model
+constexpr int NJ_FULL = 7;
+template <int NJ>
+constexpr bool kWide = NJ > NJ_FULL;
+// dispatch-table cases of the wide joint counts: the runtime model's general-topology instance (a chain is
+// a tree; one instance per joint count keeps the build's size)
+#define TMPC_WIDE_CASES(LAUNCH, CALL)                  \
+  case 8: LAUNCH<8, false, ModelRef>::CALL; break;     \
+  case 9: LAUNCH<9, false, ModelRef>::CALL; break;     \
+  case 10: LAUNCH<10, false, ModelRef>::CALL; break;   \
+  case 11: LAUNCH<11, false, ModelRef>::CALL; break;   \
+  case 12: LAUNCH<12, false, ModelRef>::CALL; break;
 
 struct ModelDev {
   int n;

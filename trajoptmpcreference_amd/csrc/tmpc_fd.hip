@@ -355,12 +355,15 @@ template <int NJ, bool CHAIN, class MT>
 struct LaunchFD {
   static void qp_fd(bool f32, hipStream_t s, const ModelDev* M, PList P, int B, int N, double dt, const double* x,
                     const double* u, const double* xs, const int* need, double* qdd, double* cvec) {
-    if (f32)
-      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), P, B, N, dt, x, u,
-                         xs, need, qdd, cvec);
-    else
-      hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), P, B, N, dt, x, u,
-                         xs, need, qdd, cvec);
+    if constexpr (!kWide<NJ>) {   // fp32 instances for up to NJ_FULL joints only
+      if (f32) {
+        hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), P, B, N, dt, x, u,
+                           xs, need, qdd, cvec);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_qp_fd<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1), 256), 0, s, MT::make(M), P, B, N, dt, x, u,
+                       xs, need, qdd, cvec);
   }
   // a runtime model (ModelRef) takes the general-topology line-search instance even for a chain: with
   // runtime coefficients the chain specialisation's unrolled recursion spills 9x more (k_ls_terms<6,
@@ -374,16 +377,23 @@ struct LaunchFD {
 #define TMPC_LS(SOFTV, RV)                                                                                        \
     hipLaunchKernelGGL((k_ls_terms<NJ, LCHAIN, SOFTV, MT, RV>), TMPC_GRID(B * T * N, 256), 0, s, MT::make(M), C, Cs, mu, \
                        lam, P, B, N, T, dt, alphas, x, u, xs, dx, du, active, terms);
-    if (mu) { if (f32) { TMPC_LS(true, float) } else { TMPC_LS(true, double) } }
-    else { if (f32) { TMPC_LS(false, float) } else { TMPC_LS(false, double) } }
+    if constexpr (kWide<NJ>) {   // a wide model: fp64 without soft limits only (check_ready refuses the rest)
+      TMPC_LS(false, double)
+    } else {
+      if (mu) { if (f32) { TMPC_LS(true, float) } else { TMPC_LS(true, double) } }
+      else { if (f32) { TMPC_LS(false, float) } else { TMPC_LS(false, double) } }
+    }
 #undef TMPC_LS
   }
   static void unit_fd(bool f32, hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* u,
                       double* xnext, double* qdd) {
-    if (f32)
-      hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT, float>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
-    else
-      hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT, double>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
+    if constexpr (!kWide<NJ>) {   // fp32 instances for up to NJ_FULL joints only
+      if (f32) {
+        hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT, float>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_unit_fd<NJ, CHAIN, MT, double>), TMPC_GRID(K, 256), 0, s, MT::make(M), K, dt, x, u, xnext, qdd);
   }
   static void mpc_shift(hipStream_t s, const ModelDev* M, int B, int N, double dt, int step, int steps, double* x,
                         double* u, double* xe, double* ue) {
@@ -392,10 +402,13 @@ struct LaunchFD {
   }
   static void rollout(bool f32, hipStream_t s, const ModelDev* M, int B, int N, double dt, double* x, const double* u,
                       PList P, const int* mask) {
-    if (f32)
-      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, float>), TMPC_GRID(B, 64), 0, s, MT::make(M), P, B, N, dt, x, u, mask);
-    else
-      hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, double>), TMPC_GRID(B, 64), 0, s, MT::make(M), P, B, N, dt, x, u, mask);
+    if constexpr (!kWide<NJ>) {   // fp32 instances for up to NJ_FULL joints only
+      if (f32) {
+        hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, float>), TMPC_GRID(B, 64), 0, s, MT::make(M), P, B, N, dt, x, u, mask);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_rollout<NJ, CHAIN, MT, double>), TMPC_GRID(B, 64), 0, s, MT::make(M), P, B, N, dt, x, u, mask);
   }
 };
 
@@ -413,6 +426,7 @@ struct LaunchFD {
     case 5: if (chain) LaunchFD<5, true, ModelRef>::CALL; else LaunchFD<5, false, ModelRef>::CALL; break;  \
     case 6: if (chain) LaunchFD<6, true, ModelRef>::CALL; else LaunchFD<6, false, ModelRef>::CALL; break;  \
     case 7: if (chain) LaunchFD<7, true, ModelRef>::CALL; else LaunchFD<7, false, ModelRef>::CALL; break;  \
+    TMPC_WIDE_CASES(LaunchFD, CALL)                                                                    \
     default: return -2;                                                                                \
   }                                                                                                    \
   return 0;

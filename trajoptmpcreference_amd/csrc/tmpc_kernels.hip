@@ -204,6 +204,68 @@ __global__ void __launch_bounds__(64) k_ginv(const CostDev* __restrict__ C, PLis
   }
 }
 
+// k_ginv for the wide models (NX > 16): one 32-lane group per matrix, the pivot row
+// broadcast by a lane shuffle instead of a 16-lane DPP row; the operations of gj_pivot, pivot by pivot.
+template <int P, int NX>
+__device__ __forceinline__ void gj_pivot_wide(double (&a)[NX], int r, int base) {
+  double pr[NX];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) pr[c] = __shfl(a[c], base + P, 64);
+  const double rp = 1.0 / pr[P];
+#pragma unroll
+  for (int c = 0; c < NX; ++c) pr[c] *= rp;
+  const double f = a[P];
+  if (r == P) {
+#pragma unroll
+    for (int c = 0; c < NX; ++c) a[c] = pr[c];
+    a[P] = rp;
+  } else {
+#pragma unroll
+    for (int c = 0; c < NX; ++c) a[c] = fma(-f, pr[c], a[c]);
+    a[P] = -f * rp;
+  }
+}
+template <int P, int NX>
+struct GjSweepWide {
+  static __device__ __forceinline__ void run(double (&a)[NX], int r, int base) {
+    gj_pivot_wide<P, NX>(a, r, base);
+    GjSweepWide<P + 1, NX>::run(a, r, base);
+  }
+};
+template <int NX>
+struct GjSweepWide<NX, NX> {
+  static __device__ __forceinline__ void run(double (&)[NX], int, int) {}
+};
+template <int NJ>
+__global__ void __launch_bounds__(64) k_ginv_wide(const CostDev* __restrict__ C, PList P, int B,
+                                                  const double* __restrict__ rho, const int* __restrict__ active,
+                                                  double* __restrict__ Ginv) {
+  constexpr int NX = 2 * NJ;
+  static_assert(NX <= 32, "one matrix per 32 lanes");
+  const int lane = threadIdx.x & 63;
+  const int slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 5;   // one matrix per 32 lanes
+  const int r = lane & 31, base = lane & 32;
+  const int ps = slot / 3;
+  const bool in_range = slot < B * 3 && P.has(ps, B);
+  const int b = in_range ? P.at(ps) : 0, which = in_range ? slot - 3 * ps : 0;
+  const bool act = in_range && active[b];
+  const int n = which == 2 ? NJ : NX;
+  const double* src = which == 0 ? C->Q : (which == 1 ? C->QF : C->R);
+  if (!__any(act)) return;   // wave-uniform exit
+  const double rh = act ? rho[b] : 0.0;
+  double a[NX];
+#pragma unroll
+  for (int c = 0; c < NX; ++c)
+    a[c] = (act && r < n && c < n) ? src[r * n + c] + (r == c ? rh : 0.0) : (r == c ? 1.0 : 0.0);
+  GjSweepWide<0, NX>::run(a, r, base);
+  if (act && r < n) {
+    double* out = Ginv + ((size_t)b * 3 + which) * NX * NX;
+#pragma unroll
+    for (int c = 0; c < NX; ++c)
+      if (c < n) out[r * n + c] = a[c];
+  }
+}
+
 // cost-to-go helpers (QuadraticCost.get_currQ, TrajoptCost.py:40-47)
 __device__ __forceinline__ bool use_QF(const CostDev* C, int k, int N) {
   return (k == N - 1) || (C->QF_start >= 0 && k >= C->QF_start);
@@ -852,6 +914,7 @@ int launch_btsolve(hipStream_t s, int nx, int B, int N, const int* active, const
 #define CASE_BT(V) \
   case V: hipLaunchKernelGGL((k_btsolve<V>), dim3(B), dim3(64), 0, s, N, active, Sd, Sl, gam, U, Y, lam); return 0;
     CASE_BT(2) CASE_BT(4) CASE_BT(6) CASE_BT(8) CASE_BT(10) CASE_BT(12) CASE_BT(14)
+    CASE_BT(16) CASE_BT(18) CASE_BT(20) CASE_BT(22) CASE_BT(24)
 #undef CASE_BT
     default: return -2;
   }
@@ -1087,12 +1150,15 @@ template <int NJ, bool CHAIN, class MT>
 struct Launch {
   static void qp_minv(bool f32, hipStream_t s, const ModelDev* M, PList P, int B, int N, const double* x,
                       const int* need, double* minv) {
-    if (f32)
-      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), P, B, N,
-                         x, need, minv);
-    else
-      hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), P, B, N,
-                         x, need, minv);
+    if constexpr (!kWide<NJ>) {   // fp32 instances for up to NJ_FULL joints only
+      if (f32) {
+        hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, float>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), P, B, N,
+                           x, need, minv);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_qp_minv<NJ, CHAIN, MT, double>), TMPC_GRID(B * (N - 1) * NJ, 256), 0, s, MT::make(M), P, B, N,
+                       x, need, minv);
   }
   // a runtime model (ModelRef) takes the general-topology gradient instance even for a chain: with runtime
   // coefficients the chain specialisation's unrolled recursion spills 2.5x more (k_qp_grad<6, chain,
@@ -1100,34 +1166,46 @@ struct Launch {
   static constexpr bool GCHAIN = MT::STATIC ? CHAIN : false;
   static void qp_grad(bool f32, hipStream_t s, const ModelDev* M, PList P, int B, int N, double dt, const double* x,
                       const int* need, const double* qdd, const double* minv, double* A, double* Bm) {
-    if (f32)
-      hipLaunchKernelGGL((k_qp_grad<NJ, GCHAIN, MT, float>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P, B,
-                         N, dt, x, need, qdd, minv, A, Bm);
-    else
-      hipLaunchKernelGGL((k_qp_grad<NJ, GCHAIN, MT, double>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P,
-                         B, N, dt, x, need, qdd, minv, A, Bm);
+    if constexpr (!kWide<NJ>) {   // fp32 instances for up to NJ_FULL joints only
+      if (f32) {
+        hipLaunchKernelGGL((k_qp_grad<NJ, GCHAIN, MT, float>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P, B,
+                           N, dt, x, need, qdd, minv, A, Bm);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_qp_grad<NJ, GCHAIN, MT, double>), TMPC_GRID(B * (N - 1) * 2 * NJ, 256), 0, s, MT::make(M), P,
+                       B, N, dt, x, need, qdd, minv, A, Bm);
   }
   static void unit_minv(bool f32, hipStream_t s, const ModelDev* M, int K, const double* x, double* minv) {
-    if (f32)
-      hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT, float>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
-    else
-      hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT, double>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
+    if constexpr (!kWide<NJ>) {   // fp32 instances for up to NJ_FULL joints only
+      if (f32) {
+        hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT, float>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_unit_minv<NJ, CHAIN, MT, double>), TMPC_GRID(K * NJ, 256), 0, s, MT::make(M), K, x, minv);
   }
   static void unit_grad(bool f32, hipStream_t s, const ModelDev* M, int K, double dt, const double* x, const double* qdd,
                         const double* minv, double* A, double* Bm, double* dqdd) {
-    if (f32)
-      hipLaunchKernelGGL((k_unit_grad<NJ, GCHAIN, MT, float>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
-                         minv, A, Bm, dqdd);
-    else
-      hipLaunchKernelGGL((k_unit_grad<NJ, GCHAIN, MT, double>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
-                         minv, A, Bm, dqdd);
+    if constexpr (!kWide<NJ>) {   // fp32 instances for up to NJ_FULL joints only
+      if (f32) {
+        hipLaunchKernelGGL((k_unit_grad<NJ, GCHAIN, MT, float>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
+                           minv, A, Bm, dqdd);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_unit_grad<NJ, GCHAIN, MT, double>), TMPC_GRID(K * 2 * NJ, 256), 0, s, MT::make(M), K, dt, x, qdd,
+                       minv, A, Bm, dqdd);
   }
 };
 
 template <int NJ>
 struct LaunchNJ {
   static void ginv(hipStream_t s, const CostDev* C, PList P, int B, const double* rho, const int* active, double* G) {
-    hipLaunchKernelGGL((k_ginv<NJ>), TMPC_GRID(B * 3 * 16, 64), 0, s, C, P, B, rho, active, G);
+    if constexpr (2 * NJ > 16)
+      hipLaunchKernelGGL((k_ginv_wide<NJ>), TMPC_GRID(B * 3 * 32, 64), 0, s, C, P, B, rho, active, G);
+    else
+      hipLaunchKernelGGL((k_ginv<NJ>), TMPC_GRID(B * 3 * 16, 64), 0, s, C, P, B, rho, active, G);
   }
   static void qp(hipStream_t s, const CostDev* C, PList P, int B, int N, double dt, int precond, int mode, const double* x,
                  const double* u,
@@ -1138,7 +1216,7 @@ struct LaunchNJ {
     const int rows = N * NX;
     // S / P^-1 rows in HBM (Sg), two rows per lane, up to 1024 lanes (method S past 1024 rows runs the
     // same instance for its prologue / epilogue modes, which never touch Sg)
-    const bool gm = rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG);
+    const bool gm = !kWide<NJ> && (rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG));
     const int rpl = gm ? 2 : pcg_rpl(N, NX);
     const int threads = ((rows / rpl + 63) / 64) * 64;
     const size_t lds = qp_lds_doubles(N, NX, NJ, gm ? QP_MAX_ROWS : 1024) * sizeof(double);
@@ -1151,13 +1229,25 @@ struct LaunchNJ {
       hipLaunchKernelGGL((k_qp<NJ, 1, 768, PKV, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);        \
     else                                                                                                   \
       hipLaunchKernelGGL((k_qp<NJ, 2, 512, PKV, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);
-    // soft limits (jsoft != null): per-knot Ghat from HBM
-    if (mode == QP_MODE_PCG) {
-      if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_PCG) } else { TMPC_QP_LAUNCH(false, QP_MODE_PCG) }
-    } else if (mode == QP_MODE_SCHUR) {
-      if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_SCHUR) } else { TMPC_QP_LAUNCH(false, QP_MODE_SCHUR) }
+    if constexpr (kWide<NJ>) {   // a wide model: registers / two rows per lane, no soft limits (launch_qp checks)
+#define TMPC_QP_LAUNCH_W(MODEV)                                                                            \
+      if (rpl == 1)                                                                                        \
+        hipLaunchKernelGGL((k_qp<NJ, 1, 768, false, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);    \
+      else                                                                                                 \
+        hipLaunchKernelGGL((k_qp<NJ, 2, 512, false, MODEV>), dim3(B), dim3(threads), lds, TMPC_QP_ARGS);
+      if (mode == QP_MODE_PCG) { TMPC_QP_LAUNCH_W(QP_MODE_PCG) }
+      else if (mode == QP_MODE_SCHUR) { TMPC_QP_LAUNCH_W(QP_MODE_SCHUR) }
+      else { TMPC_QP_LAUNCH_W(QP_MODE_DXU) }
+#undef TMPC_QP_LAUNCH_W
     } else {
-      if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_DXU) } else { TMPC_QP_LAUNCH(false, QP_MODE_DXU) }
+      // soft limits (jsoft != null): per-knot Ghat from HBM
+      if (mode == QP_MODE_PCG) {
+        if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_PCG) } else { TMPC_QP_LAUNCH(false, QP_MODE_PCG) }
+      } else if (mode == QP_MODE_SCHUR) {
+        if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_SCHUR) } else { TMPC_QP_LAUNCH(false, QP_MODE_SCHUR) }
+      } else {
+        if (jsoft) { TMPC_QP_LAUNCH(true, QP_MODE_DXU) } else { TMPC_QP_LAUNCH(false, QP_MODE_DXU) }
+      }
     }
 #undef TMPC_QP_LAUNCH
 #undef TMPC_QP_ARGS
@@ -1165,9 +1255,11 @@ struct LaunchNJ {
   static void ginv_soft(hipStream_t s, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N, const double* rho,
                         const int* active, const double* x, const double* u, const double* mu, const double* lam,
                         double* Gk, double* jsoft) {
-    const int wpp = (2 * N + 4 * GINV_SOFT_GROUPS - 1) / (4 * GINV_SOFT_GROUPS);
-    hipLaunchKernelGGL((k_ginv_soft<NJ>), dim3(B * wpp), dim3(64), 0, s, C, Cs, P, B, N, rho, active, x, u, mu, lam, Gk,
-                       jsoft);
+    if constexpr (!kWide<NJ>) {   // no soft limits on a wide model (launch_ginv_soft refuses it)
+      const int wpp = (2 * N + 4 * GINV_SOFT_GROUPS - 1) / (4 * GINV_SOFT_GROUPS);
+      hipLaunchKernelGGL((k_ginv_soft<NJ>), dim3(B * wpp), dim3(64), 0, s, C, Cs, P, B, N, rho, active, x, u, mu, lam,
+                         Gk, jsoft);
+    }
   }
 };
 
@@ -1196,6 +1288,16 @@ int pcg_set_max_lds() {
   SETQ(TMPC_DEV_NJ)
 #else
   SETQ(1) SETQ(2) SETQ(3) SETQ(4) SETQ(5) SETQ(6) SETQ(7)
+  // the wide models' instances (registers / two rows per lane, no soft limits)
+#define SETQW1(V, MD)                                                                                    \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 1, 768, false, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  bytes);                                                              \
+  err |= (int)hipFuncSetAttribute((const void*)k_qp<V, 2, 512, false, MD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  bytes);
+#define SETQW(V) SETQW1(V, QP_MODE_PCG) SETQW1(V, QP_MODE_SCHUR) SETQW1(V, QP_MODE_DXU)
+  SETQW(8) SETQW(9) SETQW(10) SETQW(11) SETQW(12)
+#undef SETQW
+#undef SETQW1
 #endif
 #undef SETQ
 #undef SETQ1
@@ -1589,6 +1691,7 @@ void launch_stream_init(hipStream_t s, int B, const StreamDev& sd, double* x, do
     case 5: if (chain) Launch<5, true, ModelRef>::CALL; else Launch<5, false, ModelRef>::CALL; break;  \
     case 6: if (chain) Launch<6, true, ModelRef>::CALL; else Launch<6, false, ModelRef>::CALL; break;  \
     case 7: if (chain) Launch<7, true, ModelRef>::CALL; else Launch<7, false, ModelRef>::CALL; break;  \
+    TMPC_WIDE_CASES(Launch, CALL)                                                                      \
     default: return -2;                                                                                \
   }                                                                                                    \
   return 0;
@@ -1610,6 +1713,11 @@ void launch_stream_init(hipStream_t s, int B, const StreamDev& sd, double* x, do
     case 5: LaunchNJ<5>::CALL; break;        \
     case 6: LaunchNJ<6>::CALL; break;        \
     case 7: LaunchNJ<7>::CALL; break;        \
+    case 8: LaunchNJ<8>::CALL; break;        \
+    case 9: LaunchNJ<9>::CALL; break;        \
+    case 10: LaunchNJ<10>::CALL; break;      \
+    case 11: LaunchNJ<11>::CALL; break;      \
+    case 12: LaunchNJ<12>::CALL; break;      \
     default: return -2;                      \
   }                                                                                \
   return 0;
@@ -1643,7 +1751,8 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, do
               double* Pd, const double* jsoft, const double* guess, double* Sg) {
   const int rows = N * 2 * nj;
   if (rows > QP_MAX_ROWS) return -1;
-  const bool gm = rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG);
+  if (nj > NJ_FULL && (rows > 1024 || jsoft)) return -2;   // a wide model: no HBM-row instance, no soft limits
+  const bool gm = nj <= NJ_FULL && (rows > 1024 || (rows >= qp_gm_min_rows() && mode == QP_MODE_PCG));
   if (gm && mode == QP_MODE_PCG && !Sg) return -4;
   if (qp_lds_doubles(N, 2 * nj, nj, gm ? QP_MAX_ROWS : 1024) * sizeof(double) > 160 * 1024) return -3;
   TMPC_DISPATCH_NJ2(nj, qp(s, C, P, B, N, dt, precond, mode, x, u, active, G, A, Bm, cvec, tol, max_iter, iters, dx, du, lam,
@@ -1652,6 +1761,7 @@ int launch_qp(hipStream_t s, int nj, const CostDev* C, PList P, int B, int N, do
 int launch_ginv_soft(hipStream_t s, int nj, const CostDev* C, const ConstrDev* Cs, PList P, int B, int N,
                      const double* rho, const int* active, const double* x, const double* u, const double* mu,
                      const double* lam, double* Gk, double* jsoft) {
+  if (nj > NJ_FULL) return -2;
   TMPC_DISPATCH_NJ2(nj, ginv_soft(s, C, Cs, P, B, N, rho, active, x, u, mu, lam, Gk, jsoft))
 }
 
