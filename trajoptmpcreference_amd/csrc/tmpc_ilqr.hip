@@ -1030,12 +1030,18 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int N
   const int b = P.at(blockIdx.x);
   if (!st.active[b]) return;
   __shared__ int s_choice;
+  __shared__ double s_al[64], s_J[64];
   const int t = threadIdx.x;
   const int W = o.max_iter_sqp + 1;
   const int K = N - 1;
+  if (t < T) {   // the trials' alphas and costs loaded by their lanes at once (lane 0 walks them below)
+    s_al[t] = alphas[t];
+    s_J[t] = Jt[(size_t)b * T + t];
+  }
+  __syncthreads();
   if (t == 0) {
     if (init) {
-      const double J = Jt[(size_t)b * T];
+      const double J = s_J[0];
       st.J[b] = J;
       st.c[b] = 0.0;
       st.merit[b] = J;
@@ -1058,9 +1064,9 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int N
       double al = 0.0, ratio = __builtin_nan(""), Jn = J, deltaJ = 0.0;
       if (bok) {
         for (int tt = 0; tt < T; ++tt) {
-          al = alphas[tt];
+          al = s_al[tt];
           ls = tt;
-          Jn = Jt[(size_t)b * T + tt];
+          Jn = s_J[tt];
           deltaJ = J - Jn;
           ratio = deltaJ / (-al * (dV1 + al * dV2));
           if (ratio >= o.exp_red_min && ratio <= o.exp_red_max) {

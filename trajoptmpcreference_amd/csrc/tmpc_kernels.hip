@@ -935,15 +935,33 @@ __global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX,
                                                   unsigned long long* __restrict__ counters,
                                                   const double* __restrict__ hterms,
                                                   const int* __restrict__ qp_singular,
-                                                  int* __restrict__ activate) {
+                                                  int* __restrict__ activate, int stage_bytes) {
   if (!P.has(blockIdx.x, B)) return;
   const int b = P.at(blockIdx.x);
   if (!st.active[b]) return;
-  __shared__ double sJ[64], sC[64], sD[64];
+  __shared__ double sJ[64], sC[64], sD[64], s_al[64];
   __shared__ int s_choice;
   const int t = threadIdx.x;
+  if (t < T) s_al[t] = alphas[t];   // (published by the barrier after the sums)
+  // the problem's line-search terms staged in LDS by all 64 lanes at once (dynamic LDS of T N 4 + T N
+  // doubles when the launch gives it, LS_DECIDE_STAGE_MAX): one round of independent loads instead of the
+  // trial lanes' serial walks through HBM; the sums below read the same values in the same order
+  extern __shared__ double s_terms[];
+  const bool staged = stage_bytes > 0;
+  if (staged) {
+    const double* src = terms + (size_t)b * T * N * 4;
+    const int ne = T * N * 4;
+#pragma unroll 8
+    for (int e = t; e < ne; e += 64) s_terms[e] = src[e];
+    if (hterms) {
+      const double* hs = hterms + (size_t)b * T * N;
+#pragma unroll 4
+      for (int e = t; e < T * N; e += 64) s_terms[ne + e] = hs[e];
+    }
+    __syncthreads();
+  }
   if (t < T) {
-    const double* tm = terms + ((size_t)b * T + t) * N * 4;
+    const double* tm = staged ? s_terms + (size_t)t * N * 4 : terms + ((size_t)b * T + t) * N * 4;
     double J = 0.0, c = 0.0, D = 0.0;
     for (int k = 0; k < N - 1; ++k) J = J + tm[k * 4 + 0];
     J = J + tm[(N - 1) * 4 + 0];
@@ -956,7 +974,7 @@ __global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX,
     for (int k = 0; k < N - 1; ++k) D += tm[k * 4 + 2];
     D += tm[(N - 1) * 4 + 2];
     if (hterms) {   // hard box-constraint terms after the dynamics ones, knot by knot (:286-293)
-      const double* th = hterms + ((size_t)b * T + t) * N;
+      const double* th = staged ? s_terms + (size_t)T * N * 4 + (size_t)t * N : hterms + ((size_t)b * T + t) * N;
       for (int k = 0; k < N; ++k) c = c + th[k];
     }
     sJ[t] = J;
@@ -987,7 +1005,7 @@ __global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX,
       double D = 0.0, ratio = 0.0, Jn = 0.0, cn = 0.0, mn = 0.0, al = 1.0;
       int ls = 0;
       for (int tt = 0; tt < T; ++tt) {
-        al = alphas[tt];
+        al = s_al[tt];
         ls = tt;
         Jn = sJ[tt];
         cn = sC[tt];
@@ -1343,8 +1361,13 @@ void launch_ls_decide(hipStream_t s, PList P, int B, int N, int NX, int NU, int 
                       const double* dx, const double* du, const ProbState& st, const int* pcg_iters,
                       const TraceDev& tr, int* active_count, unsigned long long* counters, const double* hterms,
                       const int* qp_singular, int* activate) {
-  hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), 0, s, P, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u, dx,
-                     du, st, pcg_iters, tr, active_count, counters, hterms, qp_singular, activate);
+  // LDS staging of the terms up to LS_DECIDE_STAGE_MAX bytes (within the default dynamic-LDS limit; N = 64,
+  // T = 9: 18 kB), the direct HBM walks past it
+  constexpr size_t LS_DECIDE_STAGE_MAX = 60 * 1024;
+  size_t stage = ((size_t)T * N * 4 + (hterms ? (size_t)T * N : 0)) * sizeof(double);
+  if (stage > LS_DECIDE_STAGE_MAX) stage = 0;
+  hipLaunchKernelGGL(k_ls_decide, dim3(B), dim3(64), stage, s, P, B, N, NX, NU, T, mode, soft, alphas, o, terms, x, u,
+                     dx, du, st, pcg_iters, tr, active_count, counters, hterms, qp_singular, activate, (int)stage);
 }
 
 // The problems still alive in the lock-step loop (mask != 0), ascending, and their count: one
@@ -1508,14 +1531,19 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
   auto zval = [&](int t, int i, int k) -> double {
     return t == 2 ? ub[i * K + k] : xb[(t * NJ + i) * N + k];
   };
-  // max_c over (type, knot) pairs
+  // max_c over (type, knot) pairs (the pair's 2 n values loaded together, then reduced in order)
   double mx = 0.0;
   for (int p = t0; p < 3 * N; p += 64) {
     const int t = p / N, k = p - t * N;
     if (Cs->mode[t] == SOFT_NONE || (t == 2 && k == K)) continue;
+    double zz[NJMAX];
+#pragma unroll
+    for (int i = 0; i < NJMAX; ++i) zz[i] = i < NJ ? zval(t, i, k) : 0.0;
     double mn = 0.0;
-    for (int e = 0; e < 2 * NJ; ++e) {
-      const double v = soft_v(Cs, t, e, NJ, zval(t, e < NJ ? e : e - NJ, k));
+#pragma unroll
+    for (int e = 0; e < 2 * NJMAX; ++e) {
+      if (e >= 2 * NJ) break;
+      const double v = soft_v(Cs, t, e, NJ, zz[e < NJ ? e : e - NJ]);
       mn = e == 0 ? v : fmin(mn, v);
     }
     mx = fmax(mx, fabs(mn));
@@ -1537,21 +1565,45 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
   }
   __syncthreads();
   if (s_exit == 0) {
-    for (int p = t0; p < N * MC; p += 64) {
-      const int k = p / MC, sl = p - k * MC;
-      const int t = sl / (2 * NJ), e = sl - t * 2 * NJ;
-      if (Cs->mode[t] == SOFT_NONE || (t == 2 && k == K)) continue;
-      const double v = soft_v(Cs, t, e, NJ, zval(t, e < NJ ? e : e - NJ, k));
-      const size_t o = ((size_t)b * N + k) * MC + sl;
-      if (v < 0.0 && !(fabs(v) < phi[o])) {
-        if (mu[o] < Cs->mu_max[t]) {
-          s_changed = 1;
-          mu[o] = fmin(Cs->mu_max[t], mu[o] * Cs->mu_factor[t]);
+    // update_soft_constraint_constants entry by entry; OB entries per lane have their loads issued together
+    // before any of them is updated (each entry's arithmetic is unchanged)
+    constexpr int OB = 6;
+    for (int p0 = t0; p0 < N * MC; p0 += 64 * OB) {
+      double zv[OB], ph[OB], mv[OB], lv[OB];
+      bool ok[OB];
+#pragma unroll
+      for (int j = 0; j < OB; ++j) {
+        const int p = p0 + 64 * j;
+        const int k = p / MC, sl = p - k * MC;
+        const int t = sl / (2 * NJ), e = sl - t * 2 * NJ;
+        ok[j] = p < N * MC && Cs->mode[t] != SOFT_NONE && !(t == 2 && k == K);
+        zv[j] = ph[j] = mv[j] = lv[j] = 0.0;
+        if (ok[j]) {
+          const size_t o = ((size_t)b * N + k) * MC + sl;
+          zv[j] = zval(t, e < NJ ? e : e - NJ, k);
+          ph[j] = phi[o];
+          mv[j] = mu[o];
+          lv[j] = lam[o];
         }
-      } else if (v < 0.0) {
-        s_changed = 1;
-        lam[o] += mu[o] * v;
-        phi[o] /= Cs->phi_factor[t];
+      }
+#pragma unroll
+      for (int j = 0; j < OB; ++j) {
+        if (!ok[j]) continue;
+        const int p = p0 + 64 * j;
+        const int k = p / MC, sl = p - k * MC;
+        const int t = sl / (2 * NJ), e = sl - t * 2 * NJ;
+        const double v = soft_v(Cs, t, e, NJ, zv[j]);
+        const size_t o = ((size_t)b * N + k) * MC + sl;
+        if (v < 0.0 && !(fabs(v) < ph[j])) {
+          if (mv[j] < Cs->mu_max[t]) {
+            s_changed = 1;
+            mu[o] = fmin(Cs->mu_max[t], mv[j] * Cs->mu_factor[t]);
+          }
+        } else if (v < 0.0) {
+          s_changed = 1;
+          lam[o] = lv[j] + mv[j] * v;
+          phi[o] = ph[j] / Cs->phi_factor[t];
+        }
       }
     }
   }
