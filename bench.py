@@ -897,7 +897,10 @@ def line_roofline(a, N, nx, nu, kernels, counters, hard_bytes=None):
         r = {"kernel": "k_ilqr_backward", "bound": "fp32-valu" if f32 else "fp64-valu", "achieved": ach,
              "peak": peak, "unit": "TFLOP/s", "frac": ach / peak, "traffic": traffic,
              "algorithmic_flops_per_launch": flops, "avg_launch_ms": bw["avg_ms"],
-             "note": "sequential Riccati sweep, latency-bound (one 64-lane wave per problem)"}
+             "note": "sequential Riccati sweep, latency-bound (one 64-lane wave per problem)" + (
+                 "; fp32 state and Cholesky, the Q products on the fp64 matrix cores from fp32 operands "
+                 "(k_ilqr_backward<NJ, float, true>), priced against the fp32 VALU peak" if f32 else
+                 "; Q products on v_mfma_f64_16x16x4f64")}
         if traffic:
             r.update(hbm_GBps=traffic / (bw["avg_ms"] / 1e3) / 1e9, traffic_source=src)
         fw = kernels.get("ilqr_forward")

@@ -1153,7 +1153,14 @@ struct LaunchIlqr {
       hipLaunchKernelGGL((k_ilqr_soft_jac<NJ>), TMPC_GRID(B * N, 256), 0, s, Cs, mu, lam, P, B, N, x, u, active, jscratch);
       js = jscratch;
     }
-    if (f32)
+    // fp32: the Riccati state in fp32; its Q products on the matrix cores from the fp32 operands (fp64 MFMA
+    // accumulation, rounded to fp32) unless TMPC_ILQR_F32_VALU=1 (the fp32 VALU loops)
+    const char* fv = getenv("TMPC_ILQR_F32_VALU");
+    const bool f32mf = mf && !(fv && fv[0] == '1');
+    if (f32 && f32mf)
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, float, true>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
+                         Bm, mu, lam, js, K, d, dV, ok);
+    else if (f32)
       hipLaunchKernelGGL((k_ilqr_backward<NJ, float, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
                          Bm, mu, lam, js, K, d, dV, ok);
     else if (mf)
