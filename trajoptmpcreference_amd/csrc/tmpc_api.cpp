@@ -1514,6 +1514,8 @@ static int mpc_device(tmpc_ctx* ctx, int B, int N, double dt, int solver, int st
   const bool ilqr = solver == TMPC_SOLVER_ILQR;
   int rc = check_ready(ctx, B, N, !ilqr);
   if (rc) return rc;
+  if (ctx->hmodel.n > NJ_FULL)
+    return fail(ctx, "the MPC loop supports up to %d joints (got %d)", NJ_FULL, ctx->hmodel.n);
   if (ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "the MPC loop supports QuadraticCost only");
   if (steps < 1) return fail(ctx, "steps must be >= 1");
   if (!ilqr && precond_of(solver) < 0) return fail(ctx, "solver %d: use TMPC_LINSYS_* or TMPC_SOLVER_ILQR", solver);
