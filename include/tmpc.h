@@ -174,9 +174,9 @@ const char* tmpc_last_error(const tmpc_ctx* ctx);
  * matrices X0/Xa/Xb [n][6][6] and spatial inertias I [n][6][6]; gravity is
  * options['gravity'] (TrajoptPlant.py:31, -9.81).  Replaces URDFPlant.__init__
  * (TrajoptPlant.py:275-281) + RBDReference(robot) state.  1 <= n <= 12: up to 7 joints every solver, limit
- * kind and precision mode; 8..12 joints ("wide" models, round 6) the dynamics entry points and the SQP
- * (QuadraticCost, fp64, no box limits, N * 2n <= 1024 Schur rows) on the runtime-model kernels -- the
- * other entry points fail with a message naming the limit. */
+ * kind and precision mode; 8..12 joints ("wide" models, round 6) the dynamics entry points, the SQP
+ * (N * 2n <= 1024 Schur rows) and iLQR (QuadraticCost, fp64, no box limits) on the runtime-model kernels --
+ * the other entry points fail with a message naming the limit. */
 int tmpc_set_model(tmpc_ctx* ctx, int n, const int32_t* parent, const int32_t* jtype, const int32_t* saxis,
                    const double* X0, const double* Xa, const double* Xb, const double* I, double gravity);
 

@@ -6,8 +6,10 @@ planar chains of 8, 9, 10 and 12 joints, against the oracle:
   * SQP: exit code, SQP iterations, the alpha path and every QP's PCG count identical to the oracle's run
     (oracle/sqp.py), trajectories within 1e-6; every QP of the GPU's own run replayed at its own iterate
     with the canonical-order PCG (oracle/canon.c) on that QP's S: count and lambda bit for bit;
-  * what a wide model does not run (iLQR, box limits, the precision modes, more than 1024 Schur rows) is
-    refused with a message naming the limit."""
+  * iLQR (the VALU Riccati sweep, the plain rollout) against oracle/ilqr.py: converged cost and trajectories,
+    and every iteration replayed at the GPU's own iterate (test_gpu_ilqr._replay);
+  * what a wide model does not run (box limits, the precision modes, the MPC loop, more than 1024 Schur
+    rows for the SQP) is refused with a message naming the limit."""
 import numpy as np
 import pytest
 
@@ -85,8 +87,6 @@ def test_wide_model_refusals():
     n, N = 9, 8
     x0, u0 = osqp.initial_problem(_model(n), N, 0.1, 1)
     s = _solver(n)
-    with pytest.raises(_native.NativeError, match="iLQR supports up to 7 joints"):
-        s.iLQR_batch(x0[None], u0[None], N, 0.1, {})
     with pytest.raises(_native.NativeError, match="fp64 only"):
         s.SQP_batch(x0[None], u0[None], N, 0.1, "PCG-SS", {"precision": "fp32"})
     Nl = 60   # 60 x 18 = 1080 rows
@@ -131,3 +131,19 @@ def test_wide_mpc_refused(ctx):
     ctx.set_box_limits(None)
     with pytest.raises(_native.NativeError, match="MPC loop supports up to 7 joints"):
         ctx.mpc_batch(np.zeros((1, 2 * n, N)), np.zeros((1, n, N - 1)), N, 0.1, "PCG-SS", 2)
+
+
+@pytest.mark.parametrize("n,N", [(9, 16), (12, 12)])
+def test_wide_ilqr_matches_oracle(n, N):
+    from oracle import ilqr as oilqr
+    from oracle import sqp as osqp
+    from test_gpu_ilqr import _check_full, _replay
+    m = _model(n)
+    solver = _solver(n)
+    xs, us = zip(*[osqp.initial_problem(m, N, 0.1, 960 + i) for i in range(3)])
+    r = solver.iLQR_batch(np.array(xs), np.array(us), N, 0.1, {})
+    cost = osqp.QuadCost(*quad_cost_arrays(n))
+    for i in range(3):
+        with np.errstate(all="ignore"):
+            _check_full(r, i, oilqr.ilqr(m, cost, xs[i], us[i], N, 0.1, {}))
+    _replay(solver, r, m, cost, np.array(xs), np.array(us), N)

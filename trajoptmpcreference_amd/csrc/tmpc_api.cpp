@@ -226,10 +226,10 @@ static int precond_of(int linsys) {
   }
 }
 
-// A wide model (NJ_FULL < n <= NJMAX joints) runs the dynamics on the runtime model and the SQP with the
-// fused register / two-rows-per-lane QP: fp64, QuadraticCost, no box limits, N * nx <= 1024 rows, no iLQR
-// (the Riccati sweep's MFMA tiles and the fp32 / soft / hard / HBM-row instances exist for up to NJ_FULL
-// joints)
+// A wide model (NJ_FULL < n <= NJMAX joints) runs the dynamics on the runtime model, the SQP with the fused
+// register / two-rows-per-lane QP (N * nx <= 1024 rows) and iLQR with the VALU Riccati sweep and the plain
+// rollout: fp64, QuadraticCost, no box limits (the MFMA sweep's tiles and the fp32 / soft / hard / HBM-row
+// instances exist for up to NJ_FULL joints)
 static int wide_ok(tmpc_ctx* ctx, const char* what) {
   const int n = ctx->hmodel.n;
   if (n <= NJ_FULL) return 0;
@@ -243,13 +243,12 @@ static int check_ready(tmpc_ctx* ctx, int B, int N, bool qp = true) {
   if (!ctx->has_model) return fail(ctx, "no model: call tmpc_set_model first");
   if (ctx->hmodel.n > NJ_FULL) {
     const int n = ctx->hmodel.n;
-    if (!qp) return fail(ctx, "iLQR supports up to %d joints (got %d); the SQP runs up to %d", NJ_FULL, n, NJMAX);
-    if (int rc = wide_ok(ctx, "SQP")) return rc;
+    if (int rc = wide_ok(ctx, qp ? "SQP" : "iLQR")) return rc;
     if (ctx->hlim.any)
       return fail(ctx, "box constraints with %d joints: supported up to %d joints (the soft / hard limit kernels)", n,
                   NJ_FULL);
     if (ctx->has_cost && ctx->hcost.kind != COST_QUADRATIC) return fail(ctx, "%d joints: QuadraticCost only", n);
-    if (N * 2 * n > 1024)
+    if (qp && N * 2 * n > 1024)
       return fail(ctx, "%d joints: the QP takes N * nx <= 1024 rows (N <= %d; got N = %d)", n, 1024 / (2 * n), N);
   }
   if (!ctx->has_cost) return fail(ctx, "no cost: call tmpc_set_cost_quadratic first");

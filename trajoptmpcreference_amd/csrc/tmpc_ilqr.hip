@@ -1144,31 +1144,36 @@ struct LaunchIlqr {
                        const double* u, const double* rho, const int* active, const double* A, const double* Bm,
                        const double* mu, const double* lam, double* jscratch, double* K, double* d, double* dV,
                        int* ok) {
-    // fp64: the matrix-core products (MF) unless TMPC_ILQR_VALU=1 (the VALU loops, for comparison)
-    const char* v = getenv("TMPC_ILQR_VALU");
-    const bool mf = !(v && v[0] == '1');
-    // soft limits: every knot's jacobian first, in parallel ([B][N][3 NJ] in jscratch)
-    const double* js = nullptr;
-    if (mu) {
-      hipLaunchKernelGGL((k_ilqr_soft_jac<NJ>), TMPC_GRID(B * N, 256), 0, s, Cs, mu, lam, P, B, N, x, u, active, jscratch);
-      js = jscratch;
+    if constexpr (kWide<NJ>) {   // a wide model: fp64 VALU sweep, no soft limits (check_ready refuses the rest)
+      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active,
+                         A, Bm, mu, lam, nullptr, K, d, dV, ok);
+    } else {
+      // fp64: the matrix-core products (MF) unless TMPC_ILQR_VALU=1 (the VALU loops, for comparison)
+      const char* v = getenv("TMPC_ILQR_VALU");
+      const bool mf = !(v && v[0] == '1');
+      // soft limits: every knot's jacobian first, in parallel ([B][N][3 NJ] in jscratch)
+      const double* js = nullptr;
+      if (mu) {
+        hipLaunchKernelGGL((k_ilqr_soft_jac<NJ>), TMPC_GRID(B * N, 256), 0, s, Cs, mu, lam, P, B, N, x, u, active, jscratch);
+        js = jscratch;
+      }
+      // fp32: the Riccati state in fp32; its Q products on the matrix cores from the fp32 operands (fp64 MFMA
+      // accumulation, rounded to fp32) unless TMPC_ILQR_F32_VALU=1 (the fp32 VALU loops)
+      const char* fv = getenv("TMPC_ILQR_F32_VALU");
+      const bool f32mf = mf && !(fv && fv[0] == '1');
+      if (f32 && f32mf)
+        hipLaunchKernelGGL((k_ilqr_backward<NJ, float, true>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
+                           Bm, mu, lam, js, K, d, dV, ok);
+      else if (f32)
+        hipLaunchKernelGGL((k_ilqr_backward<NJ, float, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
+                           Bm, mu, lam, js, K, d, dV, ok);
+      else if (mf)
+        hipLaunchKernelGGL((k_ilqr_backward<NJ, double, true>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
+                           Bm, mu, lam, js, K, d, dV, ok);
+      else
+        hipLaunchKernelGGL((k_ilqr_backward<NJ, double, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
+                           Bm, mu, lam, js, K, d, dV, ok);
     }
-    // fp32: the Riccati state in fp32; its Q products on the matrix cores from the fp32 operands (fp64 MFMA
-    // accumulation, rounded to fp32) unless TMPC_ILQR_F32_VALU=1 (the fp32 VALU loops)
-    const char* fv = getenv("TMPC_ILQR_F32_VALU");
-    const bool f32mf = mf && !(fv && fv[0] == '1');
-    if (f32 && f32mf)
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, float, true>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
-                         Bm, mu, lam, js, K, d, dV, ok);
-    else if (f32)
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, float, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
-                         Bm, mu, lam, js, K, d, dV, ok);
-    else if (mf)
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, true>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
-                         Bm, mu, lam, js, K, d, dV, ok);
-    else
-      hipLaunchKernelGGL((k_ilqr_backward<NJ, double, false>), dim3(B), dim3(64), 0, s, C, Cs, P, B, N, x, u, rho, active, A,
-                         Bm, mu, lam, js, K, d, dV, ok);
   }
   static void forward(bool f32, hipStream_t s, const ModelDev* M, const CostDev* C, const ConstrDev* Cs, const double* mu,
                       const double* lam, PList P, int B, int N, int T, double dt, int init, const double* alphas,
@@ -1179,6 +1184,11 @@ struct LaunchIlqr {
     const char* npf = getenv("TMPC_ILQR_NOPF");
     const size_t pf_lds = FwdPf<NJ>::lds_doubles(T) * sizeof(double);
     const bool pf = !init && pf_lds <= 48 * 1024 && !(npf && npf[0] == '1');
+    if constexpr (kWide<NJ>) {   // a wide model: fp64, no soft limits, the plain (non-prefetching) instance
+      hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, false, MT, double, false>), TMPC_GRID(B * T, 64), 0, s, MT::make(M), C,
+                         Cs, mu, lam, P, B, N, T, dt, init, alphas, x, u, K, d, active, ok, xt, ut, Jt);
+      return;
+    } else {
 #define TMPC_FWD(SOFTV, RV)                                                                                          \
     if (pf)                                                                                                          \
       hipLaunchKernelGGL((k_ilqr_forward<NJ, CHAIN, SOFTV, MT, RV, true>), TMPC_GRID(B * T, 64), pf_lds, s,           \
@@ -1194,6 +1204,7 @@ struct LaunchIlqr {
       const int tg = soft_add_group(T, N);
       hipLaunchKernelGGL((k_ilqr_soft_add<NJ>), dim3(B), dim3(64), (size_t)tg * (N + 1) * sizeof(double), s, Cs, mu, lam,
                          P, B, N, T, tg, xt, ut, active, ok, Jt);
+    }
     }
   }
 };
@@ -1213,6 +1224,7 @@ struct LaunchIlqr {
     case 5: if (chain) LaunchIlqr<5, true, ModelRef>::CALL; else LaunchIlqr<5, false, ModelRef>::CALL; break;  \
     case 6: if (chain) LaunchIlqr<6, true, ModelRef>::CALL; else LaunchIlqr<6, false, ModelRef>::CALL; break;  \
     case 7: if (chain) LaunchIlqr<7, true, ModelRef>::CALL; else LaunchIlqr<7, false, ModelRef>::CALL; break;  \
+    TMPC_WIDE_CASES(LaunchIlqr, CALL)                                                                  \
     default: return -2;                                                                                \
   }                                                                                                    \
   return 0;
@@ -1249,6 +1261,14 @@ int launch_ilqr_init_cost(hipStream_t s, int nj, const CostDev* C, const ConstrD
   switch (nj) {
     TMPC_INIT_COST(1) TMPC_INIT_COST(2) TMPC_INIT_COST(3) TMPC_INIT_COST(4) TMPC_INIT_COST(5) TMPC_INIT_COST(6)
     TMPC_INIT_COST(7)
+#define TMPC_INIT_COST_WIDE(V)   /* a wide model: no soft limits */                                         \
+  case V:                                                                                                      \
+    if (mu) return -2;                                                                                         \
+    hipLaunchKernelGGL((k_ilqr_init_cost<V, false>), dim3(B), dim3(64), lds, s, C, Cs, mu, lam, P, B, N, x, u, mask, Jt); \
+    return 0;
+    TMPC_INIT_COST_WIDE(8) TMPC_INIT_COST_WIDE(9) TMPC_INIT_COST_WIDE(10) TMPC_INIT_COST_WIDE(11)
+    TMPC_INIT_COST_WIDE(12)
+#undef TMPC_INIT_COST_WIDE
     default: return -2;
   }
 #undef TMPC_INIT_COST
