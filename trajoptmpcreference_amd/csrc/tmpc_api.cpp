@@ -264,8 +264,9 @@ static int check_ready(tmpc_ctx* ctx, int B, int N, bool qp = true) {
 // The QP takes the banded variable-block path of tmpc_hard.hip -- built for hard box constraints --
 // with hard limits, and also without them past the fused k_qp's QP_MAX_ROWS (1536) rows: there the
 // Schur complement is the same block-tridiagonal S with no constraint rows (every knot's row count 0),
-// which the banded kernels solve up to HARD_PCG_MAX_ROWS rows by PCG (and without a row limit by the
-// direct banded elimination), in their own canonical order (oracle/hard.py pcg_canonical).
+// which the banded kernels solve up to HARD_PCG_MAX_ROWS rows by PCG (and by the direct banded
+// elimination up to k_hard_schur's LDS bound, checked in setup_hard), in their own canonical order
+// (oracle/hard.py pcg_canonical).
 static bool qp_banded(const tmpc_ctx* ctx, int N) {
   return ctx->hlim.any_hard || N * 2 * ctx->hmodel.n > QP_MAX_ROWS;
 }
