@@ -1324,31 +1324,48 @@ __global__ void __launch_bounds__(64) k_hard_dxu(const CostDev* __restrict__ C, 
   const double* L = lam + (size_t)b * dmax;
   const int* ro = roff + (size_t)b * N;
   const int* ho = hoff + (size_t)b * N;
+  // every array index below is static once the loops are unrolled (round 6: the hard rows' column
+  // index and the plugin block's runtime row count had put ctl / rhs in scratch, 304 B per lane at
+  // arm6); a hard row's term goes to its column through a compare per column, the same update of the
+  // same element
   double ctl[3 * NJ];
+#pragma unroll
   for (int m = 0; m < NXU; ++m) ctl[m] = 0.0;
+#pragma unroll
   for (int i = 0; i < NX; ++i) ctl[i] = L[ro[k] + i];
   if (k < K) {
     const double* A = Aall + ((size_t)b * K + k) * NX * NX;
     const double* Bk = Ball + ((size_t)b * K + k) * NX * NU;
     const double* l1 = L + ro[k + 1];
+#pragma unroll
     for (int j = 0; j < NX; ++j) {
       double atl = 0.0;
+#pragma unroll
       for (int m = 0; m < NX; ++m) atl += A[m * NX + j] * l1[m];
       ctl[j] = ctl[j] - atl;
     }
+#pragma unroll
     for (int j = 0; j < NU; ++j) {
       double btl = 0.0;
+#pragma unroll
       for (int m = 0; m < NX; ++m) btl += Bk[m * NU + j] * l1[m];
       ctl[NX + j] = -btl;
     }
   }
   const size_t hb = ((size_t)b * N + k) * rmax;
-  for (int s = 0; s < cnt[(size_t)b * N + k]; ++s) ctl[hcol[hb + s]] += hsgn[hb + s] * L[ho[k] + s];
+  for (int s = 0; s < cnt[(size_t)b * N + k]; ++s) {
+    const int col = hcol[hb + s];
+    const double hs = hsgn[hb + s], lv = L[ho[k] + s];
+#pragma unroll
+    for (int c = 0; c < NXU; ++c)
+      if (c == col) ctl[c] += hs * lv;
+  }
   const HGhat<NJ> Gh{per_knot ? Ghat + (size_t)b * N * HGhat<NJ>::GS : Ghat + (size_t)b * 3 * NX * NX, per_knot != 0};
   const double* xb = x + (size_t)b * NX * N;
   const double* ub = u + (size_t)b * NU * K;
   const double* js = jsoft ? jsoft + (size_t)b * N * NXU : nullptr;
   double rhs[3 * NJ];
+#pragma unroll
   for (int m = 0; m < NXU; ++m)
     rhs[m] = (m < NX || k < K) ? (gvec ? gvec[((size_t)b * N + k) * NXU + m] : hard_grad<NJ>(C, xb, ub, js, N, k, m))
                                      - ctl[m]
@@ -1356,24 +1373,34 @@ __global__ void __launch_bounds__(64) k_hard_dxu(const CostDev* __restrict__ C, 
   if (per_knot == 2) {   // the plugin-hook QP's full block (k_ghat_full): dxu_k = Ghat_k (g_k - (C^T lambda)_k)
     const double* G = Ghat + ((size_t)b * N + k) * NXU * NXU;
     const int m = k < K ? NXU : NX;
-    for (int i = 0; i < m; ++i) {
+#pragma unroll
+    for (int i = 0; i < NXU; ++i) {
+      if (i >= m) break;
       double acc = 0.0;
-      for (int j = 0; j < m; ++j) acc += G[i * NXU + j] * rhs[j];
+#pragma unroll
+      for (int j = 0; j < NXU; ++j) {
+        if (j >= m) break;
+        acc += G[i * NXU + j] * rhs[j];
+      }
       if (i < NX) dx[((size_t)b * N + k) * NX + i] = acc;
       else du[((size_t)b * K + k) * NU + (i - NX)] = acc;
     }
     return;
   }
   const double* Gx = Gh.x(C, k, N);
+#pragma unroll
   for (int i = 0; i < NX; ++i) {
     double acc = 0.0;
+#pragma unroll
     for (int j = 0; j < NX; ++j) acc += Gx[i * NX + j] * rhs[j];
     dx[((size_t)b * N + k) * NX + i] = acc;
   }
   if (k < K) {
     const double* Gu = Gh.u(k);
+#pragma unroll
     for (int i = 0; i < NU; ++i) {
       double acc = 0.0;
+#pragma unroll
       for (int j = 0; j < NU; ++j) acc += Gu[i * NU + j] * rhs[NX + j];
       du[((size_t)b * K + k) * NU + i] = acc;
     }
@@ -1396,20 +1423,36 @@ __global__ void __launch_bounds__(256) k_hard_ls(const ConstrDev* __restrict__ C
   const int K = N - 1;
   const double al = alphas[t];
   double z[3 * NJ];
+#pragma unroll
   for (int m = 0; m < NX; ++m) {
     const double xm = x[((size_t)b * NX + m) * N + k];
     z[m] = dx ? xm - al * dx[((size_t)b * N + k) * NX + m] : xm;
   }
+#pragma unroll
   for (int m = 0; m < NU; ++m) {
     double um = k < K ? u[((size_t)b * NU + m) * K + k] : 0.0;
     if (dx && k < K) um = um - al * du[((size_t)b * K + k) * NU + m];
     z[NX + m] = um;
   }
-  int col[6 * NJ];
-  double sg[6 * NJ], val[6 * NJ];
-  const int m = hard_knot_rows<NJ>(Cs, z, k == K, 6 * NJ, col, sg, val);
+  // hard_knot_rows' rows in its order (type, then lower / upper bound per joint), each |value| added as it
+  // is formed: the same sum in the same order as summing its val[] afterwards.  Its row arrays, indexed
+  // by the running row count, lived in scratch here (k_hard_ls averaged 0.29 ms, profiles/r06/counters);
+  // unrolled in full every z index is static and the kernel keeps no arrays.
+  const bool terminal = k == K;
   double s = 0.0;
-  for (int i = 0; i < m; ++i) s += fabs(val[i]);
+#pragma unroll
+  for (int ty = 0; ty < 3; ++ty) {
+    const int hm = Cs->hard[ty];
+    if (hm == HARD_NONE || (ty == 2 && terminal)) continue;
+#pragma unroll
+    for (int e = 0; e < 2 * NJ; ++e) {
+      const int i = e < NJ ? e : e - NJ;
+      const double zi = z[ty * NJ + i];
+      const double v = e < NJ ? zi - Cs->lb[ty][i] : Cs->ub[ty][i] - zi;
+      if (hm == HARD_ACTIVE && !(v < 0.0)) continue;
+      s += fabs(v);
+    }
+  }
   hterms[gid] = s;
 }
 

@@ -18,6 +18,7 @@
 //                    (:457-481), the trace row and the copy of the accepted
 //                    trajectory.
 #include "tmpc_internal.h"
+#include "tmpc_copy.h"
 
 namespace tmpc {
 
@@ -1123,15 +1124,18 @@ __global__ void __launch_bounds__(64) k_ilqr_decide(PList P, int B, int N, int N
   if (choice >= 0) {
     const double* xs_ = xt + ((size_t)b * T + choice) * NX * N;
     const double* us_ = ut + ((size_t)b * T + choice) * NU * K;
-    // trial trajectories are knot-major ([k][m], see k_ilqr_forward); x / u the reference's [m][k]
-    for (int e = t; e < NX * N; e += 64) {
+    // trial trajectories are knot-major ([k][m], see k_ilqr_forward); x / u the reference's [m][k]; the
+    // loads of U passes ahead of their stores (tmpc_copy.h)
+    double* xb = x + (size_t)b * NX * N;
+    double* ub = u + (size_t)b * NU * K;
+    wg_batched<12, double>(NX * N, t, 64, [&](int e) {
       const int m = e / N, k = e - m * N;
-      x[(size_t)b * NX * N + e] = xs_[k * NX + m];
-    }
-    for (int e = t; e < NU * K; e += 64) {
+      return xs_[k * NX + m];
+    }, [&](int e, double v) { xb[e] = v; });
+    wg_batched<8, double>(NU * K, t, 64, [&](int e) {
       const int m = e / K, k = e - m * K;
-      u[(size_t)b * NU * K + e] = us_[k * NU + m];
-    }
+      return us_[k * NU + m];
+    }, [&](int e, double v) { ub[e] = v; });
   }
 }
 

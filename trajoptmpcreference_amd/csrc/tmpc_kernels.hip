@@ -19,6 +19,7 @@
 // [b][k][r][c]; Schur blocks S_diag[b][k][i][j], S_lo[b][k][i][j] = S_{k+1,k}.
 #include "tmpc_internal.h"
 #include "tmpc_pcg.h"
+#include "tmpc_copy.h"
 
 namespace tmpc {
 
@@ -951,7 +952,8 @@ __global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX,
   if (staged) {
     const double* src = terms + (size_t)b * T * N * 4;
     const int ne = T * N * 4;
-#pragma unroll 8
+    // 18 passes' loads in flight (36 per lane at T = 9, N = 64: two round trips; 8 took five)
+#pragma unroll 18
     for (int e = t; e < ne; e += 64) s_terms[e] = src[e];
     if (hterms) {
       const double* hs = hterms + (size_t)b * T * N;
@@ -1075,17 +1077,18 @@ __global__ void __launch_bounds__(64) k_ls_decide(PList P, int B, int N, int NX,
     const double al = alphas[choice];
     double* xb = x + (size_t)b * NX * N;
     const double* dxb = dx + (size_t)b * N * NX;
-    for (int e = t; e < NX * N; e += blockDim.x) {
+    // x - alpha dx, u - alpha du element by element, the loads of U passes ahead of their stores (tmpc_copy.h)
+    wg_batched<12, double>(NX * N, t, blockDim.x, [&](int e) {
       const int m = e / N, k = e - m * N;
-      xb[e] = xb[e] - al * dxb[k * NX + m];
-    }
+      return xb[e] - al * dxb[k * NX + m];
+    }, [&](int e, double v) { xb[e] = v; });
     const int K = N - 1;
     double* ub = u + (size_t)b * NU * K;
     const double* dub = du + (size_t)b * K * NU;
-    for (int e = t; e < NU * K; e += blockDim.x) {
+    wg_batched<8, double>(NU * K, t, blockDim.x, [&](int e) {
       const int m = e / K, k = e - m * K;
-      ub[e] = ub[e] - al * dub[k * NU + m];
-    }
+      return ub[e] - al * dub[k * NU + m];
+    }, [&](int e, double v) { ub[e] = v; });
   } else if (choice == -2 && t == 0) {
     *active_count = 1;
   }
@@ -1451,10 +1454,10 @@ __device__ void stream_handover(int s, const StreamDev& sd, double* __restrict__
   double* ub = u + (size_t)s * UN;
   if (t == 0) s_next = atomicAdd(sd.next, 1);
   if (old_l >= 0) {
-    if (sd.x_out)
-      for (int e = t; e < XN; e += nt) sd.x_out[(size_t)old * XN + e] = xb[e];
-    if (sd.u_out)
-      for (int e = t; e < UN; e += nt) sd.u_out[(size_t)old * UN + e] = ub[e];
+    // the rows' loads batched ahead of their stores (tmpc_copy.h): 12 + 6 passes at arm6 N = 64 were
+    // that many dependent round trips
+    if (sd.x_out) wg_copy<12>(sd.x_out + (size_t)old * XN, xb, XN, t, nt);
+    if (sd.u_out) wg_copy<8>(sd.u_out + (size_t)old * UN, ub, UN, t, nt);
     if (sd.status && t == 0) {
       int* so = sd.status + (size_t)old * 4;
       so[0] = st.exit_sqp[s];
@@ -1464,14 +1467,12 @@ __device__ void stream_handover(int s, const StreamDev& sd, double* __restrict__
     }
     const TraceDev& to = sd.tr_out;
     const size_t ri = (size_t)s * W, ro = (size_t)old * W;
-    for (int r = t; r < W; r += nt) {
 #define TMPC_TR_COPY(f) \
-  if (to.f) to.f[ro + r] = tr.f[ri + r];
-      TMPC_TR_COPY(iteration) TMPC_TR_COPY(ls_iter) TMPC_TR_COPY(alpha) TMPC_TR_COPY(rho) TMPC_TR_COPY(J)
-      TMPC_TR_COPY(c) TMPC_TR_COPY(merit) TMPC_TR_COPY(D) TMPC_TR_COPY(ratio) TMPC_TR_COPY(accepted)
-      TMPC_TR_COPY(pcg_iters) TMPC_TR_COPY(singular)
+  if (to.f) wg_copy<4>(to.f + ro, tr.f + ri, W, t, nt);
+    TMPC_TR_COPY(iteration) TMPC_TR_COPY(ls_iter) TMPC_TR_COPY(alpha) TMPC_TR_COPY(rho) TMPC_TR_COPY(J)
+    TMPC_TR_COPY(c) TMPC_TR_COPY(merit) TMPC_TR_COPY(D) TMPC_TR_COPY(ratio) TMPC_TR_COPY(accepted)
+    TMPC_TR_COPY(pcg_iters) TMPC_TR_COPY(singular)
 #undef TMPC_TR_COPY
-    }
   }
   __syncthreads();   // every read of the finished problem precedes the writes of the next one
   const int nw = s_next;
@@ -1480,8 +1481,8 @@ __device__ void stream_handover(int s, const StreamDev& sd, double* __restrict__
     return;
   }
   const size_t src = (size_t)((sd.pbase + nw) % sd.period);
-  for (int e = t; e < XN; e += nt) xb[e] = sd.x_in[src * XN + e];
-  for (int e = t; e < UN; e += nt) ub[e] = sd.u_in[src * UN + e];
+  wg_copy<12>(xb, sd.x_in + src * XN, XN, t, nt);
+  wg_copy<8>(ub, sd.u_in + src * UN, UN, t, nt);
   for (int m = t; m < sd.NX; m += nt) xs[(size_t)s * sd.NX + m] = sd.x_in[src * XN + (size_t)m * sd.N];
   if (mu) {
     const int MC = sd.MC;
@@ -1531,22 +1532,41 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
   auto zval = [&](int t, int i, int k) -> double {
     return t == 2 ? ub[i * K + k] : xb[(t * NJ + i) * N + k];
   };
-  // max_c over (type, knot) pairs (the pair's 2 n values loaded together, then reduced in order)
+  // max_c over (type, knot) pairs (the pair's 2 n values loaded together, then reduced in order); PB pairs'
+  // loads per lane issued before any is reduced (one round trip for arm6 N = 64's three passes)
   double mx = 0.0;
-  for (int p = t0; p < 3 * N; p += 64) {
-    const int t = p / N, k = p - t * N;
-    if (Cs->mode[t] == SOFT_NONE || (t == 2 && k == K)) continue;
-    double zz[NJMAX];
+  constexpr int PB = 4;
+  for (int p0 = t0; p0 < 3 * N; p0 += 64 * PB) {
+    double zz[PB][NJMAX];
+    bool okp[PB];
 #pragma unroll
-    for (int i = 0; i < NJMAX; ++i) zz[i] = i < NJ ? zval(t, i, k) : 0.0;
-    double mn = 0.0;
+    for (int j = 0; j < PB; ++j) {
+      const int p = p0 + 64 * j;
+      const int t = p / N, k = p - t * N;
+      okp[j] = p < 3 * N && Cs->mode[t] != SOFT_NONE && !(t == 2 && k == K);
 #pragma unroll
-    for (int e = 0; e < 2 * NJMAX; ++e) {
-      if (e >= 2 * NJ) break;
-      const double v = soft_v(Cs, t, e, NJ, zz[e < NJ ? e : e - NJ]);
-      mn = e == 0 ? v : fmin(mn, v);
+      for (int i = 0; i < NJMAX; ++i) zz[j][i] = (okp[j] && i < NJ) ? zval(t, i, k) : 0.0;
     }
-    mx = fmax(mx, fabs(mn));
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      if (!okp[j]) continue;
+      const int t = (p0 + 64 * j) / N;
+      // the lower bounds' values, then the upper ones' (e = i, then NJ + i): the pair's order, with
+      // static indices into zz (NJ is a launch argument: zz[e - NJ] had put zz in scratch)
+      double mn = 0.0;
+#pragma unroll
+      for (int i = 0; i < NJMAX; ++i) {
+        if (i >= NJ) break;
+        const double v = soft_v(Cs, t, i, NJ, zz[j][i]);
+        mn = i == 0 ? v : fmin(mn, v);
+      }
+#pragma unroll
+      for (int i = 0; i < NJMAX; ++i) {
+        if (i >= NJ) break;
+        mn = fmin(mn, soft_v(Cs, t, NJ + i, NJ, zz[j][i]));
+      }
+      mx = fmax(mx, fabs(mn));
+    }
   }
   __shared__ double smax[64];
   __shared__ int s_exit, s_changed, s_done;
@@ -1567,7 +1587,7 @@ __global__ void __launch_bounds__(64) k_soft_outer(const ConstrDev* __restrict__
   if (s_exit == 0) {
     // update_soft_constraint_constants entry by entry; OB entries per lane have their loads issued together
     // before any of them is updated (each entry's arithmetic is unchanged)
-    constexpr int OB = 6;
+    constexpr int OB = 18;
     for (int p0 = t0; p0 < N * MC; p0 += 64 * OB) {
       double zv[OB], ph[OB], mv[OB], lv[OB];
       bool ok[OB];
@@ -1709,8 +1729,8 @@ __global__ void __launch_bounds__(256) k_stream_init(int B, StreamDev sd, double
   const int s = blockIdx.x, t = threadIdx.x;
   const int XN = sd.NX * sd.N, UN = sd.NU * (sd.N - 1);
   const size_t src = (size_t)((sd.pbase + s) % sd.period);
-  for (int e = t; e < XN; e += blockDim.x) x[(size_t)s * XN + e] = sd.x_in[src * XN + e];
-  for (int e = t; e < UN; e += blockDim.x) u[(size_t)s * UN + e] = sd.u_in[src * UN + e];
+  wg_copy<4>(x + (size_t)s * XN, sd.x_in + src * XN, XN, t, blockDim.x);
+  wg_copy<4>(u + (size_t)s * UN, sd.u_in + src * UN, UN, t, blockDim.x);
   if (t == 0) {
     sd.slot_pid[s] = s;
     if (s == 0) *sd.next = B;   // the next pending problem (stream_handover takes them with atomics)
